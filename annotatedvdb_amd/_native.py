@@ -1,0 +1,146 @@
+"""ctypes binding of ``libavdb_hip.so`` (the C ABI declared in ``include/avdb.h``).
+
+The product path has exactly one implementation: the HIP kernels in this
+library.  There is no CPU fallback — if the library (or a GPU) is missing,
+every compute call raises :class:`NativeUnavailable`.
+
+``torch`` is imported first on purpose: it bundles ``libamdhip64.so.7`` and the
+library must bind to that same HIP runtime instance (one runtime per process),
+so device pointers from torch's allocator are valid inside our kernels.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch  # noqa: F401  (loads torch's HIP runtime before ours; see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libavdb_hip.so")
+
+AVDB_OK = 0
+AVDB_EINVAL = -1
+AVDB_EHIP = -2
+AVDB_ENOMEM = -3
+AVDB_ERANGE = -4
+
+STATUS_OK = 0
+STATUS_UNKNOWN_CHROM = 1
+STATUS_OUT_OF_RANGE = 2
+STATUS_END_BEFORE_START = 3
+BIN_NONE = 0xFFFFFFFF
+N_LEVELS = 14
+MAX_CHROM = 64
+DIGEST_CHARS = 32
+MAX_PATH = 128
+N_COUNTERS = 32
+CTR_LEVEL0 = 0
+CTR_STATUS0 = 16
+CTR_RECORDS = 20
+CTR_DUPLICATES = 21
+CTR_HASH_COLLISIONS = 22
+CTR_LONG = 23
+
+# every symbol include/avdb.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED_SYMBOLS = [
+    "avdb_abi_version", "avdb_last_error", "avdb_device_count",
+    "avdb_ctx_create", "avdb_ctx_destroy", "avdb_ctx_n_chrom",
+    "avdb_ctx_set_sequence_digests", "avdb_l8_bin_count",
+    "avdb_bin_assign", "avdb_record_prep",
+    "avdb_pk_dedup_workspace_size", "avdb_pk_dedup",
+    "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest",
+    "avdb_format_bin_path", "avdb_format_bin_paths",
+]
+
+
+class NativeUnavailable(RuntimeError):
+    """libavdb_hip.so (or a GPU to run it on) is not available."""
+
+
+class NativeError(RuntimeError):
+    def __init__(self, fn: str, rc: int, msg: str):
+        super().__init__(f"{fn} failed (rc={rc}): {msg}")
+        self.rc = rc
+
+
+_lib = None
+_lock = threading.Lock()
+
+P = ctypes.c_void_p
+SZ = ctypes.c_size_t
+U32 = ctypes.c_uint32
+I32 = ctypes.c_int
+U8 = ctypes.c_uint8
+
+
+def _sig(lib):
+    f = lib
+    f.avdb_abi_version.restype = I32
+    f.avdb_last_error.restype = ctypes.c_char_p
+    f.avdb_device_count.argtypes = [ctypes.POINTER(I32)]
+    f.avdb_ctx_create.argtypes = [I32, ctypes.POINTER(U32), I32, ctypes.POINTER(P)]
+    f.avdb_ctx_destroy.argtypes = [P]
+    f.avdb_ctx_n_chrom.argtypes = [P]
+    f.avdb_ctx_set_sequence_digests.argtypes = [P, ctypes.c_char_p, I32]
+    f.avdb_l8_bin_count.argtypes = [P, ctypes.POINTER(U32)]
+    f.avdb_bin_assign.argtypes = [P, P, P, P, SZ, P, P, P, P, P]
+    f.avdb_record_prep.argtypes = [P, P, P, P, P, P, P, SZ, P, P, P, P, P, P, P]
+    f.avdb_pk_dedup_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
+    f.avdb_pk_dedup.argtypes = [P, P, P, P, P, P, P, P, SZ, I32, P, SZ, P, P, P]
+    f.avdb_sha512t24u.argtypes = [P, P, P, P, SZ, P, P]
+    f.avdb_vrs_digest_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
+    f.avdb_vrs_digest.argtypes = [P, P, P, P, P, P, P, SZ, U32, P, SZ, P, P, P]
+    f.avdb_format_bin_path.argtypes = [P, U8, U32, ctypes.c_char_p, SZ]
+    f.avdb_format_bin_paths.argtypes = [P, P, P, SZ, P, SZ, P]
+    for name in EXPORTED_SYMBOLS:
+        if name not in ("avdb_last_error",):
+            getattr(f, name).restype = I32
+
+
+def load_library(path: Optional[str] = None):
+    """Load (once) and return the ctypes handle; raise loudly if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or os.environ.get("AVDB_LIB", LIB_PATH)
+        if not os.path.exists(p):
+            raise NativeUnavailable(
+                f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        lib = ctypes.CDLL(p)
+        _sig(lib)
+        if lib.avdb_abi_version() != 1:
+            raise NativeUnavailable("libavdb_hip ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    return load_library().avdb_last_error().decode(errors="replace")
+
+
+def check(fn: str, rc: int) -> int:
+    if rc < 0:
+        raise NativeError(fn, rc, last_error())
+    return rc
+
+
+def ptr(t) -> int:
+    """Raw device/host address of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise NativeUnavailable("no ROCm GPU visible (torch.cuda.is_available() is False); "
+                                "the avdb kernels run only on gfx950 — there is no CPU fallback")

@@ -1,0 +1,350 @@
+// K1 bin_assign and K2 record_prep — gfx950.
+//
+// K1 replaces BinIndex.find_bin_index (BinIndex/lib/python/bin_index.py:59-75)
+// and the SQL find_bin_index it reaches through BIN_INDEX_SQL (:9-14): the
+// deepest BinIndexRef row (generate_bin_index_references.py:46-83) whose
+// (lo,hi] holds the closed interval [start,end].  The table is nested and
+// aligned, so the search is closed-form integer arithmetic: two magic-multiply
+// divisions by 15,625, an XOR and a count-leading-zeros.
+//
+// K2 fuses the per-alt end inference (variant_annotator.py:36-121) in front of
+// the same bin computation (vcf_variant_loader.py:309-311).
+//
+// Both are HBM-streaming kernels (9-13 algorithmic bytes per record for K1):
+// coalesced 16-B-per-lane loads/stores, a block-contiguous partition of the
+// batch (so a position-sorted batch hits a narrow, LDS-resident slice of the
+// histogram), per-contig lengths and L8 offsets staged in LDS, and
+// wave-ballot run aggregation for the histogram atomics.
+#include "avdb_internal.hpp"
+
+namespace avdb {
+
+// stage the per-lane-indexed part of the chromosome table + zero LDS state
+__device__ __forceinline__ void stage_table(const ChromTable& tab, uint32_t* s_len, uint32_t* s_l8off,
+                                            unsigned long long* s_ctr, uint32_t* s_hist,
+                                            bool lds_hist) {
+  const int t = threadIdx.x;
+  if (t < AVDB_MAX_CHROM) {
+    s_len[t] = tab.len[t];
+    s_l8off[t] = tab.l8_off[t];
+  }
+  if (t < AVDB_N_COUNTERS) s_ctr[t] = 0;
+  if (lds_hist)
+    for (uint32_t b = t; b < tab.n_l8; b += blockDim.x) s_hist[b] = 0;
+  __syncthreads();
+}
+
+__device__ __forceinline__ void publish(const ChromTable& tab, const unsigned long long* s_ctr,
+                                        const uint32_t* s_hist, bool lds_hist, bool hist,
+                                        uint32_t* __restrict__ g_hist,
+                                        unsigned long long* __restrict__ g_ctr) {
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (g_ctr && t < AVDB_N_COUNTERS && s_ctr[t]) atomicAdd(&g_ctr[t], s_ctr[t]);
+  if (hist && lds_hist)
+    for (uint32_t b = t; b < tab.n_l8; b += blockDim.x)
+      if (s_hist[b]) atomicAdd(&g_hist[b], s_hist[b]);
+}
+
+__device__ __forceinline__ uint32_t l8_key(uint32_t c, uint32_t s, uint32_t code,
+                                           const uint32_t* s_l8off) {
+  return code == AVDB_BIN_NONE ? 0xFFFFFFFFu : s_l8off[c] + (s - 1u) / kL8Width;
+}
+
+// ---------------------------------------------------------------------------
+// K1, vector form: 4 records per lane-group (u32 of chrom codes, uint4 of
+// starts/ends/codes), UNROLL groups in flight per lane.
+// ---------------------------------------------------------------------------
+template <bool HAS_END, bool HIST>
+__global__ __launch_bounds__(kBlock) void k_bin_assign4(
+    const uint32_t* __restrict__ chrom4, const u32x4* __restrict__ start4,
+    const u32x4* __restrict__ end4, size_t ngroups, u32x4* __restrict__ code4,
+    uint32_t* __restrict__ status4, ChromTable tab, uint32_t* __restrict__ g_hist,
+    unsigned long long* __restrict__ g_ctr, int lds_hist,
+    // scalar tail [tail_begin, n): block 0, wave 0
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ start,
+    const uint32_t* __restrict__ end, size_t tail_begin, size_t n,
+    uint32_t* __restrict__ code, uint8_t* __restrict__ status) {
+  extern __shared__ uint32_t s_hist[];
+  __shared__ uint32_t s_len[AVDB_MAX_CHROM];
+  __shared__ uint32_t s_l8off[AVDB_MAX_CHROM];
+  __shared__ unsigned long long s_ctr[AVDB_N_COUNTERS];
+  const bool use_lds = HIST && lds_hist;
+  stage_table(tab, s_len, s_l8off, s_ctr, s_hist, use_lds);
+  uint32_t* hist = use_lds ? s_hist : g_hist;
+  const bool ctrs = g_ctr != nullptr;
+  const int n_chrom = tab.n;
+
+  // block-contiguous chunk of groups
+  const size_t per = (ngroups + gridDim.x - 1) / gridDim.x;
+  const size_t g0 = size_t(blockIdx.x) * per;
+  const size_t g1 = g0 + per < ngroups ? g0 + per : ngroups;
+
+  constexpr int UNROLL = 4;
+  LaneCounters lc;
+  int since_flush = 0;
+  for (size_t base = g0; base < g1; base += size_t(kBlock) * UNROLL) {
+    uint32_t c4[UNROLL];
+    u32x4 s4[UNROLL], e4[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const size_t j = base + size_t(u) * kBlock + threadIdx.x;
+      if (j < g1) {
+        c4[u] = __builtin_nontemporal_load(&chrom4[j]);
+        s4[u] = __builtin_nontemporal_load(&start4[j]);
+        if (HAS_END) e4[u] = __builtin_nontemporal_load(&end4[j]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const size_t j = base + size_t(u) * kBlock + threadIdx.x;
+      const bool live = j < g1;
+      const uint32_t sv[4] = {s4[u].x, s4[u].y, s4[u].z, s4[u].w};
+      uint32_t ev[4] = {sv[0], sv[1], sv[2], sv[3]};
+      if (HAS_END) { ev[0] = e4[u].x; ev[1] = e4[u].y; ev[2] = e4[u].z; ev[3] = e4[u].w; }
+      uint32_t cv[4], st = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t c = (c4[u] >> (8 * k)) & 0xFFu;
+        const uint32_t s_k = classify(c, sv[k], ev[k], n_chrom, s_len, &cv[k]);
+        st |= s_k << (8 * k);
+        if (ctrs && live) lc.add(cv[k], s_k);
+        if (HIST) wave_hist_add(live ? l8_key(c, sv[k], cv[k], s_l8off) : 0xFFFFFFFFu, hist);
+      }
+      if (live) {
+        __builtin_nontemporal_store(u32x4{cv[0], cv[1], cv[2], cv[3]}, &code4[j]);
+        if (status4) __builtin_nontemporal_store(st, &status4[j]);
+      }
+    }
+    if (ctrs && ++since_flush == 15) {  // 15 * UNROLL * 4 = 240 < 256 per 8-bit field
+      lc.flush(s_ctr);
+      since_flush = 0;
+    }
+  }
+  // scalar tail (< 4 records)
+  if (blockIdx.x == 0 && threadIdx.x < kWave) {
+    const size_t i = tail_begin + threadIdx.x;
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < n) {
+      const uint32_t c = chrom[i], s = start[i], e = HAS_END ? end[i] : s;
+      uint32_t cv;
+      const uint32_t s_k = classify(c, s, e, n_chrom, s_len, &cv);
+      code[i] = cv;
+      if (status) status[i] = uint8_t(s_k);
+      if (ctrs) lc.add(cv, s_k);
+      key = l8_key(c, s, cv, s_l8off);
+    }
+    if (HIST) wave_hist_add(key, hist);
+  }
+  if (ctrs) {
+    lc.flush(s_ctr);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const size_t recs = (g1 > g0 ? (g1 - g0) * 4 : 0) + (blockIdx.x == 0 ? n - tail_begin : 0);
+      atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)recs);
+    }
+  }
+  publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
+}
+
+// K1, scalar form: any alignment, one record per lane.
+template <bool HAS_END, bool HIST>
+__global__ __launch_bounds__(kBlock) void k_bin_assign1(
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ start,
+    const uint32_t* __restrict__ end, size_t n, uint32_t* __restrict__ code,
+    uint8_t* __restrict__ status, ChromTable tab, uint32_t* __restrict__ g_hist,
+    unsigned long long* __restrict__ g_ctr, int lds_hist) {
+  extern __shared__ uint32_t s_hist[];
+  __shared__ uint32_t s_len[AVDB_MAX_CHROM];
+  __shared__ uint32_t s_l8off[AVDB_MAX_CHROM];
+  __shared__ unsigned long long s_ctr[AVDB_N_COUNTERS];
+  const bool use_lds = HIST && lds_hist;
+  stage_table(tab, s_len, s_l8off, s_ctr, s_hist, use_lds);
+  uint32_t* hist = use_lds ? s_hist : g_hist;
+  const bool ctrs = g_ctr != nullptr;
+  const size_t per = (n + gridDim.x - 1) / gridDim.x;
+  const size_t i0 = size_t(blockIdx.x) * per;
+  const size_t i1 = i0 + per < n ? i0 + per : n;
+  LaneCounters lc;
+  int since = 0;
+  for (size_t base = i0; base < i1; base += kBlock) {
+    const size_t i = base + threadIdx.x;
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < i1) {
+      const uint32_t c = chrom[i], s = start[i], e = HAS_END ? end[i] : s;
+      uint32_t cv;
+      const uint32_t s_k = classify(c, s, e, tab.n, s_len, &cv);
+      code[i] = cv;
+      if (status) status[i] = uint8_t(s_k);
+      if (ctrs) lc.add(cv, s_k);
+      key = l8_key(c, s, cv, s_l8off);
+    }
+    if (HIST) wave_hist_add(key, hist);
+    if (ctrs && ++since == 255) { lc.flush(s_ctr); since = 0; }
+  }
+  if (ctrs) {
+    lc.flush(s_ctr);
+    __syncthreads();
+    if (threadIdx.x == 0 && i1 > i0) atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)(i1 - i0));
+  }
+  publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
+}
+
+// ---------------------------------------------------------------------------
+// K2: end inference (+ common-prefix length) fused with the bin computation.
+// ---------------------------------------------------------------------------
+// variant_annotator.py:36-79 with lcp from __normalize_alleles (:82-121).
+__device__ __forceinline__ uint32_t infer_end(const uint8_t* __restrict__ heap, uint64_t off,
+                                              uint32_t r, uint32_t a, uint32_t pos,
+                                              uint32_t* lcp_out) {
+  if (r == 1u && a == 1u) { *lcp_out = 0; return pos; }        // SNV (:54-55)
+  const uint8_t* ref = heap + off;
+  const uint8_t* alt = ref + r;
+  const uint32_t m = r < a ? r : a;
+  uint32_t n = 0;
+  while (n < m && ref[n] == alt[n]) ++n;                       // lcp (:100-108)
+  *lcp_out = n;
+  const uint32_t nr = r - n, na = a - n;
+  if (r == a) {                                                // MNV (:57-65)
+    bool inv = true;
+    for (uint32_t i = 0; i < r; ++i)
+      if (ref[i] != alt[r - 1u - i]) { inv = false; break; }
+    return inv ? pos + r - 1u : pos + nr - 1u;
+  }
+  if (na >= 1u)                                                // insertion (:67-74)
+    return nr >= 1u ? pos + nr : (r > 1u ? pos + r - 1u : pos + 1u);
+  return nr == 0u ? pos + r - 1u : pos + nr;                   // deletion (:77-79)
+}
+
+template <bool HIST>
+__global__ __launch_bounds__(kBlock) void k_record_prep(
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
+    const uint64_t* __restrict__ allele_off, const uint32_t* __restrict__ ref_len,
+    const uint32_t* __restrict__ alt_len, const uint8_t* __restrict__ heap, size_t n,
+    uint32_t* __restrict__ end_out, uint32_t* __restrict__ code, uint8_t* __restrict__ status,
+    uint32_t* __restrict__ lcp, ChromTable tab, uint32_t* __restrict__ g_hist,
+    unsigned long long* __restrict__ g_ctr, int lds_hist) {
+  extern __shared__ uint32_t s_hist[];
+  __shared__ uint32_t s_len[AVDB_MAX_CHROM];
+  __shared__ uint32_t s_l8off[AVDB_MAX_CHROM];
+  __shared__ unsigned long long s_ctr[AVDB_N_COUNTERS];
+  const bool use_lds = HIST && lds_hist;
+  stage_table(tab, s_len, s_l8off, s_ctr, s_hist, use_lds);
+  uint32_t* hist = use_lds ? s_hist : g_hist;
+  const bool ctrs = g_ctr != nullptr;
+  const size_t per = (n + gridDim.x - 1) / gridDim.x;
+  const size_t i0 = size_t(blockIdx.x) * per;
+  const size_t i1 = i0 + per < n ? i0 + per : n;
+  LaneCounters lc;
+  int since = 0;
+  for (size_t base = i0; base < i1; base += kBlock) {
+    const size_t i = base + threadIdx.x;
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < i1) {
+      const uint32_t c = chrom[i], p = pos[i];
+      uint32_t l;
+      const uint32_t e = infer_end(heap, allele_off[i], ref_len[i], alt_len[i], p, &l);
+      uint32_t cv;
+      const uint32_t s_k = classify(c, p, e, tab.n, s_len, &cv);
+      end_out[i] = e;
+      code[i] = cv;
+      if (status) status[i] = uint8_t(s_k);
+      if (lcp) lcp[i] = l;
+      if (ctrs) lc.add(cv, s_k);
+      key = l8_key(c, p, cv, s_l8off);
+    }
+    if (HIST) wave_hist_add(key, hist);
+    if (ctrs && ++since == 255) { lc.flush(s_ctr); since = 0; }
+  }
+  if (ctrs) {
+    lc.flush(s_ctr);
+    __syncthreads();
+    if (threadIdx.x == 0 && i1 > i0) atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)(i1 - i0));
+  }
+  publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
+}
+
+}  // namespace avdb
+
+using namespace avdb;
+
+static inline bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+static int check_ctx(const avdb_ctx* ctx) {
+  if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
+  return AVDB_OK;
+}
+
+extern "C" int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* start,
+                               const uint32_t* end, size_t n, uint32_t* bin_code, uint8_t* status,
+                               uint32_t* hist_l8, uint64_t* counters, void* stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  if (n == 0) return AVDB_OK;
+  if (!chrom || !start || !bin_code) { avdb_set_error("avdb_bin_assign: null array"); return AVDB_EINVAL; }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool hist = hist_l8 != nullptr;
+  const int lds_hist = hist && ctx->tab.n_l8 <= uint32_t(kMaxLdsHistBins);
+  const size_t shm = lds_hist ? size_t(ctx->tab.n_l8) * 4 : 0;
+  auto* ctr = reinterpret_cast<unsigned long long*>(counters);
+  const bool vec = aligned(chrom, 4) && aligned(start, 16) && (!end || aligned(end, 16)) &&
+                   aligned(bin_code, 16) && (!status || aligned(status, 4)) && n >= 4;
+  if (vec) {
+    const size_t ngroups = n / 4;
+    // ~16 groups (64 records) per lane-pass keeps 4 loads in flight; 2048 WGs = 8/CU
+    const unsigned grid = stream_grid(ngroups, kBlock * 4, 2048);
+    const size_t tail = ngroups * 4;
+#define K1V(HE, HI)                                                                          \
+  hipLaunchKernelGGL((k_bin_assign4<HE, HI>), dim3(grid), dim3(kBlock), shm, s,             \
+                     reinterpret_cast<const uint32_t*>(chrom),                               \
+                     reinterpret_cast<const u32x4*>(start), reinterpret_cast<const u32x4*>(end), \
+                     ngroups, reinterpret_cast<u32x4*>(bin_code),                            \
+                     reinterpret_cast<uint32_t*>(status), ctx->tab, hist_l8, ctr, lds_hist,  \
+                     chrom, start, end, tail, n, bin_code, status)
+    if (end) { if (hist) K1V(true, true); else K1V(true, false); }
+    else { if (hist) K1V(false, true); else K1V(false, false); }
+#undef K1V
+    AVDB_LAUNCH_CHECK("k_bin_assign4");
+  } else {
+    const unsigned grid = stream_grid(n, kBlock * 8, 2048);
+#define K1S(HE, HI)                                                                  \
+  hipLaunchKernelGGL((k_bin_assign1<HE, HI>), dim3(grid), dim3(kBlock), shm, s, chrom, \
+                     start, end, n, bin_code, status, ctx->tab, hist_l8, ctr, lds_hist)
+    if (end) { if (hist) K1S(true, true); else K1S(true, false); }
+    else { if (hist) K1S(false, true); else K1S(false, false); }
+#undef K1S
+    AVDB_LAUNCH_CHECK("k_bin_assign1");
+  }
+  return AVDB_OK;
+}
+
+extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                const uint64_t* allele_off, const uint32_t* ref_len,
+                                const uint32_t* alt_len, const uint8_t* heap, size_t n,
+                                uint32_t* end_out, uint32_t* bin_code, uint8_t* status,
+                                uint32_t* lcp, uint32_t* hist_l8, uint64_t* counters,
+                                void* stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  if (n == 0) return AVDB_OK;
+  if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap || !end_out || !bin_code) {
+    avdb_set_error("avdb_record_prep: null array");
+    return AVDB_EINVAL;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool hist = hist_l8 != nullptr;
+  const int lds_hist = hist && ctx->tab.n_l8 <= uint32_t(kMaxLdsHistBins);
+  const size_t shm = lds_hist ? size_t(ctx->tab.n_l8) * 4 : 0;
+  auto* ctr = reinterpret_cast<unsigned long long*>(counters);
+  const unsigned grid = stream_grid(n, kBlock * 8, 2048);
+  if (hist)
+    hipLaunchKernelGGL((k_record_prep<true>), dim3(grid), dim3(kBlock), shm, s, chrom, pos,
+                       allele_off, ref_len, alt_len, heap, n, end_out, bin_code, status, lcp,
+                       ctx->tab, hist_l8, ctr, lds_hist);
+  else
+    hipLaunchKernelGGL((k_record_prep<false>), dim3(grid), dim3(kBlock), shm, s, chrom, pos,
+                       allele_off, ref_len, alt_len, heap, n, end_out, bin_code, status, lcp,
+                       ctx->tab, hist_l8, ctr, lds_hist);
+  AVDB_LAUNCH_CHECK("k_record_prep");
+  return AVDB_OK;
+}

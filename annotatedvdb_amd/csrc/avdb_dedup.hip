@@ -1,0 +1,209 @@
+// K3 pk_dedup — in-batch primary-key deduplication, gfx950.
+//
+// The key is chr:pos:ref:alt[:refSNP] (primary_key_generator.py:99-122; the
+// long-allele form swaps ref:alt for a digest of (chr,pos,ref,alt)), so two
+// records share a key iff (chrom, pos, ref bytes, alt bytes, ext_id) are equal.
+// The reference never dedups within a batch — COPY inserts duplicates and
+// Load/lib/sql/annotatedvdb_schema/patches/removeDuplicates.sql:2-24 removes
+// them after the fact; the contract here is keep-first-occurrence, stable order.
+//
+// grouped path: equal (chrom,pos) records are contiguous (position-sorted VCF),
+//   so each record only looks back over its own (chrom,pos) run.
+// hash path: 64-bit fingerprints, an open-addressing table that keeps the
+//   minimum record index per fingerprint (atomicMin), then a byte-exact compare
+//   against the winner; a fingerprint collision falls back to an exact scan.
+#include "avdb_internal.hpp"
+
+namespace avdb {
+
+__device__ __forceinline__ bool same_record(const uint8_t* __restrict__ heap,
+                                            const uint64_t* __restrict__ off,
+                                            const uint32_t* __restrict__ rl,
+                                            const uint32_t* __restrict__ al,
+                                            const uint64_t* __restrict__ ext, size_t i, size_t j) {
+  const uint32_t r = rl[i], a = al[i];
+  if (rl[j] != r || al[j] != a) return false;
+  if (ext && ext[i] != ext[j]) return false;
+  const uint8_t* p = heap + off[i];
+  const uint8_t* q = heap + off[j];
+  if (p == q) return true;
+  const uint32_t L = r + a;
+  for (uint32_t k = 0; k < L; ++k)
+    if (p[k] != q[k]) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dedup_grouped(
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap,
+    const uint64_t* __restrict__ ext, size_t n, uint8_t* __restrict__ keep,
+    unsigned long long* __restrict__ g_ctr) {
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  uint32_t dups = 0;
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint8_t c = chrom[i];
+    const uint32_t p = pos[i];
+    uint8_t k = 1;
+    for (size_t j = i; j-- > 0;) {
+      if (chrom[j] != c || pos[j] != p) break;
+      if (same_record(heap, off, rl, al, ext, i, j)) { k = 0; break; }
+    }
+    keep[i] = k;
+    dups += 1u - k;
+  }
+  if (g_ctr) {
+    // wave reduce then one atomic per wave
+    for (int d = 32; d > 0; d >>= 1) dups += __shfl_down(dups, d, kWave);
+    if (__lane_id() == 0 && dups) atomicAdd(&g_ctr[AVDB_CTR_DUPLICATES], (unsigned long long)dups);
+  }
+}
+
+// 64-bit fingerprint of (chrom, pos, ext, ref_len, alt_len, bytes)
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ uint64_t fingerprint(const uint8_t* __restrict__ heap, uint64_t off,
+                                                uint32_t r, uint32_t a, uint8_t c, uint32_t p,
+                                                uint64_t e) {
+  uint64_t h = mix64((uint64_t(c) << 32) ^ p ^ 0x9E3779B97F4A7C15ull);
+  h = mix64(h ^ e);
+  h = mix64(h ^ ((uint64_t(r) << 32) | a));
+  const uint8_t* s = heap + off;
+  const uint32_t L = r + a;
+  uint64_t w = 0;
+  uint32_t k = 0;
+  for (; k < L; ++k) {
+    w = (w << 8) | s[k];
+    if ((k & 7u) == 7u) { h = mix64(h ^ w); w = 0; }
+  }
+  if (k & 7u) h = mix64(h ^ w ^ (uint64_t(k & 7u) << 56));
+  return h ? h : 1ull;  // 0 marks an empty slot
+}
+
+__global__ __launch_bounds__(kBlock) void k_dedup_insert(
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap,
+    const uint64_t* __restrict__ ext, size_t n, uint64_t* __restrict__ fp,
+    unsigned long long* __restrict__ tkey, uint32_t* __restrict__ tidx, uint64_t mask) {
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t h = fingerprint(heap, off[i], rl[i], al[i], chrom[i], pos[i], ext ? ext[i] : 0);
+    fp[i] = h;
+    uint64_t slot = mix64(h) & mask;
+    for (;;) {  // table has >= 2n slots: always terminates
+      const unsigned long long prev = atomicCAS(&tkey[slot], 0ull, (unsigned long long)h);
+      if (prev == 0ull || prev == h) { atomicMin(&tidx[slot], uint32_t(i)); break; }
+      slot = (slot + 1) & mask;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dedup_resolve(
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap,
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
+    const uint64_t* __restrict__ ext, size_t n, const uint64_t* __restrict__ fp,
+    const unsigned long long* __restrict__ tkey, const uint32_t* __restrict__ tidx,
+    uint64_t mask, uint8_t* __restrict__ keep, unsigned long long* __restrict__ g_ctr) {
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  uint32_t dups = 0, coll = 0;
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t h = fp[i];
+    uint64_t slot = mix64(h) & mask;
+    while (tkey[slot] != h) slot = (slot + 1) & mask;
+    const uint32_t w = tidx[slot];
+    uint8_t k = 1;
+    if (w != uint32_t(i)) {
+      if (chrom[w] == chrom[i] && pos[w] == pos[i] && same_record(heap, off, rl, al, ext, i, w)) {
+        k = 0;
+      } else {
+        // fingerprint collision with a different key: exact scan of earlier
+        // records carrying the same fingerprint (astronomically rare)
+        ++coll;
+        for (size_t j = 0; j < i; ++j)
+          if (fp[j] == h && chrom[j] == chrom[i] && pos[j] == pos[i] &&
+              same_record(heap, off, rl, al, ext, i, j)) { k = 0; break; }
+      }
+    }
+    keep[i] = k;
+    dups += 1u - k;
+  }
+  if (g_ctr) {
+    for (int d = 32; d > 0; d >>= 1) {
+      dups += __shfl_down(dups, d, kWave);
+      coll += __shfl_down(coll, d, kWave);
+    }
+    if (__lane_id() == 0) {
+      if (dups) atomicAdd(&g_ctr[AVDB_CTR_DUPLICATES], (unsigned long long)dups);
+      if (coll) atomicAdd(&g_ctr[AVDB_CTR_HASH_COLLISIONS], (unsigned long long)coll);
+    }
+  }
+}
+
+}  // namespace avdb
+
+using namespace avdb;
+
+static uint64_t table_slots(size_t n) {
+  uint64_t s = 1024;
+  while (s < 2ull * n) s <<= 1;
+  return s;
+}
+
+extern "C" int avdb_pk_dedup_workspace_size(size_t n, size_t* bytes) {
+  if (!bytes) return AVDB_EINVAL;
+  const uint64_t slots = table_slots(n);
+  // fp[n] u64 | keys[slots] u64 | idx[slots] u32
+  *bytes = size_t(8 * n + 8 * slots + 4 * slots + 256);
+  return AVDB_OK;
+}
+
+extern "C" int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                             const uint64_t* allele_off, const uint32_t* ref_len,
+                             const uint32_t* alt_len, const uint8_t* heap, const uint64_t* ext_id,
+                             size_t n, int grouped, void* workspace, size_t workspace_bytes,
+                             uint8_t* keep, uint64_t* counters, void* stream) {
+  if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
+  if (n == 0) return AVDB_OK;
+  if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap || !keep) {
+    avdb_set_error("avdb_pk_dedup: null array");
+    return AVDB_EINVAL;
+  }
+  if (n >= 0xFFFFFFFFull) { avdb_set_error("avdb_pk_dedup: n must be < 2^32"); return AVDB_EINVAL; }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto* ctr = reinterpret_cast<unsigned long long*>(counters);
+  const unsigned grid = stream_grid(n, kBlock * 4, 4096);
+  if (grouped) {
+    hipLaunchKernelGGL(k_dedup_grouped, dim3(grid), dim3(kBlock), 0, s, chrom, pos, allele_off,
+                       ref_len, alt_len, heap, ext_id, n, keep, ctr);
+    AVDB_LAUNCH_CHECK("k_dedup_grouped");
+    return AVDB_OK;
+  }
+  size_t need = 0;
+  avdb_pk_dedup_workspace_size(n, &need);
+  if (!workspace || workspace_bytes < need) {
+    avdb_set_error("avdb_pk_dedup: workspace of %zu bytes required", need);
+    return AVDB_ERANGE;
+  }
+  const uint64_t slots = table_slots(n);
+  char* w = static_cast<char*>(workspace);
+  uint64_t* fp = reinterpret_cast<uint64_t*>(w);
+  auto* tkey = reinterpret_cast<unsigned long long*>(w + 8 * n);
+  uint32_t* tidx = reinterpret_cast<uint32_t*>(w + 8 * n + 8 * slots);
+  AVDB_HIP_TRY(hipMemsetAsync(tkey, 0, 8 * slots, s));
+  AVDB_HIP_TRY(hipMemsetAsync(tidx, 0xFF, 4 * slots, s));
+  hipLaunchKernelGGL(k_dedup_insert, dim3(grid), dim3(kBlock), 0, s, chrom, pos, allele_off,
+                     ref_len, alt_len, heap, ext_id, n, fp, tkey, tidx, slots - 1);
+  AVDB_LAUNCH_CHECK("k_dedup_insert");
+  hipLaunchKernelGGL(k_dedup_resolve, dim3(grid), dim3(kBlock), 0, s, allele_off, ref_len,
+                     alt_len, heap, chrom, pos, ext_id, n, fp, tkey, tidx, slots - 1, keep, ctr);
+  AVDB_LAUNCH_CHECK("k_dedup_resolve");
+  return AVDB_OK;
+}

@@ -1,0 +1,150 @@
+// Internal declarations shared by the libavdb_hip translation units.
+// gfx950 (CDNA4) only: wave64, 160 KiB LDS per CU, 256 CUs in 8 XCDs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/avdb.h"
+
+namespace avdb {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;               // 4 waves per workgroup
+constexpr uint32_t kLeafWidth = 15625;    // L13 bin width, generate_bin_index_references.py:93
+constexpr uint32_t kL8Width = 500000;     // L8 bin width (histogram granularity)
+constexpr int kMaxLdsHistBins = 16384;    // 64 KiB LDS histogram; larger tables go straight to HBM
+
+// Chromosome table passed BY VALUE as a kernel argument (lands in SGPRs /
+// the kernarg segment); each workgroup stages the part it indexes per lane
+// into LDS.  This is all of BinIndexRef the closed form needs: per-contig
+// length (generate_bin_index_references.py:17-25,62-65) plus the prefix sum
+// of L8 bins used by the histogram.
+struct ChromTable {
+  uint32_t len[AVDB_MAX_CHROM];
+  uint32_t l8_off[AVDB_MAX_CHROM];
+  int32_t n;
+  uint32_t n_l8;
+};
+
+// smallest enclosing bin of the closed interval [lo, hi], 1 <= lo <= hi.
+// Level = largest l in 1..13 with (lo-1)/w_l == (hi-1)/w_l, w_l = 15625<<(13-l),
+// else 0 (whole chromosome) — BinIndexRef's nested (lo,hi] rows.
+__device__ __forceinline__ uint32_t bin_code_closed(uint32_t lo, uint32_t hi) {
+  const uint32_t qs = (lo - 1u) / kLeafWidth;   // magic-multiply, no divide
+  const uint32_t qe = (hi - 1u) / kLeafWidth;
+  const uint32_t x = qs ^ qe;
+  const int blen = x ? 32 - __clz(x) : 0;
+  const int level = blen <= 12 ? 13 - blen : 0;
+  const uint32_t idx = level ? (qs >> (13 - level)) : 0u;
+  return (uint32_t(level) << 28) | idx;
+}
+
+// Full classification of one record against the staged length table.
+// Returns the status; writes code (AVDB_BIN_NONE when unmappable).
+__device__ __forceinline__ uint32_t classify(uint32_t c, uint32_t s, uint32_t e, int n_chrom,
+                                             const uint32_t* __restrict__ s_len, uint32_t* code) {
+  if (c >= uint32_t(n_chrom)) { *code = AVDB_BIN_NONE; return AVDB_STATUS_UNKNOWN_CHROM; }
+  uint32_t st = AVDB_STATUS_OK;
+  uint32_t lo = s, hi = e;
+  if (e < s) { lo = e; hi = s; st = AVDB_STATUS_END_BEFORE_START; }
+  const uint32_t L = s_len[c];
+  if (lo < 1u || hi > L) { *code = AVDB_BIN_NONE; return AVDB_STATUS_OUT_OF_RANGE; }
+  *code = bin_code_closed(lo, hi);
+  return st;
+}
+
+// ---- per-lane packed counters -------------------------------------------
+// levels 0..13 in two u64 of 8-bit fields, statuses 0..3 in a u32 of 8-bit
+// fields; flushed to LDS before any field can reach 256.
+struct LaneCounters {
+  uint64_t lv_lo = 0, lv_hi = 0;
+  uint32_t st = 0;
+  __device__ __forceinline__ void add(uint32_t code, uint32_t status) {
+    if (code != AVDB_BIN_NONE) {
+      const uint32_t level = code >> 28;
+      const uint64_t one = 1ull << ((level & 7u) * 8u);
+      lv_lo += level < 8 ? one : 0ull;
+      lv_hi += level < 8 ? 0ull : one;
+    }
+    st += 1u << (status * 8u);
+  }
+  __device__ __forceinline__ void flush(unsigned long long* s_ctr) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t a = uint32_t(lv_lo >> (8 * k)) & 0xFFu;
+      const uint32_t b = uint32_t(lv_hi >> (8 * k)) & 0xFFu;
+      if (a) atomicAdd(&s_ctr[k], (unsigned long long)a);
+      if (k < 6 && b) atomicAdd(&s_ctr[8 + k], (unsigned long long)b);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t a = (st >> (8 * k)) & 0xFFu;
+      if (a) atomicAdd(&s_ctr[AVDB_CTR_STATUS0 + k], (unsigned long long)a);
+    }
+    lv_lo = lv_hi = 0;
+    st = 0;
+  }
+};
+
+// ---- wave-aggregated histogram add --------------------------------------
+// Adds 1 to hist[key] for every active lane with key != ~0u.  Position-sorted
+// input gives runs of equal keys in consecutive lanes: only the head lane of
+// each run issues the (LDS or HBM) atomic, with the run length.  The whole
+// wave must call it (ballots).
+__device__ __forceinline__ void wave_hist_add(uint32_t key, uint32_t* hist) {
+  const int lane = __lane_id();
+  const uint32_t prev = __shfl_up(key, 1, kWave);
+  const bool valid = key != 0xFFFFFFFFu;
+  const bool head = valid && (lane == 0 || prev != key);
+  // a run ends at the next lane whose key differs (head or invalid)
+  const uint64_t breaks = __ballot(!valid || lane == 0 || prev != key);
+  if (head) {
+    const uint64_t above = (lane == 63) ? 0ull : (breaks >> (lane + 1)) << (lane + 1);
+    const int next = above ? __ffsll((unsigned long long)above) - 1 : kWave;
+    atomicAdd(&hist[key], uint32_t(next - lane));
+  }
+}
+
+}  // namespace avdb
+
+struct avdb_ctx {
+  int device;
+  avdb::ChromTable tab;
+  char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
+  bool has_digests;
+};
+
+void avdb_set_error(const char* fmt, ...);
+
+#define AVDB_HIP_TRY(expr)                                                         \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) {                                                        \
+      avdb_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                     __LINE__);                                                    \
+      return AVDB_EHIP;                                                            \
+    }                                                                              \
+  } while (0)
+
+#define AVDB_LAUNCH_CHECK(name)                                                    \
+  do {                                                                             \
+    hipError_t _e = hipGetLastError();                                             \
+    if (_e != hipSuccess) {                                                        \
+      avdb_set_error("launch of %s failed: %s", name, hipGetErrorString(_e));      \
+      return AVDB_EHIP;                                                            \
+    }                                                                              \
+  } while (0)
+
+// grid size for a streaming kernel: enough workgroups to fill 256 CUs at the
+// occupancy the kernel reaches, capped so each workgroup owns a contiguous
+// chunk (keeps a sorted batch's histogram keys local to one workgroup).
+static inline unsigned stream_grid(size_t work_items, unsigned per_block, unsigned cap = 2048) {
+  size_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return unsigned(g);
+}

@@ -1,0 +1,354 @@
+"""Device engine: one ``avdb_ctx`` per GPU plus torch-owned HBM buffers.
+
+Everything here goes through ``libavdb_hip.so``; torch supplies device memory,
+the current HIP stream and host<->device copies (plumbing, not compute).
+
+Data layout in HBM (structure of arrays, one row per alt allele; see
+``include/avdb.h``):
+
+=============  =======  =====================================================
+chrom          uint8    contig code (``chromosomes.CHROM_NAMES`` order)
+pos            int32    1-based VCF POS (stored as u32 by the kernels)
+end            int32    1-based inclusive end (optional, K1 only)
+allele_off     int64    offset of REF in ``heap``; ALT follows REF
+ref_len        int32
+alt_len        int32
+ext_id         int64    refSNP key (0 = none), see :func:`ext_id_key`
+heap           uint8    concatenated raw REF+ALT bytes
+=============  =======  =====================================================
+"""
+
+from __future__ import annotations
+
+import ctypes
+import re
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .chromosomes import CHROM_NAMES, N_CHROM, length_table
+
+
+# ---------------------------------------------------------------------------
+# record batch (SoA)
+# ---------------------------------------------------------------------------
+@dataclass
+class RecordBatch:
+    chrom: torch.Tensor
+    pos: torch.Tensor
+    allele_off: Optional[torch.Tensor] = None
+    ref_len: Optional[torch.Tensor] = None
+    alt_len: Optional[torch.Tensor] = None
+    heap: Optional[torch.Tensor] = None
+    ext_id: Optional[torch.Tensor] = None
+    end: Optional[torch.Tensor] = None
+
+    @property
+    def n(self) -> int:
+        return int(self.chrom.numel())
+
+    @property
+    def device(self):
+        return self.chrom.device
+
+    def to(self, device, non_blocking=False) -> "RecordBatch":
+        kw = {}
+        for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap", "ext_id", "end"):
+            t = getattr(self, f)
+            kw[f] = None if t is None else t.to(device, non_blocking=non_blocking)
+        return RecordBatch(**kw)
+
+    def has_alleles(self) -> bool:
+        return self.heap is not None
+
+
+_RS_RE = re.compile(r"^rs([1-9][0-9]{0,17})$")
+
+
+class ExtIdInterner:
+    """Maps external-id strings to the u64 ``ext_id`` keys the kernels compare.
+
+    Canonical ``rs<N>`` ids map to ``N`` (N < 2^62); any other string gets
+    ``2^63 | k`` for an interned index ``k``; ``None`` is 0.  Equal keys <=>
+    equal strings, which is all the dedup contract needs."""
+
+    def __init__(self):
+        self._ids: Dict[str, int] = {}
+        self._rev: List[str] = []
+
+    def key(self, s: Optional[str]) -> int:
+        if s is None:
+            return 0
+        m = _RS_RE.match(s)
+        if m:
+            return int(m.group(1))
+        k = self._ids.get(s)
+        if k is None:
+            k = len(self._rev)
+            self._ids[s] = k
+            self._rev.append(s)
+        return (1 << 63) | k
+
+    def to_str(self, key: int) -> Optional[str]:
+        if key == 0:
+            return None
+        if key >> 63:
+            return self._rev[key & ((1 << 63) - 1)]
+        return "rs%d" % key
+
+
+def pack_records(chrom_codes: Sequence[int], pos: Sequence[int], refs: Sequence[bytes],
+                 alts: Sequence[bytes], ext_ids: Optional[Sequence[int]] = None) -> RecordBatch:
+    """Host-side SoA packing (numpy -> pinned CPU tensors)."""
+    n = len(pos)
+    rl = np.fromiter((len(r) for r in refs), dtype=np.int64, count=n)
+    al = np.fromiter((len(a) for a in alts), dtype=np.int64, count=n)
+    tot = rl + al
+    off = np.zeros(n, dtype=np.int64)
+    if n:
+        np.cumsum(tot[:-1], out=off[1:])
+    heap = b"".join(r + a for r, a in zip(refs, alts))
+    heap_np = np.frombuffer(heap, dtype=np.uint8) if heap else np.zeros(1, dtype=np.uint8)
+    ext = np.zeros(n, dtype=np.int64) if ext_ids is None else \
+        np.asarray([int(x) if x < (1 << 63) else int(x) - (1 << 64) for x in ext_ids], dtype=np.int64)
+    return RecordBatch(
+        chrom=torch.from_numpy(np.asarray(chrom_codes, dtype=np.uint8)),
+        pos=torch.from_numpy(np.asarray(pos, dtype=np.int64).astype(np.int32)),
+        allele_off=torch.from_numpy(off),
+        ref_len=torch.from_numpy(rl.astype(np.int32)),
+        alt_len=torch.from_numpy(al.astype(np.int32)),
+        heap=torch.from_numpy(heap_np.copy()),
+        ext_id=torch.from_numpy(ext),
+    )
+
+
+def as_u32(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+# ---------------------------------------------------------------------------
+# engine
+# ---------------------------------------------------------------------------
+class Engine:
+    """A context on one GPU: chromosome-length table + kernel entry points."""
+
+    def __init__(self, device=None, lengths: Optional[Sequence[int]] = None, assembly: str = "GRCh38",
+                 sequence_digests: Optional[Sequence[str]] = None):
+        N.require_gpu()
+        self.lib = N.load_library()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", int(device) if not isinstance(device, torch.device)
+                                   else (device.index or 0))
+        self.lengths = list(lengths) if lengths is not None else length_table(assembly)
+        arr = (ctypes.c_uint32 * len(self.lengths))(*self.lengths)
+        h = ctypes.c_void_p()
+        N.check("avdb_ctx_create", self.lib.avdb_ctx_create(self.device.index, arr, len(self.lengths),
+                                                            ctypes.byref(h)))
+        self._ctx = h
+        nb = ctypes.c_uint32()
+        self.lib.avdb_l8_bin_count(self._ctx, ctypes.byref(nb))
+        self.n_l8 = int(nb.value)
+        if sequence_digests is not None:
+            self.set_sequence_digests(sequence_digests)
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self.lib.avdb_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self):
+        if not self._ctx:
+            raise N.NativeUnavailable("engine closed")
+        return self._ctx
+
+    def _stream(self):
+        return N.stream_handle(self.device)
+
+    def set_sequence_digests(self, digests: Sequence[str]):
+        if len(digests) != len(self.lengths) or any(len(d) != N.DIGEST_CHARS for d in digests):
+            raise ValueError("need one 32-character refget digest per chromosome")
+        blob = "".join(digests).encode("ascii")
+        N.check("avdb_ctx_set_sequence_digests",
+                self.lib.avdb_ctx_set_sequence_digests(self.ctx, blob, len(digests)))
+
+    # -- buffers -----------------------------------------------------------
+    def empty(self, n, dtype):
+        return torch.empty(n, dtype=dtype, device=self.device)
+
+    def new_histogram(self) -> torch.Tensor:
+        return torch.zeros(self.n_l8, dtype=torch.int32, device=self.device)
+
+    def new_counters(self) -> torch.Tensor:
+        return torch.zeros(N.N_COUNTERS, dtype=torch.int64, device=self.device)
+
+    def _dev(self, t: Optional[torch.Tensor]):
+        if t is None:
+            return None
+        if t.device != self.device:
+            t = t.to(self.device, non_blocking=True)
+        return t.contiguous()
+
+    # -- K1 ----------------------------------------------------------------
+    def bin_assign(self, chrom: torch.Tensor, start: torch.Tensor, end: Optional[torch.Tensor] = None,
+                   *, want_status: bool = True, hist: Optional[torch.Tensor] = None,
+                   counters: Optional[torch.Tensor] = None,
+                   out_code: Optional[torch.Tensor] = None,
+                   out_status: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        chrom, start, end = self._dev(chrom), self._dev(start), self._dev(end)
+        n = chrom.numel()
+        if start.numel() != n or (end is not None and end.numel() != n):
+            raise ValueError("chrom/start/end length mismatch")
+        if chrom.dtype != torch.uint8 or start.element_size() != 4 or (end is not None and end.element_size() != 4):
+            raise TypeError("chrom must be uint8, start/end 32-bit")
+        code = out_code if out_code is not None else self.empty(n, torch.int32)
+        status = None
+        if want_status:
+            status = out_status if out_status is not None else self.empty(n, torch.uint8)
+        if hist is not None and hist.numel() != self.n_l8:
+            raise ValueError("histogram must have n_l8 bins")
+        N.check("avdb_bin_assign", self.lib.avdb_bin_assign(
+            self.ctx, N.ptr(chrom), N.ptr(start), N.ptr(end), n, N.ptr(code), N.ptr(status),
+            N.ptr(hist), N.ptr(counters), self._stream()))
+        return code, status
+
+    # -- K2 ----------------------------------------------------------------
+    def record_prep(self, b: RecordBatch, *, want_lcp: bool = True, hist: Optional[torch.Tensor] = None,
+                    counters: Optional[torch.Tensor] = None):
+        """Returns ``(end, code, status, lcp)`` device tensors."""
+        b = b if b.device == self.device else b.to(self.device)
+        n = b.n
+        self._check_alleles(b)
+        end = self.empty(n, torch.int32)
+        code = self.empty(n, torch.int32)
+        status = self.empty(n, torch.uint8)
+        lcp = self.empty(n, torch.int32) if want_lcp else None
+        N.check("avdb_record_prep", self.lib.avdb_record_prep(
+            self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
+            N.ptr(b.alt_len), N.ptr(b.heap), n, N.ptr(end), N.ptr(code), N.ptr(status), N.ptr(lcp),
+            N.ptr(hist), N.ptr(counters), self._stream()))
+        return end, code, status, lcp
+
+    # -- K3 ----------------------------------------------------------------
+    def pk_dedup(self, b: RecordBatch, *, grouped: bool = True,
+                 counters: Optional[torch.Tensor] = None,
+                 workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+        b = b if b.device == self.device else b.to(self.device)
+        n = b.n
+        self._check_alleles(b)
+        keep = self.empty(n, torch.uint8)
+        ws = None
+        ws_bytes = 0
+        if not grouped:
+            sz = ctypes.c_size_t()
+            self.lib.avdb_pk_dedup_workspace_size(n, ctypes.byref(sz))
+            ws_bytes = int(sz.value)
+            ws = workspace if workspace is not None and workspace.numel() >= ws_bytes else \
+                self.empty(ws_bytes, torch.uint8)
+        N.check("avdb_pk_dedup", self.lib.avdb_pk_dedup(
+            self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
+            N.ptr(b.alt_len), N.ptr(b.heap), N.ptr(b.ext_id), n, 1 if grouped else 0,
+            N.ptr(ws), ws_bytes, N.ptr(keep), N.ptr(counters), self._stream()))
+        return keep
+
+    # -- K4 ----------------------------------------------------------------
+    def vrs_digest(self, b: RecordBatch, max_seq_len: int = 50,
+                   workspace: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Returns ``(digests uint8[n,32], is_long uint8[n])``; rows that are not
+        long are left zero."""
+        b = b if b.device == self.device else b.to(self.device)
+        n = b.n
+        self._check_alleles(b)
+        dig = torch.zeros((n, N.DIGEST_CHARS), dtype=torch.uint8, device=self.device)
+        is_long = self.empty(n, torch.uint8)
+        sz = ctypes.c_size_t()
+        self.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
+        ws = workspace if workspace is not None and workspace.numel() >= sz.value else \
+            self.empty(int(sz.value), torch.uint8)
+        N.check("avdb_vrs_digest", self.lib.avdb_vrs_digest(
+            self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
+            N.ptr(b.alt_len), N.ptr(b.heap), n, int(max_seq_len), N.ptr(ws), int(sz.value),
+            N.ptr(dig), N.ptr(is_long), self._stream()))
+        return dig, is_long
+
+    def sha512t24u(self, blobs: Sequence[bytes]) -> List[str]:
+        n = len(blobs)
+        if n == 0:
+            return []
+        lens = np.fromiter((len(x) for x in blobs), dtype=np.int64, count=n)
+        off = np.zeros(n, dtype=np.int64)
+        np.cumsum(lens[:-1], out=off[1:])
+        data = b"".join(blobs) or b"\0"
+        d_data = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).to(self.device)
+        d_off = torch.from_numpy(off).to(self.device)
+        d_len = torch.from_numpy(lens.astype(np.int32)).to(self.device)
+        out = self.empty(n * N.DIGEST_CHARS, torch.uint8)
+        N.check("avdb_sha512t24u", self.lib.avdb_sha512t24u(
+            self.ctx, N.ptr(d_data), N.ptr(d_off), N.ptr(d_len), n, N.ptr(out), self._stream()))
+        raw = out.cpu().numpy().tobytes()
+        return [raw[i * 32:(i + 1) * 32].decode("ascii") for i in range(n)]
+
+    # -- formatting (host) ---------------------------------------------------
+    def format_path(self, chrom_code: int, code: int) -> Optional[str]:
+        buf = ctypes.create_string_buffer(N.MAX_PATH)
+        rc = self.lib.avdb_format_bin_path(self.ctx, chrom_code, code & 0xFFFFFFFF, buf, N.MAX_PATH)
+        if rc < 0:
+            return None
+        return buf.raw[:rc].decode("ascii")
+
+    def format_paths(self, chrom_codes: np.ndarray, codes: np.ndarray) -> List[Optional[str]]:
+        """Host batch formatting of kernel outputs into ltree strings (None for
+        unmappable rows)."""
+        chrom_codes = np.ascontiguousarray(chrom_codes, dtype=np.uint8)
+        codes = np.ascontiguousarray(codes).view(np.uint32)
+        n = len(codes)
+        cap = max(1, n * 88)
+        out = np.empty(cap, dtype=np.uint8)
+        offs = np.empty(n + 1, dtype=np.uint64)
+        N.check("avdb_format_bin_paths", self.lib.avdb_format_bin_paths(
+            self.ctx, chrom_codes.ctypes.data, codes.ctypes.data, n, out.ctypes.data, cap,
+            offs.ctypes.data))
+        raw = out[: int(offs[n])].tobytes().decode("ascii")
+        res: List[Optional[str]] = []
+        for i in range(n):
+            a, b = int(offs[i]), int(offs[i + 1])
+            res.append(raw[a:b] if b > a else None)
+        return res
+
+    @staticmethod
+    def _check_alleles(b: RecordBatch):
+        if not b.has_alleles():
+            raise ValueError("batch has no allele heap")
+        if b.allele_off.dtype != torch.int64 or b.ref_len.element_size() != 4 or b.alt_len.element_size() != 4:
+            raise TypeError("allele_off must be int64, ref_len/alt_len 32-bit")
+        n = b.n
+        for t in (b.pos, b.allele_off, b.ref_len, b.alt_len):
+            if t.numel() != n:
+                raise ValueError("record arrays must all have n entries")
+        if b.ext_id is not None and b.ext_id.numel() != n:
+            raise ValueError("ext_id must have n entries")
+
+
+_ENGINES: Dict[int, Engine] = {}
+
+
+def default_engine(device=None) -> Engine:
+    """Process-wide engine per device (GRCh38 table)."""
+    N.require_gpu()
+    idx = torch.cuda.current_device() if device is None else int(device)
+    eng = _ENGINES.get(idx)
+    if eng is None:
+        eng = Engine(idx)
+        _ENGINES[idx] = eng
+    return eng

@@ -1,0 +1,156 @@
+"""Synthetic GRCh38-shaped variant batches for the benchmark configs
+(BASELINE.json ``configs``; generator shapes from SURVEY.md §8d).
+
+Generation happens on the device with a seeded ``torch.Generator`` so a
+100 M-record batch is ready in well under a second; it is never timed.  The
+same shapes are produced on the CPU (numpy PCG64) for oracle-sized tests.
+
+C2  point SNVs: chrom ∝ length, pos ~ U[1, len], sorted by (chrom, pos)
+C3  spans: 0 w.p. 0.5, geometric(1/8) w.p. 0.3, log-uniform[50, 1e6] w.p. 0.2,
+    end = min(pos + span, len)
+C4  dbSNP-scale mix: 90 % SNV / 8 % indel <= 50 bp / 2 % log-uniform <= 1 Mb
+C5  ADSP-style alleles: SNV / short indel / MNV / 5 % long (ref+alt in (50, 2000]),
+    2 % exact duplicate records injected adjacent, 60 % with an rsid
+"""
+
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from .chromosomes import length_table
+from .shard import Piece, pieces as all_pieces
+
+
+def _piece_counts(ps: Sequence[Piece], n: int) -> np.ndarray:
+    w = np.array([p.length for p in ps], dtype=np.float64)
+    c = np.floor(n * w / w.sum()).astype(np.int64)
+    c[np.argmax(w)] += n - c.sum()
+    return c
+
+
+def _positions(ps: Sequence[Piece], n: int, g: torch.Generator, device) -> tuple:
+    """Sorted (chrom u8, pos i32) over the given pieces, density ∝ length."""
+    counts = _piece_counts(ps, n)
+    cnt_t = torch.from_numpy(counts).to(device)
+    chrom = torch.repeat_interleave(torch.tensor([p.chrom for p in ps], dtype=torch.uint8, device=device),
+                                    cnt_t)
+    lo = torch.repeat_interleave(torch.tensor([p.lo for p in ps], dtype=torch.int64, device=device), cnt_t)
+    ln = torch.repeat_interleave(torch.tensor([p.length for p in ps], dtype=torch.int64, device=device), cnt_t)
+    u = torch.rand(n, generator=g, device=device, dtype=torch.float64)
+    pos = lo + 1 + (u * ln).long().clamp_(max=ln - 1)
+    # pieces are in (chrom, lo) order, so sorting positions inside each piece
+    # sorts the batch: sort the global key once
+    key = chrom.long() << 32 | pos
+    key, _ = torch.sort(key)
+    return (key >> 32).to(torch.uint8), (key & 0xFFFFFFFF).to(torch.int32)
+
+
+def point_snvs(n: int, seed: int = 2, device="cuda", pieces: Optional[Sequence[Piece]] = None):
+    """C2: returns (chrom u8, start i32) device tensors, sorted."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return _positions(pieces or all_pieces(), n, g, device)
+
+
+def spans(n: int, seed: int = 3, device="cuda", pieces: Optional[Sequence[Piece]] = None,
+          mix: str = "c3"):
+    """C3 (or C4 with mix='c4'): (chrom u8, start i32, end i32), sorted by start."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    chrom, start = _positions(pieces or all_pieces(), n, g, device)
+    lens = torch.tensor(length_table(), dtype=torch.int64, device=device)
+    u = torch.rand(n, generator=g, device=device, dtype=torch.float64)
+    geo = torch.floor(torch.log(torch.rand(n, generator=g, device=device, dtype=torch.float64).clamp_min(1e-300))
+                      / np.log(1 - 1 / 8)).long()
+    logu = torch.pow(10.0, torch.rand(n, generator=g, device=device, dtype=torch.float64)
+                     * (6 - np.log10(50)) + np.log10(50)).long()
+    if mix == "c3":
+        span = torch.where(u < 0.5, torch.zeros_like(geo), torch.where(u < 0.8, geo, logu))
+    else:  # c4: 90% SNV / 8% indel <= 50 / 2% log-uniform <= 1 Mb
+        ind = (torch.rand(n, generator=g, device=device) * 50).long()
+        span = torch.where(u < 0.9, torch.zeros_like(geo), torch.where(u < 0.98, ind, logu))
+    end = torch.minimum(start.long() + span, lens[chrom.long()]).to(torch.int32)
+    return chrom, start, end
+
+
+def alleles(n: int, seed: int = 5, device="cuda", pieces: Optional[Sequence[Piece]] = None,
+            long_frac: float = 0.05, dup_frac: float = 0.02, rs_frac: float = 0.6):
+    """C5: a RecordBatch (device) of ADSP-style records, position-sorted, with
+    exact duplicates injected adjacent (so the grouped dedup path applies)."""
+    from .engine import RecordBatch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    chrom, pos = _positions(pieces or all_pieces(), n, g, device)
+    u = torch.rand(n, generator=g, device=device)
+    r1 = torch.randint(1, 21, (n,), generator=g, device=device)
+    r2 = torch.randint(1, 21, (n,), generator=g, device=device)
+    L = torch.randint(51, 2001, (n,), generator=g, device=device)
+    split = (torch.rand(n, generator=g, device=device) * (L - 1).float()).long() + 1
+    one = torch.ones(n, dtype=torch.long, device=device)
+    # classes: SNV 80 %, insertion 5 %, deletion 5 %, MNV 5 %, long 5 % (by long_frac)
+    snv = u < 0.80
+    ins = (u >= 0.80) & (u < 0.85)
+    dele = (u >= 0.85) & (u < 0.90)
+    mnv = (u >= 0.90) & (u < 1.0 - long_frac)
+    lng = u >= 1.0 - long_frac
+    rl = torch.where(snv, one, torch.where(ins, one, torch.where(dele, r1 + 1, torch.where(mnv, r2 + 1, split))))
+    al = torch.where(snv, one, torch.where(ins, r1 + 1, torch.where(dele, one, torch.where(mnv, r2 + 1, L - split))))
+    # duplicates: record i copies record i-1 (same chrom/pos/alleles/rsid)
+    dup = torch.rand(n, generator=g, device=device) < dup_frac
+    dup[0] = False
+    src = torch.arange(n, device=device)
+    src = torch.where(dup, src - 1, src)
+    # chains of duplicates resolve to their first record
+    src = torch.cummax(torch.where(dup, torch.zeros_like(src), src), 0).values
+    rl = rl[src]
+    al = al[src]
+    chrom = chrom[src]
+    pos = pos[src]
+    tot = rl + al
+    off = torch.cumsum(tot, 0) - tot
+    H = int(tot.sum().item())
+    acgt = torch.tensor([65, 67, 71, 84], dtype=torch.uint8, device=device)
+    heap = acgt[torch.randint(0, 4, (H,), generator=g, device=device)]
+    # indel anchors: alt[0] = ref[0]
+    anchor = (ins | dele)[src] & ~dup
+    a_idx = off[anchor]
+    heap[a_idx + rl[anchor]] = heap[a_idx]
+    # copy duplicate bytes from their source record
+    if bool(dup.any()):
+        d_rows = torch.nonzero(dup).squeeze(1)
+        first = src[d_rows]
+        dl = tot[d_rows]
+        rep = torch.repeat_interleave(torch.arange(d_rows.numel(), device=device), dl)
+        within = torch.arange(int(dl.sum().item()), device=device) - torch.repeat_interleave(
+            torch.cumsum(dl, 0) - dl, dl)
+        heap[off[d_rows][rep] + within] = heap[off[first][rep] + within]
+    ext = torch.where(torch.rand(n, generator=g, device=device) < rs_frac,
+                      torch.randint(1, 10 ** 9, (n,), generator=g, device=device), torch.zeros_like(pos, dtype=torch.long))
+    ext = ext[src]
+    return RecordBatch(chrom=chrom, pos=pos, allele_off=off, ref_len=rl.to(torch.int32),
+                       alt_len=al.to(torch.int32), heap=heap, ext_id=ext)
+
+
+# ---- numpy (CPU) versions, oracle-sized ------------------------------------
+def np_point_snvs(n: int, seed: int = 2, lengths=None):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lengths = np.asarray(lengths if lengths is not None else length_table(), dtype=np.int64)
+    chrom = rng.choice(len(lengths), size=n, p=lengths / lengths.sum()).astype(np.uint8)
+    pos = (rng.random(n) * lengths[chrom]).astype(np.int64) + 1
+    order = np.lexsort((pos, chrom))
+    return chrom[order], pos[order].astype(np.int32)
+
+
+def np_spans(n: int, seed: int = 3, lengths=None):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lengths = np.asarray(lengths if lengths is not None else length_table(), dtype=np.int64)
+    chrom, start = np_point_snvs(n, seed, lengths)
+    u = rng.random(n)
+    geo = rng.geometric(1 / 8, n) - 1
+    logu = (10 ** rng.uniform(np.log10(50), 6, n)).astype(np.int64)
+    span = np.where(u < 0.5, 0, np.where(u < 0.8, geo, logu))
+    end = np.minimum(start.astype(np.int64) + span, lengths[chrom]).astype(np.int32)
+    return chrom, start, end

@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""Benchmark: variants binned(+keyed)/s on MI355X, with HBM-roofline accounting.
+
+Default workload (N=1): BASELINE.json configs[1] — 100 M synthetic GRCh38 SNVs,
+point-position bin assignment (K1 ``avdb_bin_assign`` with the fused L8
+histogram + level/status counters).  A *step* is one pass of the hot path over
+the GPU's whole resident batch.  Per-GPU work is fixed (weak scaling): each rank
+owns a length-balanced set of 64 Mb genome pieces (``annotatedvdb_amd.shard``)
+and its own 100 M records; ranks never exchange records.  The only collective
+is one RCCL all-gather of the per-rank L8 histograms + counters at the end of the
+job, inside the timed region.
+
+Other workloads (``--workload``): c3 spans (1e8, K1 with end), c5 ADSP-style
+alleles (2.5e7 per GPU: K2 record prep + K3 grouped dedup + K4 long-key digests).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c5]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "variants binned+keyed/sec (node) at 1/2/4/8 MI355X; % of HBM roofline"
+
+WORKLOADS = {
+    "c2": dict(n=100_000_000, desc="C2: synthetic GRCh38 SNVs, point-position bin assignment "
+                                   "(BASELINE configs[1]); K1 bin_assign + L8 histogram",
+               bytes_per=9, kernel="k_bin_assign4"),
+    "c3": dict(n=100_000_000, desc="C3: synthetic indels/SVs, spans <= 1 Mb, smallest enclosing bin "
+                                   "(BASELINE configs[2]); K1 bin_assign + L8 histogram",
+               bytes_per=13, kernel="k_bin_assign4"),
+    "c5": dict(n=25_000_000, desc="C5: ADSP-style alleles, end inference + bin + grouped PK dedup + "
+                                  "long-allele key digests (BASELINE configs[4])",
+               bytes_per=None, kernel="k_record_prep"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--n", type=int, default=None, help="records per GPU (default: config size)")
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="target seconds per CPU worker")
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference-structured port (oracle) on the host cores
+# ---------------------------------------------------------------------------
+_SAMPLE = None
+_TABLE = None
+
+
+def _cpu_worker(k):
+    from oracle import avdb_oracle as O
+    names, pos, ends = _SAMPLE[k]
+    bi = O.PortBinIndex(_TABLE)
+    t0 = time.perf_counter()
+    if ends is None:
+        for c, p in zip(names, pos):
+            bi.find_bin_index(c, p)
+    else:
+        for c, p, e in zip(names, pos, ends):
+            bi.find_bin_index(c, p, e)
+    return len(pos), time.perf_counter() - t0
+
+
+def cpu_baseline(workload: str, seconds_per_worker: float):
+    """Reference-structured Python port (one-bin L13 cache + BinIndexRef table
+    search on a miss, bin_index.py:59-75) over a bounded sample of the same
+    workload, one process per host core like load_vcf_file.py:307-313."""
+    global _SAMPLE, _TABLE
+    import multiprocessing as mp
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.chromosomes import CHROM_NAMES, GRCH38_LENGTHS
+    from oracle import avdb_oracle as O
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    workers = max(1, min(16, cores))
+    per = int(seconds_per_worker / 0.9e-6)  # ~0.9 us per cached find_bin_index call
+    total = per * workers
+    if workload == "c2":
+        chrom, pos = synth.np_point_snvs(total, seed=2)
+        end = None
+    else:
+        chrom, pos, end = synth.np_spans(total, seed=3)
+    names = [CHROM_NAMES[c] for c in chrom.tolist()]
+    pos = pos.tolist()
+    end = end.tolist() if end is not None else None
+    _TABLE = O.BinTable(GRCH38_LENGTHS)
+    _SAMPLE = [(names[k * per:(k + 1) * per], pos[k * per:(k + 1) * per],
+                end[k * per:(k + 1) * per] if end is not None else None) for k in range(workers)]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, range(workers))
+    wall = time.perf_counter() - t0
+    n = sum(r[0] for r in res)
+    return {"value": n / wall, "unit": "variants/s", "cores": workers, "kind": "port",
+            "sample": f"{n:,} records of the {workload.upper()} workload (numpy PCG64, sorted), "
+                      f"{workers} processes x {per:,} records; reference-structured PortBinIndex "
+                      f"(oracle/avdb_oracle.py), per-process {np.mean([r[1] for r in res]):.2f} s"}
+
+
+# ---------------------------------------------------------------------------
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CPU baseline first, before this process touches the GPU (its worker
+    # processes are forked and must not inherit an initialised HIP runtime)
+    want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and world == 1 and a.workload in ("c2", "c3"))
+    cpu = cpu_baseline(a.workload, a.cpu_seconds) if (rank == 0 and want_cpu) else None
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from annotatedvdb_amd import shard, synth
+    from annotatedvdb_amd.engine import Engine
+
+    W = WORKLOADS[a.workload]
+    n = a.n or W["n"]
+    my_pieces = shard.plan(world)[rank]
+    eng = Engine(local)
+    if a.workload == "c5":
+        digs = ["%032d" % i for i in range(25)]  # synthetic refget ids (no SeqRepo offline)
+        eng.set_sequence_digests(digs)
+
+    # ---- resident synthetic batch (untimed) ----
+    if a.workload == "c2":
+        chrom, start = synth.point_snvs(n, seed=2 + 1000 * rank, device=dev, pieces=my_pieces)
+        end = None
+    elif a.workload == "c3":
+        chrom, start, end = synth.spans(n, seed=3 + 1000 * rank, device=dev, pieces=my_pieces)
+    else:
+        batch = synth.alleles(n, seed=5 + 1000 * rank, device=dev, pieces=my_pieces)
+        heap_bytes = int(batch.heap.numel())
+    hist = eng.new_histogram()
+    ctr = eng.new_counters()
+    code = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    evs = []
+
+    def step(record: bool):
+        if a.workload in ("c2", "c3"):
+            if record:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            eng.bin_assign(chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code)
+            if record:
+                e1.record(stream)
+                evs.append((e0, e1))
+        else:
+            if record:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr)
+            if record:
+                e1.record(stream)
+                evs.append((e0, e1))
+            eng.pk_dedup(batch, grouped=True, counters=ctr)
+            eng.vrs_digest(batch, 50)
+
+    for _ in range(a.warmup):
+        step(False)
+    hist.zero_()
+    ctr.zero_()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    # job-level exchange: per-rank L8 histograms + counters (RCCL all-gather)
+    if world > 1:
+        gathered_h = [torch.empty_like(hist) for _ in range(world)]
+        gathered_c = [torch.empty_like(ctr) for _ in range(world)]
+        dist.all_gather(gathered_h, hist)
+        dist.all_gather(gathered_c, ctr)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        node_ctr = torch.stack(gathered_c).sum(0)
+    else:
+        node_ctr = ctr
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    total_records = n * world * a.steps
+    value = total_records / elapsed
+
+    if a.workload == "c5":
+        # K2 algorithmic bytes: in chrom1+pos4+off8+rlen4+alen4 + heap bytes read; out end4+code4
+        bytes_per_launch = n * (1 + 4 + 8 + 4 + 4 + 4 + 4) + heap_bytes
+    else:
+        bytes_per_launch = n * W["bytes_per"]
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{a.workload}.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "variants/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded GRCh38-shaped records generated on device)",
+        "config": {"workload": W["desc"], "records_per_gpu": n, "records_total": n * world,
+                   "parallelism": f"dp{world} (length-balanced 64 Mb genome pieces per rank)",
+                   "records_checked": int(node_ctr[20].item()) // max(1, a.steps)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": W["kernel"], "kernel_ms": kern_ms,
+                     "algorithmic_bytes_per_launch": bytes_per_launch},
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

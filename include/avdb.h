@@ -1,0 +1,165 @@
+/*
+ * avdb.h — C ABI of libavdb_hip.so, the MI355X (gfx950) kernel library behind
+ * the AnnotatedVDB batch variant -> genomic-bin / primary-key path.
+ *
+ * Plain C: no torch or HIP types in any signature.  Every entry point returns
+ * an int status (AVDB_OK == 0; negative on failure, message via
+ * avdb_last_error()).  Array arguments are DEVICE pointers (HBM) unless marked
+ * "host"; the caller owns every buffer.  `stream` is a hipStream_t passed as
+ * void* (NULL = the device's null stream); all device work is enqueued on it
+ * and nothing synchronises, so callers may capture the calls into a hipGraph.
+ *
+ * Reference interfaces replaced (paths relative to NIAGADS/AnnotatedVDB):
+ *   - BinIndex.find_bin_index(chrm, start, end=None)      BinIndex/lib/python/bin_index.py:59-75
+ *     and the external SQL find_bin_index(chr,start,end) it calls through
+ *     BIN_INDEX_SQL (bin_index.py:9-14, _update_current_bin_index :43-56)
+ *   - the BinIndexRef table it searches        BinIndex/bin/generate_bin_index_references.py:46-83
+ *   - VariantAnnotator.infer_variant_end_location  Util/lib/python/variant_annotator.py:36-79
+ *     and __normalize_alleles (common-prefix trim)  variant_annotator.py:82-121
+ *   - VariantPKGenerator.generate_primary_key / compute_vrs_identifier
+ *                                               Util/lib/python/primary_key_generator.py:99-165
+ *   - the per-alt record-prep loop              Util/lib/python/loaders/vcf_variant_loader.py:259-348
+ *   - in-batch duplicate-key semantics          Load/lib/sql/annotatedvdb_schema/patches/removeDuplicates.sql:2-24
+ *
+ * Record layout (structure of arrays, one entry per alt allele):
+ *   chrom      u8[n]   contig code, index into the context's chromosome table
+ *                      (default order chr1..chr22, chrX, chrY, chrM —
+ *                      Util/lib/python/enums/chromosomes.py:9-38)
+ *   pos/start  u32[n]  1-based VCF POS
+ *   end        u32[n]  1-based inclusive end (nullable => end = start, bin_index.py:63)
+ *   allele_off u64[n]  byte offset of the REF allele in `heap`; ALT follows at
+ *                      allele_off + ref_len (raw, un-normalised VCF bytes)
+ *   ref_len    u32[n], alt_len u32[n]
+ *   ext_id     u64[n]  external id key (refSNP); 0 = none; equal keys <=> equal ids
+ *
+ * Bin code (u32): level in bits 31..28 (0 = whole chromosome .. 13 = 15,625 bp
+ * leaf), 0-based index of the bin at that level in bits 27..0.  The ltree path
+ * "chrN.L1.B<k>...L<level>.B<k>" is a pure function of (chrom, code):
+ * avdb_format_bin_path().  AVDB_BIN_NONE marks an unmappable record (the
+ * reference raises TypeError there, bin_index.py:75).
+ */
+#ifndef AVDB_H_
+#define AVDB_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVDB_ABI_VERSION 1
+
+/* return codes */
+#define AVDB_OK 0
+#define AVDB_EINVAL (-1)   /* bad argument (null ctx, n too large, misaligned ...) */
+#define AVDB_EHIP (-2)     /* HIP runtime error (launch / allocation) */
+#define AVDB_ENOMEM (-3)
+#define AVDB_ERANGE (-4)   /* output buffer too small */
+
+/* per-record status (u8) */
+#define AVDB_STATUS_OK 0
+#define AVDB_STATUS_UNKNOWN_CHROM 1
+#define AVDB_STATUS_OUT_OF_RANGE 2      /* start < 1 or end > chromosome length */
+#define AVDB_STATUS_END_BEFORE_START 3  /* bin of [end,start]; reference answer is cache-history dependent */
+
+#define AVDB_BIN_NONE 0xFFFFFFFFu
+#define AVDB_N_LEVELS 14
+#define AVDB_MAX_CHROM 64
+#define AVDB_DIGEST_CHARS 32            /* sha512t24u: 24 bytes, base64url, no padding */
+#define AVDB_MAX_PATH 128
+
+/* counters[] slots written by avdb_bin_assign (histogram mode) and avdb_record_prep */
+#define AVDB_CTR_LEVEL0 0               /* [0..13]: records per bin level */
+#define AVDB_CTR_STATUS0 16             /* [16..19]: records per status */
+#define AVDB_CTR_RECORDS 20
+#define AVDB_CTR_DUPLICATES 21          /* records whose primary key repeats an earlier one */
+#define AVDB_CTR_HASH_COLLISIONS 22     /* fingerprint collisions resolved by byte compare */
+#define AVDB_CTR_LONG 23                /* records with ref_len + alt_len > max_seq_len */
+#define AVDB_N_COUNTERS 32
+
+typedef struct avdb_ctx avdb_ctx;
+
+int avdb_abi_version(void);
+/* Thread-local description of the last failure in this thread. */
+const char* avdb_last_error(void);
+int avdb_device_count(int* n);
+
+/* ---- context -----------------------------------------------------------
+ * One context per device.  chrom_len (host) gives each contig's length; it is
+ * the information BinIndexRef carries (generate_bin_index_references.py:17-43).
+ * Not thread-safe per context; calls are ordered on the caller's stream.  */
+int avdb_ctx_create(int device, const uint32_t* chrom_len_host, int n_chrom, avdb_ctx** out);
+int avdb_ctx_destroy(avdb_ctx* ctx);
+int avdb_ctx_n_chrom(const avdb_ctx* ctx);
+/* GA4GH refget digests (32 chars each, no "ga4gh:SQ." prefix) of every contig,
+ * host array n_chrom*32 bytes; required only by avdb_vrs_digest. */
+int avdb_ctx_set_sequence_digests(avdb_ctx* ctx, const char* digests_host, int n_chrom);
+/* Number of L8 (500 kb) bins over the whole chromosome table (histogram size). */
+int avdb_l8_bin_count(const avdb_ctx* ctx, uint32_t* n_bins);
+
+/* ---- K1: smallest enclosing bin ----------------------------------------
+ * Replaces BinIndex.find_bin_index + SQL find_bin_index (bin_index.py:43-75).
+ * end may be NULL (end = start); status may be NULL.  If hist_l8 (u32[n_l8])
+ * and/or counters (u64[AVDB_N_COUNTERS]) are non-NULL they are ACCUMULATED
+ * (caller zeroes them): L8 bin of `start` for every mappable record, records
+ * per level and per status. */
+int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* start,
+                    const uint32_t* end, size_t n, uint32_t* bin_code, uint8_t* status,
+                    uint32_t* hist_l8, uint64_t* counters, void* stream);
+
+/* ---- K2: record prep (end inference + bin, fused) ------------------------
+ * Per alt allele: common-prefix length of ref/alt (variant_annotator.py:82-121),
+ * inferred end (variant_annotator.py:36-79), then the bin of [pos,end]
+ * (vcf_variant_loader.py:310-311).  end_out/bin_code required; status, lcp,
+ * hist_l8, counters optional (NULL).  */
+int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                     const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                     const uint8_t* heap, size_t n, uint32_t* end_out, uint32_t* bin_code,
+                     uint8_t* status, uint32_t* lcp, uint32_t* hist_l8, uint64_t* counters,
+                     void* stream);
+
+/* ---- K3: in-batch primary-key dedup --------------------------------------
+ * keep[i] = 1 iff no j < i has the same primary key chr:pos:ref:alt[:ext]
+ * (primary_key_generator.py:99-122; equal keys <=> equal (chrom,pos,ref,alt,ext_id)).
+ * grouped != 0 promises records with equal (chrom,pos) are contiguous (any
+ * position-sorted VCF): a run scan, no workspace.  grouped == 0: hash path,
+ * needs `workspace` of avdb_pk_dedup_workspace_size() bytes (device).
+ * counters[AVDB_CTR_DUPLICATES / _HASH_COLLISIONS] accumulated if non-NULL. */
+int avdb_pk_dedup_workspace_size(size_t n, size_t* bytes);
+int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                  const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                  const uint8_t* heap, const uint64_t* ext_id, size_t n, int grouped,
+                  void* workspace, size_t workspace_bytes, uint8_t* keep, uint64_t* counters,
+                  void* stream);
+
+/* ---- K4: digests ---------------------------------------------------------
+ * sha512t24u of n byte strings (data + off[i], len[i]) -> out[i*32..] base64url. */
+int avdb_sha512t24u(avdb_ctx* ctx, const uint8_t* data, const uint64_t* off, const uint32_t* len,
+                    size_t n, char* out, void* stream);
+/* Long-allele key digest (compute_vrs_identifier, primary_key_generator.py:147-165):
+ * for every record with ref_len + alt_len > max_seq_len, the VRS-1.x Allele
+ * digest of interval (pos-1, pos-1+ref_len] and literal state ALT, written to
+ * digest_out[i*32..] (other rows untouched); is_long[i] set 0/1 if non-NULL.
+ * Long rows are compacted into `workspace` (avdb_vrs_digest_workspace_size()
+ * bytes, device) first.  PARITY UNPINNED. */
+int avdb_vrs_digest_workspace_size(size_t n, size_t* bytes);
+int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                    const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                    const uint8_t* heap, size_t n, uint32_t max_seq_len, void* workspace,
+                    size_t workspace_bytes, char* digest_out, uint8_t* is_long, void* stream);
+
+/* ---- host-side formatting of kernel outputs -------------------------------
+ * ltree path text (<= AVDB_MAX_PATH bytes).  Returns the length written (no
+ * NUL terminator counted; one is written if cap allows), or a negative code. */
+int avdb_format_bin_path(const avdb_ctx* ctx, uint8_t chrom, uint32_t bin_code, char* out_host,
+                         size_t cap);
+/* Batch form (host arrays): paths concatenated into out_host, out_off[i] the
+ * start of path i, out_off[n] the total; returns AVDB_ERANGE if cap is short. */
+int avdb_format_bin_paths(const avdb_ctx* ctx, const uint8_t* chrom_host, const uint32_t* code_host,
+                          size_t n, char* out_host, size_t cap, uint64_t* out_off_host);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVDB_H_ */

@@ -1,0 +1,37 @@
+"""CPU oracle (TEST INFRASTRUCTURE ONLY — the checker, never the product).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this package.  ``avdb_oracle`` is the Python/numpy restatement,
+``c_oracle()`` loads the plain-C restatement (``avdb_oracle.c``) built by
+``make -C oracle``.
+"""
+
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+C_LIB = os.path.join(_HERE, "_build", "libavdb_oracle.so")
+_c = None
+
+
+def build_c_oracle() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return C_LIB
+
+
+def c_oracle():
+    """ctypes handle of the C oracle (built on first use if gcc is present)."""
+    global _c
+    if _c is None:
+        if not os.path.exists(C_LIB):
+            build_c_oracle()
+        lib = ctypes.CDLL(C_LIB)
+        P, SZ, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        lib.avdb_oracle_bin_assign.argtypes = [P, P, P, SZ, P, I, P, P]
+        lib.avdb_oracle_record_prep.argtypes = [P, P, P, P, P, P, SZ, P, I, P, P, P, P]
+        lib.avdb_oracle_dedup_grouped.argtypes = [P, P, P, P, P, P, P, SZ, P]
+        lib.avdb_oracle_dedup_grouped.restype = ctypes.c_uint64
+        lib.avdb_oracle_sha512.argtypes = [P, SZ, P]
+        _c = lib
+    return _c

@@ -1,0 +1,345 @@
+"""CPU oracle for the AnnotatedVDB bin/key hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is the *checker*.  Only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it; the product path
+(``annotatedvdb_amd``) never does, and never falls back to it.
+
+It restates, from the reference's behaviour (not its code), every function on
+the path.  Each function cites the reference ``file:line`` it follows; paths are
+relative to the NIAGADS/AnnotatedVDB repository root.  Parity is pinned by the
+golden vectors under ``tests/golden/`` that ``tests/golden/make_golden.py``
+produced by running the reference itself (see ``tests/test_oracle_golden.py``);
+the long-allele VRS digest is the exception: **parity unpinned** (vrs-python and
+SeqRepo are absent; only the ``sha512t24u`` primitive is pinned, to hashlib).
+"""
+
+from __future__ import annotations
+
+import base64
+import bisect
+import hashlib
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+# ---------------------------------------------------------------------------
+# constants — BinIndex/bin/generate_bin_index_references.py:93
+#   increments = [-1, 64e6, 32e6, ..., 15625]; level l>=1 bin width 64e6>>(l-1)
+# ---------------------------------------------------------------------------
+N_LEVELS = 14
+LEAF_WIDTH = 15625
+INC = [0] + [64000000 >> (lvl - 1) for lvl in range(1, N_LEVELS)]
+assert INC[13] == LEAF_WIDTH
+
+STATUS_OK = 0
+STATUS_UNKNOWN_CHROM = 1
+STATUS_OUT_OF_RANGE = 2
+STATUS_END_BEFORE_START = 3  # bin of the swapped interval; reference is history-dependent
+BIN_NONE = 0xFFFFFFFF
+
+CHROM_NAMES = [str(i) for i in range(1, 23)] + ["X", "Y", "M"]
+
+
+def make_code(level: int, index: int) -> int:
+    return (level << 28) | index
+
+
+def code_level(code: int) -> int:
+    return code >> 28
+
+
+def code_index(code: int) -> int:
+    return code & 0x0FFFFFFF
+
+
+# ---------------------------------------------------------------------------
+# a2/a3: smallest enclosing bin
+#   bin_index.py:59-75 (find_bin_index; end defaults to start :63) and the
+#   BinIndexRef rows of generate_bin_index_references.py:46-83, ranges (lo,hi]
+#   (:83), clipped at the chromosome length (:62-65).  The deepest row whose
+#   (lo,hi] holds both start and end is the answer (cache test bin_index.py:70).
+# ---------------------------------------------------------------------------
+def bin_code(chrom_len: Optional[int], start: int, end: Optional[int] = None) -> Tuple[int, int]:
+    """Return ``(code, status)`` for one interval (closed, 1-based)."""
+    if end is None:
+        end = start
+    if chrom_len is None:
+        return BIN_NONE, STATUS_UNKNOWN_CHROM
+    status = STATUS_OK
+    if end < start:
+        start, end = end, start
+        status = STATUS_END_BEFORE_START
+    if start < 1 or end > chrom_len:
+        return BIN_NONE, STATUS_OUT_OF_RANGE
+    qs = (start - 1) // LEAF_WIDTH
+    qe = (end - 1) // LEAF_WIDTH
+    blen = (qs ^ qe).bit_length()
+    level = 13 - blen if blen <= 12 else 0
+    index = qs >> (13 - level) if level > 0 else 0
+    return make_code(level, index), status
+
+
+def format_bin_path(chrom_name: str, code: int) -> str:
+    """ltree path ``chrN.L1.Bk...`` — labels per generate_bin_index_references.py:54,60-61,74
+    (``B`` restarts at 1 under every parent; L0 is the bare chromosome)."""
+    level, g = code_level(code), code_index(code)
+    parts = ["chr" + chrom_name]
+    for lvl in range(1, level + 1):
+        gl = g >> (level - lvl)
+        b = gl + 1 if lvl == 1 else (gl & 1) + 1
+        parts.append("L%d.B%d" % (lvl, b))
+    return ".".join(parts)
+
+
+def bin_codes_np(chrom: np.ndarray, start: np.ndarray, end: Optional[np.ndarray],
+                 lengths: Sequence[int]) -> Tuple[np.ndarray, np.ndarray]:
+    """Vectorised :func:`bin_code` (numpy, int64 arithmetic)."""
+    chrom = np.asarray(chrom, dtype=np.int64)
+    s = np.asarray(start, dtype=np.int64)
+    e = s.copy() if end is None else np.asarray(end, dtype=np.int64)
+    lens = np.asarray(list(lengths) + [0] * (256 - len(lengths)), dtype=np.int64)
+    known = chrom < len(lengths)
+    L = lens[np.clip(chrom, 0, 255)]
+    swapped = e < s
+    lo = np.minimum(s, e)
+    hi = np.maximum(s, e)
+    inrange = (lo >= 1) & (hi <= L)
+    qs = (np.maximum(lo, 1) - 1) // LEAF_WIDTH
+    qe = (np.maximum(hi, 1) - 1) // LEAF_WIDTH
+    x = qs ^ qe
+    blen = np.zeros_like(x)
+    nz = x > 0
+    blen[nz] = np.floor(np.log2(x[nz])).astype(np.int64) + 1
+    level = np.where(blen <= 12, 13 - blen, 0)
+    index = np.where(level > 0, qs >> np.clip(13 - level, 0, 13), 0)
+    code = (level << 28) | index
+    status = np.where(swapped, STATUS_END_BEFORE_START, STATUS_OK)
+    status = np.where(inrange, status, STATUS_OUT_OF_RANGE)
+    status = np.where(known, status, STATUS_UNKNOWN_CHROM)
+    code = np.where((status == STATUS_OK) | (status == STATUS_END_BEFORE_START), code, BIN_NONE)
+    return code.astype(np.uint32), status.astype(np.uint8)
+
+
+# ---------------------------------------------------------------------------
+# a3: BinIndexRef table restated (for the reference-structured CPU baseline and
+# for table-search cross-checks).  Rows (chrom, level, path, lo, hi) in the
+# generator's depth-first order, generate_bin_index_references.py:46-77.
+# ---------------------------------------------------------------------------
+def generate_binindexref(chrom_name: str, length: int) -> List[Tuple[int, str, int, int]]:
+    rows: List[Tuple[int, str, int, int]] = []
+
+    def rec(prefix: str, lo: int, hi: int, level: int):
+        # children of the bin (lo,hi] at `level`, clipped to hi
+        if level >= N_LEVELS:
+            return
+        k = 0
+        b = lo
+        while b < hi:
+            k += 1
+            top = min(b + INC[level], hi, length)
+            path = prefix + ".B%d" % k
+            rows.append((level, path, b, top))
+            rec(path + ".L%d" % (level + 1), b, top, level + 1)
+            b = top
+
+    root = "chr" + chrom_name
+    rows.append((0, root, 0, length))
+    rec(root + ".L1", 0, length, 1)
+    return rows
+
+
+class BinTable:
+    """Per-(chrom, level) sorted (lo, hi, path) lists; deepest-containing search."""
+
+    def __init__(self, lengths: Dict[str, int]):
+        self.by: Dict[Tuple[str, int], Tuple[List[int], List[Tuple[int, int, str]]]] = {}
+        for name, L in lengths.items():
+            per: Dict[int, List[Tuple[int, int, str]]] = {}
+            for level, path, lo, hi in generate_binindexref(name, L):
+                per.setdefault(level, []).append((lo, hi, path))
+            for level, lst in per.items():
+                lst.sort()
+                self.by[("chr" + name, level)] = ([r[0] for r in lst], lst)
+
+    def find(self, chrm: str, start: int, end: int):
+        for level in range(13, -1, -1):
+            ent = self.by.get((chrm, level))
+            if ent is None:
+                continue
+            los, lst = ent
+            k = bisect.bisect_left(los, start) - 1
+            if k < 0:
+                continue
+            lo, hi, path = lst[k]
+            if lo < start <= hi and lo < end <= hi:
+                return {"chromosome": chrm, "global_bin_path": path,
+                        "location": (lo, hi), "bin_level": 1 + 2 * level}
+        return None
+
+
+class PortBinIndex:
+    """Reference-structured port of ``BinIndex`` (bin_index.py:16-75) used as the
+    CPU baseline: one-bin cache served only for L13 bins (:66-71, nlevel>=27),
+    table search on a miss in place of the SQL round trip (:43-56)."""
+
+    def __init__(self, table: BinTable):
+        self._table = table
+        self._current = None
+
+    def find_bin_index(self, chrm, start, end=None):
+        if end is None:
+            end = start
+        chrm = str(chrm)
+        if "chr" not in chrm:
+            chrm = "chr" + chrm
+        cur = self._current
+        if cur:
+            if cur["bin_level"] >= 27:
+                lo, hi = cur["location"]
+                if cur["chromosome"] == chrm and lo < start <= hi and lo < end <= hi:
+                    return cur["global_bin_path"]
+        self._current = self._table.find(chrm, start, end)
+        return self._current["global_bin_path"]  # None -> TypeError, as :75
+
+
+# ---------------------------------------------------------------------------
+# a4/a5: allele normalisation (lcp) and end inference
+#   variant_annotator.py:82-121 (__normalize_alleles: strip the longest common
+#   prefix; SNVs untouched :97-98) and :36-79 (infer_variant_end_location).
+# ---------------------------------------------------------------------------
+def common_prefix(ref: bytes, alt: bytes) -> int:
+    if len(ref) == 1 and len(alt) == 1:
+        return 0  # SNV: no normalisation (:97-98), even when ref == alt
+    n = 0
+    m = min(len(ref), len(alt))
+    while n < m and ref[n] == alt[n]:
+        n += 1
+    return n
+
+
+def infer_end(pos: int, ref, alt) -> Tuple[int, int]:
+    """Return ``(end, lcp)``; ``start`` stays at the VCF POS
+    (vcf_variant_loader.py:310)."""
+    if isinstance(ref, str):
+        ref = ref.encode()
+    if isinstance(alt, str):
+        alt = alt.encode()
+    r, a = len(ref), len(alt)
+    lcp = common_prefix(ref, alt)
+    nr, na = r - lcp, a - lcp
+    if r == 1 and a == 1:
+        return pos, lcp
+    if r == a:
+        if ref == alt[::-1]:  # inversion (:61-62)
+            return pos + r - 1, lcp
+        return pos + nr - 1, lcp  # substitution (:65)
+    if na >= 1:  # insertion / indel (:67-74)
+        if nr >= 1:
+            return pos + nr, lcp
+        if r > 1:
+            return pos + r - 1, lcp
+        return pos + 1, lcp
+    if nr == 0:  # deletion (:77-79)
+        return pos + r - 1, lcp
+    return pos + nr, lcp
+
+
+# ---------------------------------------------------------------------------
+# a6/a8: metaseq id and short primary key
+#   variant_annotator.py:124-126; primary_key_generator.py:99-122
+# ---------------------------------------------------------------------------
+MAX_SEQUENCE_LENGTH = 50  # primary_key_generator.py:53
+
+
+def metaseq_id(chrom: str, pos: int, ref: str, alt: str) -> str:
+    return ":".join((str(chrom), str(pos), ref, alt))
+
+
+def is_long(ref: str, alt: str, max_len: int = MAX_SEQUENCE_LENGTH) -> bool:
+    return len(ref) + len(alt) > max_len
+
+
+def primary_key(chrom: str, pos: int, ref: str, alt: str, external_id: Optional[str] = None,
+                digest: Optional[str] = None, max_len: int = MAX_SEQUENCE_LENGTH) -> str:
+    pk = [str(chrom), str(pos)]
+    if len(ref) + len(alt) <= max_len:
+        pk += [ref, alt]
+    else:
+        if digest is None:
+            raise ValueError("long allele needs a VRS digest (parity unpinned)")
+        pk.append(digest)
+    if external_id is not None:
+        pk.append(external_id)
+    return ":".join(pk)
+
+
+# ---------------------------------------------------------------------------
+# a9: sha512t24u (GA4GH computed-identifier digest) — the pinnable primitive.
+#   primary_key_generator.py:147-165 drops the 'ga4gh:VA.' prefix of the
+#   ga4gh_identify() result.  The Allele/SequenceLocation serialisation below is
+#   the published VRS 1.x compact form; PARITY UNPINNED (no vrs-python here).
+# ---------------------------------------------------------------------------
+def sha512t24u(blob: bytes) -> str:
+    return base64.urlsafe_b64encode(hashlib.sha512(blob).digest()[:24]).decode()
+
+
+def vrs_location_blob(sequence_digest: str, start: int, end: int) -> bytes:
+    return ('{"interval":{"end":{"type":"Number","value":%d},"start":{"type":"Number","value":%d},'
+            '"type":"SequenceInterval"},"sequence_id":"%s","type":"SequenceLocation"}'
+            % (end, start, sequence_digest)).encode()
+
+
+def vrs_allele_blob(location_digest: str, state: bytes) -> bytes:
+    return (b'{"location":"' + location_digest.encode() + b'","state":{"sequence":"' + state
+            + b'","type":"LiteralSequenceExpression"},"type":"Allele"}')
+
+
+def vrs_allele_digest(sequence_digest: str, pos: int, ref, alt) -> str:
+    """gnomAD-style ``chr-pos-ref-alt`` → Allele with interval (pos-1, pos-1+len(ref)]
+    and literal state ``alt`` (no normalisation: primary_key_generator.py:53,83)."""
+    if isinstance(ref, str):
+        ref = ref.encode()
+    if isinstance(alt, str):
+        alt = alt.encode()
+    start = pos - 1
+    loc = sha512t24u(vrs_location_blob(sequence_digest, start, start + len(ref)))
+    return sha512t24u(vrs_allele_blob(loc, alt))
+
+
+# ---------------------------------------------------------------------------
+# a12: in-batch dedup — keep the first occurrence of each primary key
+#   (stable input order).  Reference: removeDuplicates.sql:2-24 groups by
+#   record_primary_key per chromosome and keeps one row.
+# ---------------------------------------------------------------------------
+def dedup_keep(keys: Sequence) -> List[int]:
+    seen = set()
+    keep = []
+    for k in keys:
+        if k in seen:
+            keep.append(0)
+        else:
+            seen.add(k)
+            keep.append(1)
+    return keep
+
+
+# ---------------------------------------------------------------------------
+# L8 histogram (per-shard counters all-gathered across GPUs)
+# ---------------------------------------------------------------------------
+L8_WIDTH = INC[8]
+
+
+def l8_offsets(lengths: Sequence[int]) -> List[int]:
+    off = [0]
+    for L in lengths:
+        off.append(off[-1] + (L + L8_WIDTH - 1) // L8_WIDTH)
+    return off
+
+
+def l8_histogram_np(chrom, start, status, lengths) -> np.ndarray:
+    off = np.asarray(l8_offsets(lengths), dtype=np.int64)
+    chrom = np.asarray(chrom, dtype=np.int64)
+    start = np.asarray(start, dtype=np.int64)
+    ok = (np.asarray(status) == STATUS_OK) | (np.asarray(status) == STATUS_END_BEFORE_START)
+    idx = off[np.clip(chrom[ok], 0, len(lengths) - 1)] + (start[ok] - 1) // L8_WIDTH
+    return np.bincount(idx, minlength=int(off[-1])).astype(np.uint32)

@@ -1,0 +1,285 @@
+"""GPU parity: every kernel through the C ABI vs the CPU oracle and the golden
+vectors the reference produced.  Integer/byte work: bit-exact everywhere."""
+
+import gzip
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from annotatedvdb_amd.chromosomes import CHROM_NAMES, GRCH38_LENGTHS, bin_index_chrom_code, length_table
+from oracle import avdb_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+LENGTHS = length_table()
+
+
+def read_tsv(name):
+    with gzip.open(os.path.join(GOLDEN, name), "rt") as fh:
+        header = fh.readline().rstrip("\n").split("\t")
+        return [dict(zip(header, line.rstrip("\n").split("\t"))) for line in fh]
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+# ---------------------------------------------------------------------------
+# K1 bin assignment
+# ---------------------------------------------------------------------------
+def test_k1_golden_bin_queries(engine):
+    rows = read_tsv("bin_queries.tsv.gz")
+    chrom = np.array([min(bin_index_chrom_code(r["chrom"]), 255) for r in rows], dtype=np.uint8)
+    start = np.array([int(r["start"]) for r in rows], dtype=np.int32)
+    end = np.array([int(r["end"]) if r["end"] else int(r["start"]) for r in rows], dtype=np.int32)
+    code, status = engine.bin_assign(torch.from_numpy(chrom), torch.from_numpy(start), torch.from_numpy(end))
+    paths = engine.format_paths(chrom, u32(code))
+    st = status.cpu().numpy()
+    for i, r in enumerate(rows):
+        exp = r["bin_index"]
+        got = paths[i] if paths[i] is not None else "TypeError"
+        assert got == exp, (r, got, st[i])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 63, 64, 65, 1000, 4099, 1 << 20])
+def test_k1_random_spans_vs_oracle(engine, n):
+    chrom, start, end = __import__("annotatedvdb_amd.synth", fromlist=["x"]).np_spans(n, seed=n)
+    if n > 10:
+        chrom[::97] = 25 + (np.arange(chrom[::97].size) % 200)   # unknown contigs
+        start[::89] = 0                                           # start < 1
+        end[::83] = np.asarray(LENGTHS, dtype=np.int64)[np.minimum(chrom[::83], 24)] + 1
+        sw = slice(5, None, 71)
+        start[sw], end[sw] = end[sw].copy(), start[sw].copy()     # end < start
+    code, status = engine.bin_assign(torch.from_numpy(chrom), torch.from_numpy(start), torch.from_numpy(end))
+    rc, rs = O.bin_codes_np(chrom, start, end, LENGTHS)
+    assert np.array_equal(u32(code), rc)
+    assert np.array_equal(status.cpu().numpy(), rs)
+    # points (end=NULL)
+    code, status = engine.bin_assign(torch.from_numpy(chrom), torch.from_numpy(start))
+    rc, rs = O.bin_codes_np(chrom, start, None, LENGTHS)
+    assert np.array_equal(u32(code), rc)
+    assert np.array_equal(status.cpu().numpy(), rs)
+
+
+def test_k1_misaligned_scalar_path(engine):
+    chrom, start, end = __import__("annotatedvdb_amd.synth", fromlist=["x"]).np_spans(10001, seed=3)
+    dc = torch.from_numpy(chrom).cuda()[1:]
+    ds = torch.from_numpy(start).cuda()[1:]
+    de = torch.from_numpy(end).cuda()[1:]
+    code, status = engine.bin_assign(dc, ds, de)
+    rc, rs = O.bin_codes_np(chrom[1:], start[1:], end[1:], LENGTHS)
+    assert np.array_equal(u32(code), rc)
+    assert np.array_equal(status.cpu().numpy(), rs)
+
+
+@pytest.mark.parametrize("sort", [True, False])
+def test_k1_histogram_and_counters(engine, sort):
+    from annotatedvdb_amd import synth
+    chrom, start, end = synth.np_spans(300001, seed=9)
+    if not sort:
+        p = np.random.default_rng(1).permutation(len(chrom))
+        chrom, start, end = chrom[p], start[p], end[p]
+    chrom[::1001] = 77
+    hist = engine.new_histogram()
+    ctr = engine.new_counters()
+    code, status = engine.bin_assign(torch.from_numpy(chrom), torch.from_numpy(start), torch.from_numpy(end),
+                                     hist=hist, counters=ctr)
+    rc, rs = O.bin_codes_np(chrom, start, end, LENGTHS)
+    exp_hist = O.l8_histogram_np(chrom, start, rs, LENGTHS)
+    assert np.array_equal(hist.cpu().numpy().view(np.uint32), exp_hist)
+    c = ctr.cpu().numpy()
+    ok = rc != O.BIN_NONE
+    lv = np.bincount((rc[ok] >> 28).astype(np.int64), minlength=14)
+    assert np.array_equal(c[0:14], lv)
+    assert np.array_equal(c[16:20], np.bincount(rs, minlength=4))
+    assert c[20] == len(chrom)
+    # scalar path (misaligned) accumulates identically
+    hist2 = engine.new_histogram()
+    ctr2 = engine.new_counters()
+    engine.bin_assign(torch.from_numpy(chrom).cuda()[1:], torch.from_numpy(start).cuda()[1:],
+                      torch.from_numpy(end).cuda()[1:], hist=hist2, counters=ctr2)
+    exp2 = O.l8_histogram_np(chrom[1:], start[1:], rs[1:], LENGTHS)
+    assert np.array_equal(hist2.cpu().numpy().view(np.uint32), exp2)
+    assert int(ctr2[20]) == len(chrom) - 1
+
+
+@pytest.mark.slow
+def test_k1_full_size_c2_properties(engine):
+    """BASELINE config 2 at full size (1e8 points): properties + sampled oracle."""
+    from annotatedvdb_amd import synth
+    n = 100_000_000
+    chrom, start = synth.point_snvs(n, seed=2)
+    hist = engine.new_histogram()
+    ctr = engine.new_counters()
+    code, _ = engine.bin_assign(chrom, start, None, want_status=False, hist=hist, counters=ctr)
+    torch.cuda.synchronize()
+    c = ctr.cpu().numpy()
+    assert c[13] == n and c[20] == n and c[16] == n          # all points are L13 leaves, status OK
+    assert int(hist.sum()) == n
+    # leaf index == (start-1) // 15625 for every record (checked on device)
+    idx = (code & 0x0FFFFFFF).long()
+    assert bool(torch.equal(idx, ((start.long() - 1) // 15625)))
+    assert bool((code.long() >> 28 & 0xF).eq(13).all())
+    # sampled rows vs the oracle
+    sel = torch.randint(0, n, (200_000,), device="cuda")
+    rc, _ = O.bin_codes_np(chrom[sel].cpu().numpy(), start[sel].cpu().numpy(), None, LENGTHS)
+    assert np.array_equal(u32(code[sel]), rc)
+
+
+@pytest.mark.slow
+def test_k1_full_size_c3_vs_c_oracle(engine):
+    """BASELINE config 3 at full size (1e8 spans) vs the C oracle, bit-exact."""
+    import ctypes
+    import oracle
+    from annotatedvdb_amd import synth
+    n = 100_000_000
+    chrom, start, end = synth.spans(n, seed=3)
+    code, status = engine.bin_assign(chrom, start, end)
+    hc, hs, he = chrom.cpu().numpy(), start.cpu().numpy(), end.cpu().numpy()
+    rc = np.empty(n, dtype=np.uint32)
+    rs = np.empty(n, dtype=np.uint8)
+    lens = np.asarray(LENGTHS, dtype=np.uint32)
+    oracle.c_oracle().avdb_oracle_bin_assign(hc.ctypes.data, hs.ctypes.data, he.ctypes.data, n,
+                                            lens.ctypes.data, len(lens), rc.ctypes.data, rs.ctypes.data)
+    assert np.array_equal(u32(code), rc)
+    assert np.array_equal(status.cpu().numpy(), rs)
+
+
+# ---------------------------------------------------------------------------
+# K2 record prep (end inference + bin)
+# ---------------------------------------------------------------------------
+def _prep_rows(engine, chroms, pos, refs, alts):
+    from annotatedvdb_amd.engine import pack_records
+    b = pack_records(chroms, pos, [r.encode() for r in refs], [a.encode() for a in alts])
+    return engine.record_prep(b)
+
+
+def test_k2_golden_end_infer(engine):
+    rows = read_tsv("end_infer.tsv.gz")
+    end, code, status, lcp = _prep_rows(engine, [0] * len(rows), [int(r["pos"]) for r in rows],
+                                        [r["ref"] for r in rows], [r["alt"] for r in rows])
+    e = end.cpu().numpy()
+    l = lcp.cpu().numpy()
+    for i, r in enumerate(rows):
+        assert (int(e[i]), int(l[i])) == (int(r["end"]), int(r["lcp"])), r
+
+
+def test_k2_golden_long_alleles(engine):
+    rows = read_tsv("long_alleles.tsv.gz")
+    chroms = [bin_index_chrom_code(r["chrom"]) for r in rows]
+    end, code, status, lcp = _prep_rows(engine, chroms, [int(r["pos"]) for r in rows],
+                                        [r["ref"] for r in rows], [r["alt"] for r in rows])
+    paths = engine.format_paths(np.asarray(chroms, dtype=np.uint8), u32(code))
+    for i, r in enumerate(rows):
+        assert int(end[i]) == int(r["end"])
+        assert (paths[i] or "TypeError") == r["bin_index"]
+
+
+def test_k2_random_vs_c_oracle(engine):
+    """1e6 synthetic C5-shaped records vs the C oracle (end, code, status, lcp)."""
+    import oracle
+    from annotatedvdb_amd import synth
+    b = synth.alleles(1_000_000, seed=21)
+    end, code, status, lcp = engine.record_prep(b)
+    h = {k: getattr(b, k).cpu().numpy() for k in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap")}
+    n = b.n
+    re_, rc, rl = (np.empty(n, dtype=np.uint32) for _ in range(3))
+    rs = np.empty(n, dtype=np.uint8)
+    lens = np.asarray(LENGTHS, dtype=np.uint32)
+    oracle.c_oracle().avdb_oracle_record_prep(
+        h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
+        h["alt_len"].ctypes.data, h["heap"].ctypes.data, n, lens.ctypes.data, len(lens),
+        re_.ctypes.data, rc.ctypes.data, rs.ctypes.data, rl.ctypes.data)
+    assert np.array_equal(u32(end), re_)
+    assert np.array_equal(u32(code), rc)
+    assert np.array_equal(status.cpu().numpy(), rs)
+    assert np.array_equal(u32(lcp), rl)
+
+
+# ---------------------------------------------------------------------------
+# K3 dedup
+# ---------------------------------------------------------------------------
+def _oracle_keep(b):
+    import oracle
+    h = {k: getattr(b, k).cpu().numpy() for k in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap", "ext_id")}
+    keep = np.empty(b.n, dtype=np.uint8)
+    d = oracle.c_oracle().avdb_oracle_dedup_grouped(
+        h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
+        h["alt_len"].ctypes.data, h["heap"].ctypes.data, h["ext_id"].ctypes.data, b.n, keep.ctypes.data)
+    return keep, d
+
+
+def test_k3_dedup_grouped_and_hash(engine):
+    from annotatedvdb_amd import synth
+    b = synth.alleles(500_000, seed=33, dup_frac=0.05)
+    exp, ndup = _oracle_keep(b)
+    assert ndup > 1000
+    ctr = engine.new_counters()
+    keep = engine.pk_dedup(b, grouped=True, counters=ctr)
+    assert np.array_equal(keep.cpu().numpy(), exp)
+    assert int(ctr[21]) == ndup
+    ctr = engine.new_counters()
+    keep = engine.pk_dedup(b, grouped=False, counters=ctr)
+    assert np.array_equal(keep.cpu().numpy(), exp)
+    assert int(ctr[21]) == ndup and int(ctr[22]) == 0
+
+
+def test_k3_dedup_small_cases(engine):
+    from annotatedvdb_amd.engine import pack_records
+    recs = [(0, 5, "A", "G", 0), (0, 5, "A", "T", 0), (0, 5, "A", "G", 0), (0, 5, "A", "G", 7),
+            (0, 5, "A", "G", 0), (0, 6, "A", "G", 0), (1, 6, "A", "G", 0), (1, 6, "AC", "G", 0),
+            (1, 6, "A", "CG", 0), (1, 6, "A", "G", 0)]
+    b = pack_records([r[0] for r in recs], [r[1] for r in recs], [r[2].encode() for r in recs],
+                     [r[3].encode() for r in recs], [r[4] for r in recs])
+    exp = O.dedup_keep([(r[0], r[1], r[2], r[3], r[4]) for r in recs])
+    for grouped in (True, False):
+        keep = engine.pk_dedup(b, grouped=grouped)
+        assert keep.cpu().tolist() == exp
+    # unsorted input through the hash path: first occurrence wins
+    perm = [9, 3, 0, 7, 2, 5, 1, 8, 4, 6]
+    rp = [recs[i] for i in perm]
+    b = pack_records([r[0] for r in rp], [r[1] for r in rp], [r[2].encode() for r in rp],
+                     [r[3].encode() for r in rp], [r[4] for r in rp])
+    keep = engine.pk_dedup(b, grouped=False)
+    assert keep.cpu().tolist() == O.dedup_keep([(r[0], r[1], r[2], r[3], r[4]) for r in rp])
+
+
+# ---------------------------------------------------------------------------
+# K4 digests
+# ---------------------------------------------------------------------------
+def test_k4_sha512t24u_vs_hashlib(engine):
+    rng = np.random.default_rng(4)
+    blobs = [b"", b"ACGT", b"a" * 111, b"b" * 112, b"c" * 127, b"d" * 128, b"e" * 129, b"f" * 240]
+    blobs += [bytes(rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8)) for _ in range(500)]
+    got = engine.sha512t24u(blobs)
+    assert got == [O.sha512t24u(x) for x in blobs]
+    assert got[0] == "z4PhNX7vuL3xVChQ1m2AB9Yg5AULVxXc"
+
+
+def test_k4_vrs_digest_vs_oracle_serialisation(engine):
+    """Long-allele key digest == the oracle's VRS-1.x serialisation + sha512t24u.
+    (Parity vs vrs-python itself is UNPINNED: not available offline.)"""
+    from annotatedvdb_amd import synth
+    digs = ["%032d" % i for i in range(25)]
+    eng2 = type(engine)(0, sequence_digests=digs)
+    b = synth.alleles(20000, seed=44, long_frac=0.2)
+    d, is_long = eng2.vrs_digest(b, 50)
+    h = {k: getattr(b, k).cpu().numpy() for k in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap")}
+    il = is_long.cpu().numpy()
+    raw = d.cpu().numpy()
+    assert il.sum() > 1000
+    for i in range(b.n):
+        r, a = int(h["ref_len"][i]), int(h["alt_len"][i])
+        assert il[i] == (r + a > 50)
+        if not il[i]:
+            continue
+        o = int(h["allele_off"][i])
+        ref = h["heap"][o:o + r].tobytes()
+        alt = h["heap"][o + r:o + r + a].tobytes()
+        exp = O.vrs_allele_digest(digs[h["chrom"][i]], int(h["pos"][i]), ref, alt)
+        assert raw[i].tobytes().decode() == exp

@@ -1,0 +1,146 @@
+"""Pin the CPU oracle to the golden vectors produced by the reference itself
+(tests/golden/make_golden.py ran the reference's Python verbatim)."""
+
+import gzip
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from annotatedvdb_amd.chromosomes import CHROM_NAMES, GRCH38_LENGTHS, bin_index_chrom_code, length_table
+from oracle import avdb_oracle as O
+
+
+def read_tsv(name):
+    with gzip.open(os.path.join(GOLDEN, name), "rt") as fh:
+        header = fh.readline().rstrip("\n").split("\t")
+        return [dict(zip(header, line.rstrip("\n").split("\t"))) for line in fh]
+
+
+LENS = {"chr" + c: GRCH38_LENGTHS[c] for c in CHROM_NAMES}
+
+
+def oracle_path(chrom, start, end):
+    code = bin_index_chrom_code(chrom)
+    L = length_table()[code] if code < len(CHROM_NAMES) else None
+    c, st = O.bin_code(L, start, end)
+    if c == O.BIN_NONE:
+        return "TypeError"
+    return O.format_bin_path(CHROM_NAMES[code], c)
+
+
+def test_binindexref_table_matches_generator():
+    """The restated BinIndexRef rows equal the reference generator's rows
+    (count, per-level counts and sha256 over every row)."""
+    summ = json.load(open(os.path.join(GOLDEN, "binindexref_summary.json")))
+    h = hashlib.sha256()
+    gbin = 0
+    counts = {}
+    for c in CHROM_NAMES:
+        for level, path, lo, hi in O.generate_binindexref(c, GRCH38_LENGTHS[c]):
+            gbin += 1
+            counts.setdefault("chr" + c, [0] * 14)[level] += 1
+            h.update(("\t".join(str(x) for x in ("chr" + c, level, gbin, path, lo, hi)) + "\n").encode())
+    assert gbin == summ["n_rows"] == 395448
+    assert counts == summ["per_chrom_level_counts"]
+    assert h.hexdigest() == summ["rows_sha256"]
+
+
+def test_bin_queries_golden():
+    rows = read_tsv("bin_queries.tsv.gz")
+    assert len(rows) > 1000
+    bad = []
+    for r in rows:
+        start = int(r["start"])
+        end = int(r["end"]) if r["end"] else None
+        got = oracle_path(r["chrom"], start, end)
+        if got != r["bin_index"]:
+            bad.append((r, got))
+    assert not bad, bad[:5]
+
+
+def test_bin_queries_numpy_matches_scalar():
+    rows = [r for r in read_tsv("bin_queries.tsv.gz")]
+    chrom = np.array([min(bin_index_chrom_code(r["chrom"]), 255) for r in rows], dtype=np.uint8)
+    start = np.array([int(r["start"]) for r in rows], dtype=np.int64)
+    end = np.array([int(r["end"]) if r["end"] else int(r["start"]) for r in rows], dtype=np.int64)
+    codes, status = O.bin_codes_np(chrom, start, end, length_table())
+    for i, r in enumerate(rows):
+        L = length_table()[chrom[i]] if chrom[i] < 25 else None
+        c, s = O.bin_code(L, int(start[i]), int(end[i]))
+        assert codes[i] == c and status[i] == s, (r, codes[i], c)
+
+
+def test_table_search_equals_closed_form():
+    """Independent cross-check: deepest-containing table search over the
+    restated BinIndexRef (the SQL's semantics) == closed form."""
+    t = O.BinTable({"21": GRCH38_LENGTHS["21"], "M": GRCH38_LENGTHS["M"]})
+    rng = np.random.default_rng(11)
+    for c in ("21", "M"):
+        L = GRCH38_LENGTHS[c]
+        for _ in range(3000):
+            s = int(rng.integers(1, L + 1))
+            e = min(L, s + int(10 ** rng.uniform(0, 6.5)))
+            row = t.find("chr" + c, s, e)
+            code, _ = O.bin_code(L, s, e)
+            assert row["global_bin_path"] == O.format_bin_path(c, code)
+
+
+def test_end_inference_golden():
+    rows = read_tsv("end_infer.tsv.gz")
+    for r in rows:
+        end, lcp = O.infer_end(int(r["pos"]), r["ref"], r["alt"])
+        assert (end, lcp) == (int(r["end"]), int(r["lcp"])), r
+        assert O.metaseq_id("1", int(r["pos"]), r["ref"], r["alt"]) == r["metaseq_id"]
+
+
+def test_long_alleles_golden():
+    rows = read_tsv("long_alleles.tsv.gz")
+    for r in rows:
+        end, lcp = O.infer_end(int(r["pos"]), r["ref"], r["alt"])
+        assert (end, lcp) == (int(r["end"]), int(r["lcp"]))
+        assert oracle_path(r["chrom"], int(r["pos"]), end) == r["bin_index"]
+        assert O.is_long(r["ref"], r["alt"])
+
+
+def test_kat():
+    for k in json.load(open(os.path.join(GOLDEN, "kat.json"))):
+        if "source" in k:  # in-repo known answer, GRCh37 DB; position far from any chromosome end
+            end, _ = O.infer_end(k["pos"], k["ref"], k["alt"])
+            assert oracle_path(k["chrom"], k["pos"], end) == k["bin_index_expected"]
+            continue
+        end, _ = O.infer_end(k["pos"], k["ref"], k["alt"])
+        assert end == k["end"]
+        got = oracle_path(k["chrom"], k["pos"], end)
+        assert got == (k["bin_index"] or "TypeError")
+        if k["primary_key"]:
+            assert O.primary_key(k["chrom"], k["pos"], k["ref"], k["alt"], k["rsid"]) == k["primary_key"]
+
+
+def test_port_bin_index_cache_matches_golden():
+    """The reference-structured port (one-bin L13 cache + table search), used as
+    the CPU baseline, answers the golden queries in their recorded order."""
+    rows = read_tsv("bin_queries.tsv.gz")
+    t = O.BinTable(GRCH38_LENGTHS)
+    bi = O.PortBinIndex(t)
+    for r in rows[:8000]:
+        end = int(r["end"]) if r["end"] else None
+        try:
+            got = bi.find_bin_index(r["chrom"], int(r["start"]), end)
+        except TypeError:
+            got = "TypeError"
+        assert got == r["bin_index"], r
+
+
+def test_sha512t24u_primitive():
+    # published GA4GH example: sha512t24u(b"") == "z4PhNX7vuL3xVChQ1m2AB9Yg5AULVxXc"
+    assert O.sha512t24u(b"") == "z4PhNX7vuL3xVChQ1m2AB9Yg5AULVxXc"
+    assert O.sha512t24u(b"ACGT") == "aKF498dAxcJAqme6QYQ7EZ07-fiw8Kw2"
+
+
+def test_dedup_semantics():
+    keys = ["1:5:A:G", "1:5:A:T", "1:5:A:G", "1:5:A:G:rs1", "1:5:A:G"]
+    assert O.dedup_keep(keys) == [1, 1, 0, 1, 0]
