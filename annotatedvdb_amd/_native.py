@@ -37,7 +37,6 @@ MAX_CHROM = 64
 DIGEST_CHARS = 32
 MAX_PATH = 128
 N_COUNTERS = 32
-CTR_LEVEL0 = 0
 CTR_STATUS0 = 16
 CTR_RECORDS = 20
 CTR_DUPLICATES = 21

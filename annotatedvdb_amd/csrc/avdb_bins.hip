@@ -55,8 +55,22 @@ __device__ __forceinline__ uint32_t l8_key(uint32_t c, uint32_t s, uint32_t code
 // K1, vector form: 4 records per lane-group (u32 of chrom codes, uint4 of
 // starts/ends/codes), UNROLL groups in flight per lane.
 // ---------------------------------------------------------------------------
-template <bool HAS_END, bool HIST>
-__global__ __launch_bounds__(kBlock) void k_bin_assign4(
+// FLAGS bit0: plain (not nontemporal) loads; bit1: plain stores
+template <int FLAGS, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+  if constexpr (FLAGS & 1) return *p;
+  else return __builtin_nontemporal_load(p);
+}
+template <int FLAGS, typename T>
+__device__ __forceinline__ void st_(T v, T* p) {
+  if constexpr (FLAGS & 2) *p = v;
+  else __builtin_nontemporal_store(v, p);
+}
+
+constexpr int kK1Block = 512;  // 8 waves: one LDS histogram per 8 waves
+
+template <bool HAS_END, bool HIST, int UNROLL, int FLAGS>
+__global__ __launch_bounds__(kK1Block) void k_bin_assign4(
     const uint32_t* __restrict__ chrom4, const u32x4* __restrict__ start4,
     const u32x4* __restrict__ end4, size_t ngroups, u32x4* __restrict__ code4,
     uint32_t* __restrict__ status4, ChromTable tab, uint32_t* __restrict__ g_hist,
@@ -74,53 +88,96 @@ __global__ __launch_bounds__(kBlock) void k_bin_assign4(
   uint32_t* hist = use_lds ? s_hist : g_hist;
   const bool ctrs = g_ctr != nullptr;
   const int n_chrom = tab.n;
+  const uint32_t bdim = blockDim.x;
 
-  // block-contiguous chunk of groups
-  const size_t per = (ngroups + gridDim.x - 1) / gridDim.x;
-  const size_t g0 = size_t(blockIdx.x) * per;
-  const size_t g1 = g0 + per < ngroups ? g0 + per : ngroups;
+  // FLAGS bit2: grid-stride sweep; otherwise each workgroup owns one
+  // contiguous chunk (a sorted batch then touches a narrow histogram slice)
+  size_t g0, g1, step;
+  if (FLAGS & 4) {
+    g0 = size_t(blockIdx.x) * bdim * UNROLL;
+    g1 = ngroups;
+    step = size_t(gridDim.x) * bdim * UNROLL;
+  } else {
+    const size_t per = (ngroups + gridDim.x - 1) / gridDim.x;
+    g0 = size_t(blockIdx.x) * per;
+    g1 = g0 + per < ngroups ? g0 + per : ngroups;
+    step = size_t(bdim) * UNROLL;
+  }
 
-  constexpr int UNROLL = 4;
-  LaneCounters lc;
+  // error statuses only (OK = records - errors): 8-bit fields for status 1..3
+  uint32_t err = 0;
+  uint32_t nrec = 0;
   int since_flush = 0;
-  for (size_t base = g0; base < g1; base += size_t(kBlock) * UNROLL) {
+  // wave-uniform run of histogram keys (sorted batches): one LDS atomic per run
+  uint32_t run_key = 0xFFFFFFFFu, run_cnt = 0;
+  for (size_t base = g0; base < g1; base += step) {
     uint32_t c4[UNROLL];
     u32x4 s4[UNROLL], e4[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const size_t j = base + size_t(u) * kBlock + threadIdx.x;
+      const size_t j = base + size_t(u) * bdim + threadIdx.x;
       if (j < g1) {
-        c4[u] = __builtin_nontemporal_load(&chrom4[j]);
-        s4[u] = __builtin_nontemporal_load(&start4[j]);
-        if (HAS_END) e4[u] = __builtin_nontemporal_load(&end4[j]);
+        c4[u] = ld<FLAGS>(&chrom4[j]);
+        s4[u] = ld<FLAGS>(&start4[j]);
+        if (HAS_END) e4[u] = ld<FLAGS>(&end4[j]);
       }
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const size_t j = base + size_t(u) * kBlock + threadIdx.x;
+      const size_t j = base + size_t(u) * bdim + threadIdx.x;
       const bool live = j < g1;
       const uint32_t sv[4] = {s4[u].x, s4[u].y, s4[u].z, s4[u].w};
       uint32_t ev[4] = {sv[0], sv[1], sv[2], sv[3]};
       if (HAS_END) { ev[0] = e4[u].x; ev[1] = e4[u].y; ev[2] = e4[u].z; ev[3] = e4[u].w; }
-      uint32_t cv[4], st = 0;
+      uint32_t cv[4], st = 0, key[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t c = (c4[u] >> (8 * k)) & 0xFFu;
         const uint32_t s_k = classify(c, sv[k], ev[k], n_chrom, s_len, &cv[k]);
         st |= s_k << (8 * k);
-        if (ctrs && live) lc.add(cv[k], s_k);
-        if (HIST) wave_hist_add(live ? l8_key(c, sv[k], cv[k], s_l8off) : 0xFFFFFFFFu, hist);
+        key[k] = live ? l8_key(c, sv[k], cv[k], s_l8off) : 0xFFFFFFFFu;
+      }
+      if (ctrs && live) {
+        nrec += 4;
+        if (st) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t s_k = (st >> (8 * k)) & 0xFFu;
+            err += s_k ? (1u << (8 * (s_k - 1))) : 0u;
+          }
+        }
+      }
+      if (HIST) {
+        // lane key: the 4 records' common key, or MIXED; dead lanes match anything
+        const bool same = key[0] == key[1] && key[1] == key[2] && key[2] == key[3];
+        const uint32_t lk = same ? key[0] : 0xFFFFFFFEu;
+        const uint32_t first = __builtin_amdgcn_readfirstlane(lk);
+        const uint64_t ok = __ballot(!live || lk == first);
+        if (ok == ~0ull && first < 0xFFFFFFFEu) {
+          const uint32_t cnt = 4u * uint32_t(__popcll(__ballot(live)));
+          if (first == run_key) {
+            run_cnt += cnt;
+          } else {
+            if (run_cnt && __lane_id() == 0) atomicAdd(&hist[run_key], run_cnt);
+            run_key = first;
+            run_cnt = cnt;
+          }
+        } else if (!(ok == ~0ull && first == 0xFFFFFFFFu)) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) wave_hist_add(key[k], hist);
+        }
       }
       if (live) {
-        __builtin_nontemporal_store(u32x4{cv[0], cv[1], cv[2], cv[3]}, &code4[j]);
-        if (status4) __builtin_nontemporal_store(st, &status4[j]);
+        st_<FLAGS>(u32x4{cv[0], cv[1], cv[2], cv[3]}, &code4[j]);
+        if (status4) st_<FLAGS>(st, &status4[j]);
       }
     }
-    if (ctrs && ++since_flush == 15) {  // 15 * UNROLL * 4 = 240 < 256 per 8-bit field
-      lc.flush(s_ctr);
+    if (ctrs && ++since_flush == 255 / (UNROLL * 4)) {  // 8-bit error fields never wrap
+      flush_errors(err, s_ctr);
       since_flush = 0;
     }
   }
+  if (HIST && run_cnt && __lane_id() == 0) atomicAdd(&hist[run_key], run_cnt);
   // scalar tail (< 4 records)
   if (blockIdx.x == 0 && threadIdx.x < kWave) {
     const size_t i = tail_begin + threadIdx.x;
@@ -131,17 +188,22 @@ __global__ __launch_bounds__(kBlock) void k_bin_assign4(
       const uint32_t s_k = classify(c, s, e, n_chrom, s_len, &cv);
       code[i] = cv;
       if (status) status[i] = uint8_t(s_k);
-      if (ctrs) lc.add(cv, s_k);
+      nrec += 1;
+      err += s_k ? (1u << (8 * (s_k - 1))) : 0u;
       key = l8_key(c, s, cv, s_l8off);
     }
     if (HIST) wave_hist_add(key, hist);
   }
   if (ctrs) {
-    lc.flush(s_ctr);
+    flush_errors(err, s_ctr);
+    // records per workgroup: wave reduce, one LDS atomic per wave
+    for (int d = 32; d > 0; d >>= 1) nrec += __shfl_down(nrec, d, kWave);
+    if (__lane_id() == 0 && nrec) atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)nrec);
     __syncthreads();
     if (threadIdx.x == 0) {
-      const size_t recs = (g1 > g0 ? (g1 - g0) * 4 : 0) + (blockIdx.x == 0 ? n - tail_begin : 0);
-      atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)recs);
+      const unsigned long long bad = s_ctr[AVDB_CTR_STATUS0 + 1] + s_ctr[AVDB_CTR_STATUS0 + 2] +
+                                     s_ctr[AVDB_CTR_STATUS0 + 3];
+      s_ctr[AVDB_CTR_STATUS0] = s_ctr[AVDB_CTR_RECORDS] - bad;
     }
   }
   publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
@@ -165,8 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_assign1(
   const size_t per = (n + gridDim.x - 1) / gridDim.x;
   const size_t i0 = size_t(blockIdx.x) * per;
   const size_t i1 = i0 + per < n ? i0 + per : n;
-  LaneCounters lc;
-  int since = 0;
+  ErrCounters ec;
   for (size_t base = i0; base < i1; base += kBlock) {
     const size_t i = base + threadIdx.x;
     uint32_t key = 0xFFFFFFFFu;
@@ -176,17 +237,13 @@ __global__ __launch_bounds__(kBlock) void k_bin_assign1(
       const uint32_t s_k = classify(c, s, e, tab.n, s_len, &cv);
       code[i] = cv;
       if (status) status[i] = uint8_t(s_k);
-      if (ctrs) lc.add(cv, s_k);
+      if (ctrs) ec.add(s_k);
       key = l8_key(c, s, cv, s_l8off);
     }
     if (HIST) wave_hist_add(key, hist);
-    if (ctrs && ++since == 255) { lc.flush(s_ctr); since = 0; }
+    if (ctrs) ec.tick(s_ctr);
   }
-  if (ctrs) {
-    lc.flush(s_ctr);
-    __syncthreads();
-    if (threadIdx.x == 0 && i1 > i0) atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)(i1 - i0));
-  }
+  if (ctrs) ec.finish(s_ctr);
   publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
 }
 
@@ -235,8 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_record_prep(
   const size_t per = (n + gridDim.x - 1) / gridDim.x;
   const size_t i0 = size_t(blockIdx.x) * per;
   const size_t i1 = i0 + per < n ? i0 + per : n;
-  LaneCounters lc;
-  int since = 0;
+  ErrCounters ec;
   for (size_t base = i0; base < i1; base += kBlock) {
     const size_t i = base + threadIdx.x;
     uint32_t key = 0xFFFFFFFFu;
@@ -250,17 +306,13 @@ __global__ __launch_bounds__(kBlock) void k_record_prep(
       code[i] = cv;
       if (status) status[i] = uint8_t(s_k);
       if (lcp) lcp[i] = l;
-      if (ctrs) lc.add(cv, s_k);
+      if (ctrs) ec.add(s_k);
       key = l8_key(c, p, cv, s_l8off);
     }
     if (HIST) wave_hist_add(key, hist);
-    if (ctrs && ++since == 255) { lc.flush(s_ctr); since = 0; }
+    if (ctrs) ec.tick(s_ctr);
   }
-  if (ctrs) {
-    lc.flush(s_ctr);
-    __syncthreads();
-    if (threadIdx.x == 0 && i1 > i0) atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)(i1 - i0));
-  }
+  if (ctrs) ec.finish(s_ctr);
   publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
 }
 
@@ -291,18 +343,39 @@ extern "C" int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32
                    aligned(bin_code, 16) && (!status || aligned(status, 4)) && n >= 4;
   if (vec) {
     const size_t ngroups = n / 4;
-    // ~16 groups (64 records) per lane-pass keeps 4 loads in flight; 2048 WGs = 8/CU
-    const unsigned grid = stream_grid(ngroups, kBlock * 4, 2048);
+    // One resident wave of workgroups (n_cu x blocks_per_cu), each owning a
+    // contiguous chunk: no partial second round, and the per-workgroup LDS
+    // histogram zero/flush is amortised over the whole chunk.
+    const unsigned bdim = unsigned(ctx->k1_block);
+    const unsigned grid =
+        stream_grid(ngroups, bdim * ctx->k1_unroll, unsigned(ctx->n_cu * ctx->k1_blocks_per_cu));
     const size_t tail = ngroups * 4;
-#define K1V(HE, HI)                                                                          \
-  hipLaunchKernelGGL((k_bin_assign4<HE, HI>), dim3(grid), dim3(kBlock), shm, s,             \
+#define K1V(HE, HI, U, F)                                                                    \
+  hipLaunchKernelGGL((k_bin_assign4<HE, HI, U, F>), dim3(grid), dim3(bdim), shm, s,         \
                      reinterpret_cast<const uint32_t*>(chrom),                               \
                      reinterpret_cast<const u32x4*>(start), reinterpret_cast<const u32x4*>(end), \
                      ngroups, reinterpret_cast<u32x4*>(bin_code),                            \
                      reinterpret_cast<uint32_t*>(status), ctx->tab, hist_l8, ctr, lds_hist,  \
                      chrom, start, end, tail, n, bin_code, status)
-    if (end) { if (hist) K1V(true, true); else K1V(true, false); }
-    else { if (hist) K1V(false, true); else K1V(false, false); }
+#define K1F(HE, HI, U)                                       \
+  do {                                                       \
+    switch (ctx->k1_flags) {                                 \
+      case 1: K1V(HE, HI, U, 1); break;                      \
+      case 2: K1V(HE, HI, U, 2); break;                      \
+      case 3: K1V(HE, HI, U, 3); break;                      \
+      case 6: K1V(HE, HI, U, 6); break;                      \
+      default: K1V(HE, HI, U, 0); break;                     \
+    }                                                        \
+  } while (0)
+#define K1U(HE, HI)                                          \
+  do {                                                       \
+    if (ctx->k1_unroll == 2) K1F(HE, HI, 2);                 \
+    else K1F(HE, HI, 4);                                     \
+  } while (0)
+    if (end) { if (hist) K1U(true, true); else K1U(true, false); }
+    else { if (hist) K1U(false, true); else K1U(false, false); }
+#undef K1U
+#undef K1F
 #undef K1V
     AVDB_LAUNCH_CHECK("k_bin_assign4");
   } else {

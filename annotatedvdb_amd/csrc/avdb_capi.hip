@@ -7,6 +7,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <stdlib.h>
 
 static thread_local char g_err[512] = "";
 
@@ -54,6 +55,7 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     off += (chrom_len[i] + avdb::kL8Width - 1) / avdb::kL8Width;
   }
   c->tab.n_l8 = off;
+  c->n_cu = 256;
   if (device >= 0) {
     int nd = 0;
     hipError_t e = hipGetDeviceCount(&nd);
@@ -63,6 +65,33 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
                      hipGetErrorString(e));
       return AVDB_EHIP;
     }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cus > 0)
+      c->n_cu = cus;
+  }
+  // K1 defaults from the on-device sweep (tools/k1_sweep.py, profiles/r01_k1_sweep*.log):
+  // 512-thread workgroups x 4 per CU (32 waves, one 24.7 KB LDS histogram per
+  // 8 waves), 2 lane-groups in flight, nontemporal loads + plain stores.
+  c->k1_blocks_per_cu = 4;
+  c->k1_unroll = 2;
+  if (const char* s = getenv("AVDB_K1_BLOCKS_PER_CU")) {
+    const int v = atoi(s);
+    if (v >= 1 && v <= 64) c->k1_blocks_per_cu = v;
+  }
+  if (const char* s = getenv("AVDB_K1_UNROLL")) {
+    const int v = atoi(s);
+    if (v == 2 || v == 4) c->k1_unroll = v;
+  }
+  c->k1_block = 512;
+  if (const char* s = getenv("AVDB_K1_BLOCK")) {
+    const int v = atoi(s);
+    if (v == 256 || v == 512) c->k1_block = v;
+  }
+  c->k1_flags = 2;
+  if (const char* s = getenv("AVDB_K1_FLAGS")) {
+    const int v = atoi(s);
+    if ((v >= 0 && v <= 3) || v == 6) c->k1_flags = v;
   }
   *out = c;
   return AVDB_OK;

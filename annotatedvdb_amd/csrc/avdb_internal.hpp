@@ -57,36 +57,40 @@ __device__ __forceinline__ uint32_t classify(uint32_t c, uint32_t s, uint32_t e,
   return st;
 }
 
-// ---- per-lane packed counters -------------------------------------------
-// levels 0..13 in two u64 of 8-bit fields, statuses 0..3 in a u32 of 8-bit
-// fields; flushed to LDS before any field can reach 256.
-struct LaneCounters {
-  uint64_t lv_lo = 0, lv_hi = 0;
-  uint32_t st = 0;
-  __device__ __forceinline__ void add(uint32_t code, uint32_t status) {
-    if (code != AVDB_BIN_NONE) {
-      const uint32_t level = code >> 28;
-      const uint64_t one = 1ull << ((level & 7u) * 8u);
-      lv_lo += level < 8 ? one : 0ull;
-      lv_hi += level < 8 ? 0ull : one;
-    }
-    st += 1u << (status * 8u);
+// ---- status counters ------------------------------------------------------
+// Only error statuses (1..3) are counted per lane, in 8-bit fields of one u32;
+// the OK count is records - errors, so the common path costs nothing.
+__device__ __forceinline__ void flush_errors(uint32_t& err, unsigned long long* s_ctr) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t a = (err >> (8 * k)) & 0xFFu;
+    if (a) atomicAdd(&s_ctr[AVDB_CTR_STATUS0 + 1 + k], (unsigned long long)a);
   }
-  __device__ __forceinline__ void flush(unsigned long long* s_ctr) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t a = uint32_t(lv_lo >> (8 * k)) & 0xFFu;
-      const uint32_t b = uint32_t(lv_hi >> (8 * k)) & 0xFFu;
-      if (a) atomicAdd(&s_ctr[k], (unsigned long long)a);
-      if (k < 6 && b) atomicAdd(&s_ctr[8 + k], (unsigned long long)b);
+  err = 0;
+}
+
+struct ErrCounters {
+  uint32_t err = 0, nrec = 0;
+  int since = 0;
+  __device__ __forceinline__ void add(uint32_t status) {
+    ++nrec;
+    err += status ? (1u << (8 * (status - 1))) : 0u;
+  }
+  // call once per record-slot pass by every lane of the workgroup
+  __device__ __forceinline__ void tick(unsigned long long* s_ctr) {
+    if (++since == 255) { flush_errors(err, s_ctr); since = 0; }
+  }
+  // workgroup epilogue: records + derived OK count into s_ctr (before publish)
+  __device__ __forceinline__ void finish(unsigned long long* s_ctr) {
+    flush_errors(err, s_ctr);
+    for (int d = 32; d > 0; d >>= 1) nrec += __shfl_down(nrec, d, 64);
+    if (__lane_id() == 0 && nrec) atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)nrec);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long bad = s_ctr[AVDB_CTR_STATUS0 + 1] + s_ctr[AVDB_CTR_STATUS0 + 2] +
+                                     s_ctr[AVDB_CTR_STATUS0 + 3];
+      s_ctr[AVDB_CTR_STATUS0] = s_ctr[AVDB_CTR_RECORDS] - bad;
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t a = (st >> (8 * k)) & 0xFFu;
-      if (a) atomicAdd(&s_ctr[AVDB_CTR_STATUS0 + k], (unsigned long long)a);
-    }
-    lv_lo = lv_hi = 0;
-    st = 0;
   }
 };
 
@@ -113,6 +117,11 @@ __device__ __forceinline__ void wave_hist_add(uint32_t key, uint32_t* hist) {
 
 struct avdb_ctx {
   int device;
+  int n_cu;            // compute units on the device (256 on MI355X)
+  int k1_blocks_per_cu;  // K1 grid = n_cu * k1_blocks_per_cu workgroups (env AVDB_K1_BLOCKS_PER_CU)
+  int k1_unroll;         // K1 groups in flight per lane: 2 or 4 (env AVDB_K1_UNROLL)
+  int k1_block;          // K1 workgroup size: 256 or 512 (env AVDB_K1_BLOCK)
+  int k1_flags;          // K1 memory policy bits (env AVDB_K1_FLAGS): 1 plain loads, 2 plain stores
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
   bool has_digests;

@@ -69,8 +69,9 @@ extern "C" {
 #define AVDB_DIGEST_CHARS 32            /* sha512t24u: 24 bytes, base64url, no padding */
 #define AVDB_MAX_PATH 128
 
-/* counters[] slots written by avdb_bin_assign (histogram mode) and avdb_record_prep */
-#define AVDB_CTR_LEVEL0 0               /* [0..13]: records per bin level */
+/* counters[] slots (u64, accumulated) written by avdb_bin_assign / avdb_record_prep
+ * (records, per-status) and avdb_pk_dedup / avdb_vrs_digest (dup/collision/long);
+ * slots [0..15] are reserved */
 #define AVDB_CTR_STATUS0 16             /* [16..19]: records per status */
 #define AVDB_CTR_RECORDS 20
 #define AVDB_CTR_DUPLICATES 21          /* records whose primary key repeats an earlier one */
@@ -103,7 +104,7 @@ int avdb_l8_bin_count(const avdb_ctx* ctx, uint32_t* n_bins);
  * end may be NULL (end = start); status may be NULL.  If hist_l8 (u32[n_l8])
  * and/or counters (u64[AVDB_N_COUNTERS]) are non-NULL they are ACCUMULATED
  * (caller zeroes them): L8 bin of `start` for every mappable record, records
- * per level and per status. */
+ * and records per status. */
 int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* start,
                     const uint32_t* end, size_t n, uint32_t* bin_code, uint8_t* status,
                     uint32_t* hist_l8, uint64_t* counters, void* stream);

@@ -93,9 +93,6 @@ def test_k1_histogram_and_counters(engine, sort):
     exp_hist = O.l8_histogram_np(chrom, start, rs, LENGTHS)
     assert np.array_equal(hist.cpu().numpy().view(np.uint32), exp_hist)
     c = ctr.cpu().numpy()
-    ok = rc != O.BIN_NONE
-    lv = np.bincount((rc[ok] >> 28).astype(np.int64), minlength=14)
-    assert np.array_equal(c[0:14], lv)
     assert np.array_equal(c[16:20], np.bincount(rs, minlength=4))
     assert c[20] == len(chrom)
     # scalar path (misaligned) accumulates identically
@@ -119,7 +116,7 @@ def test_k1_full_size_c2_properties(engine):
     code, _ = engine.bin_assign(chrom, start, None, want_status=False, hist=hist, counters=ctr)
     torch.cuda.synchronize()
     c = ctr.cpu().numpy()
-    assert c[13] == n and c[20] == n and c[16] == n          # all points are L13 leaves, status OK
+    assert c[20] == n and c[16] == n                         # every point mappable, status OK
     assert int(hist.sum()) == n
     # leaf index == (start-1) // 15625 for every record (checked on device)
     idx = (code & 0x0FFFFFFF).long()
