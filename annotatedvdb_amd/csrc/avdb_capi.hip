@@ -70,9 +70,11 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
         cus > 0)
       c->n_cu = cus;
   }
-  // K1 defaults from the on-device sweep (tools/k1_sweep.py, profiles/r01_k1_sweep*.log):
-  // 512-thread workgroups x 4 per CU (32 waves, one 24.7 KB LDS histogram per
-  // 8 waves), 2 lane-groups in flight, nontemporal loads + plain stores.
+  // K1 defaults from the on-device A/B (tools/k1_sweep.py, tools/k1_geom.py;
+  // profiles/r01_k1_*.log): 512-thread workgroups x 4 per CU (32 waves, one
+  // 24.7 KB LDS histogram per 8 waves), 2 lane-groups in flight, nontemporal
+  // loads + plain stores, grid-stride sweep (each workgroup step covers 4096
+  // consecutive records, so a sorted batch still hits ~1 histogram bin per step).
   c->k1_blocks_per_cu = 4;
   c->k1_unroll = 2;
   if (const char* s = getenv("AVDB_K1_BLOCKS_PER_CU")) {
@@ -88,7 +90,7 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     const int v = atoi(s);
     if (v == 256 || v == 512) c->k1_block = v;
   }
-  c->k1_flags = 2;
+  c->k1_flags = 6;
   if (const char* s = getenv("AVDB_K1_FLAGS")) {
     const int v = atoi(s);
     if ((v >= 0 && v <= 3) || v == 6) c->k1_flags = v;

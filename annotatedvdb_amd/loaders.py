@@ -1,0 +1,376 @@
+"""Drop-in ``VCFVariantLoader`` record-prep stage
+(``Util/lib/python/loaders/vcf_variant_loader.py:56-391`` and the parts of
+``variant_loader.py:82-486`` it relies on).
+
+``parse_variant(line)`` keeps the reference's contract — it returns
+``{variant.id: [{'primary_key': pk, 'bin_index': path}, ...]}`` and appends one
+``#``-delimited COPY row per alt allele (:320-343) — and ``parse_variants(lines)``
+does the same for a whole batch with one pass of the GPU kernels:
+
+    host   VCF text -> per-alt SoA (chrom u8, pos, REF/ALT heap, refSNP key)
+    K2     end inference + smallest enclosing bin      (avdb_record_prep)
+    K4     long-allele key digests (if any)            (avdb_vrs_digest)
+    K3     in-batch primary-key dedup (optional)       (avdb_pk_dedup)
+    host   ltree path / key text, COPY rows, mapping
+
+``parse_variant`` is ``parse_variants([line])``: one code path, one set of
+semantics.  Exceptions match the reference at the same record: ``ValueError``
+when a key cannot be built (e.g. ``':'`` inside an allele breaks
+``metaseqId.split(':')``, primary_key_generator.py:106, through the retry
+ladder :234-256), ``TypeError`` when the location has no bin
+(bin_index.py:75).  Database-backed features (``--skipExisting`` lookups, ADSP
+duplicate updates, ``update_existing``, COPY into Postgres) are outside the
+bin/key path and raise ``NotImplementedError``.  The ``display_attributes``
+COPY column is written as ``NULL``.
+"""
+
+from __future__ import annotations
+
+import logging
+from io import StringIO
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .chromosomes import UNKNOWN_CHROM, bin_index_chrom_code
+from .parsers import VcfEntryParser, _xstr
+
+REQUIRED_COPY_FIELDS = ["chromosome", "record_primary_key", "position", "metaseq_id", "bin_index",
+                        "row_algorithm_id"]
+ALLOWABLE_COPY_FIELDS = ["chromosome", "record_primary_key", "position", "is_multi_allelic",
+                         "is_adsp_variant", "ref_snp_id", "metaseq_id", "bin_index", "display_attributes",
+                         "allele_frequencies", "cadd_scores", "adsp_most_severe_consequence",
+                         "adsp_ranked_consequences", "loss_of_function", "vep_output", "adsp_qc",
+                         "gwas_flags", "other_annotation", "row_algorithm_id"]
+
+
+class _AltError(Exception):
+    pass
+
+
+class VCFVariantLoader(object):
+    """GPU-backed drop-in for the reference ``VCFVariantLoader``'s record prep."""
+
+    def __init__(self, datasource, verbose=False, debug=False, device=None):
+        self.logger = logging.getLogger(__name__)
+        self._verbose = verbose
+        self._debug = debug
+        self._datasource = datasource.lower() if datasource is not None else None
+        self._device = device
+        self._alg_invocation_id = None
+        self._pk_generator = None
+        self._bin_indexer = None
+        self._engine = None
+        self._counters = {}
+        self._chromosome_map = None
+        self._resume_after_variant = None
+        self._resume = True
+        self._current_variant = {}
+        self._copy_buffer = None
+        self._copy_fields = None
+        self._copy_sql = None
+        self._skip_existing = False
+        self._update_existing = False
+        self._vcf_header_fields = None
+        self._initialize_counters()
+        self.initialize_copy_buffer()
+        self.logger.info(type(self).__name__ + " initialized")
+
+    # ---- configuration (variant_loader.py / vcf_variant_loader.py) ---------
+    def initialize_bin_indexer(self, gusConfigFile):
+        from .bin_index import BinIndex
+        self._bin_indexer = BinIndex(gusConfigFile, verbose=False, device=self._device)
+        self._engine = self._bin_indexer._engine
+
+    def initialize_pk_generator(self, genomeBuild, seqrepoProxyPath, **kw):
+        from .primary_key_generator import VariantPKGenerator
+        self._pk_generator = VariantPKGenerator(genomeBuild, seqrepoProxyPath, device=self._device, **kw)
+
+    def set_algorithm_invocation_id(self, alg_id):
+        """Stands in for ``set_algorithm_invocation`` (variant_loader.py:431-437),
+        which inserts an AlgorithmInvocation row (database, out of scope)."""
+        self._alg_invocation_id = _xstr(alg_id)
+
+    def set_algorithm_invocation(self, callingScript, comment, commit=True):
+        raise NotImplementedError("AlgorithmInvocation rows live in the database (out of scope); "
+                                  "use set_algorithm_invocation_id()")
+
+    def alg_invocation_id(self):
+        return self._alg_invocation_id
+
+    get_algorithm_invocation_id = alg_invocation_id
+
+    def initialize_copy_sql(self, copyFields=None):
+        fields = list(REQUIRED_COPY_FIELDS) + ["ref_snp_id", "is_multi_allelic", "display_attributes",
+                                                "allele_frequencies"]
+        if copyFields:
+            fields.extend(copyFields)
+        if not set(fields) <= set(ALLOWABLE_COPY_FIELDS):
+            raise ValueError("Copy fields include invalid columns from AnnotatedVDB.Variant")
+        if self.is_adsp() and "is_adsp_variant" not in fields:
+            fields.append("is_adsp_variant")
+        self._copy_fields = fields
+        self._copy_sql = "COPY AnnotatedVDB.Variant(" + ",".join(fields) + \
+            ") FROM STDIN WITH (NULL 'NULL', DELIMITER '#')"
+
+    def set_chromosome_map(self, chrmMap):
+        self._chromosome_map = chrmMap
+
+    def set_vcf_header_fields(self, fields):
+        self._vcf_header_fields = fields
+
+    def vcf_header_fields(self):
+        return self._vcf_header_fields
+
+    def set_skip_existing(self, skipDuplicates, gusConfigFile=None):
+        if skipDuplicates:
+            raise NotImplementedError("--skipExisting checks the database (map_variants); out of scope")
+        self._skip_existing = False
+
+    def skip_existing(self):
+        return self._skip_existing
+
+    def set_update_existing(self, updateExisting):
+        if updateExisting:
+            raise NotImplementedError("updating existing rows needs the database; out of scope")
+
+    def update_existing(self):
+        return self._update_existing
+
+    def get_datasource(self):
+        return self._datasource
+
+    def is_dbsnp(self):
+        return self._datasource == "dbsnp"
+
+    def is_adsp(self):
+        return self._datasource == "adsp"
+
+    def is_eva(self):
+        return self._datasource == "eva"
+
+    def bin_indexer(self):
+        return self._bin_indexer
+
+    def pk_generators(self):
+        return self._pk_generator
+
+    # ---- resume (variant_loader.py:342-354,440-454) -------------------------
+    def resume_load(self):
+        return self._resume
+
+    def set_resume_after_variant(self, variantId):
+        self._resume_after_variant = variantId
+        self._resume = False
+
+    def _update_resume_status(self, variantId):
+        if not self.resume_load():
+            self.increment_counter("skipped")
+            self._resume = variantId == self._resume_after_variant
+            if self.resume_load() is True:
+                self.logger.warning(("Resuming after", self._resume_after_variant))
+
+    # ---- counters and COPY buffer ---------------------------------------------
+    def _initialize_counters(self, additionalCounters=None):
+        self._counters = {"line": 0, "variant": 0, "skipped": 0, "duplicates": 0, "update": 0}
+        for ac in additionalCounters or []:
+            self._counters[ac] = 0
+
+    def get_count(self, counter):
+        return self._counters[counter]
+
+    def increment_counter(self, counter, by=1):
+        self._counters[counter] = self._counters[counter] + by
+
+    def initialize_copy_buffer(self):
+        self._copy_buffer = StringIO()
+
+    def close_copy_buffer(self):
+        self._copy_buffer.close()
+
+    def reset_copy_buffer(self):
+        self.close_copy_buffer()
+        self.initialize_copy_buffer()
+
+    def copy_buffer(self, sizeOnly=False):
+        return self._copy_buffer.tell() if sizeOnly else self._copy_buffer
+
+    def add_copy_str(self, copyStr):
+        self._copy_buffer.write(copyStr + "\n")
+
+    def load_variants(self):
+        raise NotImplementedError("COPY into Postgres is out of scope; read copy_buffer()")
+
+    def close(self):
+        self.close_copy_buffer()
+
+    def get_current_variant(self, toStr=False):
+        return str(self._current_variant) if toStr else self._current_variant
+
+    def get_current_variant_id(self):
+        return self._current_variant.id if self._current_variant else None
+
+    # ---- record prep ----------------------------------------------------------
+    def parse_variant(self, line, flags=None):
+        """One VCF line -> ``{variant.id: [{primary_key, bin_index}, ...]}``
+        (vcf_variant_loader.py:351-391)."""
+        return self.parse_variants([line], flags)[0]
+
+    def parse_variants(self, lines: Sequence, flags=None, errors: str = "raise", dedup: bool = False):
+        """Batched ``parse_variant``.  ``errors='raise'`` stops at the first
+        failing line exactly like a loop of ``parse_variant`` would (earlier
+        lines fully applied, the failing line's earlier alts applied);
+        ``errors='record'`` returns the exception object for failing lines.
+        ``dedup=True`` also skips the COPY row of any alt whose primary key
+        already appeared in this batch (keep-first; the reference leaves that
+        to removeDuplicates.sql) and counts it under ``'duplicates'``."""
+        if self._bin_indexer is None or self._pk_generator is None:
+            raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
+        if flags is not None:
+            raise NotImplementedError("update flags are a database-update feature; out of scope")
+        if self.is_adsp():
+            raise NotImplementedError("ADSP loads check duplicates in the database (is_duplicate); out of scope")
+
+        # ---- phase 1: host parse (stops at the first parse error) --------------
+        parsed = []  # (entry, variant) | ("skip",) | ("error", exc)
+        for line in lines:
+            if self.resume_load() is False and self._resume_after_variant is None:
+                parsed.append(("error", ValueError("Must set VariantLoader resume_afer_variant if resuming load")))
+                break
+            try:
+                entry = VcfEntryParser(line, self._vcf_header_fields) if isinstance(line, str) else line
+                if not self.resume_load():
+                    self._update_resume_status(entry.get("id"))
+                    parsed.append(("skip",))
+                    continue
+                entry.update_chromosome(self._chromosome_map)
+                variant = entry.get_variant(dbSNP=self.is_dbsnp(), namespace=True)
+                parsed.append((entry, variant))
+            except Exception as err:  # noqa: BLE001 — re-raised in phase 3
+                parsed.append(("error", err))
+                if errors == "raise":
+                    break
+
+        # ---- phase 2: per-alt records -> GPU --------------------------------
+        recs = []          # (line_idx, alt, metaseq, pk_or_error, long)
+        max_len = self._pk_generator.max_sequence_length()
+        for li, p in enumerate(parsed):
+            if len(p) != 2 or p[0] in ("skip", "error"):
+                continue
+            entry, v = p
+            for alt in v.alt_alleles:
+                if alt == ".":
+                    continue
+                ref = v.ref_allele
+                metaseq = ":".join((_xstr(v.chromosome), _xstr(v.position), ref, alt))
+                pk_err = None
+                if len(metaseq.split(":")) != 4:
+                    # metaseqId.split(':') fails on every rung of the retry ladder
+                    pk_err = ValueError("too many values to unpack (expected 4)")
+                recs.append([li, alt, metaseq, pk_err, len(ref) + len(alt) > max_len, v])
+        n = len(recs)
+        end = code = status = keep = None
+        pks: List[Optional[str]] = [None] * n
+        if n:
+            import torch
+            from .engine import ExtIdInterner, pack_records
+            interner = ExtIdInterner()
+            chrom_codes = [min(bin_index_chrom_code("chr" + r[5].chromosome if "chr" not in r[5].chromosome
+                                                    else r[5].chromosome), 255) for r in recs]
+            b = pack_records(chrom_codes, [r[5].position for r in recs],
+                             [r[5].ref_allele.encode() for r in recs], [r[1].encode() for r in recs],
+                             [interner.key(r[5].ref_snp_id) for r in recs])
+            eng = self._engine
+            db = b.to(eng.device)
+            d_end, d_code, d_status, _ = eng.record_prep(db, want_lcp=False)
+            d_keep = eng.pk_dedup(db, grouped=False) if dedup else None
+            end = d_end.cpu().numpy()
+            code = d_code.cpu().numpy().view(np.uint32)
+            status = d_status.cpu().numpy()
+            keep = d_keep.cpu().numpy() if d_keep is not None else None
+            paths = eng.format_paths(np.asarray(chrom_codes, dtype=np.uint8), code)
+            # primary keys (short: text; long: K4 digests in one launch)
+            items, idx = [], []
+            for i, r in enumerate(recs):
+                if r[3] is None:
+                    items.append((r[2], r[5].ref_snp_id))
+                    idx.append(i)
+            try:
+                keys = self._pk_generator.generate_primary_keys(items)
+                for i, k in zip(idx, keys):
+                    pks[i] = k
+            except ValueError:
+                for i, it in zip(idx, items):  # isolate the failing records
+                    try:
+                        pks[i] = self._pk_generator.generate_primary_keys([it])[0]
+                    except ValueError as err:
+                        recs[i][3] = err
+        else:
+            paths = []
+
+        # ---- phase 3: emit in order ------------------------------------------------
+        out = []
+        ri = 0
+        for li, p in enumerate(parsed):
+            self.increment_counter("line")
+            if p[0] == "skip":
+                out.append(None)
+                continue
+            if p[0] == "error":
+                if errors == "raise":
+                    raise p[1]
+                out.append(p[1])
+                continue
+            entry, v = p
+            self._current_variant = v
+            mapping = []
+            failed = None
+            for alt in v.alt_alleles:
+                if alt == ".":
+                    self.logger.warning("Skipping variant " + v.id + "; no alt allele (alt = .)")
+                    self.increment_counter("skipped")
+                    continue
+                r = recs[ri]
+                i = ri
+                ri += 1
+                if r[3] is not None:
+                    failed = r[3] if isinstance(r[3], Exception) else ValueError(str(r[3]))
+                    break
+                path = paths[i]
+                if path is None:
+                    failed = TypeError("'NoneType' object is not subscriptable")
+                    break
+                pk = pks[i]
+                if keep is not None and not keep[i]:
+                    self.increment_counter("duplicates")
+                else:
+                    self.add_copy_str("#".join([
+                        "chr" + _xstr(v.chromosome), pk, _xstr(v.position), r[2], path,
+                        _xstr(self._alg_invocation_id), _xstr(v.ref_snp_id, nullStr="NULL"),
+                        _xstr(v.is_multi_allelic, falseAsNull=True, nullStr="NULL"),
+                        "NULL", _freq_str(entry, alt)]))
+                    self.increment_counter("variant")
+                mapping.append({"primary_key": pk, "bin_index": path})
+            if failed is not None:
+                if errors == "raise":
+                    raise failed
+                out.append(failed)
+                ri = _next_line_start(recs, ri, li)  # past this line's remaining alts
+                continue
+            out.append({v.id: mapping})
+        return out
+
+
+def _next_line_start(recs, ri, li):
+    while ri < len(recs) and recs[ri][0] == li:
+        ri += 1
+    return ri
+
+
+def _freq_str(entry, alt):
+    import json
+    try:
+        f = entry.get_frequencies(alt)
+    except Exception:  # noqa: BLE001 — malformed FREQ: reference would raise; keep NULL
+        return "NULL"
+    return "NULL" if f is None else json.dumps(f)

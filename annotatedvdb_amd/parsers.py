@@ -1,0 +1,154 @@
+"""Host-side VCF entry parsing — drop-in for the parts of
+``Util/lib/python/parsers/vcf_parser.py`` (``VcfEntryParser``, :34-240) that feed
+the bin/key path: field split, numeric coercion, INFO parsing, chromosome
+normalisation (``MT``→``M`` :136-137, ``chr`` strip :150), multi-allelic split
+(:138), variant id (:140-142) and refSNP id (:158-169).
+
+This is text handling on the host (SURVEY.md §8f rank 1 is a GPU tokenizer);
+the numeric work on the parsed records runs in the kernels.  End inference is
+delegated to the GPU-backed ``VariantAnnotator``.
+"""
+
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+from .variant_annotator import VariantAnnotator
+
+
+def to_numeric(value):
+    """int, else float, else the value (GenomicsDBData ``to_numeric`` behaviour)."""
+    try:
+        return int(value)
+    except (ValueError, TypeError):
+        try:
+            return float(value)
+        except (ValueError, TypeError):
+            return value
+
+
+def convert_str2numeric_values(d: dict) -> dict:
+    return {k: (to_numeric(v) if isinstance(v, str) else v) for k, v in d.items()}
+
+
+def _xstr(v, nullStr="", falseAsNull=False):
+    if v is None:
+        return nullStr
+    if falseAsNull and v is False:
+        return nullStr
+    return str(v)
+
+
+DEFAULT_FIELDS = ["chrom", "pos", "id", "ref", "alt", "qual", "filter", "info"]
+
+
+class VcfEntryParser(object):
+    """Drop-in for the reference ``VcfEntryParser`` (hot-path subset)."""
+
+    def __init__(self, entry, headerFields=None, identityOnly=False, verbose=False, debug=False,
+                 loader=None):
+        self.__debug = debug
+        self.__verbose = verbose
+        self._header_fields = ["chrom", "pos", "id", "ref", "alt"] if identityOnly \
+            else DEFAULT_FIELDS if headerFields is None \
+            else [x.lower().replace("#", "") for x in headerFields]
+        self.__entry = None if entry is None else self.parse_entry(entry)
+
+    def parse_entry(self, inputStr):
+        """vcf_parser.py:76-114"""
+        fields = self._header_fields
+        values = inputStr.split("\t")
+        try:
+            entry = dict(zip(fields, values)) if len(fields) == len(values) \
+                else {field: values[index] for index, field in enumerate(fields)}
+            result = convert_str2numeric_values(entry)
+            if "info" in result:
+                infoStr = result["info"].replace("\\x2c", ",")
+                infoStr = infoStr.replace("\\x59", "/")
+                infoStr = infoStr.replace("#", ":")
+                info = dict(item.split("=", 1) if "=" in item else [item, True] for item in infoStr.split(";"))
+                result["info"] = convert_str2numeric_values(info)
+        except IndexError:
+            raise IndexError("The number of fields in the VCF entry do not match number expected "
+                             "from provided VCF Header")
+        except Exception as err:
+            raise ImportError(f"Unable to parse VCF entry: {inputStr}; ERROR: {str(err)}")
+        return result
+
+    def update_chromosome(self, chrmMap):
+        self.__verify_entry()
+        if chrmMap is not None:
+            self.__entry["chrom"] = chrmMap.get(self.__entry["chrom"])
+
+    def get_variant(self, dbSNP=False, namespace=False):
+        """vcf_parser.py:127-155"""
+        chrom = _xstr(self.get("chrom"))
+        if chrom == "MT":
+            chrom = "M"
+        altAlleles = self.get("alt").split(",")
+        vid = self.get("id")
+        if vid == "." or vid.startswith("rs"):
+            vid = ":".join((chrom.replace("chr", ""), _xstr(self.get("pos")), self.get("ref"), self.get("alt")))
+        variant = {
+            "id": vid,
+            "ref_snp_id": self.get_refsnp(),
+            "ref_allele": self.get("ref"),
+            "alt_alleles": altAlleles,
+            "is_multi_allelic": len(altAlleles) > 1,
+            "chromosome": _xstr(chrom).replace("chr", ""),
+            "position": int(self.get("pos")),
+            "rs_position": self.get_info("RSPOS"),
+        }
+        return SimpleNamespace(**variant) if namespace else variant
+
+    def get_refsnp(self):
+        """vcf_parser.py:158-169"""
+        self.__verify_entry()
+        if "rs" in self.__entry["id"]:
+            return self.__entry["id"]
+        if "info" in self.__entry and "RS" in self.__entry["info"]:
+            return "rs" + str(self.__entry["info"]["RS"])
+        return None
+
+    def get_entry(self):
+        return self.__entry
+
+    def get(self, key, raiseError=True):
+        self.__verify_entry()
+        try:
+            return self.__entry[key]
+        except KeyError as err:
+            if raiseError:
+                raise err
+            return None
+
+    def get_info(self, key, default=None):
+        self.__verify_entry()
+        if "info" not in self.__entry:
+            return None
+        if key in self.__entry["info"]:
+            return self.__entry["info"][key]
+        return default
+
+    def get_frequencies(self, allele):
+        """vcf_parser.py:195-222 (INFO FREQ)."""
+        vcfGMAFs = self.get_info("FREQ")
+        if vcfGMAFs is None:
+            return None
+        zeroValues = [".", "0"]
+        altAlleles = self.get("alt").split(",")
+        altIndex = altAlleles.index(allele) + 1
+        populationFrequencies = {pop.split(":")[0]: pop.split(":")[1] for pop in vcfGMAFs.split("|")}
+        vcfFreqs = {pop: {"gmaf": to_numeric(freq.split(",")[altIndex])}
+                    for pop, freq in populationFrequencies.items()
+                    if freq.split(",")[altIndex] not in zeroValues}
+        return None if len(vcfFreqs) == 0 else vcfFreqs
+
+    def infer_variant_end_location(self, alt):
+        """vcf_parser.py:225-231 (GPU-backed VariantAnnotator)."""
+        annotator = VariantAnnotator(self.get("ref"), alt, self.get("chrom"), int(self.get("pos")))
+        return annotator.infer_variant_end_location()
+
+    def __verify_entry(self):
+        assert self.__entry is not None, \
+            "DEBUG - must set value of _entry in the VCF parser before attempting to access"

@@ -1,0 +1,116 @@
+"""Host-side logic on CPU: VCF text -> records (vs the reference's own loader
+output in tests/golden/vcf_lines.tsv.gz), record packing, shard planning."""
+
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from annotatedvdb_amd import shard
+from annotatedvdb_amd.chromosomes import CHROM_NAMES, GRCH38_LENGTHS, bin_index_chrom_code, length_table
+from annotatedvdb_amd.parsers import VcfEntryParser
+from oracle import avdb_oracle as O
+
+
+def golden_lines():
+    with gzip.open(os.path.join(GOLDEN, "vcf_lines.tsv.gz"), "rt") as fh:
+        fh.readline()
+        for line in fh:
+            raw, mapping, copy5, ends = line.rstrip("\n").split("\t")
+            yield raw.replace("\\t", "\t"), json.loads(mapping), json.loads(copy5), json.loads(ends)
+
+
+def oracle_path(chrom, start, end):
+    code = bin_index_chrom_code(chrom)
+    if code >= 25:
+        return None
+    c, _ = O.bin_code(length_table()[code], start, end)
+    return None if c == O.BIN_NONE else O.format_bin_path(CHROM_NAMES[code], c)
+
+
+def test_vcf_lines_host_parse_plus_oracle_reproduce_reference_loader():
+    """VcfEntryParser (host) + oracle arithmetic reproduce the reference
+    loader's mapping, COPY prefix and end coordinates on every golden line."""
+    n = 0
+    for raw, mapping, copy5, ends in golden_lines():
+        entry = VcfEntryParser(raw)
+        try:
+            v = entry.get_variant(namespace=True)
+        except Exception as err:  # noqa: BLE001
+            assert "__error__" in mapping, (raw, err)
+            continue
+        exp_rows = []
+        got_map = []
+        error = None
+        for k, alt in enumerate(v.alt_alleles):
+            if alt == ".":
+                continue
+            metaseq = O.metaseq_id(v.chromosome, v.position, v.ref_allele, alt)
+            if len(metaseq.split(":")) != 4:
+                error = "ValueError"
+                break
+            end, _ = O.infer_end(v.position, v.ref_allele, alt)
+            assert end == ends[k]
+            path = oracle_path(v.chromosome, v.position, end)
+            if path is None:
+                error = "TypeError"
+                break
+            pk = O.primary_key(v.chromosome, v.position, v.ref_allele, alt, v.ref_snp_id)
+            got_map.append({"primary_key": pk, "bin_index": path})
+            exp_rows.append("#".join(["chr" + v.chromosome, pk, str(v.position), metaseq, path]))
+        if error:
+            assert mapping == {"__error__": error}, raw
+        else:
+            assert mapping == {v.id: got_map}, raw
+            assert copy5 == exp_rows
+        n += 1
+    assert n > 7000
+
+
+def test_pack_records_layout():
+    from annotatedvdb_amd.engine import ExtIdInterner, pack_records
+    it = ExtIdInterner()
+    keys = [it.key(x) for x in [None, "rs5", "rs0", "rs5", "foo", "rs007", "foo"]]
+    assert keys[0] == 0 and keys[1] == keys[3] == 5
+    assert keys[4] == keys[6] and keys[4] >> 63 == 1 and keys[2] != keys[5] and keys[2] >> 63 == 1
+    assert it.to_str(keys[4]) == "foo" and it.to_str(5) == "rs5"
+    b = pack_records([0, 1, 2], [10, 20, 30], [b"A", b"CAT", b""], [b"G", b"C", b"TT"], keys[:3])
+    heap = b.heap.numpy().tobytes()
+    off = b.allele_off.numpy()
+    rl = b.ref_len.numpy()
+    al = b.alt_len.numpy()
+    assert heap == b"AGCATCTT"
+    assert list(off) == [0, 2, 6] and list(rl) == [1, 3, 0] and list(al) == [1, 1, 2]
+    assert b.ext_id.numpy()[2] < 0  # 2^63|k stored as int64 bit pattern
+
+
+def test_shard_plan_covers_genome_once():
+    lens = length_table()
+    for w in (1, 2, 4, 8):
+        plan = shard.plan(w)
+        cover = {}
+        for ps in plan:
+            for p in ps:
+                cover.setdefault(p.chrom, []).append((p.lo, p.hi))
+        for c, L in enumerate(lens):
+            iv = sorted(cover[c])
+            assert iv[0][0] == 0 and iv[-1][1] == L
+            assert all(a[1] == b[0] for a, b in zip(iv, iv[1:]))
+        assert shard.imbalance(plan) < 1.02
+    plan = shard.plan(8)
+    assert shard.shard_of(plan, 0, 1) >= 0
+    assert shard.shard_of(plan, 24, GRCH38_LENGTHS["M"]) >= 0
+
+
+def test_synthetic_numpy_generators_shape():
+    from annotatedvdb_amd import synth
+    c, s = synth.np_point_snvs(10000, seed=1)
+    assert np.all(np.diff(c.astype(np.int64) * 2**32 + s) >= 0)
+    lens = np.asarray(length_table())
+    assert np.all(s >= 1) and np.all(s <= lens[c])
+    c, s, e = synth.np_spans(10000, seed=1)
+    assert np.all(e >= s) and np.all(e <= lens[c])
+    assert np.mean(e == s) > 0.4
