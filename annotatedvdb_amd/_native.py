@@ -86,12 +86,12 @@ def _sig(lib):
     f.avdb_ctx_set_sequence_digests.argtypes = [P, ctypes.c_char_p, I32]
     f.avdb_l8_bin_count.argtypes = [P, ctypes.POINTER(U32)]
     f.avdb_bin_assign.argtypes = [P, P, P, P, SZ, P, P, P, P, P]
-    f.avdb_record_prep.argtypes = [P, P, P, P, P, P, P, SZ, P, P, P, P, P, P, P]
+    f.avdb_record_prep.argtypes = [P, P, P, P, P, P, P, SZ, SZ, P, P, P, P, P, P, P]
     f.avdb_pk_dedup_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
-    f.avdb_pk_dedup.argtypes = [P, P, P, P, P, P, P, P, SZ, I32, P, SZ, P, P, P]
+    f.avdb_pk_dedup.argtypes = [P, P, P, P, P, P, P, SZ, P, SZ, I32, P, SZ, P, P, P]
     f.avdb_sha512t24u.argtypes = [P, P, P, P, SZ, P, P]
     f.avdb_vrs_digest_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
-    f.avdb_vrs_digest.argtypes = [P, P, P, P, P, P, P, SZ, U32, P, SZ, P, P, P]
+    f.avdb_vrs_digest.argtypes = [P, P, P, P, P, P, P, SZ, SZ, U32, P, SZ, P, P, P]
     f.avdb_format_bin_path.argtypes = [P, U8, U32, ctypes.c_char_p, SZ]
     f.avdb_format_bin_paths.argtypes = [P, P, P, SZ, P, SZ, P]
     for name in EXPORTED_SYMBOLS:

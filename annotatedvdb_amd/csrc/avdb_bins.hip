@@ -251,21 +251,31 @@ __global__ __launch_bounds__(kBlock) void k_bin_assign1(
 // K2: end inference (+ common-prefix length) fused with the bin computation.
 // ---------------------------------------------------------------------------
 // variant_annotator.py:36-79 with lcp from __normalize_alleles (:82-121).
-__device__ __forceinline__ uint32_t infer_end(const uint8_t* __restrict__ heap, uint64_t off,
-                                              uint32_t r, uint32_t a, uint32_t pos,
-                                              uint32_t* lcp_out) {
+// Allele bytes are compared 8 at a time (first mismatch via count-trailing-zeros
+// of the XOR); the inversion test reverses 8-byte chunks with a byte swap.
+__device__ __forceinline__ uint32_t infer_end(const Heap& h, uint64_t off, uint32_t r, uint32_t a,
+                                              uint32_t pos, uint32_t* lcp_out) {
   if (r == 1u && a == 1u) { *lcp_out = 0; return pos; }        // SNV (:54-55)
-  const uint8_t* ref = heap + off;
-  const uint8_t* alt = ref + r;
+  const uint64_t alt = off + r;
   const uint32_t m = r < a ? r : a;
-  uint32_t n = 0;
-  while (n < m && ref[n] == alt[n]) ++n;                       // lcp (:100-108)
+  uint32_t n = 0;                                              // lcp (:100-108)
+  while (n < m) {
+    const uint64_t x = (heap_u64(h, off + n) ^ heap_u64(h, alt + n)) & low_bytes_mask(m - n);
+    if (x) { n += uint32_t(__builtin_ctzll(x)) >> 3; break; }
+    n += 8;
+  }
+  if (n > m) n = m;
   *lcp_out = n;
   const uint32_t nr = r - n, na = a - n;
   if (r == a) {                                                // MNV (:57-65)
-    bool inv = true;
-    for (uint32_t i = 0; i < r; ++i)
-      if (ref[i] != alt[r - 1u - i]) { inv = false; break; }
+    bool inv = true;                                           // ref == alt[::-1]
+    for (uint32_t i = 0; i < r && inv; i += 8) {
+      const uint32_t c = r - i < 8 ? r - i : 8;
+      const uint64_t mk = low_bytes_mask(c);
+      const uint64_t fw = heap_u64(h, off + i) & mk;
+      const uint64_t bw = __builtin_bswap64(heap_u64(h, alt + (r - i - c)) & mk) >> (8 * (8 - c));
+      inv = fw == bw;
+    }
     return inv ? pos + r - 1u : pos + nr - 1u;
   }
   if (na >= 1u)                                                // insertion (:67-74)
@@ -277,10 +287,11 @@ template <bool HIST>
 __global__ __launch_bounds__(kBlock) void k_record_prep(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ allele_off, const uint32_t* __restrict__ ref_len,
-    const uint32_t* __restrict__ alt_len, const uint8_t* __restrict__ heap, size_t n,
-    uint32_t* __restrict__ end_out, uint32_t* __restrict__ code, uint8_t* __restrict__ status,
-    uint32_t* __restrict__ lcp, ChromTable tab, uint32_t* __restrict__ g_hist,
-    unsigned long long* __restrict__ g_ctr, int lds_hist) {
+    const uint32_t* __restrict__ alt_len, const uint8_t* __restrict__ heap, size_t heap_bytes,
+    size_t n, uint32_t* __restrict__ end_out, uint32_t* __restrict__ code,
+    uint8_t* __restrict__ status, uint32_t* __restrict__ lcp, ChromTable tab,
+    uint32_t* __restrict__ g_hist, unsigned long long* __restrict__ g_ctr, int lds_hist) {
+  const Heap hp = make_heap(heap, heap_bytes);
   extern __shared__ uint32_t s_hist[];
   __shared__ uint32_t s_len[AVDB_MAX_CHROM];
   __shared__ uint32_t s_l8off[AVDB_MAX_CHROM];
@@ -299,7 +310,7 @@ __global__ __launch_bounds__(kBlock) void k_record_prep(
     if (i < i1) {
       const uint32_t c = chrom[i], p = pos[i];
       uint32_t l;
-      const uint32_t e = infer_end(heap, allele_off[i], ref_len[i], alt_len[i], p, &l);
+      const uint32_t e = infer_end(hp, allele_off[i], ref_len[i], alt_len[i], p, &l);
       uint32_t cv;
       const uint32_t s_k = classify(c, p, e, tab.n, s_len, &cv);
       end_out[i] = e;
@@ -393,8 +404,8 @@ extern "C" int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32
 
 extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                 const uint64_t* allele_off, const uint32_t* ref_len,
-                                const uint32_t* alt_len, const uint8_t* heap, size_t n,
-                                uint32_t* end_out, uint32_t* bin_code, uint8_t* status,
+                                const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                                size_t n, uint32_t* end_out, uint32_t* bin_code, uint8_t* status,
                                 uint32_t* lcp, uint32_t* hist_l8, uint64_t* counters,
                                 void* stream) {
   if (int rc = check_ctx(ctx)) return rc;
@@ -412,11 +423,11 @@ extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint3
   const unsigned grid = stream_grid(n, kBlock * 8, 2048);
   if (hist)
     hipLaunchKernelGGL((k_record_prep<true>), dim3(grid), dim3(kBlock), shm, s, chrom, pos,
-                       allele_off, ref_len, alt_len, heap, n, end_out, bin_code, status, lcp,
+                       allele_off, ref_len, alt_len, heap, heap_bytes, n, end_out, bin_code, status, lcp,
                        ctx->tab, hist_l8, ctr, lds_hist);
   else
     hipLaunchKernelGGL((k_record_prep<false>), dim3(grid), dim3(kBlock), shm, s, chrom, pos,
-                       allele_off, ref_len, alt_len, heap, n, end_out, bin_code, status, lcp,
+                       allele_off, ref_len, alt_len, heap, heap_bytes, n, end_out, bin_code, status, lcp,
                        ctx->tab, hist_l8, ctr, lds_hist);
   AVDB_LAUNCH_CHECK("k_record_prep");
   return AVDB_OK;

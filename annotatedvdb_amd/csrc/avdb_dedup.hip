@@ -12,48 +12,110 @@
 // hash path: 64-bit fingerprints, an open-addressing table that keeps the
 //   minimum record index per fingerprint (atomicMin), then a byte-exact compare
 //   against the winner; a fingerprint collision falls back to an exact scan.
+// Allele bytes are compared / hashed 8 bytes per load (Heap helpers).
 #include "avdb_internal.hpp"
 
 namespace avdb {
 
-__device__ __forceinline__ bool same_record(const uint8_t* __restrict__ heap,
-                                            const uint64_t* __restrict__ off,
+__device__ __forceinline__ bool same_record(const Heap& h, const uint64_t* __restrict__ off,
                                             const uint32_t* __restrict__ rl,
                                             const uint32_t* __restrict__ al,
                                             const uint64_t* __restrict__ ext, size_t i, size_t j) {
   const uint32_t r = rl[i], a = al[i];
   if (rl[j] != r || al[j] != a) return false;
   if (ext && ext[i] != ext[j]) return false;
-  const uint8_t* p = heap + off[i];
-  const uint8_t* q = heap + off[j];
-  if (p == q) return true;
-  const uint32_t L = r + a;
-  for (uint32_t k = 0; k < L; ++k)
-    if (p[k] != q[k]) return false;
+  return heap_equal(h, off[i], off[j], r + a);
+}
+
+// Byte compares longer than this run wave-cooperatively (64 lanes x 8 bytes per
+// step) instead of serially in one lane.
+constexpr uint32_t kCoopBytes = 64;
+
+// Whole-wave equality test of L bytes at heap offsets p and q (all lanes call
+// with the same arguments; returns the same answer in every lane).
+__device__ __forceinline__ bool wave_heap_equal(const Heap& h, uint64_t p, uint64_t q, uint32_t L) {
+  const uint32_t lane = __lane_id();
+  for (uint32_t base = 0; base < L; base += 8 * kWave) {
+    const uint32_t k = base + 8 * lane;
+    bool diff = false;
+    if (k < L) {
+      const uint64_t m = low_bytes_mask(L - k);
+      diff = ((heap_u64(h, p + k) ^ heap_u64(h, q + k)) & m) != 0;
+    }
+    if (__ballot(diff)) return false;
+  }
   return true;
 }
 
 __global__ __launch_bounds__(kBlock) void k_dedup_grouped(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
-    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
     const uint64_t* __restrict__ ext, size_t n, uint8_t* __restrict__ keep,
     unsigned long long* __restrict__ g_ctr) {
+  const Heap h = make_heap(heap, heap_bytes);
   const size_t stride = size_t(gridDim.x) * blockDim.x;
   uint32_t dups = 0;
-  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint8_t c = chrom[i];
-    const uint32_t p = pos[i];
+  // wave-uniform trip count so every lane reaches the cooperative compares
+  for (size_t base = size_t(blockIdx.x) * blockDim.x; base < n; base += stride) {
+    const size_t i = base + threadIdx.x;
+    const bool live = i < n;
     uint8_t k = 1;
-    for (size_t j = i; j-- > 0;) {
-      if (chrom[j] != c || pos[j] != p) break;
-      if (same_record(heap, off, rl, al, ext, i, j)) { k = 0; break; }
+    // candidate: the nearest earlier record of this (chrom,pos) run with the same
+    // lengths and external id; short candidates are compared in-lane, long ones
+    // are queued for the whole wave.  Earlier run members are scanned in order,
+    // so the first equal one decides (keep-first).
+    size_t j = i;
+    uint32_t L = 0;
+    bool pending = false;
+    if (live) {
+      const uint8_t c = chrom[i];
+      const uint32_t p = pos[i];
+      const uint32_t r = rl[i], a = al[i];
+      const uint64_t e = ext ? ext[i] : 0;
+      L = r + a;
+      while (j-- > 0) {
+        if (chrom[j] != c || pos[j] != p) break;
+        if (rl[j] != r || al[j] != a || (ext && ext[j] != e)) continue;
+        if (L > kCoopBytes) { pending = true; break; }
+        if (heap_equal(h, off[i], off[j], L)) { k = 0; break; }
+      }
     }
-    keep[i] = k;
-    dups += 1u - k;
+    // long candidates: one cooperative compare per queued lane; a mismatch sends
+    // that lane on to its next candidate (rare: equal lengths at one position)
+    uint64_t q = __ballot(pending);
+    while (q) {
+      const int l = __ffsll((unsigned long long)q) - 1;
+      const uint64_t pi = __shfl(live ? off[i] : 0ull, l, kWave);
+      const uint64_t pj = __shfl(pending ? off[j] : 0ull, l, kWave);
+      const uint32_t Ll = __shfl(L, l, kWave);
+      const bool eq = wave_heap_equal(h, pi, pj, Ll);
+      if (__lane_id() == l) {
+        if (eq) {
+          k = 0;
+          pending = false;
+        } else {  // continue this lane's scan past j
+          pending = false;
+          const uint8_t c = chrom[i];
+          const uint32_t p = pos[i];
+          const uint32_t r = rl[i], a = al[i];
+          const uint64_t e = ext ? ext[i] : 0;
+          while (j-- > 0) {
+            if (chrom[j] != c || pos[j] != p) break;
+            if (rl[j] != r || al[j] != a || (ext && ext[j] != e)) continue;
+            pending = true;
+            break;
+          }
+        }
+      }
+      q = __ballot(pending);
+    }
+    if (live) {
+      keep[i] = k;
+      dups += 1u - k;
+    }
   }
   if (g_ctr) {
-    // wave reduce then one atomic per wave
     for (int d = 32; d > 0; d >>= 1) dups += __shfl_down(dups, d, kWave);
     if (__lane_id() == 0 && dups) atomicAdd(&g_ctr[AVDB_CTR_DUPLICATES], (unsigned long long)dups);
   }
@@ -67,33 +129,26 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
-__device__ __forceinline__ uint64_t fingerprint(const uint8_t* __restrict__ heap, uint64_t off,
-                                                uint32_t r, uint32_t a, uint8_t c, uint32_t p,
-                                                uint64_t e) {
+__device__ __forceinline__ uint64_t fingerprint(const Heap& hp, uint64_t off, uint32_t r, uint32_t a,
+                                                uint8_t c, uint32_t p, uint64_t e) {
   uint64_t h = mix64((uint64_t(c) << 32) ^ p ^ 0x9E3779B97F4A7C15ull);
   h = mix64(h ^ e);
   h = mix64(h ^ ((uint64_t(r) << 32) | a));
-  const uint8_t* s = heap + off;
   const uint32_t L = r + a;
-  uint64_t w = 0;
-  uint32_t k = 0;
-  for (; k < L; ++k) {
-    w = (w << 8) | s[k];
-    if ((k & 7u) == 7u) { h = mix64(h ^ w); w = 0; }
-  }
-  if (k & 7u) h = mix64(h ^ w ^ (uint64_t(k & 7u) << 56));
+  for (uint32_t k = 0; k < L; k += 8) h = mix64(h ^ (heap_u64(hp, off + k) & low_bytes_mask(L - k)));
   return h ? h : 1ull;  // 0 marks an empty slot
 }
 
 __global__ __launch_bounds__(kBlock) void k_dedup_insert(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
-    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
     const uint64_t* __restrict__ ext, size_t n, uint64_t* __restrict__ fp,
     unsigned long long* __restrict__ tkey, uint32_t* __restrict__ tidx, uint64_t mask) {
+  const Heap hp = make_heap(heap, heap_bytes);
   const size_t stride = size_t(gridDim.x) * blockDim.x;
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint64_t h = fingerprint(heap, off[i], rl[i], al[i], chrom[i], pos[i], ext ? ext[i] : 0);
+    const uint64_t h = fingerprint(hp, off[i], rl[i], al[i], chrom[i], pos[i], ext ? ext[i] : 0);
     fp[i] = h;
     uint64_t slot = mix64(h) & mask;
     for (;;) {  // table has >= 2n slots: always terminates
@@ -106,11 +161,12 @@ __global__ __launch_bounds__(kBlock) void k_dedup_insert(
 
 __global__ __launch_bounds__(kBlock) void k_dedup_resolve(
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
-    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ ext, size_t n, const uint64_t* __restrict__ fp,
     const unsigned long long* __restrict__ tkey, const uint32_t* __restrict__ tidx,
     uint64_t mask, uint8_t* __restrict__ keep, unsigned long long* __restrict__ g_ctr) {
+  const Heap hp = make_heap(heap, heap_bytes);
   const size_t stride = size_t(gridDim.x) * blockDim.x;
   uint32_t dups = 0, coll = 0;
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -120,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_resolve(
     const uint32_t w = tidx[slot];
     uint8_t k = 1;
     if (w != uint32_t(i)) {
-      if (chrom[w] == chrom[i] && pos[w] == pos[i] && same_record(heap, off, rl, al, ext, i, w)) {
+      if (chrom[w] == chrom[i] && pos[w] == pos[i] && same_record(hp, off, rl, al, ext, i, w)) {
         k = 0;
       } else {
         // fingerprint collision with a different key: exact scan of earlier
@@ -128,7 +184,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_resolve(
         ++coll;
         for (size_t j = 0; j < i; ++j)
           if (fp[j] == h && chrom[j] == chrom[i] && pos[j] == pos[i] &&
-              same_record(heap, off, rl, al, ext, i, j)) { k = 0; break; }
+              same_record(hp, off, rl, al, ext, i, j)) { k = 0; break; }
       }
     }
     keep[i] = k;
@@ -166,9 +222,10 @@ extern "C" int avdb_pk_dedup_workspace_size(size_t n, size_t* bytes) {
 
 extern "C" int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                              const uint64_t* allele_off, const uint32_t* ref_len,
-                             const uint32_t* alt_len, const uint8_t* heap, const uint64_t* ext_id,
-                             size_t n, int grouped, void* workspace, size_t workspace_bytes,
-                             uint8_t* keep, uint64_t* counters, void* stream) {
+                             const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                             const uint64_t* ext_id, size_t n, int grouped, void* workspace,
+                             size_t workspace_bytes, uint8_t* keep, uint64_t* counters,
+                             void* stream) {
   if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
   if (n == 0) return AVDB_OK;
   if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap || !keep) {
@@ -182,7 +239,7 @@ extern "C" int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t
   const unsigned grid = stream_grid(n, kBlock * 4, 4096);
   if (grouped) {
     hipLaunchKernelGGL(k_dedup_grouped, dim3(grid), dim3(kBlock), 0, s, chrom, pos, allele_off,
-                       ref_len, alt_len, heap, ext_id, n, keep, ctr);
+                       ref_len, alt_len, heap, heap_bytes, ext_id, n, keep, ctr);
     AVDB_LAUNCH_CHECK("k_dedup_grouped");
     return AVDB_OK;
   }
@@ -200,10 +257,11 @@ extern "C" int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t
   AVDB_HIP_TRY(hipMemsetAsync(tkey, 0, 8 * slots, s));
   AVDB_HIP_TRY(hipMemsetAsync(tidx, 0xFF, 4 * slots, s));
   hipLaunchKernelGGL(k_dedup_insert, dim3(grid), dim3(kBlock), 0, s, chrom, pos, allele_off,
-                     ref_len, alt_len, heap, ext_id, n, fp, tkey, tidx, slots - 1);
+                     ref_len, alt_len, heap, heap_bytes, ext_id, n, fp, tkey, tidx, slots - 1);
   AVDB_LAUNCH_CHECK("k_dedup_insert");
   hipLaunchKernelGGL(k_dedup_resolve, dim3(grid), dim3(kBlock), 0, s, allele_off, ref_len,
-                     alt_len, heap, chrom, pos, ext_id, n, fp, tkey, tidx, slots - 1, keep, ctr);
+                     alt_len, heap, heap_bytes, chrom, pos, ext_id, n, fp, tkey, tidx, slots - 1,
+                     keep, ctr);
   AVDB_LAUNCH_CHECK("k_dedup_resolve");
   return AVDB_OK;
 }

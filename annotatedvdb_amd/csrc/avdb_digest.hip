@@ -7,11 +7,18 @@
 // UNPINNED (vrs-python / SeqRepo are absent); the SHA-512 primitive is pinned
 // against hashlib in tests.
 //
-// Long records are a few % of a batch, so they are first compacted with a
-// wave ballot + one atomic per wave (k_long_compact), then hashed one record
-// per lane by a persistent grid (k_vrs_digest).  Each lane's 128-byte SHA-512
-// message block lives in LDS, laid out [word][lane] (conflict-free 8-byte
-// accesses); the 80 rounds run in registers with a static-indexed schedule.
+// Pipeline for a batch:
+//   k_long_hist     per-workgroup histogram of long records by SHA block count
+//   k_long_scan     one workgroup: bucket-major exclusive scan -> offsets
+//   k_long_scatter  list of long record indices, grouped by block count
+//   k_vrs_digest    one lane per long record: SequenceLocation digest (2 blocks)
+//                   then Allele digest, block-synchronously
+// Grouping by block count keeps the 64 lanes of a wave on the same number of
+// compressions.  Message words are built 8 bytes at a time: a word lying inside
+// the ALT bytes is one funnel-shifted 8-byte heap load + byte swap; only the few
+// words at segment boundaries are assembled bytewise.  The SHA-512 state and
+// the 16-word schedule stay in registers; the compression has a single call
+// site per kernel.
 #include "avdb_internal.hpp"
 
 namespace avdb {
@@ -38,17 +45,53 @@ __constant__ uint64_t K512[80] = {
     0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
     0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
 
+__constant__ uint64_t kIV[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull,
+                                0xa54ff53a5f1d36f1ull, 0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                                0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+
+__constant__ char kB64url[65] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+
+// VRS 1.x compact serialisations (keys sorted, no whitespace)
+#define LOC0 "{\"interval\":{\"end\":{\"type\":\"Number\",\"value\":"
+#define LOC1 "},\"start\":{\"type\":\"Number\",\"value\":"
+#define LOC2 "},\"type\":\"SequenceInterval\"},\"sequence_id\":\""
+#define LOC3 "\",\"type\":\"SequenceLocation\"}"
+#define AL0 "{\"location\":\""
+#define AL1 "\",\"state\":{\"sequence\":\""
+#define AL2 "\",\"type\":\"LiteralSequenceExpression\"},\"type\":\"Allele\"}"
+__constant__ char kLoc0[] = LOC0;
+__constant__ char kLoc1[] = LOC1;
+__constant__ char kLoc2[] = LOC2;
+__constant__ char kLoc3[] = LOC3;
+__constant__ char kAl0[] = AL0;
+__constant__ char kAl1[] = AL1;
+__constant__ char kAl2[] = AL2;
+constexpr uint32_t nL0 = sizeof(LOC0) - 1;
+constexpr uint32_t nL1 = sizeof(LOC1) - 1;
+constexpr uint32_t nL2 = sizeof(LOC2) - 1;
+constexpr uint32_t nL3 = sizeof(LOC3) - 1;
+constexpr uint32_t nA0 = sizeof(AL0) - 1;
+constexpr uint32_t nA1 = sizeof(AL1) - 1;
+constexpr uint32_t nA2 = sizeof(AL2) - 1;
+constexpr uint32_t kAlPrefix = nA0 + AVDB_DIGEST_CHARS + nA1;  // ALT starts here
+static_assert(kAlPrefix == 68, "allele prefix");
+
+constexpr int kLongBuckets = 64;
+constexpr int kCompactGrid = 1024;  // 4 workgroups per CU for the streaming passes
+
+__device__ __forceinline__ uint32_t sha_blocks(uint64_t msg_bytes) {
+  return uint32_t((msg_bytes + 17 + 127) / 128);
+}
+
+__device__ __forceinline__ uint32_t allele_blocks(uint32_t a) {
+  return sha_blocks(uint64_t(kAlPrefix) + a + nA2);
+}
+
 __device__ __forceinline__ uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 
-// SHA-512 compression of one 128-byte block.  Both the block (16 words) and
-// the chaining state (8 words) live in LDS, [word][lane], so this single
-// out-of-line copy needs no scratch and no struct pointer.
-__device__ __noinline__ void sha512_compress(uint64_t* buf, uint64_t* hs) {
-  uint64_t w[16];
-#pragma unroll
-  for (int t = 0; t < 16; ++t) w[t] = buf[t * kBlock];
-  uint64_t a = hs[0], b = hs[kBlock], c = hs[2 * kBlock], d = hs[3 * kBlock];
-  uint64_t e = hs[4 * kBlock], f = hs[5 * kBlock], g = hs[6 * kBlock], hh = hs[7 * kBlock];
+// One SHA-512 compression; state and schedule in registers.
+__device__ __forceinline__ void sha512_block(uint64_t* H, uint64_t* w) {
+  uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], hh = H[7];
 #pragma unroll 1
   for (int r = 0; r < 80; r += 16) {
 #pragma unroll
@@ -68,168 +111,296 @@ __device__ __noinline__ void sha512_compress(uint64_t* buf, uint64_t* hs) {
       const uint64_t t1 = hh + S1 + ch + K512[r + j] + wt;
       const uint64_t S0 = rotr(a, 28) ^ rotr(a, 34) ^ rotr(a, 39);
       const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-      const uint64_t t2 = S0 + mj;
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
     }
   }
-  hs[0] += a; hs[kBlock] += b; hs[2 * kBlock] += c; hs[3 * kBlock] += d;
-  hs[4 * kBlock] += e; hs[5 * kBlock] += f; hs[6 * kBlock] += g; hs[7 * kBlock] += hh;
+  H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += hh;
 }
 
-// Streaming byte feeder; acc/nb/widx/total stay in registers.
-struct Sha512 {
-  uint64_t acc;
-  uint32_t nb;      // bytes in acc (0..7)
-  uint32_t widx;    // words in block buffer (0..15)
-  uint64_t total;   // message bytes
-  uint64_t* buf;    // LDS: word w of this lane at buf[w * kBlock]
-  uint64_t* hs;     // LDS: chaining word k of this lane at hs[k * kBlock]
+// SHA padding byte at message position q for a message of T bytes in nb blocks
+__device__ __forceinline__ uint8_t pad_byte(uint64_t q, uint64_t T, uint32_t nb) {
+  if (q == T) return 0x80;
+  const uint64_t end = uint64_t(nb) * 128;
+  if (q >= end - 8) return uint8_t((T * 8) >> (8 * (end - 1 - q)));
+  return 0;
+}
 
-  __device__ __forceinline__ void init(uint64_t* lds_buf, uint64_t* lds_h) {
-    buf = lds_buf; hs = lds_h;
-    hs[0] = 0x6a09e667f3bcc908ull; hs[kBlock] = 0xbb67ae8584caa73bull;
-    hs[2 * kBlock] = 0x3c6ef372fe94f82bull; hs[3 * kBlock] = 0xa54ff53a5f1d36f1ull;
-    hs[4 * kBlock] = 0x510e527fade682d1ull; hs[5 * kBlock] = 0x9b05688c2b3e6c1full;
-    hs[6 * kBlock] = 0x1f83d9abfb41bd6bull; hs[7 * kBlock] = 0x5be0cd19137e2179ull;
-    acc = 0; nb = 0; widx = 0; total = 0;
-  }
-  __device__ __forceinline__ void put_raw(uint8_t byte) {
-    acc = (acc << 8) | byte;
-    if (++nb == 8) {
-      buf[widx * kBlock] = acc;
-      acc = 0; nb = 0;
-      if (++widx == 16) { sha512_compress(buf, hs); widx = 0; }
+// base64url of the first 24 digest bytes, packed as 4 little-endian words of chars
+__device__ __forceinline__ void t24u_words(const uint64_t* H, uint64_t* out) {
+#pragma unroll
+  for (int o = 0; o < 4; ++o) out[o] = 0;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {  // 3 digest bytes -> 4 chars
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int i = 3 * g + k;
+      v = (v << 8) | uint32_t((H[i >> 3] >> (56 - 8 * (i & 7))) & 0xFF);
     }
-  }
-  __device__ __forceinline__ void put(uint8_t byte) { put_raw(byte); ++total; }
-  __device__ __forceinline__ void put_str(const char* s, int n) { for (int i = 0; i < n; ++i) put(uint8_t(s[i])); }
-  __device__ __forceinline__ void put_bytes(const uint8_t* s, uint32_t n) { for (uint32_t i = 0; i < n; ++i) put(s[i]); }
-  __device__ __forceinline__ void put_u32_dec(uint32_t v) {
-    uint32_t p10 = 1;
-    while (v / p10 >= 10u) p10 *= 10u;
-    for (; p10; p10 /= 10u) put(uint8_t('0' + (v / p10) % 10u));
-  }
-  __device__ __forceinline__ void finish() {
-    const uint64_t bits = total * 8;
-    put_raw(0x80);
-    while (widx * 8 + nb != 112) put_raw(0);
-    for (int i = 0; i < 8; ++i) put_raw(0);  // high 64 bits of the length
-    for (int i = 7; i >= 0; --i) put_raw(uint8_t(bits >> (8 * i)));
-  }
-  __device__ __forceinline__ uint64_t h(int k) const { return hs[k * kBlock]; }
-};
-
-__constant__ char kB64url[65] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
-
-// base64url of the first 24 digest bytes -> 32 chars
-__device__ __forceinline__ void t24u(const Sha512& sh, char* out) {
-  const uint64_t h0 = sh.h(0), h1 = sh.h(1), h2 = sh.h(2);
-  uint8_t d[24];
 #pragma unroll
-  for (int i = 0; i < 24; ++i) {
-    const uint64_t hw = i < 8 ? h0 : (i < 16 ? h1 : h2);
-    d[i] = uint8_t(hw >> (56 - 8 * (i & 7)));
-  }
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    const uint32_t v = (uint32_t(d[3 * g]) << 16) | (uint32_t(d[3 * g + 1]) << 8) | d[3 * g + 2];
-    out[4 * g + 0] = kB64url[(v >> 18) & 63];
-    out[4 * g + 1] = kB64url[(v >> 12) & 63];
-    out[4 * g + 2] = kB64url[(v >> 6) & 63];
-    out[4 * g + 3] = kB64url[v & 63];
+    for (int k = 0; k < 4; ++k) {
+      const int ci = 4 * g + k;
+      const uint64_t ch = uint64_t(uint8_t(kB64url[(v >> (18 - 6 * k)) & 63]));
+      out[ci >> 3] |= ch << (8 * (ci & 7));
+    }
   }
 }
 
+__device__ __forceinline__ uint8_t word_char(const uint64_t* w4, uint32_t k) {  // k < 32
+  const uint32_t q = k >> 3;
+  const uint64_t x = q == 0 ? w4[0] : q == 1 ? w4[1] : q == 2 ? w4[2] : w4[3];
+  return uint8_t(x >> (8 * (k & 7)));
+}
+
+__device__ __forceinline__ uint32_t ndigits(uint32_t v) {
+  uint32_t d = 1;
+  while (v >= 10u) { v /= 10u; ++d; }
+  return d;
+}
+
+__device__ __forceinline__ uint8_t digit_at(uint32_t v, uint32_t d, uint32_t k) {  // k-th of d digits
+  for (uint32_t i = k + 1; i < d; ++i) v /= 10u;
+  return uint8_t('0' + v % 10u);
+}
+
+__device__ __forceinline__ void store_digest(char* o, const uint64_t* cw) {
+  if ((reinterpret_cast<uintptr_t>(o) & 7) == 0) {
+    uint64_t* dst = reinterpret_cast<uint64_t*>(o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = cw[k];
+  } else {
+    for (uint32_t k = 0; k < 32; ++k) o[k] = char(word_char(cw, k));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// generic sha512t24u over caller byte strings
+// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_sha512t24u(const uint8_t* __restrict__ data,
                                                        const uint64_t* __restrict__ off,
                                                        const uint32_t* __restrict__ len, size_t n,
                                                        char* __restrict__ out) {
-  __shared__ uint64_t s_buf[16 * kBlock];
-  __shared__ uint64_t s_h[8 * kBlock];
+  // wide loads are only used for 8 bytes wholly inside a string, so both
+  // aligned words they touch hold string bytes: unbounded heap is safe here
+  const Heap hp{reinterpret_cast<uintptr_t>(data), ~uintptr_t(0)};
   const size_t stride = size_t(gridDim.x) * blockDim.x;
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-    Sha512 sh;
-    sh.init(&s_buf[threadIdx.x], &s_h[threadIdx.x]);
-    sh.put_bytes(data + off[i], len[i]);
-    sh.finish();
-    t24u(sh, out + i * AVDB_DIGEST_CHARS);
+    const uint64_t o = off[i];
+    const uint64_t T = len[i];
+    const uint32_t nb = sha_blocks(T);
+    uint64_t H[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) H[k] = kIV[k];
+    for (uint32_t b = 0; b < nb; ++b) {
+      uint64_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint64_t p = uint64_t(b) * 128 + 8 * j;
+        if (p + 8 <= T) {
+          w[j] = __builtin_bswap64(heap_u64(hp, o + p));
+        } else {
+          uint64_t x = 0;
+          for (int k = 0; k < 8; ++k) {
+            const uint64_t q = p + k;
+            const uint8_t by = q < T ? data[o + q] : pad_byte(q, T, nb);
+            x = (x << 8) | by;
+          }
+          w[j] = x;
+        }
+      }
+      sha512_block(H, w);
+    }
+    uint64_t cw[4];
+    t24u_words(H, cw);
+    store_digest(out + i * AVDB_DIGEST_CHARS, cw);
   }
 }
 
-// compact indices of long records (wave ballot + one atomic per wave)
-__global__ __launch_bounds__(kBlock) void k_long_compact(const uint32_t* __restrict__ rl,
-                                                         const uint32_t* __restrict__ al, size_t n,
-                                                         uint32_t max_len, uint8_t* __restrict__ is_long,
-                                                         uint32_t* __restrict__ list,
-                                                         unsigned int* __restrict__ count) {
-  const size_t stride = size_t(gridDim.x) * blockDim.x;
-  const size_t base0 = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (size_t i = base0; i - threadIdx.x < n; i += stride) {  // wave-uniform trip count
-    const bool live = i < n;
-    const bool lg = live && (uint64_t(rl[i]) + al[i] > max_len);
-    if (live && is_long) is_long[i] = lg;
-    const uint64_t m = __ballot(lg);
-    if (m) {
-      const int lane = __lane_id();
-      unsigned int base = 0;
-      if (lane == 0) base = atomicAdd(count, (unsigned int)__popcll(m));
-      base = __shfl(base, 0, kWave);
-      if (lg) {
-        const uint64_t below = lane ? (m << (64 - lane)) : 0ull;
-        list[base + __popcll(below)] = uint32_t(i);
-      }
+// ---------------------------------------------------------------------------
+// long-record list, grouped by allele-message block count (deterministic
+// bucket-major layout: no contended atomics)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool is_long_rec(uint32_t r, uint32_t a, uint32_t max_len) {
+  return uint64_t(r) + a > max_len;
+}
+
+__device__ __forceinline__ uint32_t bucket_of(uint32_t a) {
+  const uint32_t nb = allele_blocks(a);
+  return nb < kLongBuckets ? nb : kLongBuckets - 1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_long_hist(const uint32_t* __restrict__ rl,
+                                                      const uint32_t* __restrict__ al, size_t n,
+                                                      uint32_t max_len, uint8_t* __restrict__ is_long,
+                                                      uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_cnt[kLongBuckets];
+  if (threadIdx.x < kLongBuckets) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t per = (n + gridDim.x - 1) / gridDim.x;
+  const size_t i0 = size_t(blockIdx.x) * per;
+  const size_t i1 = i0 + per < n ? i0 + per : n;
+  for (size_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint32_t a = al[i];
+    const bool lg = is_long_rec(rl[i], a, max_len);
+    if (is_long) is_long[i] = lg;
+    if (lg) atomicAdd(&s_cnt[bucket_of(a)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kLongBuckets) counts[threadIdx.x * gridDim.x + blockIdx.x] = s_cnt[threadIdx.x];
+}
+
+// exclusive scan of m = kLongBuckets * G counts by one 1024-thread workgroup
+__global__ __launch_bounds__(1024) void k_long_scan(uint32_t* __restrict__ counts, uint32_t m,
+                                                    unsigned int* __restrict__ total) {
+  __shared__ uint32_t s_part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (m + 1023) / 1024;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t idx = t * per + k;
+    if (idx < m) sum += counts[idx];
+  }
+  s_part[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t v = t >= d ? s_part[t - d] : 0u;
+    __syncthreads();
+    s_part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = s_part[t] - sum;  // exclusive prefix of this thread's slice
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t idx = t * per + k;
+    if (idx < m) {
+      const uint32_t c = counts[idx];
+      counts[idx] = run;
+      run += c;
     }
   }
+  if (t == 1023) *total = s_part[1023];
 }
 
-__constant__ char kLoc0[] = "{\"interval\":{\"end\":{\"type\":\"Number\",\"value\":";
-__constant__ char kLoc1[] = "},\"start\":{\"type\":\"Number\",\"value\":";
-__constant__ char kLoc2[] = "},\"type\":\"SequenceInterval\"},\"sequence_id\":\"";
-__constant__ char kLoc3[] = "\",\"type\":\"SequenceLocation\"}";
-__constant__ char kAl0[] = "{\"location\":\"";
-__constant__ char kAl1[] = "\",\"state\":{\"sequence\":\"";
-__constant__ char kAl2[] = "\",\"type\":\"LiteralSequenceExpression\"},\"type\":\"Allele\"}";
+__global__ __launch_bounds__(kBlock) void k_long_scatter(const uint32_t* __restrict__ rl,
+                                                         const uint32_t* __restrict__ al, size_t n,
+                                                         uint32_t max_len,
+                                                         const uint32_t* __restrict__ offs,
+                                                         uint32_t* __restrict__ list) {
+  __shared__ uint32_t s_cur[kLongBuckets];
+  if (threadIdx.x < kLongBuckets) s_cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const size_t per = (n + gridDim.x - 1) / gridDim.x;
+  const size_t i0 = size_t(blockIdx.x) * per;
+  const size_t i1 = i0 + per < n ? i0 + per : n;
+  for (size_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint32_t a = al[i];
+    if (is_long_rec(rl[i], a, max_len)) list[atomicAdd(&s_cur[bucket_of(a)], 1u)] = uint32_t(i);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// VRS Allele digest per long record
+// ---------------------------------------------------------------------------
+struct LocMsg {
+  uint32_t E, S, dE, dS, T;
+  const char* dig;  // 32 refget chars of the contig
+};
+
+__device__ __forceinline__ uint8_t loc_byte(const LocMsg& m, uint32_t p) {
+  if (p < nL0) return uint8_t(kLoc0[p]);
+  p -= nL0;
+  if (p < m.dE) return digit_at(m.E, m.dE, p);
+  p -= m.dE;
+  if (p < nL1) return uint8_t(kLoc1[p]);
+  p -= nL1;
+  if (p < m.dS) return digit_at(m.S, m.dS, p);
+  p -= m.dS;
+  if (p < nL2) return uint8_t(kLoc2[p]);
+  p -= nL2;
+  if (p < AVDB_DIGEST_CHARS) return uint8_t(m.dig[p]);
+  p -= AVDB_DIGEST_CHARS;
+  return uint8_t(kLoc3[p]);
+}
 
 __global__ __launch_bounds__(kBlock) void k_vrs_digest(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
-    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
     const uint32_t* __restrict__ list, const unsigned int* __restrict__ count,
     const char* __restrict__ seq_digest, int n_chrom, char* __restrict__ out) {
-  __shared__ uint64_t s_buf[16 * kBlock];
-  __shared__ uint64_t s_h[8 * kBlock];
+  const Heap hp = make_heap(heap, heap_bytes);
   const unsigned int cnt = *count;
   const size_t stride = size_t(gridDim.x) * blockDim.x;
   for (size_t t = size_t(blockIdx.x) * blockDim.x + threadIdx.x; t < cnt; t += stride) {
     const uint32_t i = list[t];
     const uint32_t c = chrom[i];
-    const uint32_t start = pos[i] - 1u;  // gnomAD chr-pos-ref-alt -> interbase (pos-1, pos-1+len(ref)]
     const uint32_t r = rl[i], a = al[i];
     char* o = out + size_t(i) * AVDB_DIGEST_CHARS;
     if (c >= uint32_t(n_chrom)) {
       for (int k = 0; k < AVDB_DIGEST_CHARS; ++k) o[k] = '?';
       continue;
     }
-    Sha512 sh;
-    sh.init(&s_buf[threadIdx.x], &s_h[threadIdx.x]);
-    sh.put_str(kLoc0, sizeof(kLoc0) - 1);
-    sh.put_u32_dec(start + r);
-    sh.put_str(kLoc1, sizeof(kLoc1) - 1);
-    sh.put_u32_dec(start);
-    sh.put_str(kLoc2, sizeof(kLoc2) - 1);
-    sh.put_str(seq_digest + size_t(c) * AVDB_DIGEST_CHARS, AVDB_DIGEST_CHARS);
-    sh.put_str(kLoc3, sizeof(kLoc3) - 1);
-    sh.finish();
-    char loc[AVDB_DIGEST_CHARS];
-    t24u(sh, loc);
-    sh.init(&s_buf[threadIdx.x], &s_h[threadIdx.x]);
-    sh.put_str(kAl0, sizeof(kAl0) - 1);
-    sh.put_str(loc, AVDB_DIGEST_CHARS);
-    sh.put_str(kAl1, sizeof(kAl1) - 1);
-    sh.put_bytes(heap + off[i] + r, a);
-    sh.put_str(kAl2, sizeof(kAl2) - 1);
-    sh.finish();
-    t24u(sh, o);
+    // gnomAD chr-pos-ref-alt -> interbase interval (pos-1, pos-1+len(ref)]
+    LocMsg lm;
+    lm.S = pos[i] - 1u;
+    lm.E = lm.S + r;
+    lm.dE = ndigits(lm.E);
+    lm.dS = ndigits(lm.S);
+    lm.T = nL0 + lm.dE + nL1 + lm.dS + nL2 + AVDB_DIGEST_CHARS + nL3;
+    lm.dig = seq_digest + size_t(c) * AVDB_DIGEST_CHARS;
+    const uint64_t altoff = off[i] + r;
+    const uint64_t TA = uint64_t(kAlPrefix) + a + nA2;
+    const uint32_t nbA = sha_blocks(TA);
+    const uint32_t nbL = sha_blocks(lm.T);  // 2 for every 32-bit position
+    uint64_t H[8], locw[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) H[k] = kIV[k];
+    for (uint32_t b = 0; b < nbL + nbA; ++b) {
+      uint64_t w[16];
+      if (b < nbL) {  // SequenceLocation message
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t p = b * 128 + 8 * j;
+          uint64_t x = 0;
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t q = p + k;
+            x = (x << 8) | (q < lm.T ? loc_byte(lm, q) : pad_byte(q, lm.T, nbL));
+          }
+          w[j] = x;
+        }
+      } else {  // Allele message
+        const uint64_t bb = b - nbL;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const uint64_t p = bb * 128 + 8 * j;
+          if (p >= kAlPrefix && p + 8 <= kAlPrefix + uint64_t(a)) {
+            w[j] = __builtin_bswap64(heap_u64(hp, altoff + (p - kAlPrefix)));
+          } else {
+            uint64_t x = 0;
+            for (int k = 0; k < 8; ++k) {
+              const uint64_t q = p + k;
+              uint8_t by;
+              if (q < nA0) by = uint8_t(kAl0[q]);
+              else if (q < nA0 + AVDB_DIGEST_CHARS) by = word_char(locw, uint32_t(q - nA0));
+              else if (q < kAlPrefix) by = uint8_t(kAl1[q - nA0 - AVDB_DIGEST_CHARS]);
+              else if (q < kAlPrefix + uint64_t(a)) by = heap[altoff + (q - kAlPrefix)];
+              else if (q < TA) by = uint8_t(kAl2[q - kAlPrefix - a]);
+              else by = pad_byte(q, TA, nbA);
+              x = (x << 8) | by;
+            }
+            w[j] = x;
+          }
+        }
+      }
+      sha512_block(H, w);
+      if (b + 1 == nbL) {  // location digest done: its chars feed the Allele blob
+        t24u_words(H, locw);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) H[k] = kIV[k];
+      }
+    }
+    uint64_t cw[4];
+    t24u_words(H, cw);
+    store_digest(o, cw);
   }
 }
 
@@ -252,15 +423,16 @@ extern "C" int avdb_sha512t24u(avdb_ctx* ctx, const uint8_t* data, const uint64_
 
 extern "C" int avdb_vrs_digest_workspace_size(size_t n, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
-  *bytes = 256 + 4 * n;
+  *bytes = 256 + 4 * size_t(kLongBuckets) * kCompactGrid + 4 * n;
   return AVDB_OK;
 }
 
 extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                const uint64_t* allele_off, const uint32_t* ref_len,
-                               const uint32_t* alt_len, const uint8_t* heap, size_t n,
-                               uint32_t max_seq_len, void* workspace, size_t workspace_bytes,
-                               char* digest_out, uint8_t* is_long, void* stream) {
+                               const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                               size_t n, uint32_t max_seq_len, void* workspace,
+                               size_t workspace_bytes, char* digest_out, uint8_t* is_long,
+                               void* stream) {
   if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
   if (n == 0) return AVDB_OK;
   if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap || !digest_out) {
@@ -280,16 +452,22 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   }
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  auto* count = static_cast<unsigned int*>(workspace);
-  auto* list = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + 256);
-  AVDB_HIP_TRY(hipMemsetAsync(count, 0, sizeof(unsigned int), s));
-  const unsigned g1 = stream_grid(n, kBlock * 8, 4096);
-  hipLaunchKernelGGL(k_long_compact, dim3(g1), dim3(kBlock), 0, s, ref_len, alt_len, n,
-                     max_seq_len, is_long, list, count);
-  AVDB_LAUNCH_CHECK("k_long_compact");
-  // persistent grid over the compacted list: 4 workgroups per CU
-  hipLaunchKernelGGL(k_vrs_digest, dim3(1024), dim3(kBlock), 0, s, chrom, pos, allele_off,
-                     ref_len, alt_len, heap, list, count, ctx->d_seq_digest, ctx->tab.n, digest_out);
+  auto* total = static_cast<unsigned int*>(workspace);
+  auto* counts = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + 256);
+  auto* list = counts + size_t(kLongBuckets) * kCompactGrid;
+  hipLaunchKernelGGL(k_long_hist, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
+                     max_seq_len, is_long, counts);
+  AVDB_LAUNCH_CHECK("k_long_hist");
+  hipLaunchKernelGGL(k_long_scan, dim3(1), dim3(1024), 0, s, counts,
+                     uint32_t(kLongBuckets * kCompactGrid), total);
+  AVDB_LAUNCH_CHECK("k_long_scan");
+  hipLaunchKernelGGL(k_long_scatter, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
+                     max_seq_len, counts, list);
+  AVDB_LAUNCH_CHECK("k_long_scatter");
+  // persistent grid over the grouped list
+  hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * 4), dim3(kBlock), 0, s, chrom, pos, allele_off,
+                     ref_len, alt_len, heap, heap_bytes, list, total, ctx->d_seq_digest, ctx->tab.n,
+                     digest_out);
   AVDB_LAUNCH_CHECK("k_vrs_digest");
   return AVDB_OK;
 }

@@ -57,6 +57,54 @@ __device__ __forceinline__ uint32_t classify(uint32_t c, uint32_t s, uint32_t e,
   return st;
 }
 
+// ---- allele heap access ----------------------------------------------------
+// Allele bytes are read as naturally aligned 8-byte words (one global_load_dwordx2
+// per 8 bytes instead of 8 byte loads) and funnel-shifted into place; words
+// straddling either end of the heap allocation are assembled bytewise, so no
+// access ever leaves [heap, heap + heap_bytes).
+struct Heap {
+  uintptr_t lo, hi;
+};
+
+__device__ __forceinline__ Heap make_heap(const uint8_t* p, size_t bytes) {
+  return Heap{reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + bytes};
+}
+
+__device__ __forceinline__ uint64_t heap_word(uintptr_t a, const Heap& h) {  // a 8-aligned
+  if (a >= h.lo && a + 8 <= h.hi) return *reinterpret_cast<const uint64_t*>(a);
+  uint64_t v = 0;
+  for (int k = 0; k < 8; ++k) {
+    const uintptr_t b = a + k;
+    if (b >= h.lo && b < h.hi) v |= uint64_t(*reinterpret_cast<const uint8_t*>(b)) << (8 * k);
+  }
+  return v;
+}
+
+// little-endian 8 bytes starting at heap offset p (bytes past the heap read 0)
+__device__ __forceinline__ uint64_t heap_u64(const Heap& h, uint64_t p) {
+  const uintptr_t addr = h.lo + p;
+  const uintptr_t a = addr & ~uintptr_t(7);
+  const uint32_t sh = uint32_t(addr & 7) * 8;
+  const uint64_t lo = heap_word(a, h);
+  if (!sh) return lo;
+  const uint64_t hi = heap_word(a + 8, h);
+  return (lo >> sh) | (hi << (64 - sh));
+}
+
+__device__ __forceinline__ uint64_t low_bytes_mask(uint32_t k) {  // k in 0..8
+  return k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1);
+}
+
+// byte-exact equality of L bytes at heap offsets p and q
+__device__ __forceinline__ bool heap_equal(const Heap& h, uint64_t p, uint64_t q, uint32_t L) {
+  if (p == q) return true;
+  for (uint32_t k = 0; k < L; k += 8) {
+    const uint64_t m = low_bytes_mask(L - k);
+    if ((heap_u64(h, p + k) ^ heap_u64(h, q + k)) & m) return false;
+  }
+  return true;
+}
+
 // ---- status counters ------------------------------------------------------
 // Only error statuses (1..3) are counted per lane, in 8-bit fields of one u32;
 // the OK count is records - errors, so the common path costs nothing.

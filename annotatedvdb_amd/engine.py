@@ -236,7 +236,8 @@ class Engine:
         lcp = self.empty(n, torch.int32) if want_lcp else None
         N.check("avdb_record_prep", self.lib.avdb_record_prep(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
-            N.ptr(b.alt_len), N.ptr(b.heap), n, N.ptr(end), N.ptr(code), N.ptr(status), N.ptr(lcp),
+            N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, N.ptr(end), N.ptr(code), N.ptr(status),
+            N.ptr(lcp),
             N.ptr(hist), N.ptr(counters), self._stream()))
         return end, code, status, lcp
 
@@ -258,7 +259,7 @@ class Engine:
                 self.empty(ws_bytes, torch.uint8)
         N.check("avdb_pk_dedup", self.lib.avdb_pk_dedup(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
-            N.ptr(b.alt_len), N.ptr(b.heap), N.ptr(b.ext_id), n, 1 if grouped else 0,
+            N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), n, 1 if grouped else 0,
             N.ptr(ws), ws_bytes, N.ptr(keep), N.ptr(counters), self._stream()))
         return keep
 
@@ -278,7 +279,7 @@ class Engine:
             self.empty(int(sz.value), torch.uint8)
         N.check("avdb_vrs_digest", self.lib.avdb_vrs_digest(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
-            N.ptr(b.alt_len), N.ptr(b.heap), n, int(max_seq_len), N.ptr(ws), int(sz.value),
+            N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, int(max_seq_len), N.ptr(ws), int(sz.value),
             N.ptr(dig), N.ptr(is_long), self._stream()))
         return dig, is_long
 

@@ -31,6 +31,9 @@
  *                      allele_off + ref_len (raw, un-normalised VCF bytes)
  *   ref_len    u32[n], alt_len u32[n]
  *   ext_id     u64[n]  external id key (refSNP); 0 = none; equal keys <=> equal ids
+ *   heap_bytes         size of the heap allocation: kernels read allele bytes as
+ *                      8-byte-aligned words and never touch memory outside
+ *                      [heap, heap + heap_bytes)
  *
  * Bin code (u32): level in bits 31..28 (0 = whole chromosome .. 13 = 15,625 bp
  * leaf), 0-based index of the bin at that level in bits 27..0.  The ltree path
@@ -116,7 +119,8 @@ int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* start,
  * hist_l8, counters optional (NULL).  */
 int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                      const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
-                     const uint8_t* heap, size_t n, uint32_t* end_out, uint32_t* bin_code,
+                     const uint8_t* heap, size_t heap_bytes, size_t n, uint32_t* end_out,
+                     uint32_t* bin_code,
                      uint8_t* status, uint32_t* lcp, uint32_t* hist_l8, uint64_t* counters,
                      void* stream);
 
@@ -130,7 +134,8 @@ int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
 int avdb_pk_dedup_workspace_size(size_t n, size_t* bytes);
 int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                   const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
-                  const uint8_t* heap, const uint64_t* ext_id, size_t n, int grouped,
+                  const uint8_t* heap, size_t heap_bytes, const uint64_t* ext_id, size_t n,
+                  int grouped,
                   void* workspace, size_t workspace_bytes, uint8_t* keep, uint64_t* counters,
                   void* stream);
 
@@ -147,7 +152,8 @@ int avdb_sha512t24u(avdb_ctx* ctx, const uint8_t* data, const uint64_t* off, con
 int avdb_vrs_digest_workspace_size(size_t n, size_t* bytes);
 int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                     const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
-                    const uint8_t* heap, size_t n, uint32_t max_seq_len, void* workspace,
+                    const uint8_t* heap, size_t heap_bytes, size_t n, uint32_t max_seq_len,
+                    void* workspace,
                     size_t workspace_bytes, char* digest_out, uint8_t* is_long, void* stream);
 
 /* ---- host-side formatting of kernel outputs -------------------------------
