@@ -148,6 +148,45 @@ def generate_binindexref(chrom_name: str, length: int) -> List[Tuple[int, str, i
     return rows
 
 
+class LeftOpenRange:
+    """``(lo, hi]`` containment with the published control flow of psycopg2's
+    ``Range.__contains__`` (bounds string checked per call) — the object
+    ``NumericRange(lo, hi, '(]')`` the cache test at bin_index.py:70 calls."""
+
+    __slots__ = ("_lower", "_upper", "_bounds")
+
+    def __init__(self, lower, upper, bounds="(]"):
+        self._lower = lower
+        self._upper = upper
+        self._bounds = bounds
+
+    def __contains__(self, x):
+        if self._bounds is None:
+            return False
+        if self._lower is not None:
+            if self._bounds[0] == "[":
+                if x < self._lower:
+                    return False
+            elif x <= self._lower:
+                return False
+        if self._upper is not None:
+            if self._bounds[1] == "]":
+                if x > self._upper:
+                    return False
+            elif x >= self._upper:
+                return False
+        return True
+
+
+def xstr(value, nullStr="", falseAsNull=False):
+    """GenomicsDBData ``xstr`` as used by bin_index.py:64 (str of a non-null value)."""
+    if value is None:
+        return nullStr
+    if falseAsNull and value is False:
+        return nullStr
+    return str(value)
+
+
 class BinTable:
     """Per-(chrom, level) sorted (lo, hi, path) lists; deepest-containing search."""
 
@@ -173,33 +212,36 @@ class BinTable:
             lo, hi, path = lst[k]
             if lo < start <= hi and lo < end <= hi:
                 return {"chromosome": chrm, "global_bin_path": path,
-                        "location": (lo, hi), "bin_level": 1 + 2 * level}
+                        "location": LeftOpenRange(lo, hi), "bin_level": 1 + 2 * level}
         return None
 
 
 class PortBinIndex:
     """Reference-structured port of ``BinIndex`` (bin_index.py:16-75) used as the
-    CPU baseline: one-bin cache served only for L13 bins (:66-71, nlevel>=27),
-    table search on a miss in place of the SQL round trip (:43-56)."""
+    CPU baseline: one-bin cache served only for L13 bins (:66-71, nlevel>=27,
+    range containment through a ``__contains__`` call like NumericRange), table
+    search on a miss in place of the SQL round trip (:43-56)."""
 
     def __init__(self, table: BinTable):
         self._table = table
-        self._current = None
+        self._currentBin = {}
+
+    def _update_current_bin_index(self, chrm, start, end):
+        self._currentBin = self._table.find(chrm, start, end)
 
     def find_bin_index(self, chrm, start, end=None):
         if end is None:
             end = start
-        chrm = str(chrm)
         if "chr" not in chrm:
-            chrm = "chr" + chrm
-        cur = self._current
-        if cur:
-            if cur["bin_level"] >= 27:
-                lo, hi = cur["location"]
-                if cur["chromosome"] == chrm and lo < start <= hi and lo < end <= hi:
-                    return cur["global_bin_path"]
-        self._current = self._table.find(chrm, start, end)
-        return self._current["global_bin_path"]  # None -> TypeError, as :75
+            chrm = "chr" + xstr(chrm)
+        if bool(self._currentBin):
+            if self._currentBin["bin_level"] >= 27:
+                brange = self._currentBin["location"]
+                if self._currentBin["chromosome"] == chrm \
+                        and start in brange and end in brange:
+                    return self._currentBin["global_bin_path"]
+        self._update_current_bin_index(chrm, start, end)
+        return self._currentBin["global_bin_path"]  # None -> TypeError, as :75
 
 
 # ---------------------------------------------------------------------------
