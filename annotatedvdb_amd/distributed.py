@@ -1,0 +1,87 @@
+"""Multi-GPU orchestration: one process per GPU, genome pieces sharded by
+length-balanced LPT (``shard.plan``), no record exchange.  The single
+collective is an all-gather of every rank's L8 histogram and counters
+ — RCCL (``nccl`` backend) over xGMI on MI355X nodes, ``gloo``
+for the CPU tests.
+
+The reference's only parallelism is one OS process per chromosome file
+(``Load/bin/load_vcf_file.py:307-313``) with no communication at all; the
+all-gather replaces the per-file log summaries with node-level statistics.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import shard
+
+
+@dataclass
+class RankInfo:
+    rank: int
+    world: int
+    local: int
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+
+def rank_info() -> RankInfo:
+    return RankInfo(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+                    int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: Optional[str] = None) -> RankInfo:
+    """Initialise the process group from torchrun's environment (no-op at N=1)."""
+    ri = rank_info()
+    if ri.distributed and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(ri.local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", ri.local))
+        else:
+            dist.init_process_group(backend)
+    return ri
+
+
+def my_pieces(ri: RankInfo, lengths=None) -> List[shard.Piece]:
+    return shard.plan(ri.world, lengths)[ri.rank]
+
+
+def allgather_stats(hist: torch.Tensor, counters: torch.Tensor, ri: RankInfo
+                    ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All-gather every rank's L8 histogram and counters; returns the node
+    totals (sum over ranks).  One collective per tensor, issued back to back."""
+    if not ri.distributed:
+        return hist.clone(), counters.clone()
+    hs = [torch.empty_like(hist) for _ in range(ri.world)]
+    cs = [torch.empty_like(counters) for _ in range(ri.world)]
+    dist.all_gather(hs, hist)
+    dist.all_gather(cs, counters)
+    return torch.stack(hs).sum(0), torch.stack(cs).sum(0)
+
+
+def max_over_ranks(value: float, ri: RankInfo, device=None) -> float:
+    if not ri.distributed:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(ri: RankInfo):
+    if ri.distributed:
+        dist.barrier()
+
+
+def finalize(ri: RankInfo):
+    if ri.distributed and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()

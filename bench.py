@@ -30,7 +30,6 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "variants binned+keyed/sec (node) at 1/2/4/8 MI355X; % of HBM roofline"
@@ -123,38 +122,37 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
 # ---------------------------------------------------------------------------
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from annotatedvdb_amd import distributed as D
+    ri = D.rank_info()
     # CPU baseline first, before this process touches the GPU (its worker
     # processes are forked and must not inherit an initialised HIP runtime)
-    want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and world == 1 and a.workload in ("c2", "c3"))
-    cpu = cpu_baseline(a.workload, a.cpu_seconds) if (rank == 0 and want_cpu) else None
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and ri.world == 1
+                                          and a.workload in ("c2", "c3"))
+    cpu = cpu_baseline(a.workload, a.cpu_seconds) if (ri.rank == 0 and want_cpu) else None
+    ri = D.init("nccl")
+    dev = torch.device("cuda", ri.local)
     torch.cuda.set_device(dev)
 
-    from annotatedvdb_amd import shard, synth
+    from annotatedvdb_amd import synth
     from annotatedvdb_amd.engine import Engine
 
     W = WORKLOADS[a.workload]
     n = a.n or W["n"]
-    my_pieces = shard.plan(world)[rank]
-    eng = Engine(local)
+    pieces = D.my_pieces(ri)
+    eng = Engine(ri.local)
     if a.workload == "c5":
         digs = ["%032d" % i for i in range(25)]  # synthetic refget ids (no SeqRepo offline)
         eng.set_sequence_digests(digs)
 
     # ---- resident synthetic batch (untimed) ----
+    seed = 1000 * ri.rank
     if a.workload == "c2":
-        chrom, start = synth.point_snvs(n, seed=2 + 1000 * rank, device=dev, pieces=my_pieces)
+        chrom, start = synth.point_snvs(n, seed=2 + seed, device=dev, pieces=pieces)
         end = None
     elif a.workload == "c3":
-        chrom, start, end = synth.spans(n, seed=3 + 1000 * rank, device=dev, pieces=my_pieces)
+        chrom, start, end = synth.spans(n, seed=3 + seed, device=dev, pieces=pieces)
     else:
-        batch = synth.alleles(n, seed=5 + 1000 * rank, device=dev, pieces=my_pieces)
+        batch = synth.alleles(n, seed=5 + seed, device=dev, pieces=pieces)
         heap_bytes = int(batch.heap.numel())
     hist = eng.new_histogram()
     ctr = eng.new_counters()
@@ -162,63 +160,53 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
-    evs = []
+    evs = {}
+
+    def timed(name, record, fn):
+        if not record:
+            fn()
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        evs.setdefault(name, []).append((e0, e1))
 
     def step(record: bool):
         if a.workload in ("c2", "c3"):
-            if record:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-            eng.bin_assign(chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code)
-            if record:
-                e1.record(stream)
-                evs.append((e0, e1))
+            timed("bin_assign", record, lambda: eng.bin_assign(
+                chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
         else:
-            if record:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-            eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr)
-            if record:
-                e1.record(stream)
-                evs.append((e0, e1))
-            eng.pk_dedup(batch, grouped=True, counters=ctr)
-            eng.vrs_digest(batch, 50)
+            timed("record_prep", record, lambda: eng.record_prep(batch, want_lcp=False, hist=hist,
+                                                                 counters=ctr))
+            timed("pk_dedup", record, lambda: eng.pk_dedup(batch, grouped=True, counters=ctr))
+            timed("vrs_digest", record, lambda: eng.vrs_digest(batch, 50))
 
     for _ in range(a.warmup):
         step(False)
     hist.zero_()
     ctr.zero_()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier(ri)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(True)
     # job-level exchange: per-rank L8 histograms + counters (RCCL all-gather)
-    if world > 1:
-        gathered_h = [torch.empty_like(hist) for _ in range(world)]
-        gathered_c = [torch.empty_like(ctr) for _ in range(world)]
-        dist.all_gather(gathered_h, hist)
-        dist.all_gather(gathered_c, ctr)
+    node_hist, node_ctr = D.allgather_stats(hist, ctr, ri)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier(ri)
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        node_ctr = torch.stack(gathered_c).sum(0)
-    else:
-        node_ctr = ctr
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
-    total_records = n * world * a.steps
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, ri, device=dev)
+    stage_ms = {k: float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])) for k, v in evs.items()}
+    kname = "bin_assign" if a.workload in ("c2", "c3") else "record_prep"
+    kern_ms = stage_ms[kname]
+    total_records = n * ri.world * a.steps
     value = total_records / elapsed
 
     if a.workload == "c5":
-        # K2 algorithmic bytes: in chrom1+pos4+off8+rlen4+alen4 + heap bytes read; out end4+code4
+        # K2 algorithmic bytes per record: in chrom 1 + pos 4 + allele_off 8 + ref_len 4 +
+        # alt_len 4 (+ the heap bytes it reads, bounded by the heap); out end 4 + code 4
         bytes_per_launch = n * (1 + 4 + 8 + 4 + 4 + 4 + 4) + heap_bytes
     else:
         bytes_per_launch = n * W["bytes_per"]
@@ -235,7 +223,7 @@ def main():
         "metric": METRIC,
         "value": value,
         "unit": "variants/s",
-        "n_gpus": world,
+        "n_gpus": ri.world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": elapsed * 1e3 / a.steps,
@@ -244,20 +232,19 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (seeded GRCh38-shaped records generated on device)",
-        "config": {"workload": W["desc"], "records_per_gpu": n, "records_total": n * world,
-                   "parallelism": f"dp{world} (length-balanced 64 Mb genome pieces per rank)",
-                   "records_checked": int(node_ctr[20].item()) // max(1, a.steps)},
+        "config": {"workload": W["desc"], "records_per_gpu": n, "records_total": n * ri.world,
+                   "parallelism": f"dp{ri.world} (length-balanced 64 Mb genome pieces per rank)",
+                   "records_checked": int(node_ctr[20].item()) // max(1, a.steps),
+                   "stage_ms": stage_ms},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": W["kernel"], "kernel_ms": kern_ms,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "cpu_baseline": cpu,
     }
-    if rank == 0:
+    if ri.rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    D.finalize(ri)
 
 
 if __name__ == "__main__":
