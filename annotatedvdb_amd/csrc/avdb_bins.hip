@@ -69,16 +69,30 @@ __device__ __forceinline__ void st_(T v, T* p) {
 
 constexpr int kK1Block = 512;  // 8 waves: one LDS histogram per 8 waves
 
-template <bool HAS_END, bool HIST, int UNROLL, int FLAGS>
+// chrom codes of one lane-group: V u32 words (4 codes each)
+template <int V> struct ChromVec;
+template <> struct ChromVec<1> { typedef uint32_t T; };
+template <> struct ChromVec<2> { typedef uint32_t T __attribute__((ext_vector_type(2))); };
+template <> struct ChromVec<4> { typedef u32x4 T; };
+
+template <int V>
+__device__ __forceinline__ uint32_t vec_word(const typename ChromVec<V>::T& x, int v) {
+  if constexpr (V == 1) return x;
+  else return x[v];
+}
+
+// V: u32x4 start vectors per lane-group (4V records per lane per step)
+template <bool HAS_END, bool HIST, int V, int UNROLL, int FLAGS>
 __global__ __launch_bounds__(kK1Block) void k_bin_assign4(
-    const uint32_t* __restrict__ chrom4, const u32x4* __restrict__ start4,
+    const typename ChromVec<V>::T* __restrict__ chromv, const u32x4* __restrict__ start4,
     const u32x4* __restrict__ end4, size_t ngroups, u32x4* __restrict__ code4,
-    uint32_t* __restrict__ status4, ChromTable tab, uint32_t* __restrict__ g_hist,
+    typename ChromVec<V>::T* __restrict__ statusv, ChromTable tab, uint32_t* __restrict__ g_hist,
     unsigned long long* __restrict__ g_ctr, int lds_hist,
     // scalar tail [tail_begin, n): block 0, wave 0
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ start,
     const uint32_t* __restrict__ end, size_t tail_begin, size_t n,
     uint32_t* __restrict__ code, uint8_t* __restrict__ status) {
+  typedef typename ChromVec<V>::T CT;
   extern __shared__ uint32_t s_hist[];
   __shared__ uint32_t s_len[AVDB_MAX_CHROM];
   __shared__ uint32_t s_l8off[AVDB_MAX_CHROM];
@@ -89,6 +103,7 @@ __global__ __launch_bounds__(kK1Block) void k_bin_assign4(
   const bool ctrs = g_ctr != nullptr;
   const int n_chrom = tab.n;
   const uint32_t bdim = blockDim.x;
+  constexpr int R = 4 * V;  // records per lane-group
 
   // FLAGS bit2: grid-stride sweep; otherwise each workgroup owns one
   // contiguous chunk (a sorted batch then touches a narrow histogram slice)
@@ -111,50 +126,63 @@ __global__ __launch_bounds__(kK1Block) void k_bin_assign4(
   // wave-uniform run of histogram keys (sorted batches): one LDS atomic per run
   uint32_t run_key = 0xFFFFFFFFu, run_cnt = 0;
   for (size_t base = g0; base < g1; base += step) {
-    uint32_t c4[UNROLL];
-    u32x4 s4[UNROLL], e4[UNROLL];
+    CT c4[UNROLL];
+    u32x4 s4[UNROLL][V], e4[UNROLL][V];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const size_t j = base + size_t(u) * bdim + threadIdx.x;
       if (j < g1) {
-        c4[u] = ld<FLAGS>(&chrom4[j]);
-        s4[u] = ld<FLAGS>(&start4[j]);
-        if (HAS_END) e4[u] = ld<FLAGS>(&end4[j]);
+        c4[u] = ld<FLAGS>(&chromv[j]);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          s4[u][v] = ld<FLAGS>(&start4[size_t(V) * j + v]);
+          if (HAS_END) e4[u][v] = ld<FLAGS>(&end4[size_t(V) * j + v]);
+        }
       }
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const size_t j = base + size_t(u) * bdim + threadIdx.x;
       const bool live = j < g1;
-      const uint32_t sv[4] = {s4[u].x, s4[u].y, s4[u].z, s4[u].w};
-      uint32_t ev[4] = {sv[0], sv[1], sv[2], sv[3]};
-      if (HAS_END) { ev[0] = e4[u].x; ev[1] = e4[u].y; ev[2] = e4[u].z; ev[3] = e4[u].w; }
-      uint32_t cv[4], st = 0, key[4];
+      uint32_t cv[R], key[R], stw[V];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t c = (c4[u] >> (8 * k)) & 0xFFu;
-        const uint32_t s_k = classify(c, sv[k], ev[k], n_chrom, s_len, &cv[k]);
-        st |= s_k << (8 * k);
-        key[k] = live ? l8_key(c, sv[k], cv[k], s_l8off) : 0xFFFFFFFFu;
+      for (int v = 0; v < V; ++v) {
+        const uint32_t cw = vec_word<V>(c4[u], v);
+        uint32_t st = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t c = (cw >> (8 * k)) & 0xFFu;
+          const uint32_t sv = s4[u][v][k];
+          const uint32_t ev = HAS_END ? e4[u][v][k] : sv;
+          const uint32_t s_k = classify(c, sv, ev, n_chrom, s_len, &cv[4 * v + k]);
+          st |= s_k << (8 * k);
+          key[4 * v + k] = live ? l8_key(c, sv, cv[4 * v + k], s_l8off) : 0xFFFFFFFFu;
+        }
+        stw[v] = st;
       }
       if (ctrs && live) {
-        nrec += 4;
-        if (st) {
+        nrec += R;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t s_k = (st >> (8 * k)) & 0xFFu;
-            err += s_k ? (1u << (8 * (s_k - 1))) : 0u;
+        for (int v = 0; v < V; ++v) {
+          if (stw[v]) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t s_k = (stw[v] >> (8 * k)) & 0xFFu;
+              err += s_k ? (1u << (8 * (s_k - 1))) : 0u;
+            }
           }
         }
       }
       if (HIST) {
-        // lane key: the 4 records' common key, or MIXED; dead lanes match anything
-        const bool same = key[0] == key[1] && key[1] == key[2] && key[2] == key[3];
+        // lane key: the group's common key, or MIXED; dead lanes match anything
+        bool same = true;
+#pragma unroll
+        for (int k = 1; k < R; ++k) same = same && key[k] == key[0];
         const uint32_t lk = same ? key[0] : 0xFFFFFFFEu;
         const uint32_t first = __builtin_amdgcn_readfirstlane(lk);
         const uint64_t ok = __ballot(!live || lk == first);
         if (ok == ~0ull && first < 0xFFFFFFFEu) {
-          const uint32_t cnt = 4u * uint32_t(__popcll(__ballot(live)));
+          const uint32_t cnt = uint32_t(R) * uint32_t(__popcll(__ballot(live)));
           if (first == run_key) {
             run_cnt += cnt;
           } else {
@@ -164,21 +192,32 @@ __global__ __launch_bounds__(kK1Block) void k_bin_assign4(
           }
         } else if (!(ok == ~0ull && first == 0xFFFFFFFFu)) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) wave_hist_add(key[k], hist);
+          for (int k = 0; k < R; ++k) wave_hist_add(key[k], hist);
         }
       }
       if (live) {
-        st_<FLAGS>(u32x4{cv[0], cv[1], cv[2], cv[3]}, &code4[j]);
-        if (status4) st_<FLAGS>(st, &status4[j]);
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+          st_<FLAGS>(u32x4{cv[4 * v], cv[4 * v + 1], cv[4 * v + 2], cv[4 * v + 3]},
+                     &code4[size_t(V) * j + v]);
+        if (statusv) {
+          CT sw;
+          if constexpr (V == 1) sw = stw[0];
+          else {
+#pragma unroll
+            for (int v = 0; v < V; ++v) sw[v] = stw[v];
+          }
+          st_<FLAGS>(sw, &statusv[j]);
+        }
       }
     }
-    if (ctrs && ++since_flush == 255 / (UNROLL * 4)) {  // 8-bit error fields never wrap
+    if (ctrs && ++since_flush == 255 / (UNROLL * R)) {  // 8-bit error fields never wrap
       flush_errors(err, s_ctr);
       since_flush = 0;
     }
   }
   if (HIST && run_cnt && __lane_id() == 0) atomicAdd(&hist[run_key], run_cnt);
-  // scalar tail (< 4 records)
+  // scalar tail (< 4V records)
   if (blockIdx.x == 0 && threadIdx.x < kWave) {
     const size_t i = tail_begin + threadIdx.x;
     uint32_t key = 0xFFFFFFFFu;
@@ -350,43 +389,43 @@ extern "C" int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   const int lds_hist = hist && ctx->tab.n_l8 <= uint32_t(kMaxLdsHistBins);
   const size_t shm = lds_hist ? size_t(ctx->tab.n_l8) * 4 : 0;
   auto* ctr = reinterpret_cast<unsigned long long*>(counters);
-  const bool vec = aligned(chrom, 4) && aligned(start, 16) && (!end || aligned(end, 16)) &&
-                   aligned(bin_code, 16) && (!status || aligned(status, 4)) && n >= 4;
+  // K1 variants (records per lane-group 4V, groups in flight U, memory flags F);
+  // the default was chosen by on-device A/B (tools/k1_geom.py)
+  struct K1Var { int V, U, F; };
+  static const K1Var kVars[] = {{1, 2, 6}, {2, 1, 6}, {2, 2, 6}, {4, 1, 6}, {1, 2, 2}, {1, 4, 6}};
+  const K1Var kv = kVars[(ctx->k1_variant >= 0 && ctx->k1_variant < 6) ? ctx->k1_variant : 0];
+  const int R = 4 * kv.V;
+  const bool vec = aligned(chrom, size_t(R)) && aligned(start, 16) && (!end || aligned(end, 16)) &&
+                   aligned(bin_code, 16) && (!status || aligned(status, size_t(R))) && n >= size_t(R);
   if (vec) {
-    const size_t ngroups = n / 4;
-    // One resident wave of workgroups (n_cu x blocks_per_cu), each owning a
-    // contiguous chunk: no partial second round, and the per-workgroup LDS
-    // histogram zero/flush is amortised over the whole chunk.
+    const size_t ngroups = n / R;
+    // One resident wave of workgroups (n_cu x blocks_per_cu); each step of a
+    // workgroup covers bdim*U*R consecutive records.
     const unsigned bdim = unsigned(ctx->k1_block);
     const unsigned grid =
-        stream_grid(ngroups, bdim * ctx->k1_unroll, unsigned(ctx->n_cu * ctx->k1_blocks_per_cu));
-    const size_t tail = ngroups * 4;
-#define K1V(HE, HI, U, F)                                                                    \
-  hipLaunchKernelGGL((k_bin_assign4<HE, HI, U, F>), dim3(grid), dim3(bdim), shm, s,         \
-                     reinterpret_cast<const uint32_t*>(chrom),                               \
+        stream_grid(ngroups, bdim * kv.U, unsigned(ctx->n_cu * ctx->k1_blocks_per_cu));
+    const size_t tail = ngroups * R;
+#define K1V(HE, HI, V_, U_, F_)                                                                 \
+  hipLaunchKernelGGL((k_bin_assign4<HE, HI, V_, U_, F_>), dim3(grid), dim3(bdim), shm, s,       \
+                     reinterpret_cast<const typename ChromVec<V_>::T*>(chrom),                   \
                      reinterpret_cast<const u32x4*>(start), reinterpret_cast<const u32x4*>(end), \
-                     ngroups, reinterpret_cast<u32x4*>(bin_code),                            \
-                     reinterpret_cast<uint32_t*>(status), ctx->tab, hist_l8, ctr, lds_hist,  \
-                     chrom, start, end, tail, n, bin_code, status)
-#define K1F(HE, HI, U)                                       \
-  do {                                                       \
-    switch (ctx->k1_flags) {                                 \
-      case 1: K1V(HE, HI, U, 1); break;                      \
-      case 2: K1V(HE, HI, U, 2); break;                      \
-      case 3: K1V(HE, HI, U, 3); break;                      \
-      case 6: K1V(HE, HI, U, 6); break;                      \
-      default: K1V(HE, HI, U, 0); break;                     \
-    }                                                        \
+                     ngroups, reinterpret_cast<u32x4*>(bin_code),                               \
+                     reinterpret_cast<typename ChromVec<V_>::T*>(status), ctx->tab, hist_l8, ctr, \
+                     lds_hist, chrom, start, end, tail, n, bin_code, status)
+#define K1ALL(HE, HI)                                                        \
+  do {                                                                       \
+    switch (ctx->k1_variant) {                                               \
+      case 1: K1V(HE, HI, 2, 1, 6); break;                                   \
+      case 2: K1V(HE, HI, 2, 2, 6); break;                                   \
+      case 3: K1V(HE, HI, 4, 1, 6); break;                                   \
+      case 4: K1V(HE, HI, 1, 2, 2); break;                                   \
+      case 5: K1V(HE, HI, 1, 4, 6); break;                                   \
+      default: K1V(HE, HI, 1, 2, 6); break;                                  \
+    }                                                                        \
   } while (0)
-#define K1U(HE, HI)                                          \
-  do {                                                       \
-    if (ctx->k1_unroll == 2) K1F(HE, HI, 2);                 \
-    else K1F(HE, HI, 4);                                     \
-  } while (0)
-    if (end) { if (hist) K1U(true, true); else K1U(true, false); }
-    else { if (hist) K1U(false, true); else K1U(false, false); }
-#undef K1U
-#undef K1F
+    if (end) { if (hist) K1ALL(true, true); else K1ALL(true, false); }
+    else { if (hist) K1ALL(false, true); else K1ALL(false, false); }
+#undef K1ALL
 #undef K1V
     AVDB_LAUNCH_CHECK("k_bin_assign4");
   } else {

@@ -76,24 +76,19 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
   // loads + plain stores, grid-stride sweep (each workgroup step covers 4096
   // consecutive records, so a sorted batch still hits ~1 histogram bin per step).
   c->k1_blocks_per_cu = 4;
-  c->k1_unroll = 2;
   if (const char* s = getenv("AVDB_K1_BLOCKS_PER_CU")) {
     const int v = atoi(s);
     if (v >= 1 && v <= 64) c->k1_blocks_per_cu = v;
   }
-  if (const char* s = getenv("AVDB_K1_UNROLL")) {
+  c->k1_variant = 0;
+  if (const char* s = getenv("AVDB_K1_VARIANT")) {
     const int v = atoi(s);
-    if (v == 2 || v == 4) c->k1_unroll = v;
+    if (v >= 0 && v <= 5) c->k1_variant = v;
   }
   c->k1_block = 512;
   if (const char* s = getenv("AVDB_K1_BLOCK")) {
     const int v = atoi(s);
     if (v == 256 || v == 512) c->k1_block = v;
-  }
-  c->k1_flags = 6;
-  if (const char* s = getenv("AVDB_K1_FLAGS")) {
-    const int v = atoi(s);
-    if ((v >= 0 && v <= 3) || v == 6) c->k1_flags = v;
   }
   *out = c;
   return AVDB_OK;

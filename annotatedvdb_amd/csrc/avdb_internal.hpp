@@ -167,9 +167,8 @@ struct avdb_ctx {
   int device;
   int n_cu;            // compute units on the device (256 on MI355X)
   int k1_blocks_per_cu;  // K1 grid = n_cu * k1_blocks_per_cu workgroups (env AVDB_K1_BLOCKS_PER_CU)
-  int k1_unroll;         // K1 groups in flight per lane: 2 or 4 (env AVDB_K1_UNROLL)
+  int k1_variant;        // K1 lane-group shape / memory policy (env AVDB_K1_VARIANT, bins.hip)
   int k1_block;          // K1 workgroup size: 256 or 512 (env AVDB_K1_BLOCK)
-  int k1_flags;          // K1 memory policy bits (env AVDB_K1_FLAGS): 1 plain loads, 2 plain stores
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
   bool has_digests;

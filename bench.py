@@ -41,6 +41,9 @@ WORKLOADS = {
     "c3": dict(n=100_000_000, desc="C3: synthetic indels/SVs, spans <= 1 Mb, smallest enclosing bin "
                                    "(BASELINE configs[2]); K1 bin_assign + L8 histogram",
                bytes_per=13, kernel="k_bin_assign4"),
+    "c4": dict(n=125_000_000, desc="C4: dbSNP-scale mix (90% SNV / 8% indel <= 50 bp / 2% <= 1 Mb), "
+                                   "1e9 over 8 GPUs = 1.25e8 per GPU (BASELINE configs[3]); K1 + L8 histogram",
+               bytes_per=13, kernel="k_bin_assign4"),
     "c5": dict(n=25_000_000, desc="C5: ADSP-style alleles, end inference + bin + grouped PK dedup + "
                                   "long-allele key digests (BASELINE configs[4])",
                bytes_per=None, kernel="k_record_prep"),
@@ -149,8 +152,9 @@ def main():
     if a.workload == "c2":
         chrom, start = synth.point_snvs(n, seed=2 + seed, device=dev, pieces=pieces)
         end = None
-    elif a.workload == "c3":
-        chrom, start, end = synth.spans(n, seed=3 + seed, device=dev, pieces=pieces)
+    elif a.workload in ("c3", "c4"):
+        chrom, start, end = synth.spans(n, seed=(3 if a.workload == "c3" else 4) + seed, device=dev,
+                                        pieces=pieces, mix=a.workload)
     else:
         batch = synth.alleles(n, seed=5 + seed, device=dev, pieces=pieces)
         heap_bytes = int(batch.heap.numel())
@@ -173,7 +177,7 @@ def main():
         evs.setdefault(name, []).append((e0, e1))
 
     def step(record: bool):
-        if a.workload in ("c2", "c3"):
+        if a.workload in ("c2", "c3", "c4"):
             timed("bin_assign", record, lambda: eng.bin_assign(
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
         else:
@@ -199,7 +203,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, ri, device=dev)
     stage_ms = {k: float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])) for k, v in evs.items()}
-    kname = "bin_assign" if a.workload in ("c2", "c3") else "record_prep"
+    kname = "bin_assign" if a.workload in ("c2", "c3", "c4") else "record_prep"
     kern_ms = stage_ms[kname]
     total_records = n * ri.world * a.steps
     value = total_records / elapsed

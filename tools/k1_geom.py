@@ -6,9 +6,9 @@ import numpy as np, torch
 from annotatedvdb_amd import synth
 from annotatedvdb_amd.engine import Engine
 
-VARIANTS = [dict(AVDB_K1_BLOCK=b, AVDB_K1_BLOCKS_PER_CU=p, AVDB_K1_UNROLL=u, AVDB_K1_FLAGS=f)
-            for (b, p, u, f) in [(512, 4, 2, 2), (512, 4, 2, 6), (256, 8, 2, 2), (256, 8, 2, 6),
-                                 (512, 4, 2, 0), (512, 4, 4, 2), (512, 2, 2, 2), (256, 6, 2, 2)]]
+VARIANTS = [dict(AVDB_K1_VARIANT=v, AVDB_K1_BLOCK=b, AVDB_K1_BLOCKS_PER_CU=p)
+            for (v, b, p) in [(0, 512, 4), (1, 512, 4), (1, 512, 3), (2, 512, 3), (3, 512, 3),
+                              (3, 512, 2), (5, 512, 4), (0, 256, 8), (4, 512, 4)]]
 
 def main():
     n = int(os.environ.get("N", 100_000_000)); reps = int(os.environ.get("REPS", 20))
