@@ -321,12 +321,16 @@ __device__ __forceinline__ uint8_t loc_byte(const LocMsg& m, uint32_t p) {
   return uint8_t(kLoc3[p]);
 }
 
-__global__ __launch_bounds__(kBlock) void k_vrs_digest(
+// 3 waves per SIMD (<= 168 VGPRs): the SHA-512 chains are latency-bound, so
+// occupancy is what the VALU pipe needs (rocprof: 1 VALU issue per ~12 cycles
+// per wave at 2 waves/SIMD)
+__global__ __launch_bounds__(kBlock, 3) void k_vrs_digest(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
     const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
     const uint32_t* __restrict__ list, const unsigned int* __restrict__ count,
     const char* __restrict__ seq_digest, int n_chrom, char* __restrict__ out) {
+  __shared__ uint64_t s_w[16 * kBlock];
   const Heap hp = make_heap(heap, heap_bytes);
   const unsigned int cnt = *count;
   const size_t stride = size_t(gridDim.x) * blockDim.x;
@@ -354,28 +358,24 @@ __global__ __launch_bounds__(kBlock) void k_vrs_digest(
     uint64_t H[8], locw[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 8; ++k) H[k] = kIV[k];
+    uint64_t* slot = &s_w[threadIdx.x];  // this lane's 16 message words, [word][lane]
     for (uint32_t b = 0; b < nbL + nbA; ++b) {
-      uint64_t w[16];
-      if (b < nbL) {  // SequenceLocation message
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
+      // build the block's 16 words (not unrolled: keeps the register budget for
+      // the compression), then reload them with static indices
+#pragma unroll 1
+      for (int j = 0; j < 16; ++j) {
+        uint64_t x = 0;
+        if (b < nbL) {  // SequenceLocation message
           const uint32_t p = b * 128 + 8 * j;
-          uint64_t x = 0;
           for (int k = 0; k < 8; ++k) {
             const uint32_t q = p + k;
             x = (x << 8) | (q < lm.T ? loc_byte(lm, q) : pad_byte(q, lm.T, nbL));
           }
-          w[j] = x;
-        }
-      } else {  // Allele message
-        const uint64_t bb = b - nbL;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const uint64_t p = bb * 128 + 8 * j;
+        } else {  // Allele message
+          const uint64_t p = uint64_t(b - nbL) * 128 + 8 * j;
           if (p >= kAlPrefix && p + 8 <= kAlPrefix + uint64_t(a)) {
-            w[j] = __builtin_bswap64(heap_u64(hp, altoff + (p - kAlPrefix)));
+            x = __builtin_bswap64(heap_u64(hp, altoff + (p - kAlPrefix)));
           } else {
-            uint64_t x = 0;
             for (int k = 0; k < 8; ++k) {
               const uint64_t q = p + k;
               uint8_t by;
@@ -387,10 +387,13 @@ __global__ __launch_bounds__(kBlock) void k_vrs_digest(
               else by = pad_byte(q, TA, nbA);
               x = (x << 8) | by;
             }
-            w[j] = x;
           }
         }
+        slot[j * kBlock] = x;
       }
+      uint64_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = slot[j * kBlock];
       sha512_block(H, w);
       if (b + 1 == nbL) {  // location digest done: its chars feed the Allele blob
         t24u_words(H, locw);
@@ -465,7 +468,7 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
                      max_seq_len, counts, list);
   AVDB_LAUNCH_CHECK("k_long_scatter");
   // persistent grid over the grouped list
-  hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * 4), dim3(kBlock), 0, s, chrom, pos, allele_off,
+  hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * 3), dim3(kBlock), 0, s, chrom, pos, allele_off,
                      ref_len, alt_len, heap, heap_bytes, list, total, ctx->d_seq_digest, ctx->tab.n,
                      digest_out);
   AVDB_LAUNCH_CHECK("k_vrs_digest");
