@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = [
     "avdb_pk_dedup_workspace_size", "avdb_pk_dedup",
     "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest",
     "avdb_format_bin_path", "avdb_format_bin_paths",
+    "avdb_vcf_workspace_size", "avdb_vcf_count_lines", "avdb_vcf_parse_lines", "avdb_vcf_emit",
 ]
 
 
@@ -94,6 +95,10 @@ def _sig(lib):
     f.avdb_vrs_digest.argtypes = [P, P, P, P, P, P, P, SZ, SZ, U32, P, SZ, P, P, P]
     f.avdb_format_bin_path.argtypes = [P, U8, U32, ctypes.c_char_p, SZ]
     f.avdb_format_bin_paths.argtypes = [P, P, P, SZ, P, SZ, P]
+    f.avdb_vcf_workspace_size.argtypes = [SZ, SZ, ctypes.POINTER(SZ)]
+    f.avdb_vcf_count_lines.argtypes = [P, P, SZ, P, SZ, P, P]
+    f.avdb_vcf_parse_lines.argtypes = [P, P, SZ, SZ, P, SZ, P, P, P, P]
+    f.avdb_vcf_emit.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, P, P, P, P, P, P]
     for name in EXPORTED_SYMBOLS:
         if name not in ("avdb_last_error",):
             getattr(f, name).restype = I32

@@ -1,0 +1,491 @@
+// K0 — VCF text -> per-alt record SoA on the GPU (gfx950).
+//
+// Text half of VcfEntryParser (Util/lib/python/parsers/vcf_parser.py:76-169) and the
+// per-alt loop head of VCFVariantLoader.__parse_alt_alleles
+// (vcf_variant_loader.py:273-280), for a batch of lines resident in HBM:
+//   k_vcf_count    per-workgroup count of '\n' bytes (8 bytes per step, SWAR zero-byte
+//                  detection), block-contiguous chunks
+//   k_vcf_starts   ordered line table: per-thread sub-chunk counts -> workgroup
+//                  exclusive scan in LDS -> each thread writes its lines' starts
+//   k_vcf_parse    one lane per line: rstrip, tab fields, CHROM -> contig code,
+//                  POS, ID / INFO RS -> refSNP key, ALT count, heap bytes
+//   (hipCUB exclusive scans: record and heap offsets per line)
+//   k_vcf_emit     one lane per line: one record per ALT != '.', REF+ALT copied to
+//                  the allele heap
+// Only canonical text is resolved here; the rest is flagged (AVDB_VCF_*_HOST) for
+// the host to resolve with Python's own coercion rules.
+#include "avdb_internal.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+namespace avdb {
+
+constexpr int kVcfGrid = 1024;
+
+__device__ __forceinline__ uint64_t zero_bytes_mask(uint64_t y) {  // bit 7 of each zero byte
+  const uint64_t lo7 = 0x7F7F7F7F7F7F7F7Full;
+  return ~(((y & lo7) + lo7) | y | lo7);
+}
+
+__device__ __forceinline__ uint32_t count_byte(uint64_t x, uint64_t pattern) {
+  return uint32_t(__popcll(zero_bytes_mask(x ^ pattern)));
+}
+
+constexpr uint64_t kNL = 0x0A0A0A0A0A0A0A0Aull;
+
+// 8 bytes at aligned address a (bytes outside [lo,hi) read as 0x00)
+__device__ __forceinline__ uint64_t text_word(uintptr_t a, const Heap& h) { return heap_word(a, h); }
+
+// byte range [b0, b1) of the text handled by workgroup `blk` of `nblk` (8-aligned cuts)
+__device__ __forceinline__ void block_range(size_t text_bytes, int blk, int nblk, size_t* b0,
+                                            size_t* b1) {
+  size_t per = (text_bytes + nblk - 1) / nblk;
+  per = (per + 7) & ~size_t(7);
+  *b0 = size_t(blk) * per;
+  *b1 = *b0 + per < text_bytes ? *b0 + per : text_bytes;
+  if (*b0 > text_bytes) *b0 = text_bytes;
+}
+
+// newline count of [b0,b1) using aligned words; masks bytes outside the range
+__device__ __forceinline__ uint32_t count_nl(const Heap& h, size_t b0, size_t b1) {
+  uint32_t c = 0;
+  const uintptr_t base = h.lo;
+  uintptr_t a = (base + b0) & ~uintptr_t(7);
+  const uintptr_t end = base + b1;
+  for (; a < end; a += 8) {
+    uint64_t m = zero_bytes_mask(text_word(a, h) ^ kNL);
+    // keep only bytes inside [base+b0, end)
+    const uintptr_t lo = base + b0;
+    if (a < lo) m &= ~0ull << (8 * (lo - a));
+    if (a + 8 > end) m &= (end - a) >= 8 ? ~0ull : ((1ull << (8 * (end - a))) - 1);
+    c += uint32_t(__popcll(m & 0x8080808080808080ull));
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_vcf_count(const uint8_t* __restrict__ text,
+                                                      size_t text_bytes,
+                                                      unsigned long long* __restrict__ blk_counts) {
+  __shared__ unsigned long long s_sum;
+  if (threadIdx.x == 0) s_sum = 0;
+  __syncthreads();
+  const Heap h = make_heap(text, text_bytes);
+  size_t b0, b1;
+  block_range(text_bytes, blockIdx.x, gridDim.x, &b0, &b1);
+  // threads stride over 8-byte words of the block's chunk (coalesced)
+  uint32_t c = 0;
+  const uintptr_t lo = h.lo + b0, end = h.lo + b1;
+  for (uintptr_t a = (lo & ~uintptr_t(7)) + 8 * threadIdx.x; a < end; a += 8 * blockDim.x) {
+    uint64_t m = zero_bytes_mask(text_word(a, h) ^ kNL) & 0x8080808080808080ull;
+    if (a < lo) m &= ~0ull << (8 * (lo - a));
+    if (a + 8 > end) m &= ((1ull << (8 * (end - a))) - 1);
+    c += uint32_t(__popcll(m));
+  }
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_down(c, d, kWave);
+  if (__lane_id() == 0 && c) atomicAdd(&s_sum, (unsigned long long)c);
+  __syncthreads();
+  if (threadIdx.x == 0) blk_counts[blockIdx.x] = s_sum;
+}
+
+// exclusive scan of kVcfGrid block counts (one workgroup of kVcfGrid threads)
+__global__ __launch_bounds__(kVcfGrid) void k_vcf_scan_blocks(unsigned long long* __restrict__ c,
+                                                              unsigned long long* __restrict__ total) {
+  __shared__ unsigned long long s[kVcfGrid];
+  const int t = threadIdx.x;
+  const unsigned long long v = c[t];
+  s[t] = v;
+  __syncthreads();
+  for (int d = 1; d < kVcfGrid; d <<= 1) {
+    const unsigned long long x = t >= d ? s[t - d] : 0ull;
+    __syncthreads();
+    s[t] += x;
+    __syncthreads();
+  }
+  c[t] = s[t] - v;
+  if (t == kVcfGrid - 1 && total) *total = s[t];
+}
+
+// line starts in order: line 0 starts at 0, line k+1 after the k-th newline
+__global__ __launch_bounds__(kBlock) void k_vcf_starts(const uint8_t* __restrict__ text,
+                                                       size_t text_bytes,
+                                                       const unsigned long long* __restrict__ blk_off,
+                                                       size_t n_lines,
+                                                       avdb_vcf_line* __restrict__ lines) {
+  __shared__ unsigned long long s_cnt[kBlock];
+  const Heap h = make_heap(text, text_bytes);
+  size_t b0, b1;
+  block_range(text_bytes, blockIdx.x, gridDim.x, &b0, &b1);
+  // per-thread contiguous sub-chunk (8-aligned)
+  const size_t len = b1 > b0 ? b1 - b0 : 0;
+  size_t per = (len + blockDim.x - 1) / blockDim.x;
+  per = (per + 7) & ~size_t(7);
+  size_t t0 = b0 + per * threadIdx.x, t1 = t0 + per;
+  if (t0 > b1) t0 = b1;
+  if (t1 > b1) t1 = b1;
+  const uint32_t mine = t1 > t0 ? count_nl(h, t0, t1) : 0u;
+  s_cnt[threadIdx.x] = mine;
+  __syncthreads();
+  for (unsigned d = 1; d < blockDim.x; d <<= 1) {
+    const unsigned long long x = threadIdx.x >= d ? s_cnt[threadIdx.x - d] : 0ull;
+    __syncthreads();
+    s_cnt[threadIdx.x] += x;
+    __syncthreads();
+  }
+  unsigned long long k = blk_off[blockIdx.x] + s_cnt[threadIdx.x] - mine;  // newlines before t0
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n_lines) lines[0].start = 0;
+  if (mine == 0) return;
+  const uintptr_t base = h.lo;
+  for (uintptr_t a = (base + t0) & ~uintptr_t(7); a < base + t1; a += 8) {
+    uint64_t m = zero_bytes_mask(text_word(a, h) ^ kNL) & 0x8080808080808080ull;
+    if (a < base + t0) m &= ~0ull << (8 * (base + t0 - a));
+    if (a + 8 > base + t1) m &= ((1ull << (8 * (base + t1 - a))) - 1);
+    while (m) {
+      const int bit = __builtin_ctzll(m);
+      m &= m - 1;
+      const size_t nlpos = size_t(a - base) + size_t(bit >> 3);
+      if (k + 1 < n_lines) lines[k + 1].start = nlpos + 1;
+      ++k;
+    }
+  }
+}
+
+__device__ __forceinline__ bool is_ws(uint8_t c) {
+  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
+}
+__device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+__device__ __forceinline__ bool is_alnum(uint8_t c) {
+  return is_digit(c) || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z');
+}
+
+// contig code of a CHROM field (vcf_parser.py:133-150 + bin_index.py:64): plain
+// digits go through int(); 'MT' -> 'M'; every 'chr' removed in one left-to-right
+// pass (str.replace); then chr1..22, X, Y, M.  *host set for non-alphanumeric bytes.
+__device__ uint8_t chrom_code_of(const uint8_t* p, uint32_t n, bool* host) {
+  *host = false;
+  if (n == 0) return 255;
+  bool digits = true;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!is_alnum(p[i])) { *host = true; return 255; }
+    digits = digits && is_digit(p[i]);
+  }
+  if (digits) {
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      v = v * 10 + (p[i] - '0');
+      if (v > 1000) return 255;
+    }
+    return (v >= 1 && v <= 22) ? uint8_t(v - 1) : 255;
+  }
+  if (n == 2 && p[0] == 'M' && p[1] == 'T') return 24;
+  uint8_t lab[3];
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n;) {
+    if (i + 3 <= n && p[i] == 'c' && p[i + 1] == 'h' && p[i + 2] == 'r') { i += 3; continue; }
+    if (m == 3) return 255;
+    lab[m++] = p[i++];
+  }
+  if (m == 1) {
+    if (lab[0] >= '1' && lab[0] <= '9') return uint8_t(lab[0] - '1');
+    if (lab[0] == 'X') return 22;
+    if (lab[0] == 'Y') return 23;
+    if (lab[0] == 'M') return 24;
+    return 255;
+  }
+  if (m == 2 && is_digit(lab[0]) && is_digit(lab[1]) && lab[0] != '0') {
+    const uint32_t v = (lab[0] - '0') * 10 + (lab[1] - '0');
+    return (v >= 10 && v <= 22) ? uint8_t(v - 1) : 255;
+  }
+  return 255;
+}
+
+// canonical refSNP number of "rs<N>" bytes (N without leading zeros, < 10^18), else 0
+__device__ uint64_t rs_number(const uint8_t* p, uint32_t n) {
+  if (n < 3 || n > 20 || p[0] != 'r' || p[1] != 's' || p[2] == '0') return 0;
+  uint64_t v = 0;
+  for (uint32_t i = 2; i < n; ++i) {
+    if (!is_digit(p[i])) return 0;
+    v = v * 10 + (p[i] - '0');
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict__ text,
+                                                      size_t text_bytes, size_t n_lines,
+                                                      avdb_vcf_line* __restrict__ lines,
+                                                      unsigned long long* __restrict__ rec_cnt,
+                                                      unsigned long long* __restrict__ heap_cnt) {
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  for (size_t li = size_t(blockIdx.x) * blockDim.x + threadIdx.x; li < n_lines; li += stride) {
+    avdb_vcf_line L;
+    L.start = lines[li].start;
+    const size_t next = li + 1 < n_lines ? lines[li + 1].start - 1 : text_bytes;  // newline or end
+    const uint8_t* s = text + L.start;
+    uint32_t len = uint32_t(next - L.start);
+    while (len && is_ws(s[len - 1])) --len;  // str.rstrip()
+    L.len = len;
+    L.flags = 0;
+    L.pos = 0;
+    L.ext_id = 0;
+    L.n_alt = 0;
+    L.n_rec = 0;
+    L.chrom = 255;
+    L.pad[0] = L.pad[1] = L.pad[2] = 0;
+    uint32_t nf = 1;
+    L.field[0] = 0;
+    for (int k = 1; k < 8; ++k) L.field[k] = len + 1;
+    L.field_end8 = len;
+    if (len && s[0] == '#') L.flags |= AVDB_VCF_COMMENT;
+    if (!len) L.flags |= AVDB_VCF_EMPTY;
+    // tab-separated fields (first 8 starts; INFO ends at the 8th tab or the end)
+    for (uint32_t i = 0; i < len; ++i) {
+      if (s[i] == '\t') {
+        if (nf < 8) L.field[nf] = i + 1;
+        else if (nf == 8) L.field_end8 = i;
+        ++nf;
+      }
+    }
+    L.n_fields = nf;
+    uint64_t recs = 0, hbytes = 0;
+    if (!(L.flags & (AVDB_VCF_COMMENT | AVDB_VCF_EMPTY))) {
+      if (nf < 8) L.flags |= AVDB_VCF_FEW_FIELDS;
+      const uint32_t nfields = nf < 8 ? nf : 8;
+      auto fend = [&](int k) -> uint32_t {  // end of field k (exclusive)
+        return (k + 1 < int(nfields)) ? L.field[k + 1] - 1 : (k == 7 ? L.field_end8 : len);
+      };
+      if (!(L.flags & AVDB_VCF_FEW_FIELDS)) {
+        // CHROM
+        bool host = false;
+        L.chrom = chrom_code_of(s, fend(0), &host);
+        if (host) L.flags |= AVDB_VCF_CHROM_HOST;
+        // POS: plain decimal < 2^32
+        {
+          const uint8_t* p = s + L.field[1];
+          const uint32_t n = fend(1) - L.field[1];
+          uint64_t v = 0;
+          bool ok = n > 0 && n <= 10;
+          for (uint32_t i = 0; ok && i < n; ++i) {
+            ok = is_digit(p[i]);
+            v = v * 10 + (p[i] - '0');
+          }
+          if (ok && v <= 0xFFFFFFFFull) L.pos = uint32_t(v); else L.flags |= AVDB_VCF_BAD_POS;
+        }
+        // ID
+        const uint8_t* id = s + L.field[2];
+        const uint32_t idn = fend(2) - L.field[2];
+        {
+          bool numlike = idn > 0, has_digit = false;
+          for (uint32_t i = 0; i < idn; ++i) {
+            const uint8_t c = id[i];
+            has_digit = has_digit || is_digit(c);
+            numlike = numlike && (is_digit(c) || c == '+' || c == '-' || c == '.' || c == 'e' ||
+                                  c == 'E' || c == '_');
+          }
+          if (numlike && has_digit) L.flags |= AVDB_VCF_ID_HOST;  // Python coerces it to a number
+        }
+        bool has_rs = false;
+        for (uint32_t i = 0; i + 1 < idn; ++i) has_rs = has_rs || (id[i] == 'r' && id[i + 1] == 's');
+        if ((idn == 1 && id[0] == '.') || (idn >= 2 && id[0] == 'r' && id[1] == 's'))
+          L.flags |= AVDB_VCF_ID_METASEQ;
+        if (has_rs) {
+          L.flags |= AVDB_VCF_ID_RS;
+          L.ext_id = rs_number(id, idn);
+          if (!L.ext_id) L.flags |= AVDB_VCF_EXT_HOST;
+        } else {
+          // INFO: last entry whose key is exactly "RS" (dict(...) keeps the last)
+          const uint8_t* inf = s + L.field[7];
+          const uint32_t in = fend(7) - L.field[7];
+          int64_t vs = -1, ve = -1;
+          bool bare = false;
+          for (uint32_t i = 0; i < in;) {
+            uint32_t j = i;
+            while (j < in && inf[j] != ';') ++j;
+            if (j - i >= 2 && inf[i] == 'R' && inf[i + 1] == 'S') {
+              if (j - i == 2) { bare = true; vs = ve = -1; }
+              else if (inf[i + 2] == '=') { bare = false; vs = i + 3; ve = j; }
+            }
+            i = j + 1;
+          }
+          if (vs >= 0 || bare) {
+            L.flags |= AVDB_VCF_INFO_RS;
+            uint64_t v = 0;
+            bool ok = !bare && ve > vs && ve - vs <= 18;
+            for (int64_t i = vs; ok && i < ve; ++i) {
+              ok = is_digit(inf[i]);
+              v = v * 10 + (inf[i] - '0');
+            }
+            if (ok && v >= 1) L.ext_id = v;  // 'rs' + str(int(value))
+            else L.flags |= AVDB_VCF_EXT_HOST;
+          }
+        }
+        // REF / ALT
+        const uint32_t rlen = fend(3) - L.field[3];
+        const uint8_t* alt = s + L.field[4];
+        const uint32_t an = fend(4) - L.field[4];
+        uint32_t a0 = 0;
+        for (uint32_t i = 0; i <= an; ++i) {
+          if (i == an || alt[i] == ',') {
+            const uint32_t al = i - a0;
+            ++L.n_alt;
+            if (!(al == 1 && alt[a0] == '.')) {
+              ++L.n_rec;
+              hbytes += rlen + al;
+            }
+            a0 = i + 1;
+          }
+        }
+        recs = L.n_rec;
+      }
+    }
+    lines[li] = L;
+    rec_cnt[li] = recs;
+    heap_cnt[li] = hbytes;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_vcf_emit(
+    const uint8_t* __restrict__ text, size_t n_lines, const avdb_vcf_line* __restrict__ lines,
+    const uint64_t* __restrict__ rec_off, const uint64_t* __restrict__ heap_off,
+    uint8_t* __restrict__ chrom, uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
+    uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len, uint64_t* __restrict__ ext_id,
+    uint8_t* __restrict__ heap, uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  for (size_t li = size_t(blockIdx.x) * blockDim.x + threadIdx.x; li < n_lines; li += stride) {
+    const avdb_vcf_line& L = lines[li];
+    if (L.n_rec == 0) continue;
+    const uint8_t* s = text + L.start;
+    const uint32_t nfields = L.n_fields < 8 ? L.n_fields : 8;
+    const uint32_t rend = L.field[4] - 1;
+    const uint32_t aend = 5 < nfields ? L.field[5] - 1 : L.len;
+    const uint8_t* ref = s + L.field[3];
+    const uint32_t rlen = rend - L.field[3];
+    const uint8_t* alt = s + L.field[4];
+    const uint32_t an = aend - L.field[4];
+    uint64_t r = rec_off[li];
+    uint64_t h = heap_off[li];
+    uint32_t a0 = 0, ai = 0;
+    for (uint32_t i = 0; i <= an; ++i) {
+      if (i == an || alt[i] == ',') {
+        const uint32_t al = i - a0;
+        if (!(al == 1 && alt[a0] == '.')) {
+          chrom[r] = L.chrom;
+          pos[r] = L.pos;
+          allele_off[r] = h;
+          ref_len[r] = rlen;
+          alt_len[r] = al;
+          ext_id[r] = L.ext_id;
+          rec_line[r] = uint32_t(li);
+          rec_alt[r] = ai;
+          for (uint32_t k = 0; k < rlen; ++k) heap[h + k] = ref[k];
+          for (uint32_t k = 0; k < al; ++k) heap[h + rlen + k] = alt[a0 + k];
+          h += rlen + al;
+          ++r;
+        }
+        ++ai;
+        a0 = i + 1;
+      }
+    }
+  }
+}
+
+}  // namespace avdb
+
+using namespace avdb;
+
+static size_t scan_temp_bytes(size_t n) {
+  size_t t = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, static_cast<const unsigned long long*>(nullptr),
+                                         static_cast<unsigned long long*>(nullptr), n);
+  return (t + 255) & ~size_t(255);
+}
+
+extern "C" int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes) {
+  (void)text_bytes;
+  if (!bytes) return AVDB_EINVAL;
+  // block counts | total | scan temp
+  *bytes = 8 * kVcfGrid + 256 + scan_temp_bytes(n_lines + 1) + 256;
+  return AVDB_OK;
+}
+
+extern "C" int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes,
+                                    void* workspace, size_t workspace_bytes, uint64_t* n_newlines,
+                                    void* stream) {
+  if (!ctx || !n_newlines) { avdb_set_error("avdb_vcf_count_lines: null argument"); return AVDB_EINVAL; }
+  if (!workspace || workspace_bytes < 8 * kVcfGrid + 256) {
+    avdb_set_error("avdb_vcf_count_lines: workspace too small");
+    return AVDB_ERANGE;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (text_bytes == 0) return hipMemsetAsync(n_newlines, 0, 8, s) == hipSuccess ? AVDB_OK : AVDB_EHIP;
+  auto* blk = static_cast<unsigned long long*>(workspace);
+  hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk);
+  AVDB_LAUNCH_CHECK("k_vcf_count");
+  hipLaunchKernelGGL(k_vcf_scan_blocks, dim3(1), dim3(kVcfGrid), 0, s, blk,
+                     reinterpret_cast<unsigned long long*>(n_newlines));
+  AVDB_LAUNCH_CHECK("k_vcf_scan_blocks");
+  return AVDB_OK;
+}
+
+extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes,
+                                    size_t n_lines, void* workspace, size_t workspace_bytes,
+                                    avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off,
+                                    void* stream) {
+  if (!ctx || !lines || !rec_off || !heap_off) {
+    avdb_set_error("avdb_vcf_parse_lines: null argument");
+    return AVDB_EINVAL;
+  }
+  size_t need = 0;
+  avdb_vcf_workspace_size(text_bytes, n_lines, &need);
+  if (!workspace || workspace_bytes < need) {
+    avdb_set_error("avdb_vcf_parse_lines: workspace of %zu bytes required", need);
+    return AVDB_ERANGE;
+  }
+  if (n_lines == 0) return AVDB_OK;
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto* blk = static_cast<unsigned long long*>(workspace);
+  void* tmp = static_cast<char*>(workspace) + 8 * kVcfGrid + 256;
+  size_t tmp_bytes = scan_temp_bytes(n_lines + 1);
+  // block newline counts -> exclusive offsets (same partition as k_vcf_starts)
+  hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk);
+  AVDB_LAUNCH_CHECK("k_vcf_count");
+  hipLaunchKernelGGL(k_vcf_scan_blocks, dim3(1), dim3(kVcfGrid), 0, s, blk,
+                     static_cast<unsigned long long*>(nullptr));
+  AVDB_LAUNCH_CHECK("k_vcf_scan_blocks");
+  hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk,
+                     n_lines, lines);
+  AVDB_LAUNCH_CHECK("k_vcf_starts");
+  auto* rc = reinterpret_cast<unsigned long long*>(rec_off);
+  auto* hc = reinterpret_cast<unsigned long long*>(heap_off);
+  AVDB_HIP_TRY(hipMemsetAsync(rc + n_lines, 0, 8, s));
+  AVDB_HIP_TRY(hipMemsetAsync(hc + n_lines, 0, 8, s));
+  const unsigned grid = stream_grid(n_lines, kBlock, 4096);
+  hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, lines,
+                     rc, hc);
+  AVDB_LAUNCH_CHECK("k_vcf_parse");
+  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, rc, rc, n_lines + 1, s));
+  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, hc, hc, n_lines + 1, s));
+  return AVDB_OK;
+}
+
+extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                             const avdb_vcf_line* lines, const uint64_t* rec_off,
+                             const uint64_t* heap_off, uint8_t* chrom, uint32_t* pos,
+                             uint64_t* allele_off, uint32_t* ref_len, uint32_t* alt_len,
+                             uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line, uint32_t* rec_alt,
+                             void* stream) {
+  (void)text_bytes;
+  if (!ctx || !lines || !rec_off || !heap_off || !chrom || !pos || !allele_off || !ref_len ||
+      !alt_len || !ext_id || !heap || !rec_line || !rec_alt) {
+    avdb_set_error("avdb_vcf_emit: null argument");
+    return AVDB_EINVAL;
+  }
+  if (n_lines == 0) return AVDB_OK;
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  const unsigned grid = stream_grid(n_lines, kBlock, 4096);
+  hipLaunchKernelGGL(k_vcf_emit, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                     text, n_lines, lines, rec_off, heap_off, chrom, pos, allele_off, ref_len,
+                     alt_len, ext_id, heap, rec_line, rec_alt);
+  AVDB_LAUNCH_CHECK("k_vcf_emit");
+  return AVDB_OK;
+}

@@ -129,6 +129,43 @@ def as_u32(t: torch.Tensor) -> np.ndarray:
     return t.detach().cpu().numpy().view(np.uint32)
 
 
+# avdb_vcf_line (include/avdb.h), 80 bytes
+VCF_LINE_DTYPE = np.dtype([("start", "<u8"), ("len", "<u4"), ("n_fields", "<u4"), ("field", "<u4", (8,)),
+                           ("field_end8", "<u4"), ("pos", "<u4"), ("ext_id", "<u8"), ("n_alt", "<u4"),
+                           ("n_rec", "<u4"), ("flags", "<u4"), ("chrom", "u1"), ("pad", "u1", (3,))])
+assert VCF_LINE_DTYPE.itemsize == 80
+
+VCF_COMMENT = 0x001
+VCF_FEW_FIELDS = 0x002
+VCF_BAD_POS = 0x004
+VCF_EXT_HOST = 0x008
+VCF_ID_RS = 0x010
+VCF_INFO_RS = 0x020
+VCF_ID_METASEQ = 0x040
+VCF_CHROM_HOST = 0x080
+VCF_EMPTY = 0x100
+VCF_ID_HOST = 0x200
+VCF_HOST_FLAGS = VCF_BAD_POS | VCF_EXT_HOST | VCF_CHROM_HOST | VCF_ID_HOST
+
+
+@dataclass
+class VcfBatch:
+    """Output of ``Engine.vcf_tokenize``: device text, per-line table, records."""
+    text: torch.Tensor
+    n_lines: int
+    lines: torch.Tensor          # uint8[n_lines * 80] (VCF_LINE_DTYPE)
+    rec_off: torch.Tensor        # int64[n_lines + 1]
+    heap_off: torch.Tensor
+    records: RecordBatch
+    rec_line: torch.Tensor       # int32[n_rec]
+    rec_alt: torch.Tensor
+
+    def lines_host(self) -> np.ndarray:
+        if self.n_lines == 0:
+            return np.zeros(0, dtype=VCF_LINE_DTYPE)
+        return self.lines.cpu().numpy()[: self.n_lines * 80].view(VCF_LINE_DTYPE)
+
+
 # ---------------------------------------------------------------------------
 # engine
 # ---------------------------------------------------------------------------
@@ -299,6 +336,58 @@ class Engine:
             self.ctx, N.ptr(d_data), N.ptr(d_off), N.ptr(d_len), n, N.ptr(out), self._stream()))
         raw = out.cpu().numpy().tobytes()
         return [raw[i * 32:(i + 1) * 32].decode("ascii") for i in range(n)]
+
+    # -- K0: VCF text -> records ---------------------------------------------
+    def vcf_tokenize(self, text) -> "VcfBatch":
+        """Parse VCF data lines (bytes or a uint8 tensor) on the GPU into the
+        record SoA (one row per ALT != '.') plus the per-line table."""
+        if isinstance(text, (bytes, bytearray, memoryview)):
+            host = bytes(text)
+            t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
+            if not host:
+                t = t[:0]
+            text_t = t.to(self.device)
+            last_nl = host.endswith(b"\n") if host else True
+        else:
+            text_t = self._dev(text)
+            last_nl = bool(text_t.numel() == 0 or int(text_t[-1].item()) == 10)
+        nb = int(text_t.numel())
+        tp = N.ptr(text_t) if nb else None
+        s = self._stream()
+        ws0 = self.empty(8 * 1024 + 256, torch.uint8)
+        nl = torch.zeros(1, dtype=torch.int64, device=self.device)
+        N.check("avdb_vcf_count_lines", self.lib.avdb_vcf_count_lines(
+            self.ctx, tp, nb, N.ptr(ws0), ws0.numel(), N.ptr(nl), s))
+        n_nl = int(nl.item())
+        n_lines = n_nl + (0 if (last_nl or nb == 0) else 1)
+        sz = ctypes.c_size_t()
+        self.lib.avdb_vcf_workspace_size(nb, n_lines, ctypes.byref(sz))
+        ws = self.empty(int(sz.value), torch.uint8)
+        lines = self.empty(max(1, n_lines) * VCF_LINE_DTYPE.itemsize, torch.uint8)
+        rec_off = self.empty(n_lines + 1, torch.int64)
+        heap_off = self.empty(n_lines + 1, torch.int64)
+        N.check("avdb_vcf_parse_lines", self.lib.avdb_vcf_parse_lines(
+            self.ctx, tp, nb, n_lines, N.ptr(ws), ws.numel(), N.ptr(lines), N.ptr(rec_off),
+            N.ptr(heap_off), s))
+        if n_lines:
+            tot = torch.stack([rec_off[n_lines], heap_off[n_lines]]).cpu().tolist()
+        else:
+            tot = [0, 0]
+        n_rec, n_heap = int(tot[0]), int(tot[1])
+        b = RecordBatch(chrom=self.empty(n_rec, torch.uint8), pos=self.empty(n_rec, torch.int32),
+                        allele_off=self.empty(n_rec, torch.int64),
+                        ref_len=self.empty(n_rec, torch.int32), alt_len=self.empty(n_rec, torch.int32),
+                        heap=self.empty(max(1, n_heap), torch.uint8),
+                        ext_id=self.empty(n_rec, torch.int64))
+        rec_line = self.empty(n_rec, torch.int32)
+        rec_alt = self.empty(n_rec, torch.int32)
+        if n_rec:
+            N.check("avdb_vcf_emit", self.lib.avdb_vcf_emit(
+                self.ctx, tp, nb, n_lines, N.ptr(lines), N.ptr(rec_off), N.ptr(heap_off),
+                N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
+                N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s))
+        return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
+                        records=b, rec_line=rec_line, rec_alt=rec_alt)
 
     # -- formatting (host) ---------------------------------------------------
     def format_path(self, chrom_code: int, code: int) -> Optional[str]:

