@@ -203,7 +203,7 @@ def test_loader_text_path_comments_and_edge_lines(loader):
             b"1\t10177\trs367896724\tA\tAC\t.\t.\tRS=367896724\n"
             b"chr2\t00500\t.\tG\tT,.\t.\t.\tRS=5;RS=0007\n"
             b"MT\t100\tid1\tC\tT\t.\t.\t.  \r\n"
-            b"22\t1\t.\tAT\tAT\t.\t.\t.")  # no trailing newline; end < start quirk
+            b"22\t2\t.\tAT\tAT\t.\t.\t.")  # no trailing newline; end < start quirk (end = pos-1)
     loader.reset_copy_buffer()
     outs = loader.parse_vcf_text(text)
     assert outs[0] == {"1:10177:A:AC": [{"primary_key": "1:10177:A:AC:rs367896724",
@@ -211,7 +211,9 @@ def test_loader_text_path_comments_and_edge_lines(loader):
     assert list(outs[1].keys()) == ["2:500:G:T,."]
     assert outs[1]["2:500:G:T,."][0]["primary_key"] == "2:500:G:T:rs7"
     assert list(outs[2].keys()) == ["id1"] and outs[2]["id1"][0]["primary_key"] == "M:100:C:T"
-    assert outs[3]["22:1:AT:AT"][0]["bin_index"].startswith("chr22.L1.B1")
+    assert outs[3]["22:2:AT:AT"][0]["bin_index"].startswith("chr22.L1.B1")
+    with pytest.raises(TypeError):  # pos 1: end 0 is off the chromosome, as in the reference
+        loader.parse_vcf_text(b"22\t1\t.\tAT\tAT\t.\t.\t.\n")
     host = []
     for ln in text.decode().split("\n"):
         if ln and not ln.startswith("#"):
