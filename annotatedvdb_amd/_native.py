@@ -97,7 +97,7 @@ def _sig(lib):
     f.avdb_format_bin_paths.argtypes = [P, P, P, SZ, P, SZ, P]
     f.avdb_vcf_workspace_size.argtypes = [SZ, SZ, ctypes.POINTER(SZ)]
     f.avdb_vcf_count_lines.argtypes = [P, P, SZ, P, SZ, P, P]
-    f.avdb_vcf_parse_lines.argtypes = [P, P, SZ, SZ, P, SZ, P, P, P, P]
+    f.avdb_vcf_parse_lines.argtypes = [P, P, SZ, SZ, P, P, SZ, P, P, P, P]
     f.avdb_vcf_emit.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, P, P, P, P, P, P]
     for name in EXPORTED_SYMBOLS:
         if name not in ("avdb_last_error",):

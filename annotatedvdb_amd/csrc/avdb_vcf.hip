@@ -3,15 +3,19 @@
 // Text half of VcfEntryParser (Util/lib/python/parsers/vcf_parser.py:76-169) and the
 // per-alt loop head of VCFVariantLoader.__parse_alt_alleles
 // (vcf_variant_loader.py:273-280), for a batch of lines resident in HBM:
-//   k_vcf_count    per-workgroup count of '\n' bytes (8 bytes per step, SWAR zero-byte
-//                  detection), block-contiguous chunks
-//   k_vcf_starts   ordered line table: per-thread sub-chunk counts -> workgroup
-//                  exclusive scan in LDS -> each thread writes its lines' starts
-//   k_vcf_parse    one lane per line: rstrip, tab fields, CHROM -> contig code,
-//                  POS, ID / INFO RS -> refSNP key, ALT count, heap bytes
+//   k_vcf_count    per-workgroup count of '\n' bytes (8 bytes per lane-step, SWAR
+//                  zero-byte detection), block-contiguous chunks, coalesced
+//   k_vcf_starts   ordered line starts: each wave walks a contiguous sub-chunk 512 B
+//                  at a time; a lane's newline count is ranked inside the wave with
+//                  4 ballots + mbcnt (no LDS), so every start is written in order
+//   k_vcf_parse    256 consecutive lines per workgroup: their text span is staged in
+//                  LDS with 16-byte coalesced loads, then one lane per line parses from
+//                  LDS: rstrip, tab fields, CHROM -> contig code, POS, ID / INFO RS ->
+//                  refSNP key, ALT count, heap bytes (spans over kStage bytes parse
+//                  straight from global memory)
 //   (hipCUB exclusive scans: record and heap offsets per line)
-//   k_vcf_emit     one lane per line: one record per ALT != '.', REF+ALT copied to
-//                  the allele heap
+//   k_vcf_emit     same staging; one lane per line: one record per ALT != '.',
+//                  REF+ALT copied to the allele heap
 // Only canonical text is resolved here; the rest is flagged (AVDB_VCF_*_HOST) for
 // the host to resolve with Python's own coercion rules.
 #include "avdb_internal.hpp"
@@ -46,22 +50,15 @@ __device__ __forceinline__ void block_range(size_t text_bytes, int blk, int nblk
   if (*b0 > text_bytes) *b0 = text_bytes;
 }
 
-// newline count of [b0,b1) using aligned words; masks bytes outside the range
-__device__ __forceinline__ uint32_t count_nl(const Heap& h, size_t b0, size_t b1) {
-  uint32_t c = 0;
-  const uintptr_t base = h.lo;
-  uintptr_t a = (base + b0) & ~uintptr_t(7);
-  const uintptr_t end = base + b1;
-  for (; a < end; a += 8) {
-    uint64_t m = zero_bytes_mask(text_word(a, h) ^ kNL);
-    // keep only bytes inside [base+b0, end)
-    const uintptr_t lo = base + b0;
-    if (a < lo) m &= ~0ull << (8 * (lo - a));
-    if (a + 8 > end) m &= (end - a) >= 8 ? ~0ull : ((1ull << (8 * (end - a))) - 1);
-    c += uint32_t(__popcll(m & 0x8080808080808080ull));
-  }
-  return c;
+__device__ __forceinline__ uint64_t nl_mask(uintptr_t a, const Heap& h, uintptr_t lo, uintptr_t end) {
+  if (a >= end) return 0;
+  uint64_t m = zero_bytes_mask(text_word(a, h) ^ kNL) & 0x8080808080808080ull;
+  if (a < lo) m &= ~0ull << (8 * (lo - a));
+  if (a + 8 > end) m &= ((1ull << (8 * (end - a))) - 1);
+  return m;
 }
+
+constexpr int kNlUnroll = 4;  // 512-byte wave steps in flight per wave
 
 __global__ __launch_bounds__(kBlock) void k_vcf_count(const uint8_t* __restrict__ text,
                                                       size_t text_bytes,
@@ -72,14 +69,17 @@ __global__ __launch_bounds__(kBlock) void k_vcf_count(const uint8_t* __restrict_
   const Heap h = make_heap(text, text_bytes);
   size_t b0, b1;
   block_range(text_bytes, blockIdx.x, gridDim.x, &b0, &b1);
-  // threads stride over 8-byte words of the block's chunk (coalesced)
+  // threads stride over 8-byte words of the block's chunk (coalesced), kNlUnroll
+  // independent loads per lane per trip
   uint32_t c = 0;
   const uintptr_t lo = h.lo + b0, end = h.lo + b1;
-  for (uintptr_t a = (lo & ~uintptr_t(7)) + 8 * threadIdx.x; a < end; a += 8 * blockDim.x) {
-    uint64_t m = zero_bytes_mask(text_word(a, h) ^ kNL) & 0x8080808080808080ull;
-    if (a < lo) m &= ~0ull << (8 * (lo - a));
-    if (a + 8 > end) m &= ((1ull << (8 * (end - a))) - 1);
-    c += uint32_t(__popcll(m));
+  const uintptr_t step = 8 * blockDim.x;
+  for (uintptr_t a = (lo & ~uintptr_t(7)) + 8 * threadIdx.x; a < end; a += kNlUnroll * step) {
+    uint64_t m[kNlUnroll];
+#pragma unroll
+    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask(a + u * step, h, lo, end);
+#pragma unroll
+    for (int u = 0; u < kNlUnroll; ++u) c += uint32_t(__popcll(m[u]));
   }
   for (int d = 32; d > 0; d >>= 1) c += __shfl_down(c, d, kWave);
   if (__lane_id() == 0 && c) atomicAdd(&s_sum, (unsigned long long)c);
@@ -105,46 +105,72 @@ __global__ __launch_bounds__(kVcfGrid) void k_vcf_scan_blocks(unsigned long long
   if (t == kVcfGrid - 1 && total) *total = s[t];
 }
 
-// line starts in order: line 0 starts at 0, line k+1 after the k-th newline
+// popcount of `m` over the lanes below this one
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+}
+
+// line starts in order: line 0 starts at 0, line k+1 after the k-th newline.
+// Each wave owns a contiguous, 8-aligned sub-chunk of its workgroup's chunk.
 __global__ __launch_bounds__(kBlock) void k_vcf_starts(const uint8_t* __restrict__ text,
                                                        size_t text_bytes,
                                                        const unsigned long long* __restrict__ blk_off,
                                                        size_t n_lines,
-                                                       avdb_vcf_line* __restrict__ lines) {
-  __shared__ unsigned long long s_cnt[kBlock];
+                                                       uint64_t* __restrict__ starts) {
+  constexpr int kWaves = kBlock / kWave;
+  __shared__ unsigned long long s_w[kWaves];
   const Heap h = make_heap(text, text_bytes);
   size_t b0, b1;
   block_range(text_bytes, blockIdx.x, gridDim.x, &b0, &b1);
-  // per-thread contiguous sub-chunk (8-aligned)
+  const int wave = threadIdx.x / kWave, lane = __lane_id();
   const size_t len = b1 > b0 ? b1 - b0 : 0;
-  size_t per = (len + blockDim.x - 1) / blockDim.x;
+  size_t per = (len + kWaves - 1) / kWaves;
   per = (per + 7) & ~size_t(7);
-  size_t t0 = b0 + per * threadIdx.x, t1 = t0 + per;
+  size_t t0 = b0 + per * wave, t1 = t0 + per;
   if (t0 > b1) t0 = b1;
   if (t1 > b1) t1 = b1;
-  const uint32_t mine = t1 > t0 ? count_nl(h, t0, t1) : 0u;
-  s_cnt[threadIdx.x] = mine;
-  __syncthreads();
-  for (unsigned d = 1; d < blockDim.x; d <<= 1) {
-    const unsigned long long x = threadIdx.x >= d ? s_cnt[threadIdx.x - d] : 0ull;
-    __syncthreads();
-    s_cnt[threadIdx.x] += x;
-    __syncthreads();
+  const uintptr_t lo = h.lo + t0, end = h.lo + t1;
+  const uintptr_t a_first = lo & ~uintptr_t(7);
+  // pass 1: newlines in this wave's sub-chunk
+  uint32_t c = 0;
+  for (uintptr_t a = a_first + 8 * lane; a < end; a += kNlUnroll * 8 * kWave) {
+    uint64_t m[kNlUnroll];
+#pragma unroll
+    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask(a + u * 8 * kWave, h, lo, end);
+#pragma unroll
+    for (int u = 0; u < kNlUnroll; ++u) c += uint32_t(__popcll(m[u]));
   }
-  unsigned long long k = blk_off[blockIdx.x] + s_cnt[threadIdx.x] - mine;  // newlines before t0
-  if (blockIdx.x == 0 && threadIdx.x == 0 && n_lines) lines[0].start = 0;
-  if (mine == 0) return;
-  const uintptr_t base = h.lo;
-  for (uintptr_t a = (base + t0) & ~uintptr_t(7); a < base + t1; a += 8) {
-    uint64_t m = zero_bytes_mask(text_word(a, h) ^ kNL) & 0x8080808080808080ull;
-    if (a < base + t0) m &= ~0ull << (8 * (base + t0 - a));
-    if (a + 8 > base + t1) m &= ((1ull << (8 * (base + t1 - a))) - 1);
-    while (m) {
-      const int bit = __builtin_ctzll(m);
-      m &= m - 1;
-      const size_t nlpos = size_t(a - base) + size_t(bit >> 3);
-      if (k + 1 < n_lines) lines[k + 1].start = nlpos + 1;
-      ++k;
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
+  if (lane == 0) s_w[wave] = c;
+  __syncthreads();
+  unsigned long long k = blk_off[blockIdx.x];  // newlines before t0
+  for (int w = 0; w < wave; ++w) k += s_w[w];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n_lines) starts[0] = 0;
+  // pass 2: rank every newline inside the wave (lane counts are 0..8: 4 ballots)
+  for (uintptr_t a0 = a_first; a0 < end; a0 += kNlUnroll * 8 * kWave) {
+    uint64_t m[kNlUnroll];
+#pragma unroll
+    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask(a0 + u * 8 * kWave + 8 * lane, h, lo, end);
+#pragma unroll
+    for (int u = 0; u < kNlUnroll; ++u) {
+      const uint32_t cnt = uint32_t(__popcll(m[u]));
+      uint32_t below = 0, total = 0;
+#pragma unroll
+      for (int bit = 0; bit < 4; ++bit) {
+        const uint64_t b = __ballot((cnt >> bit) & 1u);
+        below += lanes_below(b) << bit;
+        total += uint32_t(__popcll(b)) << bit;
+      }
+      unsigned long long kk = k + below;
+      const size_t wbase = size_t(a0 + u * 8 * kWave + 8 * lane - h.lo);
+      uint64_t mm = m[u];
+      while (mm) {
+        const int bitpos = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        if (kk + 1 < n_lines) starts[kk + 1] = wbase + size_t(bitpos >> 3) + 1;
+        ++kk;
+      }
+      k += total;
     }
   }
 }
@@ -209,18 +235,9 @@ __device__ uint64_t rs_number(const uint8_t* p, uint32_t n) {
   return v;
 }
 
-__global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict__ text,
-                                                      size_t text_bytes, size_t n_lines,
-                                                      avdb_vcf_line* __restrict__ lines,
-                                                      unsigned long long* __restrict__ rec_cnt,
-                                                      unsigned long long* __restrict__ heap_cnt) {
-  const size_t stride = size_t(gridDim.x) * blockDim.x;
-  for (size_t li = size_t(blockIdx.x) * blockDim.x + threadIdx.x; li < n_lines; li += stride) {
-    avdb_vcf_line L;
-    L.start = lines[li].start;
-    const size_t next = li + 1 < n_lines ? lines[li + 1].start - 1 : text_bytes;  // newline or end
-    const uint8_t* s = text + L.start;
-    uint32_t len = uint32_t(next - L.start);
+// one line: s points at its first byte (LDS or global), raw = bytes up to its newline
+__device__ __forceinline__ void parse_line(const uint8_t* s, uint32_t len, avdb_vcf_line& L,
+                                           uint64_t& recs, uint64_t& hbytes) {
     while (len && is_ws(s[len - 1])) --len;  // str.rstrip()
     L.len = len;
     L.flags = 0;
@@ -239,13 +256,16 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
     // tab-separated fields (first 8 starts; INFO ends at the 8th tab or the end)
     for (uint32_t i = 0; i < len; ++i) {
       if (s[i] == '\t') {
-        if (nf < 8) L.field[nf] = i + 1;
-        else if (nf == 8) L.field_end8 = i;
+#pragma unroll
+        for (int k = 1; k < 8; ++k)  // register-resident field table (no dynamic index)
+          if (nf == uint32_t(k)) L.field[k] = i + 1;
+        if (nf == 8) L.field_end8 = i;
         ++nf;
       }
     }
     L.n_fields = nf;
-    uint64_t recs = 0, hbytes = 0;
+    recs = 0;
+    hbytes = 0;
     if (!(L.flags & (AVDB_VCF_COMMENT | AVDB_VCF_EMPTY))) {
       if (nf < 8) L.flags |= AVDB_VCF_FEW_FIELDS;
       const uint32_t nfields = nf < 8 ? nf : 8;
@@ -336,23 +356,79 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
         recs = L.n_rec;
       }
     }
-    lines[li] = L;
-    rec_cnt[li] = recs;
-    heap_cnt[li] = hbytes;
+}
+
+// A workgroup's text window: the bytes of lines [base, last) staged in LDS as
+// 16-byte words.  Returns false (window not staged) when it exceeds kStage.
+constexpr uint32_t kStage = 36 * 1024;  // 4 workgroups per CU in 160 KB LDS
+
+struct Window {
+  uintptr_t a0;  // 16-aligned address of LDS byte 0
+  bool staged;
+};
+
+__device__ __forceinline__ Window stage_window(const Heap& h, size_t s0, size_t s1, u32x4* lds) {
+  Window w;
+  w.a0 = (h.lo + s0) & ~uintptr_t(15);
+  const uintptr_t end = h.lo + s1;
+  const size_t n16 = (end - w.a0 + 15) / 16;
+  w.staged = n16 * 16 <= kStage;
+  if (w.staged) {
+    for (size_t i = threadIdx.x; i < n16; i += blockDim.x) {
+      const uintptr_t a = w.a0 + 16 * i;
+      u32x4 v;
+      if (a >= h.lo && a + 16 <= h.hi) {
+        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a));
+      } else {
+        const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
+        v = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};
+      }
+      lds[i] = v;
+    }
+  }
+  __syncthreads();
+  return w;
+}
+
+__global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict__ text,
+                                                      size_t text_bytes, size_t n_lines,
+                                                      const uint64_t* __restrict__ starts,
+                                                      avdb_vcf_line* __restrict__ lines,
+                                                      unsigned long long* __restrict__ rec_cnt,
+                                                      unsigned long long* __restrict__ heap_cnt) {
+  __shared__ u32x4 s_text[kStage / 16];
+  const Heap h = make_heap(text, text_bytes);
+  for (size_t base = size_t(blockIdx.x) * kBlock; base < n_lines; base += size_t(gridDim.x) * kBlock) {
+    const size_t last = base + kBlock < n_lines ? base + kBlock : n_lines;
+    const size_t s0 = starts[base];
+    const size_t s1 = last < n_lines ? starts[last] : text_bytes;
+    const Window w = stage_window(h, s0, s1, s_text);
+    const size_t li = base + threadIdx.x;
+    if (li < n_lines) {
+      avdb_vcf_line L;
+      L.start = starts[li];
+      const size_t next = li + 1 < n_lines ? starts[li + 1] - 1 : text_bytes;  // newline or end
+      const uint32_t raw = uint32_t(next - L.start);
+      uint64_t recs, hbytes;
+      if (w.staged)
+        parse_line(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0), raw, L, recs,
+                   hbytes);
+      else
+        parse_line(text + L.start, raw, L, recs, hbytes);
+      lines[li] = L;
+      rec_cnt[li] = recs;
+      heap_cnt[li] = hbytes;
+    }
+    __syncthreads();  // the window is reused by the next trip
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_vcf_emit(
-    const uint8_t* __restrict__ text, size_t n_lines, const avdb_vcf_line* __restrict__ lines,
-    const uint64_t* __restrict__ rec_off, const uint64_t* __restrict__ heap_off,
-    uint8_t* __restrict__ chrom, uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
-    uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len, uint64_t* __restrict__ ext_id,
-    uint8_t* __restrict__ heap, uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
-  const size_t stride = size_t(gridDim.x) * blockDim.x;
-  for (size_t li = size_t(blockIdx.x) * blockDim.x + threadIdx.x; li < n_lines; li += stride) {
-    const avdb_vcf_line& L = lines[li];
-    if (L.n_rec == 0) continue;
-    const uint8_t* s = text + L.start;
+__device__ __forceinline__ void emit_line(const uint8_t* s, const avdb_vcf_line& L, size_t li,
+                                          uint64_t r, uint64_t h, uint8_t* __restrict__ chrom,
+                                          uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
+                                          uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
+                                          uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap,
+                                          uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
     const uint32_t nfields = L.n_fields < 8 ? L.n_fields : 8;
     const uint32_t rend = L.field[4] - 1;
     const uint32_t aend = 5 < nfields ? L.field[5] - 1 : L.len;
@@ -360,8 +436,6 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
     const uint32_t rlen = rend - L.field[3];
     const uint8_t* alt = s + L.field[4];
     const uint32_t an = aend - L.field[4];
-    uint64_t r = rec_off[li];
-    uint64_t h = heap_off[li];
     uint32_t a0 = 0, ai = 0;
     for (uint32_t i = 0; i <= an; ++i) {
       if (i == an || alt[i] == ',') {
@@ -384,6 +458,38 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
         a0 = i + 1;
       }
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_vcf_emit(
+    const uint8_t* __restrict__ text, size_t text_bytes, size_t n_lines,
+    const avdb_vcf_line* __restrict__ lines, const uint64_t* __restrict__ rec_off,
+    const uint64_t* __restrict__ heap_off, uint8_t* __restrict__ chrom, uint32_t* __restrict__ pos,
+    uint64_t* __restrict__ allele_off, uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
+    uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap, uint32_t* __restrict__ rec_line,
+    uint32_t* __restrict__ rec_alt) {
+  __shared__ u32x4 s_text[kStage / 16];
+  const Heap h = make_heap(text, text_bytes);
+  for (size_t base = size_t(blockIdx.x) * kBlock; base < n_lines; base += size_t(gridDim.x) * kBlock) {
+    const size_t last = base + kBlock < n_lines ? base + kBlock : n_lines;
+    // the window only has to reach the end of the last line's ALT field
+    const size_t s0 = lines[base].start;
+    const avdb_vcf_line& Z = lines[last - 1];
+    const size_t s1 = Z.start + Z.len;
+    const Window w = stage_window(h, s0, s1, s_text);
+    const size_t li = base + threadIdx.x;
+    if (li < n_lines) {
+      const avdb_vcf_line L = lines[li];
+      if (L.n_rec) {
+        if (w.staged)
+          emit_line(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0), L, li,
+                    rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id, heap,
+                    rec_line, rec_alt);
+        else
+          emit_line(text + L.start, L, li, rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len,
+                    alt_len, ext_id, heap, rec_line, rec_alt);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -401,8 +507,8 @@ static size_t scan_temp_bytes(size_t n) {
 extern "C" int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes) {
   (void)text_bytes;
   if (!bytes) return AVDB_EINVAL;
-  // block counts | total | scan temp
-  *bytes = 8 * kVcfGrid + 256 + scan_temp_bytes(n_lines + 1) + 256;
+  // block counts | total | line starts | scan temp
+  *bytes = 8 * kVcfGrid + 256 + ((8 * n_lines + 255) & ~size_t(255)) + scan_temp_bytes(n_lines + 1) + 256;
   return AVDB_OK;
 }
 
@@ -427,7 +533,8 @@ extern "C" int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
 }
 
 extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes,
-                                    size_t n_lines, void* workspace, size_t workspace_bytes,
+                                    size_t n_lines, const void* line_counts, void* workspace,
+                                    size_t workspace_bytes,
                                     avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off,
                                     void* stream) {
   if (!ctx || !lines || !rec_off || !heap_off) {
@@ -444,24 +551,29 @@ extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   auto* blk = static_cast<unsigned long long*>(workspace);
-  void* tmp = static_cast<char*>(workspace) + 8 * kVcfGrid + 256;
+  auto* starts = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + 8 * kVcfGrid + 256);
+  void* tmp = reinterpret_cast<char*>(starts) + ((8 * n_lines + 255) & ~size_t(255));
   size_t tmp_bytes = scan_temp_bytes(n_lines + 1);
-  // block newline counts -> exclusive offsets (same partition as k_vcf_starts)
-  hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk);
-  AVDB_LAUNCH_CHECK("k_vcf_count");
-  hipLaunchKernelGGL(k_vcf_scan_blocks, dim3(1), dim3(kVcfGrid), 0, s, blk,
-                     static_cast<unsigned long long*>(nullptr));
-  AVDB_LAUNCH_CHECK("k_vcf_scan_blocks");
-  hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk,
-                     n_lines, lines);
+  const unsigned long long* blk_off = static_cast<const unsigned long long*>(line_counts);
+  if (!blk_off) {
+    // block newline counts -> exclusive offsets (same partition as k_vcf_starts)
+    hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk);
+    AVDB_LAUNCH_CHECK("k_vcf_count");
+    hipLaunchKernelGGL(k_vcf_scan_blocks, dim3(1), dim3(kVcfGrid), 0, s, blk,
+                       static_cast<unsigned long long*>(nullptr));
+    AVDB_LAUNCH_CHECK("k_vcf_scan_blocks");
+    blk_off = blk;
+  }
+  hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk_off,
+                     n_lines, starts);
   AVDB_LAUNCH_CHECK("k_vcf_starts");
   auto* rc = reinterpret_cast<unsigned long long*>(rec_off);
   auto* hc = reinterpret_cast<unsigned long long*>(heap_off);
   AVDB_HIP_TRY(hipMemsetAsync(rc + n_lines, 0, 8, s));
   AVDB_HIP_TRY(hipMemsetAsync(hc + n_lines, 0, 8, s));
   const unsigned grid = stream_grid(n_lines, kBlock, 4096);
-  hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, lines,
-                     rc, hc);
+  hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, starts,
+                     lines, rc, hc);
   AVDB_LAUNCH_CHECK("k_vcf_parse");
   AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, rc, rc, n_lines + 1, s));
   AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, hc, hc, n_lines + 1, s));
@@ -474,7 +586,6 @@ extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_byt
                              uint64_t* allele_off, uint32_t* ref_len, uint32_t* alt_len,
                              uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line, uint32_t* rec_alt,
                              void* stream) {
-  (void)text_bytes;
   if (!ctx || !lines || !rec_off || !heap_off || !chrom || !pos || !allele_off || !ref_len ||
       !alt_len || !ext_id || !heap || !rec_line || !rec_alt) {
     avdb_set_error("avdb_vcf_emit: null argument");
@@ -484,7 +595,7 @@ extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_byt
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   const unsigned grid = stream_grid(n_lines, kBlock, 4096);
   hipLaunchKernelGGL(k_vcf_emit, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
-                     text, n_lines, lines, rec_off, heap_off, chrom, pos, allele_off, ref_len,
+                     text, text_bytes, n_lines, lines, rec_off, heap_off, chrom, pos, allele_off, ref_len,
                      alt_len, ext_id, heap, rec_line, rec_alt);
   AVDB_LAUNCH_CHECK("k_vcf_emit");
   return AVDB_OK;

@@ -367,7 +367,7 @@ class Engine:
         rec_off = self.empty(n_lines + 1, torch.int64)
         heap_off = self.empty(n_lines + 1, torch.int64)
         N.check("avdb_vcf_parse_lines", self.lib.avdb_vcf_parse_lines(
-            self.ctx, tp, nb, n_lines, N.ptr(ws), ws.numel(), N.ptr(lines), N.ptr(rec_off),
+            self.ctx, tp, nb, n_lines, N.ptr(ws0), N.ptr(ws), ws.numel(), N.ptr(lines), N.ptr(rec_off),
             N.ptr(heap_off), s))
         if n_lines:
             tot = torch.stack([rec_off[n_lines], heap_off[n_lines]]).cpu().tolist()

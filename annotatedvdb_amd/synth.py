@@ -154,3 +154,50 @@ def np_spans(n: int, seed: int = 3, lengths=None):
     span = np.where(u < 0.5, 0, np.where(u < 0.8, geo, logu))
     end = np.minimum(start.astype(np.int64) + span, lengths[chrom]).astype(np.int32)
     return chrom, start, end
+
+
+def vcf_text(n_lines: int, seed: int = 6, lengths=None, multi_frac: float = 0.1,
+             rs_frac: float = 0.6, info: bool = True) -> bytes:
+    """dbSNP-shaped VCF data lines (no header): sorted (chrom, pos); 80 % SNV,
+    10 % short indels, 10 % MNV; ``multi_frac`` of lines carry two ALTs; the ID
+    column holds an rsid for ``rs_frac`` of lines, otherwise '.', with RS= in
+    INFO; INFO mimics dbSNP (RS, dbSNPBuildID, SSR, VC, FREQ).  Host-side
+    (numpy PCG64 + one formatting pass), never timed."""
+    from .chromosomes import CHROM_NAMES
+    rng = np.random.Generator(np.random.PCG64(seed))
+    chrom, pos = np_point_snvs(n_lines, seed, lengths)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    u = rng.random(n_lines)
+    klen = np.where(u < 0.8, 1, rng.integers(2, 12, n_lines))
+    rbytes = acgt[rng.integers(0, 4, (n_lines, 12))]
+    abytes = acgt[rng.integers(0, 4, (n_lines, 2, 12))]
+    multi = rng.random(n_lines) < multi_frac
+    has_rs = rng.random(n_lines) < rs_frac
+    rsn = rng.integers(1, 2 * 10 ** 9, n_lines)
+    fq = rng.integers(1, 9999, n_lines)
+    out = []
+    for i in range(n_lines):
+        k = int(klen[i])
+        if u[i] < 0.8:
+            ref, alts = rbytes[i, :1].tobytes(), [abytes[i, 0, :1].tobytes()]
+            if alts[0] == ref:
+                alts[0] = b"T" if ref != b"T" else b"A"
+        elif u[i] < 0.85:      # insertion, anchored
+            ref = rbytes[i, :1].tobytes()
+            alts = [ref + abytes[i, 0, :k].tobytes()]
+        elif u[i] < 0.9:       # deletion, anchored
+            ref = rbytes[i, :k].tobytes()
+            alts = [ref[:1]]
+        else:                  # MNV
+            ref = rbytes[i, :k].tobytes()
+            alts = [abytes[i, 0, :k].tobytes()]
+        if multi[i]:
+            alts.append(abytes[i, 1, :max(1, k - 1)].tobytes())
+        alt = b",".join(alts).decode()
+        rid = "rs%d" % rsn[i] if has_rs[i] else "."
+        vc = "SNV" if u[i] < 0.8 else ("INDEL" if u[i] < 0.9 else "MNV")
+        inf = ("RS=%d;dbSNPBuildID=151;SSR=0;VC=%s;FREQ=1000Genomes:0.%04d,0.%04d"
+               % (rsn[i], vc, 10000 - fq[i], fq[i])) if info else "."
+        out.append("%s\t%d\t%s\t%s\t%s\t.\t.\t%s" % (CHROM_NAMES[chrom[i]], pos[i], rid,
+                                                    ref.decode(), alt, inf))
+    return ("\n".join(out) + "\n").encode()

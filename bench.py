@@ -47,7 +47,11 @@ WORKLOADS = {
     "c5": dict(n=25_000_000, desc="C5: ADSP-style alleles, end inference + bin + grouped PK dedup + "
                                   "long-allele key digests (BASELINE configs[4])",
                bytes_per=None, kernel="k_record_prep"),
+    "vcf": dict(n=8_388_608, desc="SURVEY 8f rank 1: dbSNP-shaped VCF text -> per-ALT record SoA on the "
+                                  "GPU (K0 tokenizer: line split + field parse + multi-allelic explode)",
+                bytes_per=None, kernel="avdb_vcf (whole tokenizer)"),
 }
+VCF_TILE = 1 << 19  # distinct synthetic lines, tiled on the device to n
 
 
 def parse():
@@ -155,6 +159,15 @@ def main():
     elif a.workload in ("c3", "c4"):
         chrom, start, end = synth.spans(n, seed=(3 if a.workload == "c3" else 4) + seed, device=dev,
                                         pieces=pieces, mix=a.workload)
+    elif a.workload == "vcf":
+        tile = synth.vcf_text(min(VCF_TILE, n), seed=6 + seed)
+        reps = -(-n // min(VCF_TILE, n))
+        text = torch.frombuffer(bytearray(tile), dtype=torch.uint8).to(dev).repeat(reps)
+        n = reps * min(VCF_TILE, n)
+        probe = eng.vcf_tokenize(text)
+        n_rec = int(probe.records.n)
+        heap_bytes = int(probe.records.heap.numel())
+        del probe
     else:
         batch = synth.alleles(n, seed=5 + seed, device=dev, pieces=pieces)
         heap_bytes = int(batch.heap.numel())
@@ -180,6 +193,8 @@ def main():
         if a.workload in ("c2", "c3", "c4"):
             timed("bin_assign", record, lambda: eng.bin_assign(
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
+        elif a.workload == "vcf":
+            timed("vcf_tokenize", record, lambda: eng.vcf_tokenize(text))
         else:
             timed("record_prep", record, lambda: eng.record_prep(batch, want_lcp=False, hist=hist,
                                                                  counters=ctr))
@@ -203,8 +218,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, ri, device=dev)
     stage_ms = {k: float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])) for k, v in evs.items()}
-    kname = "bin_assign" if a.workload in ("c2", "c3", "c4") else "record_prep"
+    kname = {"c5": "record_prep", "vcf": "vcf_tokenize"}.get(a.workload, "bin_assign")
     kern_ms = stage_ms[kname]
+    if a.workload == "vcf":
+        n_lines, n = n, n_rec  # the unit is emitted variant records (per-ALT rows)
     total_records = n * ri.world * a.steps
     value = total_records / elapsed
 
@@ -212,6 +229,10 @@ def main():
         # K2 algorithmic bytes per record: in chrom 1 + pos 4 + allele_off 8 + ref_len 4 +
         # alt_len 4 (+ the heap bytes it reads, bounded by the heap); out end 4 + code 4
         bytes_per_launch = n * (1 + 4 + 8 + 4 + 4 + 4 + 4) + heap_bytes
+    elif a.workload == "vcf":
+        # text read once + record SoA written (chrom 1, pos 4, allele_off 8, ref_len 4,
+        # alt_len 4, ext_id 8, rec_line 4, rec_alt 4 = 37 B) + allele heap written
+        bytes_per_launch = int(text.numel()) + 37 * n + heap_bytes
     else:
         bytes_per_launch = n * W["bytes_per"]
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
@@ -246,6 +267,13 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "cpu_baseline": cpu,
     }
+    if a.workload == "vcf":
+        out["dtype"] = "u8"
+        out["data"] = "synthetic dbSNP-shaped VCF text (numpy PCG64 lines tiled on the device)"
+        out["config"].update(lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
+                             records_checked=None)
+        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (5 kernels + "
+                                   "2 host syncs for the line and record totals)")
     if ri.rank == 0:
         print(json.dumps(out), flush=True)
     D.finalize(ri)

@@ -166,6 +166,8 @@ int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
  *      n_lines = n_newlines + (text does not end in '\n').
  *   2. avdb_vcf_parse_lines  -> one avdb_vcf_line per line, plus exclusive prefix sums
  *      rec_off[n_lines+1] / heap_off[n_lines+1] of records and allele-heap bytes.
+ *      `line_counts` is the workspace step 1 filled (its per-workgroup newline
+ *      offsets are reused); NULL recounts.
  *   3. avdb_vcf_emit         -> the record SoA K2/K3/K4 consume (one row per ALT that
  *      is not '.', REF+ALT copied into `heap`), with rec_line/rec_alt back-references.
  * Text cases the GPU does not canonicalise are flagged for the host (flags below). */
@@ -199,7 +201,8 @@ int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes);
 int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
                          size_t workspace_bytes, uint64_t* n_newlines, void* stream);
 int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
-                         void* workspace, size_t workspace_bytes, avdb_vcf_line* lines,
+                         const void* line_counts, void* workspace, size_t workspace_bytes,
+                         avdb_vcf_line* lines,
                          uint64_t* rec_off, uint64_t* heap_off, void* stream);
 int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
                   const avdb_vcf_line* lines, const uint64_t* rec_off, const uint64_t* heap_off,
