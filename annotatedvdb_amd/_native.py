@@ -36,6 +36,7 @@ N_LEVELS = 14
 MAX_CHROM = 64
 DIGEST_CHARS = 32
 MAX_PATH = 128
+VCF_COUNT_WORKSPACE_BYTES = 32768  # AVDB_VCF_COUNT_WORKSPACE_BYTES (include/avdb.h)
 N_COUNTERS = 32
 CTR_STATUS0 = 16
 CTR_RECORDS = 20

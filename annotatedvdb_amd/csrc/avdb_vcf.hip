@@ -40,59 +40,89 @@ constexpr uint64_t kNL = 0x0A0A0A0A0A0A0A0Aull;
 // 8 bytes at aligned address a (bytes outside [lo,hi) read as 0x00)
 __device__ __forceinline__ uint64_t text_word(uintptr_t a, const Heap& h) { return heap_word(a, h); }
 
-// byte range [b0, b1) of the text handled by workgroup `blk` of `nblk` (8-aligned cuts)
-__device__ __forceinline__ void block_range(size_t text_bytes, int blk, int nblk, size_t* b0,
-                                            size_t* b1) {
-  size_t per = (text_bytes + nblk - 1) / nblk;
-  per = (per + 7) & ~size_t(7);
-  *b0 = size_t(blk) * per;
-  *b1 = *b0 + per < text_bytes ? *b0 + per : text_bytes;
-  if (*b0 > text_bytes) *b0 = text_bytes;
+// The text is cut into kVcfGrid * kVcfWaves contiguous, 64-byte-aligned wave
+// sub-chunks; k_vcf_count and k_vcf_starts use the same cut, so the starts pass
+// reads every wave's newline offset instead of recounting.
+constexpr int kVcfWaves = kBlock / kWave;
+constexpr size_t kCountWsBlkOff = 0;                              // u64[kVcfGrid] exclusive
+constexpr size_t kCountWsTotal = 8 * kVcfGrid;                    // u64 total (+pad)
+constexpr size_t kCountWsWave = kCountWsTotal + 256;              // u32[kVcfGrid * kVcfWaves]
+constexpr size_t kCountWsBytes = kCountWsWave + 4 * kVcfGrid * kVcfWaves;
+static_assert(kCountWsBytes <= AVDB_VCF_COUNT_WORKSPACE_BYTES, "count workspace");
+
+__device__ __forceinline__ void wave_range(size_t text_bytes, size_t gw, size_t* t0, size_t* t1) {
+  const size_t nw = size_t(kVcfGrid) * kVcfWaves;
+  size_t per = (text_bytes + nw - 1) / nw;
+  per = (per + 63) & ~size_t(63);
+  *t0 = gw * per < text_bytes ? gw * per : text_bytes;
+  *t1 = *t0 + per < text_bytes ? *t0 + per : text_bytes;
 }
 
-__device__ __forceinline__ uint64_t nl_mask(uintptr_t a, const Heap& h, uintptr_t lo, uintptr_t end) {
-  if (a >= end) return 0;
-  uint64_t m = zero_bytes_mask(text_word(a, h) ^ kNL) & 0x8080808080808080ull;
-  if (a < lo) m &= ~0ull << (8 * (lo - a));
-  if (a + 8 > end) m &= ((1ull << (8 * (end - a))) - 1);
-  return m;
+// newline masks (bit 7 of each '\n' byte) of the 16 bytes at 16-aligned address a,
+// restricted to [lo, end)
+struct Mask16 {
+  uint64_t m0, m1;
+};
+
+__device__ __forceinline__ Mask16 nl_mask16(uintptr_t a, const Heap& h, uintptr_t lo, uintptr_t end) {
+  uint64_t m0 = 0, m1 = 0;
+  if (a >= end) return Mask16{0, 0};
+  uint64_t x, y;
+  if (a >= h.lo && a + 16 <= h.hi) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a));
+    x = uint64_t(v[0]) | uint64_t(v[1]) << 32;
+    y = uint64_t(v[2]) | uint64_t(v[3]) << 32;
+  } else {
+    x = text_word(a, h);
+    y = text_word(a + 8, h);
+  }
+  m0 = zero_bytes_mask(x ^ kNL) & 0x8080808080808080ull;
+  m1 = zero_bytes_mask(y ^ kNL) & 0x8080808080808080ull;
+  if (a < lo) {
+    const uint32_t sh = uint32_t(lo - a);  // 1..15 bytes before the range
+    if (sh >= 8) { m0 = 0; m1 &= ~low_bytes_mask(sh - 8); }
+    else m0 &= ~low_bytes_mask(sh);
+  }
+  if (a + 16 > end) {
+    const uint32_t keep = uint32_t(end - a);  // 1..15 bytes inside the range
+    if (keep <= 8) { m1 = 0; m0 &= low_bytes_mask(keep); }
+    else m1 &= low_bytes_mask(keep - 8);
+  }
+  return Mask16{m0, m1};
 }
 
-constexpr int kNlUnroll = 4;  // 512-byte wave steps in flight per wave
+constexpr int kNlUnroll = 4;                           // 16-byte lane loads in flight
+constexpr uintptr_t kNlStep = 16 * kWave;              // bytes per wave load
 
 __global__ __launch_bounds__(kBlock) void k_vcf_count(const uint8_t* __restrict__ text,
                                                       size_t text_bytes,
-                                                      unsigned long long* __restrict__ blk_counts) {
-  __shared__ unsigned long long s_sum;
-  if (threadIdx.x == 0) s_sum = 0;
-  __syncthreads();
+                                                      uint32_t* __restrict__ wave_cnt) {
   const Heap h = make_heap(text, text_bytes);
-  size_t b0, b1;
-  block_range(text_bytes, blockIdx.x, gridDim.x, &b0, &b1);
-  // threads stride over 8-byte words of the block's chunk (coalesced), kNlUnroll
-  // independent loads per lane per trip
+  const size_t gw = size_t(blockIdx.x) * kVcfWaves + threadIdx.x / kWave;
+  size_t t0, t1;
+  wave_range(text_bytes, gw, &t0, &t1);
+  const uintptr_t lo = h.lo + t0, end = h.lo + t1;
   uint32_t c = 0;
-  const uintptr_t lo = h.lo + b0, end = h.lo + b1;
-  const uintptr_t step = 8 * blockDim.x;
-  for (uintptr_t a = (lo & ~uintptr_t(7)) + 8 * threadIdx.x; a < end; a += kNlUnroll * step) {
-    uint64_t m[kNlUnroll];
+  for (uintptr_t a = (lo & ~uintptr_t(15)) + 16 * __lane_id(); a < end; a += kNlUnroll * kNlStep) {
+    Mask16 m[kNlUnroll];
 #pragma unroll
-    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask(a + u * step, h, lo, end);
+    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask16(a + u * kNlStep, h, lo, end);
 #pragma unroll
-    for (int u = 0; u < kNlUnroll; ++u) c += uint32_t(__popcll(m[u]));
+    for (int u = 0; u < kNlUnroll; ++u) c += uint32_t(__popcll(m[u].m0) + __popcll(m[u].m1));
   }
-  for (int d = 32; d > 0; d >>= 1) c += __shfl_down(c, d, kWave);
-  if (__lane_id() == 0 && c) atomicAdd(&s_sum, (unsigned long long)c);
-  __syncthreads();
-  if (threadIdx.x == 0) blk_counts[blockIdx.x] = s_sum;
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
+  if (__lane_id() == 0) wave_cnt[gw] = c;
 }
 
-// exclusive scan of kVcfGrid block counts (one workgroup of kVcfGrid threads)
-__global__ __launch_bounds__(kVcfGrid) void k_vcf_scan_blocks(unsigned long long* __restrict__ c,
+// per-workgroup newline totals -> exclusive offsets (one workgroup of kVcfGrid threads)
+__global__ __launch_bounds__(kVcfGrid) void k_vcf_scan_blocks(const uint32_t* __restrict__ wave_cnt,
+                                                              unsigned long long* __restrict__ blk_off,
                                                               unsigned long long* __restrict__ total) {
   __shared__ unsigned long long s[kVcfGrid];
   const int t = threadIdx.x;
-  const unsigned long long v = c[t];
+  unsigned long long v = 0;
+#pragma unroll
+  for (int w = 0; w < kVcfWaves; ++w) v += wave_cnt[t * kVcfWaves + w];
   s[t] = v;
   __syncthreads();
   for (int d = 1; d < kVcfGrid; d <<= 1) {
@@ -101,7 +131,7 @@ __global__ __launch_bounds__(kVcfGrid) void k_vcf_scan_blocks(unsigned long long
     s[t] += x;
     __syncthreads();
   }
-  c[t] = s[t] - v;
+  blk_off[t] = s[t] - v;
   if (t == kVcfGrid - 1 && total) *total = s[t];
 }
 
@@ -110,65 +140,51 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
 }
 
-// line starts in order: line 0 starts at 0, line k+1 after the k-th newline.
-// Each wave owns a contiguous, 8-aligned sub-chunk of its workgroup's chunk.
+// line starts in order: line 0 starts at 0, line k+1 after the k-th newline.  Each
+// wave walks its sub-chunk once; a lane's newline count (0..16) is ranked inside the
+// wave with 5 ballots.
 __global__ __launch_bounds__(kBlock) void k_vcf_starts(const uint8_t* __restrict__ text,
                                                        size_t text_bytes,
                                                        const unsigned long long* __restrict__ blk_off,
+                                                       const uint32_t* __restrict__ wave_cnt,
                                                        size_t n_lines,
                                                        uint64_t* __restrict__ starts) {
-  constexpr int kWaves = kBlock / kWave;
-  __shared__ unsigned long long s_w[kWaves];
   const Heap h = make_heap(text, text_bytes);
-  size_t b0, b1;
-  block_range(text_bytes, blockIdx.x, gridDim.x, &b0, &b1);
   const int wave = threadIdx.x / kWave, lane = __lane_id();
-  const size_t len = b1 > b0 ? b1 - b0 : 0;
-  size_t per = (len + kWaves - 1) / kWaves;
-  per = (per + 7) & ~size_t(7);
-  size_t t0 = b0 + per * wave, t1 = t0 + per;
-  if (t0 > b1) t0 = b1;
-  if (t1 > b1) t1 = b1;
-  const uintptr_t lo = h.lo + t0, end = h.lo + t1;
-  const uintptr_t a_first = lo & ~uintptr_t(7);
-  // pass 1: newlines in this wave's sub-chunk
-  uint32_t c = 0;
-  for (uintptr_t a = a_first + 8 * lane; a < end; a += kNlUnroll * 8 * kWave) {
-    uint64_t m[kNlUnroll];
-#pragma unroll
-    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask(a + u * 8 * kWave, h, lo, end);
-#pragma unroll
-    for (int u = 0; u < kNlUnroll; ++u) c += uint32_t(__popcll(m[u]));
-  }
-  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
-  if (lane == 0) s_w[wave] = c;
-  __syncthreads();
+  const size_t gw = size_t(blockIdx.x) * kVcfWaves + wave;
+  size_t t0, t1;
+  wave_range(text_bytes, gw, &t0, &t1);
   unsigned long long k = blk_off[blockIdx.x];  // newlines before t0
-  for (int w = 0; w < wave; ++w) k += s_w[w];
-  if (blockIdx.x == 0 && threadIdx.x == 0 && n_lines) starts[0] = 0;
-  // pass 2: rank every newline inside the wave (lane counts are 0..8: 4 ballots)
-  for (uintptr_t a0 = a_first; a0 < end; a0 += kNlUnroll * 8 * kWave) {
-    uint64_t m[kNlUnroll];
+  for (int w = 0; w < wave; ++w) k += wave_cnt[size_t(blockIdx.x) * kVcfWaves + w];
+  if (gw == 0 && lane == 0 && n_lines) starts[0] = 0;
+  const uintptr_t lo = h.lo + t0, end = h.lo + t1;
+  for (uintptr_t a0 = lo & ~uintptr_t(15); a0 < end; a0 += kNlUnroll * kNlStep) {
+    Mask16 m[kNlUnroll];
 #pragma unroll
-    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask(a0 + u * 8 * kWave + 8 * lane, h, lo, end);
+    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask16(a0 + u * kNlStep + 16 * lane, h, lo, end);
 #pragma unroll
     for (int u = 0; u < kNlUnroll; ++u) {
-      const uint32_t cnt = uint32_t(__popcll(m[u]));
+      const uint32_t cnt = uint32_t(__popcll(m[u].m0) + __popcll(m[u].m1));
       uint32_t below = 0, total = 0;
 #pragma unroll
-      for (int bit = 0; bit < 4; ++bit) {
+      for (int bit = 0; bit < 5; ++bit) {
         const uint64_t b = __ballot((cnt >> bit) & 1u);
         below += lanes_below(b) << bit;
         total += uint32_t(__popcll(b)) << bit;
       }
-      unsigned long long kk = k + below;
-      const size_t wbase = size_t(a0 + u * 8 * kWave + 8 * lane - h.lo);
-      uint64_t mm = m[u];
-      while (mm) {
-        const int bitpos = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        if (kk + 1 < n_lines) starts[kk + 1] = wbase + size_t(bitpos >> 3) + 1;
-        ++kk;
+      if (cnt) {
+        unsigned long long kk = k + below;
+        const size_t wbase = size_t(a0 + u * kNlStep + 16 * lane - h.lo);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          uint64_t mm = half ? m[u].m1 : m[u].m0;
+          while (mm) {
+            const int bitpos = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            if (kk + 1 < n_lines) starts[kk + 1] = wbase + 8 * half + size_t(bitpos >> 3) + 1;
+            ++kk;
+          }
+        }
       }
       k += total;
     }
@@ -235,9 +251,16 @@ __device__ uint64_t rs_number(const uint8_t* p, uint32_t n) {
   return v;
 }
 
-// one line: s points at its first byte (LDS or global), raw = bytes up to its newline
-__device__ __forceinline__ void parse_line(const uint8_t* s, uint32_t len, avdb_vcf_line& L,
-                                           uint64_t& recs, uint64_t& hbytes) {
+constexpr uint64_t kHiBits = 0x8080808080808080ull;
+constexpr uint64_t kTab = 0x0909090909090909ull;
+constexpr uint64_t kSemi = 0x3B3B3B3B3B3B3B3Bull;
+
+// one line: s points at its first byte (LDS or global), len = bytes up to its
+// newline; word_at/mis give the same bytes as aligned 8-byte words (SWAR scans)
+template <class WordAt>
+__device__ __forceinline__ void parse_line(const uint8_t* s, const WordAt& word_at, uint32_t mis,
+                                           uint32_t len, avdb_vcf_line& L, uint64_t& recs,
+                                           uint64_t& hbytes) {
     while (len && is_ws(s[len - 1])) --len;  // str.rstrip()
     L.len = len;
     L.flags = 0;
@@ -254,13 +277,26 @@ __device__ __forceinline__ void parse_line(const uint8_t* s, uint32_t len, avdb_
     if (len && s[0] == '#') L.flags |= AVDB_VCF_COMMENT;
     if (!len) L.flags |= AVDB_VCF_EMPTY;
     // tab-separated fields (first 8 starts; INFO ends at the 8th tab or the end)
-    for (uint32_t i = 0; i < len; ++i) {
-      if (s[i] == '\t') {
+    {
+      const uint32_t k1 = (len + mis + 7) >> 3;
+      for (uint32_t k = 0; k < k1; ++k) {
+        uint64_t m = zero_bytes_mask(word_at(k) ^ kTab) & kHiBits;
+        if (k == 0) m &= ~low_bytes_mask(mis);
+        const uint32_t hi = len + mis - 8 * k;
+        if (hi < 8) m &= low_bytes_mask(hi);
+        if (nf > 8) {  // past INFO: only the count matters
+          nf += uint32_t(__popcll(m));
+          continue;
+        }
+        while (m) {
+          const uint32_t i = 8 * k + (uint32_t(__builtin_ctzll(m)) >> 3) - mis;
+          m &= m - 1;
 #pragma unroll
-        for (int k = 1; k < 8; ++k)  // register-resident field table (no dynamic index)
-          if (nf == uint32_t(k)) L.field[k] = i + 1;
-        if (nf == 8) L.field_end8 = i;
-        ++nf;
+          for (int f = 1; f < 8; ++f)  // register-resident field table (no dynamic index)
+            if (nf == uint32_t(f)) L.field[f] = i + 1;
+          if (nf == 8) L.field_end8 = i;
+          ++nf;
+        }
       }
     }
     L.n_fields = nf;
@@ -313,17 +349,36 @@ __device__ __forceinline__ void parse_line(const uint8_t* s, uint32_t len, avdb_
         } else {
           // INFO: last entry whose key is exactly "RS" (dict(...) keeps the last)
           const uint8_t* inf = s + L.field[7];
-          const uint32_t in = fend(7) - L.field[7];
+          const uint32_t f7 = L.field[7], e7 = fend(7);
           int64_t vs = -1, ve = -1;
           bool bare = false;
-          for (uint32_t i = 0; i < in;) {
-            uint32_t j = i;
-            while (j < in && inf[j] != ';') ++j;
+          // entries are [i, j) between ';' (INFO-relative), scanned 8 bytes at a time
+          uint32_t i = 0;
+          const uint32_t in = e7 >= f7 ? e7 - f7 : 0;
+          for (uint32_t at = 0; at <= in;) {
+            // next ';' at or after `at` (SWAR), or the INFO end
+            uint32_t j = in;
+            {
+              const uint32_t from = f7 + at, to = e7;
+              const uint32_t k1 = (to + mis + 7) >> 3;
+              for (uint32_t k = (from + mis) >> 3; k < k1; ++k) {
+                uint64_t m = zero_bytes_mask(word_at(k) ^ kSemi) & kHiBits;
+                const int32_t lo = int32_t(from + mis) - int32_t(8 * k);
+                if (lo > 0) m &= ~low_bytes_mask(uint32_t(lo));
+                const uint32_t hi = to + mis - 8 * k;
+                if (hi < 8) m &= low_bytes_mask(hi);
+                if (m) {
+                  j = 8 * k + (uint32_t(__builtin_ctzll(m)) >> 3) - mis - f7;
+                  break;
+                }
+              }
+            }
             if (j - i >= 2 && inf[i] == 'R' && inf[i + 1] == 'S') {
               if (j - i == 2) { bare = true; vs = ve = -1; }
               else if (inf[i + 2] == '=') { bare = false; vs = i + 3; ve = j; }
             }
             i = j + 1;
+            at = j + 1;
           }
           if (vs >= 0 || bare) {
             L.flags |= AVDB_VCF_INFO_RS;
@@ -410,11 +465,16 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
       const size_t next = li + 1 < n_lines ? starts[li + 1] - 1 : text_bytes;  // newline or end
       const uint32_t raw = uint32_t(next - L.start);
       uint64_t recs, hbytes;
-      if (w.staged)
-        parse_line(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0), raw, L, recs,
-                   hbytes);
-      else
-        parse_line(text + L.start, raw, L, recs, hbytes);
+      const uint32_t mis = uint32_t((h.lo + L.start) & 7);
+      if (w.staged) {
+        const uint8_t* ls = reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0);
+        const uint64_t* lw = reinterpret_cast<const uint64_t*>(ls - mis);
+        parse_line(ls, [lw](uint32_t k) { return lw[k]; }, mis, raw, L, recs, hbytes);
+      } else {
+        const uintptr_t la = h.lo + L.start - mis;
+        parse_line(text + L.start, [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); },
+                   mis, raw, L, recs, hbytes);
+      }
       lines[li] = L;
       rec_cnt[li] = recs;
       heap_cnt[li] = hbytes;
@@ -497,6 +557,19 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
 
 using namespace avdb;
 
+// k_vcf_count + k_vcf_scan_blocks into a count workspace (layout: kCountWs*)
+static int count_pass(const uint8_t* text, size_t text_bytes, void* ws, unsigned long long* total,
+                      hipStream_t s) {
+  char* w = static_cast<char*>(ws);
+  auto* wave = reinterpret_cast<uint32_t*>(w + kCountWsWave);
+  auto* blk = reinterpret_cast<unsigned long long*>(w + kCountWsBlkOff);
+  hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, wave);
+  AVDB_LAUNCH_CHECK("k_vcf_count");
+  hipLaunchKernelGGL(k_vcf_scan_blocks, dim3(1), dim3(kVcfGrid), 0, s, wave, blk, total);
+  AVDB_LAUNCH_CHECK("k_vcf_scan_blocks");
+  return AVDB_OK;
+}
+
 static size_t scan_temp_bytes(size_t n) {
   size_t t = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, static_cast<const unsigned long long*>(nullptr),
@@ -507,8 +580,9 @@ static size_t scan_temp_bytes(size_t n) {
 extern "C" int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes) {
   (void)text_bytes;
   if (!bytes) return AVDB_EINVAL;
-  // block counts | total | line starts | scan temp
-  *bytes = 8 * kVcfGrid + 256 + ((8 * n_lines + 255) & ~size_t(255)) + scan_temp_bytes(n_lines + 1) + 256;
+  // count workspace | line starts | scan temp
+  *bytes = AVDB_VCF_COUNT_WORKSPACE_BYTES + ((8 * n_lines + 255) & ~size_t(255)) +
+           scan_temp_bytes(n_lines + 1) + 256;
   return AVDB_OK;
 }
 
@@ -516,20 +590,14 @@ extern "C" int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
                                     void* workspace, size_t workspace_bytes, uint64_t* n_newlines,
                                     void* stream) {
   if (!ctx || !n_newlines) { avdb_set_error("avdb_vcf_count_lines: null argument"); return AVDB_EINVAL; }
-  if (!workspace || workspace_bytes < 8 * kVcfGrid + 256) {
+  if (!workspace || workspace_bytes < AVDB_VCF_COUNT_WORKSPACE_BYTES) {
     avdb_set_error("avdb_vcf_count_lines: workspace too small");
     return AVDB_ERANGE;
   }
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (text_bytes == 0) return hipMemsetAsync(n_newlines, 0, 8, s) == hipSuccess ? AVDB_OK : AVDB_EHIP;
-  auto* blk = static_cast<unsigned long long*>(workspace);
-  hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk);
-  AVDB_LAUNCH_CHECK("k_vcf_count");
-  hipLaunchKernelGGL(k_vcf_scan_blocks, dim3(1), dim3(kVcfGrid), 0, s, blk,
-                     reinterpret_cast<unsigned long long*>(n_newlines));
-  AVDB_LAUNCH_CHECK("k_vcf_scan_blocks");
-  return AVDB_OK;
+  return count_pass(text, text_bytes, workspace, reinterpret_cast<unsigned long long*>(n_newlines), s);
 }
 
 extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes,
@@ -550,22 +618,18 @@ extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
   if (n_lines == 0) return AVDB_OK;
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  auto* blk = static_cast<unsigned long long*>(workspace);
-  auto* starts = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + 8 * kVcfGrid + 256);
+  auto* starts = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + AVDB_VCF_COUNT_WORKSPACE_BYTES);
   void* tmp = reinterpret_cast<char*>(starts) + ((8 * n_lines + 255) & ~size_t(255));
   size_t tmp_bytes = scan_temp_bytes(n_lines + 1);
-  const unsigned long long* blk_off = static_cast<const unsigned long long*>(line_counts);
-  if (!blk_off) {
-    // block newline counts -> exclusive offsets (same partition as k_vcf_starts)
-    hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk);
-    AVDB_LAUNCH_CHECK("k_vcf_count");
-    hipLaunchKernelGGL(k_vcf_scan_blocks, dim3(1), dim3(kVcfGrid), 0, s, blk,
-                       static_cast<unsigned long long*>(nullptr));
-    AVDB_LAUNCH_CHECK("k_vcf_scan_blocks");
-    blk_off = blk;
+  const char* cw = static_cast<const char*>(line_counts);
+  if (!cw) {  // recount into the front of this workspace (same cut as k_vcf_starts)
+    const int rc = count_pass(text, text_bytes, workspace, nullptr, s);
+    if (rc != AVDB_OK) return rc;
+    cw = static_cast<const char*>(workspace);
   }
-  hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk_off,
-                     n_lines, starts);
+  hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes,
+                     reinterpret_cast<const unsigned long long*>(cw + kCountWsBlkOff),
+                     reinterpret_cast<const uint32_t*>(cw + kCountWsWave), n_lines, starts);
   AVDB_LAUNCH_CHECK("k_vcf_starts");
   auto* rc = reinterpret_cast<unsigned long long*>(rec_off);
   auto* hc = reinterpret_cast<unsigned long long*>(heap_off);

@@ -354,7 +354,7 @@ class Engine:
         nb = int(text_t.numel())
         tp = N.ptr(text_t) if nb else None
         s = self._stream()
-        ws0 = self.empty(8 * 1024 + 256, torch.uint8)
+        ws0 = self.empty(N.VCF_COUNT_WORKSPACE_BYTES, torch.uint8)
         nl = torch.zeros(1, dtype=torch.int64, device=self.device)
         N.check("avdb_vcf_count_lines", self.lib.avdb_vcf_count_lines(
             self.ctx, tp, nb, N.ptr(ws0), ws0.numel(), N.ptr(nl), s))

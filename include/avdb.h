@@ -197,6 +197,7 @@ typedef struct avdb_vcf_line {
   uint8_t pad[3];
 } avdb_vcf_line;
 
+#define AVDB_VCF_COUNT_WORKSPACE_BYTES 32768u /* workspace of avdb_vcf_count_lines */
 int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes);
 int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
                          size_t workspace_bytes, uint64_t* n_newlines, void* stream);
