@@ -366,6 +366,223 @@ def dedup_keep(keys: Sequence) -> List[int]:
 
 
 # ---------------------------------------------------------------------------
+# §8f rank 3: display attributes
+#   variant_annotator.py:134-241 (get_display_attributes), with the external
+#   GenomicsDBData helpers it calls restated as published:
+#   truncate(s, n) = s if len(s) <= n else s[:n] + '...', reverse(s) = s[::-1].
+#   Returns the dict in the reference's insertion order (dict.update() of an
+#   existing key keeps its position).
+# ---------------------------------------------------------------------------
+def _truncate(s: str, n: int) -> str:
+    return s if len(s) <= n else s[:n] + "..."
+
+
+def _trunc_allele(s: str, long: bool = False) -> str:  # variant_annotator.py:8-10
+    return _truncate(s, 100) if long else _truncate(s, 8)
+
+
+def normalized_alleles(ref: str, alt: str, snv_div_minus: bool = False) -> Tuple[str, str]:
+    """variant_annotator.py:82-121."""
+    if len(ref) == 1 and len(alt) == 1:
+        return ref, alt
+    lcp = 0
+    while lcp < len(ref) and lcp < len(alt) and ref[lcp] == alt[lcp]:
+        lcp += 1
+    if lcp == 0:
+        return ref, alt
+    nref, nalt = ref[lcp:], alt[lcp:]
+    if snv_div_minus:
+        nref = nref or "-"
+        nalt = nalt or "-"
+    return nref, nalt
+
+
+def display_attributes(chrom: str, pos: int, ref: str, alt: str) -> dict:
+    """variant_annotator.py:134-241 (position is the int VCF POS)."""
+    r, a = len(ref), len(alt)
+    nref_acc, nalt_acc = normalized_alleles(ref, alt)
+    nr, na = len(nref_acc), len(nalt_acc)
+    nref, nalt = normalized_alleles(ref, alt, True)
+    end, _ = infer_end(pos, ref, alt)
+    at = {"location_start": pos, "location_end": pos}
+    nmid = ":".join((str(chrom), str(pos), nref, nalt))
+    if nmid != metaseq_id(chrom, pos, ref, alt):
+        at["normalized_metaseq_id"] = nmid
+    if r == 1 and a == 1:
+        at.update(variant_class="single nucleotide variant", variant_class_abbrev="SNV",
+                  display_allele=ref + ">" + alt, sequence_allele=ref + "/" + alt)
+    elif r == a:
+        if ref == alt[::-1]:
+            at.update(variant_class="inversion", variant_class_abbrev="MNV", display_allele="inv" + ref,
+                      sequence_allele=_trunc_allele(ref) + "/" + _trunc_allele(alt), location_end=end)
+        else:
+            at.update(variant_class="substitution", variant_class_abbrev="MNV",
+                      display_allele=nref + ">" + nalt,
+                      sequence_allele=_trunc_allele(nref) + "/" + _trunc_allele(nalt),
+                      location_start=pos, location_end=end)
+    elif na >= 1:
+        at["location_start"] = pos + 1
+        orig = ref[1:]
+        ndup = orig.count(nalt)
+        dup = orig == nalt or (ndup > 0 and len(orig) / ndup == len(nalt))
+        pre = "dup" if dup else "ins"
+        if nr >= 1:
+            at.update(location_end=end, display_allele="del" + _trunc_allele(nref, True) + pre +
+                      _trunc_allele(nalt, True), sequence_allele=_trunc_allele(nref) + "/" +
+                      _trunc_allele(nalt), variant_class="indel", variant_class_abbrev="INDEL")
+        elif end != pos + 1:
+            at.update(location_end=end, display_allele="del" + _trunc_allele(orig, True) + pre +
+                      _trunc_allele(nalt, True), sequence_allele=_trunc_allele(nref) + "/" +
+                      _trunc_allele(nalt), variant_class="indel", variant_class_abbrev="INDEL")
+        else:
+            at.update(location_end=pos + 1, display_allele=pre + _trunc_allele(nalt, True),
+                      sequence_allele=pre + _trunc_allele(nalt),
+                      variant_class="duplication" if dup else "insertion",
+                      variant_class_abbrev=pre.upper())
+    else:
+        at.update(variant_class="deletion", variant_class_abbrev="DEL", location_end=end,
+                  location_start=pos + 1, display_allele="del" + _trunc_allele(nref, True),
+                  sequence_allele=_trunc_allele(nref) + "/-")
+    return at
+
+
+# ---------------------------------------------------------------------------
+# §8f rank 2: INFO FREQ -> allele_frequencies, COPY row, .mapping line
+#   vcf_parser.py:76-114 (INFO parse: '\x2c'->',', '\x59'->'/', '#'->':',
+#   split ';', first '=', numeric coercion), :200-222 (get_frequencies),
+#   vcf_variant_loader.py:320-346 (COPY values, '#'-joined), load_vcf_file.py:116-117
+#   (mapping line = variant id TAB str(list of dicts)).
+# ---------------------------------------------------------------------------
+def to_numeric(value):
+    """GenomicsDBData ``to_numeric``: int, else float, else unchanged."""
+    try:
+        return int(value)
+    except (ValueError, TypeError):
+        try:
+            return float(value)
+        except (ValueError, TypeError):
+            return value
+
+
+def parse_info(info: str) -> dict:
+    s = info.replace("\\x2c", ",").replace("\\x59", "/").replace("#", ":")
+    d = dict(item.split("=", 1) if "=" in item else [item, True] for item in s.split(";"))
+    return {k: (to_numeric(v) if isinstance(v, str) else v) for k, v in d.items()}
+
+
+def frequencies(info: dict, alt_field: str, allele: str):
+    """vcf_parser.py:200-222; raises like the reference on malformed FREQ."""
+    g = info.get("FREQ")
+    if g is None:
+        return None
+    alts = alt_field.split(",")
+    k = alts.index(allele) + 1
+    popf = {p.split(":")[0]: p.split(":")[1] for p in g.split("|")}
+    out = {pop: {"gmaf": to_numeric(f.split(",")[k])} for pop, f in popf.items()
+           if f.split(",")[k] not in (".", "0")}
+    return None if not out else out
+
+
+def xstr_json(value, nullStr="", falseAsNull=False) -> str:
+    """``xstr`` as applied to the COPY values: None -> nullStr, False -> nullStr
+    with falseAsNull, dicts -> ``json.dumps`` (the JSONB columns'
+    serialisation), else ``str``."""
+    import json
+    if value is None:
+        return nullStr
+    if falseAsNull and value is False:
+        return nullStr
+    if isinstance(value, (dict, list)):
+        return json.dumps(value)
+    return str(value)
+
+
+def copy_row(chrom: str, pos: int, ref: str, alt: str, pk: str, bin_path: str, alg_id,
+             ref_snp_id: Optional[str], is_multi: bool, freq) -> str:
+    """One COPY line (vcf_variant_loader.py:320-343), without the newline."""
+    return "#".join(["chr" + chrom, pk, str(pos), metaseq_id(chrom, pos, ref, alt), bin_path,
+                     xstr_json(alg_id), xstr_json(ref_snp_id, nullStr="NULL"),
+                     xstr_json(is_multi, falseAsNull=True, nullStr="NULL"),
+                     xstr_json(display_attributes(chrom, pos, ref, alt), nullStr="NULL"),
+                     xstr_json(freq, nullStr="NULL")])
+
+
+def mapping_line(variant_id: str, mapping: List[dict]) -> str:
+    """load_vcf_file.py:116-117: ``print(id, pk, sep='\\t')``."""
+    return "%s\t%s" % (variant_id, mapping)
+
+
+VCF_FIELDS = ["chrom", "pos", "id", "ref", "alt", "qual", "filter", "info"]
+
+
+def parse_vcf_line(line: str) -> dict:
+    """VcfEntryParser.parse_entry (vcf_parser.py:76-114) + get_variant /
+    get_refsnp (:127-169).  Raises what the reference raises."""
+    values = line.split("\t")
+    try:
+        entry = dict(zip(VCF_FIELDS, values)) if len(values) == len(VCF_FIELDS) \
+            else {f: values[i] for i, f in enumerate(VCF_FIELDS)}
+        ent = {k: to_numeric(v) for k, v in entry.items()}
+        if "info" in ent:
+            ent["info"] = parse_info(ent["info"])
+    except IndexError:
+        raise IndexError("The number of fields in the VCF entry do not match")
+    except Exception as err:  # noqa: BLE001 — the reference wraps everything else
+        raise ImportError(str(err))
+    chrom = xstr(ent["chrom"])
+    if chrom == "MT":
+        chrom = "M"
+    alts = ent["alt"].split(",")
+    vid = ent["id"]
+    if vid == "." or vid.startswith("rs"):
+        vid = ":".join((chrom.replace("chr", ""), xstr(ent["pos"]), ent["ref"], ent["alt"]))
+    if "rs" in ent["id"]:
+        rs = ent["id"]
+    elif "RS" in ent["info"]:
+        rs = "rs" + str(ent["info"]["RS"])
+    else:
+        rs = None
+    return {"id": vid, "ref_snp_id": rs, "ref": ent["ref"], "alt_field": ent["alt"], "alts": alts,
+            "is_multi": len(alts) > 1, "chromosome": xstr(chrom).replace("chr", ""),
+            "position": int(ent["pos"]), "info": ent["info"]}
+
+
+def load_line(line: str, lengths: Sequence[int], alg_id="1", max_len: int = MAX_SEQUENCE_LENGTH):
+    """One line of the load driver (load_vcf_file.py:101-119 ->
+    VCFVariantLoader.parse_variant, vcf_variant_loader.py:259-391, short keys
+    only).  Returns ``(error_type_name | None, mapping_lines, copy_rows)``;
+    on an error the rows written before it are returned too."""
+    rows: List[str] = []
+    try:
+        v = parse_vcf_line(line.rstrip())
+        mapping = []
+        for alt in v["alts"]:
+            if alt == ".":
+                continue
+            ms = metaseq_id(v["chromosome"], v["position"], v["ref"], alt)
+            if len(ms.split(":")) != 4:
+                raise ValueError("too many values to unpack")
+            if is_long(v["ref"], alt, max_len):
+                raise ValueError("long allele: VRS digest (parity unpinned)")
+            pk = primary_key(v["chromosome"], v["position"], v["ref"], alt, v["ref_snp_id"], max_len=max_len)
+            end, _ = infer_end(v["position"], v["ref"], alt)
+            chrm = v["chromosome"] if "chr" in v["chromosome"] else "chr" + v["chromosome"]
+            name = chrm[3:] if chrm.startswith("chr") else None
+            L = lengths[CHROM_NAMES.index(name)] if name in CHROM_NAMES else None
+            code, _ = bin_code(L, v["position"], end)
+            if code == BIN_NONE:
+                raise TypeError("'NoneType' object is not subscriptable")
+            path = format_bin_path(name, code)
+            freq = frequencies(v["info"], v["alt_field"], alt)
+            rows.append(copy_row(v["chromosome"], v["position"], v["ref"], alt, pk, path, alg_id,
+                                 v["ref_snp_id"], v["is_multi"], freq))
+            mapping.append({"primary_key": pk, "bin_index": path})
+        return None, [mapping_line(v["id"], mapping)], rows
+    except Exception as err:  # noqa: BLE001
+        return type(err).__name__, [], rows
+
+
+# ---------------------------------------------------------------------------
 # L8 histogram (per-shard counters all-gathered across GPUs, SURVEY.md §8e)
 # ---------------------------------------------------------------------------
 L8_WIDTH = INC[8]

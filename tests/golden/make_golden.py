@@ -506,6 +506,137 @@ def run_loader(lines):
     return rows
 
 
+FREQ_VALUES = ["0.9990", "0.0010", "0", ".", "1", "0.0", "0.00001", "0.0001", "12.50", "5.", ".5",
+               "007", "00", "0.5", "0.123456789012345", "0.1234567890123456", "1e-05", "-0.5", "nan",
+               "0.9986", "0.001353", "0.01861", "0.0005901", "100.0", "1234567890123456789.5"]
+POPS = ["GnomAD", "Korea1K", "dbGaP_PopFreq", "1000Genomes", "TOPMED", "ALSPAC", "TWINSUK"]
+
+
+def gen_freq(rng, nalt):
+    """An INFO FREQ value; mostly well-formed (one ref + one value per ALT),
+    sometimes short (IndexError in the reference), duplicate populations, or
+    pathological entries."""
+    u = rng.random()
+    pops = rng.sample(POPS, rng.randint(1, 4))
+    if u < 0.03:
+        pops.append(pops[0])  # duplicate population: dict keeps the last value
+    items = []
+    for p in pops:
+        nv = nalt + 1 if rng.random() > 0.03 else nalt  # short list -> IndexError
+        vals = [rng.choice(FREQ_VALUES) if rng.random() < 0.3 else "0.%04d" % rng.randint(0, 9999)
+                for _ in range(nv)]
+        items.append(p + ":" + ",".join(vals))
+    v = "|".join(items)
+    if rng.random() < 0.01:
+        v = v.replace(":", "", 1)  # population without ':' -> IndexError
+    return v
+
+
+def gen_load_lines(n, rng):
+    """VCF lines for the full load-driver output (COPY rows + .mapping line):
+    dbSNP-like INFO with FREQ, every allele class, multi-allelic and repeated
+    ALTs, symbolic alleles, refSNP from ID or INFO, short alleles (ref+alt <= 50,
+    so every primary key is pinnable)."""
+    tot = sum(GRCH38_LENGTHS.values())
+    weights = [GRCH38_LENGTHS[c] / tot for c in CHROM_NAMES]
+    recs = []
+    for _ in range(n):
+        c = rng.choices(CHROM_NAMES, weights)[0]
+        L = GRCH38_LENGTHS[c]
+        u = rng.random()
+        pos = rng.randint(1, L) if u > 0.01 else rng.choice([1, 2, L, L - 1, 15625, 15626])
+        recs.append((c, pos))
+    recs.sort(key=lambda r: (CHROM_NAMES.index(r[0]), r[1]))
+    lines = []
+    for c, pos in recs:
+        nalt = 1 if rng.random() < 0.85 else rng.randint(2, 4)
+        ref, alt0 = gen_allele_pair(rng)
+        alts = [alt0] + [gen_allele_pair(rng)[1] for _ in range(nalt - 1)]
+        u = rng.random()
+        if u < 0.02:
+            alts = ["."]
+        elif u < 0.04 and nalt > 1:
+            alts[1] = alts[0]  # repeated ALT: altAlleles.index() finds the first
+        elif u < 0.06:
+            alts.append(".")
+        elif u < 0.09:  # tandem duplications / repeats (dup vs ins display class)
+            unit = rand_allele(rng, rng.randint(1, 4))
+            ref = rand_allele(rng, 1) + unit * rng.randint(1, 4)
+            alts = [ref + unit * rng.randint(1, 2)]
+        elif u < 0.11:  # long-ish deletions / insertions (display truncation at 8)
+            ref = rand_allele(rng, rng.randint(9, 30))
+            alts = [ref[0]] if rng.random() < 0.5 else [ref + rand_allele(rng, rng.randint(1, 15))]
+        alts = [a for a in alts if len(ref) + len(a) <= 50] or [ref[0] if ref else "A"]
+        u = rng.random()
+        vid = ("rs%d" % rng.randint(1, 10**9)) if u < 0.55 else ("." if u < 0.85 else "id%d" % rng.randint(1, 999))
+        info = []
+        if rng.random() < 0.4:
+            info.append("RS=%d" % rng.randint(1, 10**9))
+        info.append("dbSNPBuildID=151")
+        if rng.random() < 0.7:
+            info.append("FREQ=" + gen_freq(rng, len(alts)))
+        elif rng.random() < 0.02:
+            info.append("FREQ")
+        if rng.random() < 0.3:
+            info.append("VC=SNV")
+        cs = rng.choice([c, "chr" + c]) if c != "M" else rng.choice(["M", "MT", "chrM"])
+        lines.append("\t".join([cs, str(pos), vid, ref, ",".join(alts), ".", ".", ";".join(info)]))
+    for i in range(0, len(lines), 40):  # adjacent duplicate lines
+        lines.insert(i + 1, lines[i])
+    return lines
+
+
+def run_load_driver(lines):
+    """Per line, what Load/bin/load_vcf_file.py:101-119 produces: the COPY
+    buffer rows (all columns) and the .mapping line(s), or the exception type."""
+    from AnnotatedVDB.Util.loaders import VCFVariantLoader
+    loader = VCFVariantLoader("dbSNP")
+    loader.initialize_pk_generator("GRCh38", "/nonexistent")
+    loader.initialize_bin_indexer(None)
+    loader._alg_invocation_id = "1"
+    loader.initialize_copy_sql()
+    rows = []
+    for line in lines:
+        loader.reset_copy_buffer()
+        try:
+            pkm = loader.parse_variant(line.rstrip())
+            mapping = ["%s\t%s" % (k, v) for k, v in pkm.items()]  # print(k, v, sep='\t')
+            err = ""
+        except Exception as e:  # noqa: BLE001
+            mapping, err = [], type(e).__name__
+        copy = loader.copy_buffer().getvalue().splitlines()
+        rows.append((line.replace("\t", "\\t"), err, json.dumps(mapping, separators=(",", ":")),
+                     json.dumps(copy, separators=(",", ":"))))
+    return rows
+
+
+def gen_display_attrs(VariantAnnotator, n, rng):
+    """(chrom, pos, ref, alt) -> json.dumps(get_display_attributes()) incl. long
+    alleles (truncation at 8 and 100 characters)."""
+    rows = []
+    for i in range(n):
+        u = rng.random()
+        if u < 0.7:
+            ref, alt = gen_allele_pair(rng)
+        elif u < 0.8:
+            unit = rand_allele(rng, rng.randint(1, 5))
+            ref = rand_allele(rng, 1) + unit * rng.randint(1, 40)
+            alt = ref + unit * rng.randint(1, 3) if rng.random() < 0.7 else ref[0] + unit
+        elif u < 0.9:
+            ref = rand_allele(rng, rng.randint(1, 250))
+            alt = ref[:rng.randint(0, len(ref))] + rand_allele(rng, rng.randint(0, 250))
+            if not alt:
+                alt = "A"
+        else:
+            ref = rand_allele(rng, rng.randint(2, 150), "AT")
+            alt = ref[::-1] if rng.random() < 0.5 else rand_allele(rng, len(ref), "AT")
+        c = rng.choice(CHROM_NAMES)
+        pos = rng.randint(1, GRCH38_LENGTHS[c])
+        va = VariantAnnotator(ref, alt, c, pos)
+        rows.append((c, pos, ref, alt, json.dumps(va.get_display_attributes())))
+    return rows
+
+
 def gen_long_alleles(VariantAnnotator, bi, n, rng):
     rows = []
     tot = sum(GRCH38_LENGTHS.values())
@@ -574,17 +705,28 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--only", choices=["all", "load"], default="all",
+                    help="'load': only the load-driver fixtures (vcf_load, display_attrs)")
     a = ap.parse_args()
     rng = random.Random(a.seed)
     install_stubs()
     build_binindexref()
-    summary()
 
     from AnnotatedVDB.BinIndex.bin_index import BinIndex
     from AnnotatedVDB.Util.variant_annotator import VariantAnnotator
     bi = BinIndex(None, verbose=False)
 
     k = 0.1 if a.quick else 1.0
+    # load-driver fixtures: their own seed stream, so the older fixtures stay byte-identical
+    lrng = random.Random(a.seed + 1)
+    wtsv("vcf_load.tsv.gz", ["line", "error", "mapping", "copy_rows"],
+         run_load_driver(gen_load_lines(int(4000 * k), lrng)))
+    wtsv("display_attrs.tsv.gz", ["chrom", "pos", "ref", "alt", "attributes"],
+         gen_display_attrs(VariantAnnotator, int(6000 * k), lrng))
+    if a.only == "load":
+        print("done")
+        return
+    summary()
     rows = gen_bin_queries(bi, int(30000 * k), rng)
     for r in rows[:3]:
         print(r)

@@ -141,6 +141,43 @@ def test_sha512t24u_primitive():
     assert O.sha512t24u(b"ACGT") == "aKF498dAxcJAqme6QYQ7EZ07-fiw8Kw2"
 
 
+def test_display_attributes_golden():
+    """variant_annotator.py:134-241 restated == the reference's dicts (key order too)."""
+    rows = read_tsv("display_attrs.tsv.gz")
+    assert len(rows) > 500
+    for r in rows:
+        got = O.display_attributes(r["chrom"], int(r["pos"]), r["ref"], r["alt"])
+        assert json.dumps(got) == r["attributes"], r
+
+
+def load_rows():
+    with gzip.open(os.path.join(GOLDEN, "vcf_load.tsv.gz"), "rt") as fh:
+        fh.readline()
+        for line in fh:
+            raw, err, mapping, copy = line.rstrip("\n").split("\t")
+            yield raw.replace("\\t", "\t"), err or None, json.loads(mapping), json.loads(copy)
+
+
+def test_load_driver_golden():
+    """The whole load-driver output per line (COPY rows with every column,
+    .mapping line, or the exception) restated == the reference's."""
+    n = 0
+    for raw, err, mapping, copy in load_rows():
+        e, m, c = O.load_line(raw, length_table())
+        assert (e, c) == (err, copy), raw
+        if err is None:
+            assert m == mapping, raw
+        n += 1
+    assert n > 400
+
+
+def test_float_repr_subset():
+    """The FREQ numbers the GPU formats itself follow Python's float repr."""
+    for s in ["0.9990", "0.0010", "0.00001", "0.0001", "12.50", "5.", ".5", "100.0", "0.0", "00.000",
+              "123456789012345.0", "1234567890123456.0", "0.000123456789012345", "99999999999999.9"]:
+        assert O.xstr_json({"x": O.to_numeric(s)}) == '{"x": %r}' % float(s)
+
+
 def test_dedup_semantics():
     keys = ["1:5:A:G", "1:5:A:T", "1:5:A:G", "1:5:A:G:rs1", "1:5:A:G"]
     assert O.dedup_keep(keys) == [1, 1, 0, 1, 0]
