@@ -43,6 +43,18 @@ CTR_RECORDS = 20
 CTR_DUPLICATES = 21
 CTR_HASH_COLLISIONS = 22
 CTR_LONG = 23
+CTR_COPY_ROWS = 24
+CTR_SKIPPED_ALTS = 25
+CTR_DUP_ROWS = 26
+CTR_HOST_LINES = 27
+LINE_GPU, LINE_HOST, LINE_SKIP = 0, 1, 2
+MAX_ALG_ID = 64
+
+
+class FormatOpts(ctypes.Structure):
+    """avdb_format_opts (include/avdb.h)."""
+    _fields_ = [("alg_id", ctypes.c_char_p), ("max_seq_len", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 # every symbol include/avdb.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED_SYMBOLS = [
@@ -54,6 +66,8 @@ EXPORTED_SYMBOLS = [
     "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest",
     "avdb_format_bin_path", "avdb_format_bin_paths",
     "avdb_vcf_workspace_size", "avdb_vcf_count_lines", "avdb_vcf_parse_lines", "avdb_vcf_emit",
+    "avdb_format_workspace_size", "avdb_vcf_format_size", "avdb_vcf_format_write",
+    "avdb_display_attributes",
 ]
 
 
@@ -100,6 +114,12 @@ def _sig(lib):
     f.avdb_vcf_count_lines.argtypes = [P, P, SZ, P, SZ, P, P]
     f.avdb_vcf_parse_lines.argtypes = [P, P, SZ, SZ, P, P, SZ, P, P, P, P]
     f.avdb_vcf_emit.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, P, P, P, P, P, P]
+    f.avdb_format_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
+    f.avdb_vcf_format_size.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, ctypes.POINTER(FormatOpts),
+                                       P, SZ, P, P, P, P]
+    f.avdb_vcf_format_write.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, ctypes.POINTER(FormatOpts),
+                                        P, P, P, P, P, P, P]
+    f.avdb_display_attributes.argtypes = [P, P, P, P, P, P, P, P, SZ, SZ, P, SZ, P, P, P, P]
     for name in EXPORTED_SYMBOLS:
         if name not in ("avdb_last_error",):
             getattr(f, name).restype = I32

@@ -1,0 +1,876 @@
+// K5 — the load driver's text outputs on the GPU (gfx950).
+//
+// K5b avdb_vcf_format_{size,write}: for VCF lines tokenized by K0 and processed
+//   by K2 (end, bin), K4 (long-key digests) and optionally K3 (keep), writes
+//   byte-exact what Load/bin/load_vcf_file.py:101-119 produces per line:
+//   * COPY rows of VCFVariantLoader.__parse_alt_alleles
+//     (Util/lib/python/loaders/vcf_variant_loader.py:320-343): 'chr'+chrom, primary
+//     key (primary_key_generator.py:99-122), position, metaseq id
+//     (variant_annotator.py:124-126), bin path (bin_index.py:75), algorithm id,
+//     refSNP | NULL, True | NULL (is_multi_allelic), display attributes
+//     (variant_annotator.py:134-241) and INFO FREQ allele frequencies
+//     (vcf_parser.py:200-222), both as json.dumps text;
+//   * the .mapping line: variant id TAB str([{'primary_key': .., 'bin_index': ..}, ..])
+//     (load_vcf_file.py:116-117).
+//   SIZE pass (bytes per line) -> hipCUB exclusive scans -> WRITE pass, both the
+//   same templated code.  One lane per line, 256 consecutive lines per workgroup
+//   with their text staged in LDS (as K0).  Output goes through a per-lane 8-byte
+//   word buffer: aligned dwordx2 stores, byte stores only at the two ends of a
+//   lane's span.  A line the GPU does not render byte-exact (non-ASCII text,
+//   allele bytes that need escaping, an unmappable record (TypeError), a key the
+//   reference cannot build (':' in an allele), malformed or non-canonical FREQ
+//   numbers, K0 host-resolved fields) is marked HOST and gets zero bytes; the
+//   host renders it between its neighbours.
+// K5a avdb_display_attributes: display-attribute JSON for any record batch
+//   (allele heap), json.dumps escaping included (ASCII alleles).
+#include "avdb_internal.hpp"
+#include "avdb_text.hpp"
+
+#include <hipcub/hipcub.hpp>
+#include <string.h>
+
+namespace avdb {
+
+// ---------------------------------------------------------------------------
+// output sink: SIZE pass counts, WRITE pass stores through an aligned word
+// ---------------------------------------------------------------------------
+template <bool WRITE>
+struct Out {
+  uint8_t* base;
+  uint64_t p, lo, word;
+  __device__ __forceinline__ Out(uint8_t* b, uint64_t at) : base(b), p(at), lo(at), word(0) {}
+  __device__ __forceinline__ void put(uint32_t c) {
+    if constexpr (WRITE) {
+      word |= uint64_t(c & 0xFFu) << (8 * (p & 7));
+      if ((++p & 7) == 0) flush();
+    } else {
+      ++p;
+    }
+  }
+  __device__ __forceinline__ void flush() {  // the aligned word [p-8, p) is complete
+    const uint64_t a = p - 8;
+    if (a >= lo) {
+      *reinterpret_cast<uint64_t*>(base + a) = word;
+    } else {
+      for (uint64_t b = lo; b < p; ++b) base[b] = uint8_t(word >> (8 * (b - a)));
+    }
+    word = 0;
+  }
+  __device__ __forceinline__ void finish() {
+    if constexpr (WRITE) {
+      const uint64_t a = p & ~uint64_t(7);
+      for (uint64_t b = a > lo ? a : lo; b < p; ++b) base[b] = uint8_t(word >> (8 * (b - a)));
+    }
+  }
+  __device__ __forceinline__ void lit(const char* s) {
+    while (*s) put(uint8_t(*s++));
+  }
+  __device__ __forceinline__ void bytes(const uint8_t* s, uint32_t n) {
+    if constexpr (!WRITE) {
+      p += n;
+    } else {
+      for (uint32_t i = 0; i < n; ++i) put(s[i]);
+    }
+  }
+  __device__ __forceinline__ void u32v(uint32_t v) {
+    char t[10];
+    int k = 0;
+    do { t[k++] = char('0' + v % 10u); v /= 10u; } while (v);
+    while (k) put(uint8_t(t[--k]));
+  }
+  __device__ __forceinline__ void u64v(uint64_t v) {
+    if (v <= 0xFFFFFFFFull) { u32v(uint32_t(v)); return; }
+    char t[20];
+    int k = 0;
+    do { t[k++] = char('0' + v % 10u); v /= 10u; } while (v);
+    while (k) put(uint8_t(t[--k]));
+  }
+};
+
+// contig label (Util/lib/python/enums/chromosomes.py:9-38 order)
+template <class O>
+__device__ __forceinline__ void chrom_name(O& o, uint32_t c) {
+  if (c < 22) o.u32v(c + 1);
+  else if (c == 22) o.put('X');
+  else if (c == 23) o.put('Y');
+  else if (c == 24) o.put('M');
+  else o.u32v(c);  // contigs beyond the human 25: numeric label (matches avdb_format_bin_path)
+}
+
+// ltree path of a bin code (generate_bin_index_references.py:54,60-61,74)
+template <class O>
+__device__ __noinline__ void bin_path(O& o, uint32_t c, uint32_t code) {
+  o.lit("chr");
+  chrom_name(o, c);
+  const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
+  for (uint32_t l = 1; l <= level; ++l) {
+    const uint32_t gl = g >> (level - l);
+    o.lit(".L");
+    o.u32v(l);
+    o.lit(".B");
+    o.u32v(l == 1 ? gl + 1 : (gl & 1u) + 1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// JSON strings (json.dumps, ensure_ascii): '"' '\\' and the short escapes,
+// other bytes outside ' '..'~' as \u00XX (lowercase hex)
+// ---------------------------------------------------------------------------
+template <bool ESC, class O>
+__device__ __forceinline__ void jstr(O& o, const uint8_t* s, uint32_t n) {
+  if constexpr (!ESC) {
+    o.bytes(s, n);
+  } else {
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint8_t c = s[i];
+      if (c >= 0x20 && c < 0x7F && c != '"' && c != '\\') { o.put(c); continue; }
+      o.put('\\');
+      switch (c) {
+        case '"': o.put('"'); break;
+        case '\\': o.put('\\'); break;
+        case '\n': o.put('n'); break;
+        case '\r': o.put('r'); break;
+        case '\t': o.put('t'); break;
+        case '\b': o.put('b'); break;
+        case '\f': o.put('f'); break;
+        default: {
+          const char* hx = "0123456789abcdef";
+          o.lit("u00");
+          o.put(uint8_t(hx[c >> 4]));
+          o.put(uint8_t(hx[c & 15]));
+        }
+      }
+    }
+  }
+}
+
+// an allele in its display form: bytes, or '-' for an empty normalized allele
+// (variant_annotator.py:111-116, snvDivMinus=True)
+struct Al {
+  const uint8_t* p;
+  uint32_t n;
+  bool dash;
+};
+
+template <bool ESC, class O>
+__device__ __forceinline__ void al_str(O& o, const Al& a) {
+  if (a.dash) o.put('-');
+  else jstr<ESC>(o, a.p, a.n);
+}
+
+// truncate(s, cap) = s if len(s) <= cap else s[:cap] + '...' (variant_annotator.py:8-10)
+template <bool ESC, class O>
+__device__ __forceinline__ void al_trunc(O& o, const Al& a, uint32_t cap) {
+  if (a.dash) { o.put('-'); return; }
+  jstr<ESC>(o, a.p, a.n < cap ? a.n : cap);
+  if (a.n > cap) o.lit("...");
+}
+
+// ---------------------------------------------------------------------------
+// get_display_attributes (variant_annotator.py:134-241) as json.dumps text.
+// Keys in the reference's dict insertion order: location_start, location_end,
+// [normalized_metaseq_id], then variant_class, variant_class_abbrev,
+// display_allele, sequence_allele — except the insertion branch (:192-229),
+// whose update() lists display_allele and sequence_allele first.
+// chrom >= 25 writes no label in normalized_metaseq_id (the caller prepends it).
+// ---------------------------------------------------------------------------
+template <bool ESC, class O>
+__device__ __noinline__ void display_json(O& o, uint32_t chrom, uint32_t pos, uint32_t end, const uint8_t* ref,
+                             uint32_t r, const uint8_t* alt, uint32_t a) {
+  const bool snv = r == 1u && a == 1u;
+  uint32_t l = 0;  // common prefix (__normalize_alleles :100-107); SNVs untouched (:97-98)
+  if (!snv) {
+    const uint32_t m = r < a ? r : a;
+    while (l < m && ref[l] == alt[l]) ++l;
+  }
+  const uint32_t nr = r - l, na = a - l;
+  const Al nref{ref + l, nr, l > 0 && nr == 0}, nalt{alt + l, na, l > 0 && na == 0};
+  uint32_t ls = pos, le = pos;
+  int cls;  // 0 SNV, 1 inversion, 2 substitution, 3 indel, 4 indel (ins downstream), 5 ins/dup, 6 deletion
+  bool dup = false;
+  const Al orig{r ? ref + 1 : ref, r ? r - 1 : 0, false};
+  if (snv) {
+    cls = 0;
+  } else if (r == a) {  // MNV (:171-189)
+    bool inv = true;
+    for (uint32_t i = 0; i < r && inv; ++i) inv = ref[i] == alt[r - 1 - i];
+    cls = inv ? 1 : 2;
+    le = end;
+  } else if (na >= 1) {  // insertion (:192-229)
+    ls = pos + 1;
+    // originalRef.count(normAlt) non-overlapping and len/count == len(normAlt)
+    // <=> originalRef == normAlt * k, k >= 1
+    if (orig.n > 0 && orig.n % na == 0) {
+      dup = true;
+      for (uint32_t i = 0, j = 0; i < orig.n && dup; ++i) {
+        dup = orig.p[i] == nalt.p[j];
+        if (++j == na) j = 0;
+      }
+    }
+    if (nr >= 1) { cls = 3; le = end; }
+    else if (end != pos + 1) { cls = 4; le = end; }
+    else { cls = 5; le = pos + 1; }
+  } else {  // deletion (:231-239)
+    cls = 6;
+    ls = pos + 1;
+    le = end;
+  }
+  o.lit("{\"location_start\": ");
+  o.u32v(ls);
+  o.lit(", \"location_end\": ");
+  o.u32v(le);
+  if (!snv && l > 0) {  // normalized id differs from the metaseq id iff a prefix was trimmed
+    o.lit(", \"normalized_metaseq_id\": \"");
+    if (chrom < 25) chrom_name(o, chrom);
+    o.put(':');
+    o.u32v(pos);
+    o.put(':');
+    al_str<ESC>(o, nref);
+    o.put(':');
+    al_str<ESC>(o, nalt);
+    o.put('"');
+  }
+  const char* vc;
+  const char* vca;
+  switch (cls) {
+    case 0: vc = "single nucleotide variant"; vca = "SNV"; break;
+    case 1: vc = "inversion"; vca = "MNV"; break;
+    case 2: vc = "substitution"; vca = "MNV"; break;
+    case 3:
+    case 4: vc = "indel"; vca = "INDEL"; break;
+    case 5: vc = dup ? "duplication" : "insertion"; vca = dup ? "DUP" : "INS"; break;
+    default: vc = "deletion"; vca = "DEL"; break;
+  }
+  const bool order_b = cls >= 3 && cls <= 5;
+  if (!order_b) {
+    o.lit(", \"variant_class\": \"");
+    o.lit(vc);
+    o.lit("\", \"variant_class_abbrev\": \"");
+    o.lit(vca);
+    o.put('"');
+  }
+  const char* pre = dup ? "dup" : "ins";
+  const Al raw_ref{ref, r, false}, raw_alt{alt, a, false};
+  o.lit(", \"display_allele\": \"");
+  switch (cls) {
+    case 0: al_str<ESC>(o, raw_ref); o.put('>'); al_str<ESC>(o, raw_alt); break;
+    case 1: o.lit("inv"); al_str<ESC>(o, raw_ref); break;
+    case 2: al_str<ESC>(o, nref); o.put('>'); al_str<ESC>(o, nalt); break;
+    case 3: o.lit("del"); al_trunc<ESC>(o, nref, 100); o.lit(pre); al_trunc<ESC>(o, nalt, 100); break;
+    case 4: o.lit("del"); al_trunc<ESC>(o, orig, 100); o.lit(pre); al_trunc<ESC>(o, nalt, 100); break;
+    case 5: o.lit(pre); al_trunc<ESC>(o, nalt, 100); break;
+    default: o.lit("del"); al_trunc<ESC>(o, nref, 100); break;
+  }
+  o.lit("\", \"sequence_allele\": \"");
+  switch (cls) {
+    case 0: al_str<ESC>(o, raw_ref); o.put('/'); al_str<ESC>(o, raw_alt); break;
+    case 1: al_trunc<ESC>(o, raw_ref, 8); o.put('/'); al_trunc<ESC>(o, raw_alt, 8); break;
+    case 5: o.lit(pre); al_trunc<ESC>(o, nalt, 8); break;
+    case 6: al_trunc<ESC>(o, nref, 8); o.lit("/-"); break;
+    default: al_trunc<ESC>(o, nref, 8); o.put('/'); al_trunc<ESC>(o, nalt, 8); break;
+  }
+  o.put('"');
+  if (order_b) {
+    o.lit(", \"variant_class\": \"");
+    o.lit(vc);
+    o.lit("\", \"variant_class_abbrev\": \"");
+    o.lit(vca);
+    o.put('"');
+  }
+  o.put('}');
+}
+
+// ---------------------------------------------------------------------------
+// to_numeric(str) as json.dumps prints it, for the canonical subset:
+//   [0-9]+            int()   -> digits without leading zeros
+//   [0-9]*.[0-9]*     float() -> repr(): <= 15 significant digits round-trip to
+//                     exactly those digits, fixed notation for decimal exponent
+//                     -4..15, else d.ddde[+-]XX
+// Anything else (signs, exponents, '_', spaces, nan/inf, > 15 significant
+// digits) returns false: the line is rendered by the host.
+// ---------------------------------------------------------------------------
+template <class O>
+__device__ __noinline__ bool json_number(O& o, const uint8_t* f, uint32_t n) {
+  if (n == 0 || n > 40) return false;
+  uint32_t dot = n;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (f[i] == '.') {
+      if (dot != n) return false;
+      dot = i;
+    } else if (!is_digit(f[i])) {
+      return false;
+    }
+  }
+  if (dot == n) {  // int
+    uint32_t i = 0;
+    while (i + 1 < n && f[i] == '0') ++i;
+    o.bytes(f + i, n - i);
+    return true;
+  }
+  if (n == 1) return false;  // "." alone
+  // digits without the dot: S[k] = f[k < dot ? k : k + 1], ns = n - 1
+  const uint32_t ns = n - 1;
+  auto S = [&](uint32_t k) -> uint8_t { return f[k < dot ? k : k + 1]; };
+  int32_t f0 = -1, l0 = -1;
+  for (uint32_t k = 0; k < ns; ++k) {
+    if (S(k) != '0') {
+      if (f0 < 0) f0 = int32_t(k);
+      l0 = int32_t(k);
+    }
+  }
+  if (f0 < 0) { o.lit("0.0"); return true; }
+  const int32_t nd = l0 - f0 + 1;
+  if (nd > 15) return false;
+  const int32_t e = int32_t(dot) - 1 - f0;  // decimal exponent of the first significant digit
+  if (e >= -4 && e < 16) {
+    if (e >= 0) {
+      for (int32_t k = 0; k <= e; ++k) o.put(k < nd ? S(uint32_t(f0 + k)) : '0');
+      o.put('.');
+      if (nd > e + 1) {
+        for (int32_t k = e + 1; k < nd; ++k) o.put(S(uint32_t(f0 + k)));
+      } else {
+        o.put('0');
+      }
+    } else {
+      o.lit("0.");
+      for (int32_t k = 0; k < -e - 1; ++k) o.put('0');
+      for (int32_t k = 0; k < nd; ++k) o.put(S(uint32_t(f0 + k)));
+    }
+  } else {
+    o.put(S(uint32_t(f0)));
+    if (nd > 1) {
+      o.put('.');
+      for (int32_t k = 1; k < nd; ++k) o.put(S(uint32_t(f0 + k)));
+    }
+    o.put('e');
+    o.put(e < 0 ? '-' : '+');
+    const uint32_t ae = uint32_t(e < 0 ? -e : e);
+    if (ae < 10) o.put('0');
+    o.u32v(ae);
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// K5b: one VCF line
+// ---------------------------------------------------------------------------
+enum : uint8_t { kLineGpu = 0, kLineHost = 1, kLineSkip = 2 };
+
+constexpr uint32_t kHostFlags = AVDB_VCF_FEW_FIELDS | AVDB_VCF_BAD_POS | AVDB_VCF_EXT_HOST |
+                                AVDB_VCF_CHROM_HOST | AVDB_VCF_EMPTY | AVDB_VCF_ID_HOST;
+constexpr int kMaxPops = 64;
+
+struct FormatArgs {
+  const uint8_t* text;
+  size_t text_bytes;
+  size_t n_lines;
+  const avdb_vcf_line* lines;
+  const uint64_t* rec_off;
+  const uint32_t* end;
+  const uint32_t* code;
+  const uint8_t* status;
+  const char* digest;
+  const uint8_t* keep;
+  uint64_t* copy_off;  // SIZE: bytes per line; WRITE: offsets
+  uint64_t* map_off;
+  uint8_t* line_state;
+  uint8_t* copy_out;
+  uint8_t* map_out;
+  unsigned long long* counters;
+  uint32_t max_seq_len;
+  uint32_t alg_len;
+  char alg[AVDB_MAX_ALG_ID];
+};
+
+// allele bytes the GPU writes verbatim into JSON and Python repr text: printable
+// ASCII except '"' '\\' '\'' (escaped by json.dumps / repr) and ':' (breaks
+// metaseqId.split(':'), primary_key_generator.py:106)
+__device__ __forceinline__ bool plain_allele(const uint8_t* s, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t c = s[i];
+    if (c < 0x20 || c > 0x7E || c == '"' || c == '\\' || c == '\'' || c == ':') return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// next separator at or after i in [i, e), or e
+__device__ __forceinline__ uint32_t find_byte(const uint8_t* s, uint32_t i, uint32_t e, uint8_t c) {
+  while (i < e && s[i] != c) ++i;
+  return i;
+}
+
+// FREQ value [v0, v1) of the line: is it one the GPU renders?  Every population
+// needs a ':' (pop.split(':')[1]), a JSON-plain name, and names must be unique
+// (the reference's dict comprehension keeps the last value at the first
+// position).
+__device__ bool freq_plain(const uint8_t* s, uint32_t v0, uint32_t v1) {
+  uint32_t np = 0;
+  for (uint32_t p0 = v0; p0 <= v1; ++np) {
+    const uint32_t p1 = find_byte(s, p0, v1, '|');
+    const uint32_t c1 = find_byte(s, p0, p1, ':');
+    if (c1 == p1 || np >= kMaxPops) return false;
+    for (uint32_t i = p0; i < c1; ++i) {
+      const uint8_t c = s[i];
+      if (c < 0x20 || c > 0x7E || c == '"' || c == '\\') return false;
+    }
+    // duplicate name among the earlier populations
+    for (uint32_t q0 = v0; q0 < p0;) {
+      const uint32_t q1 = find_byte(s, q0, v1, '|');
+      const uint32_t d1 = find_byte(s, q0, q1, ':');
+      if (d1 - q0 == c1 - p0 && bytes_eq(s + q0, s + p0, c1 - p0)) return false;
+      q0 = q1 + 1;
+    }
+    p0 = p1 + 1;
+  }
+  return true;
+}
+
+// allele_frequencies of ALT index k (1-based, altAlleles.index(allele) + 1) as
+// json.dumps text or NULL; false when the reference would raise or print a
+// number the GPU does not format
+template <class O>
+__device__ __noinline__ bool freq_json(O& o, const uint8_t* s, uint32_t v0, uint32_t v1, uint32_t k) {
+  bool any = false;
+  for (uint32_t p0 = v0; p0 <= v1;) {
+    const uint32_t p1 = find_byte(s, p0, v1, '|');
+    const uint32_t c1 = find_byte(s, p0, p1, ':');
+    const uint32_t c2 = find_byte(s, c1 + 1, p1, ':');  // pop.split(':')[1]
+    // item k of the comma list [c1+1, c2)
+    uint32_t f0 = c1 + 1, idx = 0;
+    while (idx < k) {
+      const uint32_t cm = find_byte(s, f0, c2, ',');
+      if (cm == c2) return false;  // IndexError in the reference
+      f0 = cm + 1;
+      ++idx;
+    }
+    const uint32_t f1 = find_byte(s, f0, c2, ',');
+    const uint32_t fn = f1 - f0;
+    const bool zero = fn == 1 && (s[f0] == '.' || s[f0] == '0');
+    if (!zero) {
+      o.put(any ? ',' : '{');
+      if (any) o.put(' ');
+      o.put('"');
+      o.bytes(s + p0, c1 - p0);
+      o.lit("\": {\"gmaf\": ");
+      if (!json_number(o, s + f0, fn)) return false;
+      o.put('}');
+      any = true;
+    }
+    p0 = p1 + 1;
+  }
+  if (any) o.put('}');
+  else o.lit("NULL");
+  return true;
+}
+
+template <bool WRITE>
+__device__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, const uint8_t* s, size_t li,
+                               Out<WRITE>& oc, Out<WRITE>& om, uint32_t* n_rows, uint32_t* n_skip,
+                               uint32_t* n_dup) {
+  if (L.flags & AVDB_VCF_COMMENT) return kLineSkip;
+  if ((L.flags & kHostFlags) || L.chrom >= 25) return kLineHost;
+  // the reference decodes every line as UTF-8 (load_vcf_file.py:102): ASCII only here
+  for (uint32_t i = 0; i < L.len; ++i)
+    if (s[i] & 0x80) return kLineHost;
+  const uint32_t c = L.chrom;
+  const uint32_t ref0 = L.field[3], rl = L.field[4] - 1 - ref0;
+  const uint32_t alt0 = L.field[4], alt1 = L.field[5] - 1;
+  const uint8_t* ref = s + ref0;
+  if (!plain_allele(ref, rl)) return kLineHost;
+  // INFO: the last FREQ entry (dict keeps the last key); '#' or '\' in INFO are
+  // rewritten by the reference before it splits (vcf_parser.py:101-103)
+  const uint32_t i0 = L.field[7], i1 = L.field_end8;
+  int64_t fq0 = -1, fq1 = -1;
+  for (uint32_t i = i0; i < i1; ++i)
+    if (s[i] == '#' || s[i] == '\\') return kLineHost;
+  for (uint32_t e0 = i0; e0 <= i1;) {
+    const uint32_t e1 = find_byte(s, e0, i1, ';');
+    if (e1 - e0 >= 4 && s[e0] == 'F' && s[e0 + 1] == 'R' && s[e0 + 2] == 'E' && s[e0 + 3] == 'Q') {
+      if (e1 - e0 == 4) return kLineHost;  // bare flag -> True.split: AttributeError
+      if (s[e0 + 4] == '=') { fq0 = e0 + 5; fq1 = e1; }
+    }
+    e0 = e1 + 1;
+  }
+  if (fq0 >= 0 && !freq_plain(s, uint32_t(fq0), uint32_t(fq1))) return kLineHost;
+  const bool has_rs = (L.flags & (AVDB_VCF_ID_RS | AVDB_VCF_INFO_RS)) != 0;
+  // .mapping: variant id (vcf_parser.py:140-142) TAB '['
+  if (L.flags & AVDB_VCF_ID_METASEQ) {
+    chrom_name(om, c);
+    om.put(':');
+    om.u32v(L.pos);
+    om.put(':');
+    om.bytes(ref, rl);
+    om.put(':');
+    om.bytes(s + alt0, alt1 - alt0);
+  } else {
+    om.bytes(s + L.field[2], L.field[3] - 1 - L.field[2]);
+  }
+  om.lit("\t[");
+  uint64_t r = A.rec_off[li];
+  uint32_t nrec = 0, rows = 0, skip = 0, dups = 0;
+  for (uint32_t a0 = alt0, ai = 0; a0 <= alt1; ++ai) {
+    const uint32_t a1 = find_byte(s, a0, alt1, ',');
+    const uint8_t* alt = s + a0;
+    const uint32_t al = a1 - a0;
+    if (al == 1 && alt[0] == '.') {  // vcf_variant_loader.py:277-280
+      ++skip;
+      a0 = a1 + 1;
+      continue;
+    }
+    if (!plain_allele(alt, al)) return kLineHost;
+    const uint32_t st = A.status[r];
+    if (st == AVDB_STATUS_UNKNOWN_CHROM || st == AVDB_STATUS_OUT_OF_RANGE) return kLineHost;
+    const bool lng = rl + al > A.max_seq_len;
+    if (lng && !A.digest) return kLineHost;
+    const uint32_t code = A.code[r];
+    const bool keep = !A.keep || A.keep[r];
+    // altIndex = altAlleles.index(allele) + 1: the first equal ALT
+    uint32_t k = ai + 1;
+    for (uint32_t b0 = alt0, bi = 0; bi < ai; ++bi) {
+      const uint32_t b1 = find_byte(s, b0, alt1, ',');
+      if (b1 - b0 == al && bytes_eq(s + b0, alt, al)) { k = bi + 1; break; }
+      b0 = b1 + 1;
+    }
+    // primary key (primary_key_generator.py:106-122)
+    auto pk = [&](Out<WRITE>& o) {
+      chrom_name(o, c);
+      o.put(':');
+      o.u32v(L.pos);
+      o.put(':');
+      if (lng) {
+        o.bytes(reinterpret_cast<const uint8_t*>(A.digest) + 32 * r, AVDB_DIGEST_CHARS);
+      } else {
+        o.bytes(ref, rl);
+        o.put(':');
+        o.bytes(alt, al);
+      }
+      if (has_rs) {
+        o.lit(":rs");
+        o.u64v(L.ext_id);
+      }
+    };
+    if (keep) {
+      // COPY row (vcf_variant_loader.py:320-343)
+      oc.lit("chr");
+      chrom_name(oc, c);
+      oc.put('#');
+      pk(oc);
+      oc.put('#');
+      oc.u32v(L.pos);
+      oc.put('#');
+      chrom_name(oc, c);
+      oc.put(':');
+      oc.u32v(L.pos);
+      oc.put(':');
+      oc.bytes(ref, rl);
+      oc.put(':');
+      oc.bytes(alt, al);
+      oc.put('#');
+      bin_path(oc, c, code);
+      oc.put('#');
+      oc.bytes(reinterpret_cast<const uint8_t*>(A.alg), A.alg_len);
+      oc.put('#');
+      if (has_rs) {
+        oc.lit("rs");
+        oc.u64v(L.ext_id);
+      } else {
+        oc.lit("NULL");
+      }
+      oc.put('#');
+      oc.lit(L.n_alt > 1 ? "True" : "NULL");
+      oc.put('#');
+      display_json<false>(oc, c, L.pos, A.end[r], ref, rl, alt, al);
+      oc.put('#');
+      if (fq0 >= 0) {
+        if (!freq_json(oc, s, uint32_t(fq0), uint32_t(fq1), k)) return kLineHost;
+      } else {
+        oc.lit("NULL");
+      }
+      oc.put('\n');
+      ++rows;
+    } else {
+      // no COPY row, but the reference would still have evaluated FREQ
+      if (fq0 >= 0) {
+        Out<false> probe(nullptr, 0);
+        if (!freq_json(probe, s, uint32_t(fq0), uint32_t(fq1), k)) return kLineHost;
+      }
+      ++dups;
+    }
+    // .mapping entry
+    if (nrec) om.lit(", ");
+    om.lit("{'primary_key': '");
+    pk(om);
+    om.lit("', 'bin_index': '");
+    bin_path(om, c, code);
+    om.lit("'}");
+    ++nrec;
+    ++r;
+    a0 = a1 + 1;
+  }
+  om.lit("]\n");
+  *n_rows += rows;
+  *n_skip += skip;
+  *n_dup += dups;
+  return kLineGpu;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void k_vcf_format(FormatArgs A) {
+  __shared__ u32x4 s_text[kStage / 16];
+  const Heap h = make_heap(A.text, A.text_bytes);
+  uint32_t rows = 0, skip = 0, dups = 0, hosts = 0;
+  for (size_t base = size_t(blockIdx.x) * kBlock; base < A.n_lines; base += size_t(gridDim.x) * kBlock) {
+    const size_t last = base + kBlock < A.n_lines ? base + kBlock : A.n_lines;
+    const avdb_vcf_line& Z = A.lines[last - 1];
+    const Window w = stage_window(h, A.lines[base].start, Z.start + Z.len, s_text);
+    const size_t li = base + threadIdx.x;
+    if (li < A.n_lines) {
+      const avdb_vcf_line L = A.lines[li];
+      const uint8_t* s = w.staged ? reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)
+                                  : A.text + L.start;
+      if constexpr (WRITE) {
+        const uint8_t st = A.line_state[li];
+        if (st == kLineGpu) {
+          Out<true> oc(A.copy_out, A.copy_off[li]), om(A.map_out, A.map_off[li]);
+          format_line<true>(A, L, s, li, oc, om, &rows, &skip, &dups);
+          oc.finish();
+          om.finish();
+        } else if (st == kLineHost) {
+          ++hosts;
+        }
+      } else {
+        Out<false> oc(nullptr, 0), om(nullptr, 0);
+        const uint8_t st = format_line<false>(A, L, s, li, oc, om, &rows, &skip, &dups);
+        A.line_state[li] = st;
+        A.copy_off[li] = st == kLineGpu ? oc.p : 0;
+        A.map_off[li] = st == kLineGpu ? om.p : 0;
+      }
+    }
+    __syncthreads();  // the window is reused by the next trip
+  }
+  if (WRITE && A.counters) {
+    for (int d = 32; d > 0; d >>= 1) {
+      rows += __shfl_down(rows, d, kWave);
+      skip += __shfl_down(skip, d, kWave);
+      dups += __shfl_down(dups, d, kWave);
+      hosts += __shfl_down(hosts, d, kWave);
+    }
+    if (__lane_id() == 0) {
+      if (rows) atomicAdd(&A.counters[AVDB_CTR_COPY_ROWS], (unsigned long long)rows);
+      if (skip) atomicAdd(&A.counters[AVDB_CTR_SKIPPED_ALTS], (unsigned long long)skip);
+      if (dups) atomicAdd(&A.counters[AVDB_CTR_DUP_ROWS], (unsigned long long)dups);
+      if (hosts) atomicAdd(&A.counters[AVDB_CTR_HOST_LINES], (unsigned long long)hosts);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5a: display attributes of a record batch (allele heap); one lane per record
+// ---------------------------------------------------------------------------
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void k_display(const uint8_t* __restrict__ chrom,
+                                                    const uint32_t* __restrict__ pos,
+                                                    const uint32_t* __restrict__ end,
+                                                    const uint64_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ rl,
+                                                    const uint32_t* __restrict__ al,
+                                                    const uint8_t* __restrict__ heap, size_t heap_bytes,
+                                                    size_t n, uint64_t* __restrict__ out_off,
+                                                    uint8_t* __restrict__ out, uint8_t* __restrict__ state) {
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+    const uint64_t o = off[i];
+    const uint32_t r = rl[i], a = al[i];
+    if constexpr (WRITE) {
+      if (state[i]) continue;
+      Out<true> w(out, out_off[i]);
+      display_json<true>(w, chrom[i], pos[i], end[i], heap + o, r, heap + o + r, a);
+      w.finish();
+    } else {
+      uint8_t st = o + r + a > heap_bytes ? 2 : 0;
+      for (uint32_t k = 0; k < r + a && !st; ++k)
+        if (heap[o + k] & 0x80) st = 1;  // non-ASCII alleles: outside the contract
+      state[i] = st;
+      uint64_t len = 0;
+      if (!st) {
+        Out<false> w(nullptr, 0);
+        display_json<true>(w, chrom[i], pos[i], end[i], heap + o, r, heap + o + r, a);
+        len = w.p;
+      }
+      out_off[i] = len;
+    }
+  }
+}
+
+}  // namespace avdb
+
+using namespace avdb;
+
+static size_t scan_bytes(size_t n) {
+  size_t t = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, static_cast<const unsigned long long*>(nullptr),
+                                         static_cast<unsigned long long*>(nullptr), n);
+  return (t + 255) & ~size_t(255);
+}
+
+extern "C" int avdb_format_workspace_size(size_t n, size_t* bytes) {
+  if (!bytes) return AVDB_EINVAL;
+  *bytes = scan_bytes(n + 1) + 256;
+  return AVDB_OK;
+}
+
+static int fill_args(FormatArgs* A, avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                     const avdb_vcf_line* lines, const uint64_t* rec_off, const uint32_t* end,
+                     const uint32_t* bin_code, const uint8_t* status, const char* digest,
+                     const uint8_t* keep, const avdb_format_opts* opts) {
+  if (!ctx || !lines || !rec_off || !end || !bin_code || !status || (text_bytes && !text)) {
+    avdb_set_error("avdb_vcf_format: null argument");
+    return AVDB_EINVAL;
+  }
+  memset(A, 0, sizeof(*A));
+  A->text = text;
+  A->text_bytes = text_bytes;
+  A->n_lines = n_lines;
+  A->lines = lines;
+  A->rec_off = rec_off;
+  A->end = end;
+  A->code = bin_code;
+  A->status = status;
+  A->digest = digest;
+  A->keep = keep;
+  A->max_seq_len = opts ? opts->max_seq_len : 50u;
+  const char* alg = opts && opts->alg_id ? opts->alg_id : "";
+  const size_t n = strlen(alg);
+  if (n >= AVDB_MAX_ALG_ID) {
+    avdb_set_error("avdb_vcf_format: algorithm id longer than %d bytes", AVDB_MAX_ALG_ID - 1);
+    return AVDB_EINVAL;
+  }
+  memcpy(A->alg, alg, n);
+  A->alg_len = uint32_t(n);
+  return AVDB_OK;
+}
+
+extern "C" int avdb_vcf_format_size(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                                    const avdb_vcf_line* lines, const uint64_t* rec_off,
+                                    const uint32_t* end, const uint32_t* bin_code, const uint8_t* status,
+                                    const char* digest, const uint8_t* keep,
+                                    const avdb_format_opts* opts, void* workspace,
+                                    size_t workspace_bytes, uint64_t* copy_off, uint64_t* map_off,
+                                    uint8_t* line_state, void* stream) {
+  FormatArgs A;
+  if (int rc = fill_args(&A, ctx, text, text_bytes, n_lines, lines, rec_off, end, bin_code, status,
+                         digest, keep, opts))
+    return rc;
+  if (!copy_off || !map_off || !line_state) {
+    avdb_set_error("avdb_vcf_format_size: null output");
+    return AVDB_EINVAL;
+  }
+  size_t need = 0;
+  avdb_format_workspace_size(n_lines, &need);
+  if (!workspace || workspace_bytes < need) {
+    avdb_set_error("avdb_vcf_format_size: workspace of %zu bytes required", need);
+    return AVDB_ERANGE;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto* co = reinterpret_cast<unsigned long long*>(copy_off);
+  auto* mo = reinterpret_cast<unsigned long long*>(map_off);
+  AVDB_HIP_TRY(hipMemsetAsync(co + n_lines, 0, 8, s));
+  AVDB_HIP_TRY(hipMemsetAsync(mo + n_lines, 0, 8, s));
+  if (n_lines == 0) return AVDB_OK;
+  A.copy_off = copy_off;
+  A.map_off = map_off;
+  A.line_state = line_state;
+  const unsigned grid = stream_grid(n_lines, kBlock, 4096);
+  hipLaunchKernelGGL(k_vcf_format<false>, dim3(grid), dim3(kBlock), 0, s, A);
+  AVDB_LAUNCH_CHECK("k_vcf_format<size>");
+  size_t tb = scan_bytes(n_lines + 1);
+  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, co, co, n_lines + 1, s));
+  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, mo, mo, n_lines + 1, s));
+  return AVDB_OK;
+}
+
+extern "C" int avdb_vcf_format_write(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                                     const avdb_vcf_line* lines, const uint64_t* rec_off,
+                                     const uint32_t* end, const uint32_t* bin_code, const uint8_t* status,
+                                     const char* digest, const uint8_t* keep,
+                                     const avdb_format_opts* opts, const uint64_t* copy_off,
+                                     const uint64_t* map_off, const uint8_t* line_state,
+                                     uint8_t* copy_out, uint8_t* map_out, uint64_t* counters,
+                                     void* stream) {
+  FormatArgs A;
+  if (int rc = fill_args(&A, ctx, text, text_bytes, n_lines, lines, rec_off, end, bin_code, status,
+                         digest, keep, opts))
+    return rc;
+  if (!copy_off || !map_off || !line_state || !copy_out || !map_out) {
+    avdb_set_error("avdb_vcf_format_write: null output");
+    return AVDB_EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(copy_out) % 8 || reinterpret_cast<uintptr_t>(map_out) % 8) {
+    avdb_set_error("avdb_vcf_format_write: outputs must be 8-byte aligned");
+    return AVDB_EINVAL;
+  }
+  if (n_lines == 0) return AVDB_OK;
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  A.copy_off = const_cast<uint64_t*>(copy_off);
+  A.map_off = const_cast<uint64_t*>(map_off);
+  A.line_state = const_cast<uint8_t*>(line_state);
+  A.copy_out = copy_out;
+  A.map_out = map_out;
+  A.counters = reinterpret_cast<unsigned long long*>(counters);
+  const unsigned grid = stream_grid(n_lines, kBlock, 4096);
+  hipLaunchKernelGGL(k_vcf_format<true>, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), A);
+  AVDB_LAUNCH_CHECK("k_vcf_format<write>");
+  return AVDB_OK;
+}
+
+extern "C" int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                       const uint32_t* end, const uint64_t* allele_off,
+                                       const uint32_t* ref_len, const uint32_t* alt_len,
+                                       const uint8_t* heap, size_t heap_bytes, size_t n, void* workspace,
+                                       size_t workspace_bytes, uint64_t* out_off, uint8_t* out,
+                                       uint8_t* rec_state, void* stream) {
+  if (!ctx || !out_off || !rec_state) {
+    avdb_set_error("avdb_display_attributes: null argument");
+    return AVDB_EINVAL;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto* oo = reinterpret_cast<unsigned long long*>(out_off);
+  if (!out) {  // size pass + scan
+    AVDB_HIP_TRY(hipMemsetAsync(oo + n, 0, 8, s));
+    if (n == 0) return AVDB_OK;
+    if (!chrom || !pos || !end || !allele_off || !ref_len || !alt_len || !heap) {
+      avdb_set_error("avdb_display_attributes: null array");
+      return AVDB_EINVAL;
+    }
+    size_t need = 0;
+    avdb_format_workspace_size(n, &need);
+    if (!workspace || workspace_bytes < need) {
+      avdb_set_error("avdb_display_attributes: workspace of %zu bytes required", need);
+      return AVDB_ERANGE;
+    }
+    const unsigned grid = stream_grid(n, kBlock, 4096);
+    hipLaunchKernelGGL(k_display<false>, dim3(grid), dim3(kBlock), 0, s, chrom, pos, end, allele_off,
+                       ref_len, alt_len, heap, heap_bytes, n, out_off, nullptr, rec_state);
+    AVDB_LAUNCH_CHECK("k_display<size>");
+    size_t tb = scan_bytes(n + 1);
+    AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, oo, oo, n + 1, s));
+    return AVDB_OK;
+  }
+  if (n == 0) return AVDB_OK;
+  if (reinterpret_cast<uintptr_t>(out) % 8) {
+    avdb_set_error("avdb_display_attributes: output must be 8-byte aligned");
+    return AVDB_EINVAL;
+  }
+  const unsigned grid = stream_grid(n, kBlock, 4096);
+  hipLaunchKernelGGL(k_display<true>, dim3(grid), dim3(kBlock), 0, s, chrom, pos, end, allele_off, ref_len,
+                     alt_len, heap, heap_bytes, n, out_off, out, rec_state);
+  AVDB_LAUNCH_CHECK("k_display<write>");
+  return AVDB_OK;
+}

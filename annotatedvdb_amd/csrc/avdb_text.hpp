@@ -1,0 +1,60 @@
+// Text helpers shared by the VCF tokenizer (K0, avdb_vcf.hip) and the COPY /
+// .mapping formatter (K5, avdb_format.hip).
+#pragma once
+
+#include "avdb_internal.hpp"
+
+namespace avdb {
+
+__device__ __forceinline__ uint64_t zero_bytes_mask(uint64_t y) {  // bit 7 of each zero byte
+  const uint64_t lo7 = 0x7F7F7F7F7F7F7F7Full;
+  return ~(((y & lo7) + lo7) | y | lo7);
+}
+
+constexpr uint64_t kHiBits = 0x8080808080808080ull;
+
+// 8 bytes at aligned address a (bytes outside [lo,hi) read as 0x00)
+__device__ __forceinline__ uint64_t text_word(uintptr_t a, const Heap& h) { return heap_word(a, h); }
+
+__device__ __forceinline__ bool is_ws(uint8_t c) {
+  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
+}
+__device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+__device__ __forceinline__ bool is_alnum(uint8_t c) {
+  return is_digit(c) || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z');
+}
+
+// A workgroup's text window: the bytes of lines [base, last) staged in LDS as
+// 16-byte words.  staged == false when it exceeds kStage (lanes then read the
+// text from global memory).
+constexpr uint32_t kStage = 36 * 1024;  // 4 workgroups per CU in 160 KB LDS
+
+struct Window {
+  uintptr_t a0;  // 16-aligned address of LDS byte 0
+  bool staged;
+};
+
+__device__ __forceinline__ Window stage_window(const Heap& h, size_t s0, size_t s1, u32x4* lds) {
+  Window w;
+  w.a0 = (h.lo + s0) & ~uintptr_t(15);
+  const uintptr_t end = h.lo + s1;
+  const size_t n16 = (end - w.a0 + 15) / 16;
+  w.staged = n16 * 16 <= kStage;
+  if (w.staged) {
+    for (size_t i = threadIdx.x; i < n16; i += blockDim.x) {
+      const uintptr_t a = w.a0 + 16 * i;
+      u32x4 v;
+      if (a >= h.lo && a + 16 <= h.hi) {
+        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a));
+      } else {
+        const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
+        v = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};
+      }
+      lds[i] = v;
+    }
+  }
+  __syncthreads();
+  return w;
+}
+
+}  // namespace avdb

@@ -19,6 +19,7 @@
 // Only canonical text is resolved here; the rest is flagged (AVDB_VCF_*_HOST) for
 // the host to resolve with Python's own coercion rules.
 #include "avdb_internal.hpp"
+#include "avdb_text.hpp"
 
 #include <hipcub/hipcub.hpp>
 
@@ -26,19 +27,11 @@ namespace avdb {
 
 constexpr int kVcfGrid = 1024;
 
-__device__ __forceinline__ uint64_t zero_bytes_mask(uint64_t y) {  // bit 7 of each zero byte
-  const uint64_t lo7 = 0x7F7F7F7F7F7F7F7Full;
-  return ~(((y & lo7) + lo7) | y | lo7);
-}
-
 __device__ __forceinline__ uint32_t count_byte(uint64_t x, uint64_t pattern) {
   return uint32_t(__popcll(zero_bytes_mask(x ^ pattern)));
 }
 
 constexpr uint64_t kNL = 0x0A0A0A0A0A0A0A0Aull;
-
-// 8 bytes at aligned address a (bytes outside [lo,hi) read as 0x00)
-__device__ __forceinline__ uint64_t text_word(uintptr_t a, const Heap& h) { return heap_word(a, h); }
 
 // The text is cut into kVcfGrid * kVcfWaves contiguous, 64-byte-aligned wave
 // sub-chunks; k_vcf_count and k_vcf_starts use the same cut, so the starts pass
@@ -191,14 +184,6 @@ __global__ __launch_bounds__(kBlock) void k_vcf_starts(const uint8_t* __restrict
   }
 }
 
-__device__ __forceinline__ bool is_ws(uint8_t c) {
-  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
-}
-__device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
-__device__ __forceinline__ bool is_alnum(uint8_t c) {
-  return is_digit(c) || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z');
-}
-
 // contig code of a CHROM field (vcf_parser.py:133-150 + bin_index.py:64): plain
 // digits go through int(); 'MT' -> 'M'; every 'chr' removed in one left-to-right
 // pass (str.replace); then chr1..22, X, Y, M.  *host set for non-alphanumeric bytes.
@@ -251,7 +236,6 @@ __device__ uint64_t rs_number(const uint8_t* p, uint32_t n) {
   return v;
 }
 
-constexpr uint64_t kHiBits = 0x8080808080808080ull;
 constexpr uint64_t kTab = 0x0909090909090909ull;
 constexpr uint64_t kSemi = 0x3B3B3B3B3B3B3B3Bull;
 
@@ -411,38 +395,6 @@ __device__ __forceinline__ void parse_line(const uint8_t* s, const WordAt& word_
         recs = L.n_rec;
       }
     }
-}
-
-// A workgroup's text window: the bytes of lines [base, last) staged in LDS as
-// 16-byte words.  Returns false (window not staged) when it exceeds kStage.
-constexpr uint32_t kStage = 36 * 1024;  // 4 workgroups per CU in 160 KB LDS
-
-struct Window {
-  uintptr_t a0;  // 16-aligned address of LDS byte 0
-  bool staged;
-};
-
-__device__ __forceinline__ Window stage_window(const Heap& h, size_t s0, size_t s1, u32x4* lds) {
-  Window w;
-  w.a0 = (h.lo + s0) & ~uintptr_t(15);
-  const uintptr_t end = h.lo + s1;
-  const size_t n16 = (end - w.a0 + 15) / 16;
-  w.staged = n16 * 16 <= kStage;
-  if (w.staged) {
-    for (size_t i = threadIdx.x; i < n16; i += blockDim.x) {
-      const uintptr_t a = w.a0 + 16 * i;
-      u32x4 v;
-      if (a >= h.lo && a + 16 <= h.hi) {
-        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a));
-      } else {
-        const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
-        v = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};
-      }
-      lds[i] = v;
-    }
-  }
-  __syncthreads();
-  return w;
 }
 
 __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict__ text,

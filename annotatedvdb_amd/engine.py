@@ -166,6 +166,17 @@ class VcfBatch:
         return self.lines.cpu().numpy()[: self.n_lines * 80].view(VCF_LINE_DTYPE)
 
 
+@dataclass
+class FormatResult:
+    """Output of ``Engine.vcf_format`` (device tensors)."""
+    copy: torch.Tensor           # uint8: COPY rows of every GPU-rendered line, in line order
+    mapping: torch.Tensor        # uint8: .mapping lines
+    copy_off: torch.Tensor       # int64[n_lines + 1]: start of each line's rows
+    map_off: torch.Tensor        # int64[n_lines + 1]
+    line_state: torch.Tensor     # uint8[n_lines]: LINE_GPU / LINE_HOST / LINE_SKIP
+    counters: torch.Tensor
+
+
 # ---------------------------------------------------------------------------
 # engine
 # ---------------------------------------------------------------------------
@@ -388,6 +399,62 @@ class Engine:
                 N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s))
         return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
                         records=b, rec_line=rec_line, rec_alt=rec_alt)
+
+    # -- K5: COPY rows / .mapping lines / display attributes --------------------
+    def vcf_format(self, vb: "VcfBatch", end: torch.Tensor, code: torch.Tensor, status: torch.Tensor,
+                   digest: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None,
+                   alg_id="", max_seq_len: int = 50,
+                   counters: Optional[torch.Tensor] = None) -> "FormatResult":
+        """The load driver's COPY buffer and .mapping text for ``vb``'s lines
+        (K5b: size pass, scans, one host sync for the totals, write pass)."""
+        n = vb.n_lines
+        s = self._stream()
+        tp = N.ptr(vb.text) if vb.text.numel() else None
+        opts = N.FormatOpts(str(alg_id).encode(), int(max_seq_len), 0)
+        if len(opts.alg_id) >= N.MAX_ALG_ID:
+            raise ValueError("algorithm id too long")
+        sz = ctypes.c_size_t()
+        self.lib.avdb_format_workspace_size(n, ctypes.byref(sz))
+        ws = self.empty(int(sz.value), torch.uint8)
+        copy_off = self.empty(n + 1, torch.int64)
+        map_off = self.empty(n + 1, torch.int64)
+        state = self.empty(max(1, n), torch.uint8)
+        dg = None if digest is None else N.ptr(digest)
+        kp = None if keep is None else N.ptr(keep)
+        args = (self.ctx, tp, vb.text.numel(), n, N.ptr(vb.lines), N.ptr(vb.rec_off), N.ptr(end), N.ptr(code),
+                N.ptr(status), dg, kp, ctypes.byref(opts))
+        N.check("avdb_vcf_format_size", self.lib.avdb_vcf_format_size(
+            *args, N.ptr(ws), ws.numel(), N.ptr(copy_off), N.ptr(map_off), N.ptr(state), s))
+        tot = torch.stack([copy_off[n], map_off[n]]).cpu().tolist()
+        copy = self.empty(max(8, int(tot[0])), torch.uint8)
+        mapping = self.empty(max(8, int(tot[1])), torch.uint8)
+        ctr = counters if counters is not None else self.new_counters()
+        N.check("avdb_vcf_format_write", self.lib.avdb_vcf_format_write(
+            *args, N.ptr(copy_off), N.ptr(map_off), N.ptr(state), N.ptr(copy), N.ptr(mapping), N.ptr(ctr), s))
+        return FormatResult(copy=copy[: int(tot[0])], mapping=mapping[: int(tot[1])], copy_off=copy_off,
+                            map_off=map_off, line_state=state[:n], counters=ctr)
+
+    def display_attributes(self, b: RecordBatch, end: torch.Tensor):
+        """K5a: json.dumps(get_display_attributes()) per record.  Returns
+        ``(text uint8, off int64[n+1], state uint8[n])`` device tensors."""
+        b = b if b.device == self.device else b.to(self.device)
+        self._check_alleles(b)
+        n = b.n
+        s = self._stream()
+        sz = ctypes.c_size_t()
+        self.lib.avdb_format_workspace_size(n, ctypes.byref(sz))
+        ws = self.empty(int(sz.value), torch.uint8)
+        off = self.empty(n + 1, torch.int64)
+        state = self.empty(max(1, n), torch.uint8)
+        end = self._dev(end)
+        args = (self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(end), N.ptr(b.allele_off), N.ptr(b.ref_len),
+                N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, N.ptr(ws), ws.numel(), N.ptr(off))
+        N.check("avdb_display_attributes", self.lib.avdb_display_attributes(*args, None, N.ptr(state), s))
+        total = int(off[n].item())
+        out = self.empty(max(8, total), torch.uint8)
+        if n:
+            N.check("avdb_display_attributes", self.lib.avdb_display_attributes(*args, N.ptr(out), N.ptr(state), s))
+        return out[:total], off, state[:n]
 
     # -- formatting (host) ---------------------------------------------------
     def format_path(self, chrom_code: int, code: int) -> Optional[str]:

@@ -13,6 +13,11 @@ does the same for a whole batch with one pass of the GPU kernels:
     K3     in-batch primary-key dedup (optional)       (avdb_pk_dedup)
     host   ltree path / key text, COPY rows, mapping
 
+``load_vcf_text(text)`` is the whole-batch GPU path of the load driver
+(Load/bin/load_vcf_file.py:101-119): K0 tokenize, K2, K4, (K3), then K5 writes
+the COPY rows and the .mapping lines as text on the device; lines the GPU does
+not render byte-exact are rendered here, in place.
+
 ``parse_variant`` is ``parse_variants([line])``: one code path, one set of
 semantics.  Exceptions match the reference at the same record: ``ValueError``
 when a key cannot be built (e.g. ``':'`` inside an allele breaks
@@ -20,8 +25,8 @@ when a key cannot be built (e.g. ``':'`` inside an allele breaks
 ladder :234-256), ``TypeError`` when the location has no bin
 (bin_index.py:75).  Database-backed features (``--skipExisting`` lookups, ADSP
 duplicate updates, ``update_existing``, COPY into Postgres) are outside the
-bin/key path and raise ``NotImplementedError``.  The ``display_attributes``
-COPY column is written as ``NULL``.
+bin/key path and raise ``NotImplementedError``.  Display attributes come from
+K5a (``avdb_display_attributes``); alleles must be ASCII (VCF 4.x REF/ALT).
 """
 
 from __future__ import annotations
@@ -72,6 +77,7 @@ class VCFVariantLoader(object):
         self._skip_existing = False
         self._update_existing = False
         self._vcf_header_fields = None
+        self.last_load_stats = None
         self._initialize_counters()
         self.initialize_copy_buffer()
         self.logger.info(type(self).__name__ + " initialized")
@@ -216,7 +222,8 @@ class VCFVariantLoader(object):
         (vcf_variant_loader.py:351-391)."""
         return self.parse_variants([line], flags)[0]
 
-    def parse_variants(self, lines: Sequence, flags=None, errors: str = "raise", dedup: bool = False):
+    def parse_variants(self, lines: Sequence, flags=None, errors: str = "raise", dedup: bool = False,
+                       keep_override=None):
         """Batched ``parse_variant``.  ``errors='raise'`` stops at the first
         failing line exactly like a loop of ``parse_variant`` would (earlier
         lines fully applied, the failing line's earlier alts applied);
@@ -263,9 +270,9 @@ class VCFVariantLoader(object):
                              [r[5].ref_allele.encode() for r in recs], [r[1].encode() for r in recs],
                              [interner.key(r[5].ref_snp_id) for r in recs])
             db = b.to(self._engine.device)
-        paths, pks, keep = self._gpu_prep(recs, db, codes, dedup)
+        paths, pks, keep, disp = self._gpu_prep(recs, db, codes, dedup, keep_override)
         # ---- phase 3: emit in order --------------------------------------------
-        return self._emit(parsed, recs, paths, pks, keep, errors)
+        return self._emit(parsed, recs, paths, pks, keep, disp, errors)
 
     def parse_vcf_text(self, text, errors: str = "raise", dedup: bool = False):
         """``parse_variants`` for raw VCF text, tokenized on the GPU (K0).
@@ -365,8 +372,130 @@ class VCFVariantLoader(object):
             db = _select(db, sel)
             codes = codes[keep_rows]
         assert db.n == len(recs), (db.n, len(recs))
-        paths, pks, keep = self._gpu_prep(recs, db if recs else None, codes, dedup)
-        return self._emit(parsed, recs, paths, pks, keep, errors)
+        paths, pks, keep, disp = self._gpu_prep(recs, db if recs else None, codes, dedup)
+        return self._emit(parsed, recs, paths, pks, keep, disp, errors)
+
+    def load_vcf_text(self, text, dedup: bool = False, errors: str = "raise") -> str:
+        """One batch of the load driver (Load/bin/load_vcf_file.py:101-119) on the
+        GPU: appends every COPY row to ``copy_buffer()`` and returns the
+        .mapping text (one ``id<TAB>[{...}]`` line per data line).
+
+        K0 tokenizes, K2 infers ends and bins, K4 digests long keys, K3 marks
+        in-batch duplicates when ``dedup``, and K5 writes both texts on the
+        device.  Lines K5 leaves to the host (``AVDB_LINE_HOST``) are rendered
+        through ``parse_variants`` and spliced in at their position; with
+        ``errors='raise'`` the first failing line raises after everything before
+        it (and its own earlier alts) was emitted, as a loop of
+        ``parse_variant`` would."""
+        import torch
+        from .engine import VCF_HOST_FLAGS
+        from . import _native as N
+        if self._bin_indexer is None or self._pk_generator is None:
+            raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
+        if self.is_adsp():
+            raise NotImplementedError("ADSP loads check duplicates in the database (is_duplicate); out of scope")
+        raw = bytes(text)
+        if not self.resume_load() or self._chromosome_map is not None or self._vcf_header_fields:
+            lines = [ln.rstrip() for ln in raw.decode("utf-8").split("\n") if ln and not ln.startswith("#")]
+            out = self.parse_variants(lines, errors=errors, dedup=dedup)
+            return "".join("".join("%s\t%s\n" % kv for kv in o.items()) for o in out
+                           if isinstance(o, dict))
+        eng = self._engine
+        vb = eng.vcf_tokenize(raw)
+        n = vb.n_lines
+        if n == 0:
+            return ""
+        db = vb.records
+        # K0 lines with host-resolved fields: resolve chrom/pos/refSNP key on the host
+        # before K2/K3 see the records (same as parse_vcf_text)
+        flags = vb.lines[: n * 80].view(torch.int32).view(n, 20)[:, 18]
+        hl = torch.nonzero((flags & VCF_HOST_FLAGS) != 0).squeeze(1).cpu().tolist()
+        if hl:
+            self._patch_host_records(raw, vb, hl)
+        end, code, status, _ = eng.record_prep(db, want_lcp=False)
+        digest = None
+        mx = self._pk_generator.max_sequence_length()
+        if db.n and bool(((db.ref_len + db.alt_len) > mx).any()) and self._pk_generator.has_sequence_digests():
+            digest, _ = self._pk_generator._eng().vrs_digest(db, mx)
+        keep = eng.pk_dedup(db, grouped=False) if dedup and db.n else None
+        fr = eng.vcf_format(vb, end, code, status, digest, keep, alg_id=_xstr(self._alg_invocation_id),
+                            max_seq_len=mx)
+        state = fr.line_state.cpu().numpy()
+        copy_off = fr.copy_off.cpu().numpy()
+        map_off = fr.map_off.cpu().numpy()
+        copy_raw = fr.copy.cpu().numpy().tobytes().decode("ascii")
+        map_raw = fr.mapping.cpu().numpy().tobytes().decode("ascii")
+        ctr = fr.counters.cpu().numpy()
+        host = np.nonzero(state == N.LINE_HOST)[0]
+        n_data = int(np.count_nonzero(state != N.LINE_SKIP))
+        # GPU-rendered lines' counters (vcf_variant_loader.py:279,344; variant_loader.py:94)
+        self.increment_counter("line", n_data - len(host))
+        self.increment_counter("variant", int(ctr[N.CTR_COPY_ROWS]))
+        self.increment_counter("skipped", int(ctr[N.CTR_SKIPPED_ALTS]))
+        self.increment_counter("duplicates", int(ctr[N.CTR_DUP_ROWS]))
+        self.last_load_stats = {"lines": n_data, "gpu_lines": n_data - len(host), "host_lines": len(host),
+                                "copy_bytes": len(copy_raw), "mapping_bytes": len(map_raw)}
+        if len(host) == 0:
+            self._copy_buffer.write(copy_raw)
+            return map_raw
+        rec_off = vb.rec_off.cpu().numpy()
+        keep_h = keep.cpu().numpy() if keep is not None else None
+        L = vb.lines[: n * 80].view(torch.uint8)
+        maps = []
+        c0 = m0 = 0
+        for li in host.tolist():
+            # GPU text of the lines before this one
+            self._copy_buffer.write(copy_raw[c0:copy_off[li]])
+            maps.append(map_raw[m0:map_off[li]])
+            c0, m0 = int(copy_off[li]), int(map_off[li])
+            rec = np.frombuffer(L[li * 80:(li + 1) * 80].cpu().numpy().tobytes(), dtype=np.uint64)
+            st, ln = int(rec[0]), int(rec[1] & 0xFFFFFFFF)
+            line = raw[st:st + ln].decode("utf-8")
+            kov = None if keep_h is None else keep_h[rec_off[li]:rec_off[li + 1]]
+            try:
+                res = self.parse_variants([line], errors="raise", keep_override=kov)[0]
+            except Exception as err:  # noqa: BLE001
+                if errors == "raise":
+                    raise
+                maps.append("")
+                continue
+            maps.append("".join("%s\t%s\n" % kv for kv in res.items()))
+        self._copy_buffer.write(copy_raw[c0:])
+        maps.append(map_raw[m0:])
+        return "".join(maps)
+
+    def _patch_host_records(self, raw, vb, line_ids):
+        """Host resolution of K0-flagged lines' chrom / pos / refSNP key in the
+        device records (the GPU only canonicalises plain text)."""
+        import torch
+        from .engine import ExtIdInterner
+        eng = self._engine
+        db = vb.records
+        n = vb.n_lines
+        Lh = vb.lines[: n * 80].view(torch.uint8).view(n, 80)[torch.tensor(line_ids, device=eng.device)]
+        Lh = Lh.cpu().numpy()
+        rec_off = vb.rec_off[torch.tensor(line_ids, device=eng.device)].cpu().numpy()
+        nrec = vb.rec_off[torch.tensor(line_ids, device=eng.device) + 1].cpu().numpy() - rec_off
+        interner = ExtIdInterner()
+        idx, vals = [], []
+        for k in range(len(line_ids)):
+            w = np.frombuffer(Lh[k].tobytes(), dtype=np.uint64)
+            st, ln = int(w[0]), int(w[1] & 0xFFFFFFFF)
+            try:
+                v = VcfEntryParser(raw[st:st + ln].decode("utf-8")).get_variant(dbSNP=self.is_dbsnp(),
+                                                                               namespace=True)
+            except Exception:  # noqa: BLE001 — the host renderer raises it at this line
+                continue
+            key = interner.key(v.ref_snp_id)
+            for j in range(int(nrec[k])):
+                idx.append(int(rec_off[k]) + j)
+                vals.append((min(bin_index_chrom_code(v.chromosome), 255), v.position, key))
+        if idx:
+            it = torch.tensor(idx, dtype=torch.int64, device=eng.device)
+            db.chrom[it] = torch.tensor([x[0] for x in vals], dtype=torch.uint8, device=eng.device)
+            db.pos[it] = torch.tensor([x[1] for x in vals], dtype=torch.int64).to(torch.int32).to(eng.device)
+            db.ext_id[it] = torch.tensor([x[2] if x[2] < (1 << 63) else x[2] - (1 << 64) for x in vals],
+                                         dtype=torch.int64, device=eng.device)
 
     # ---- shared pieces --------------------------------------------------------
     def _records_of(self, parsed):
@@ -389,18 +518,23 @@ class VCFVariantLoader(object):
                 recs.append([li, alt, metaseq, pk_err, len(ref) + len(alt) > max_len, v])
         return recs
 
-    def _gpu_prep(self, recs, db, codes, dedup):
-        """K2 (+K3) on the device batch, then ltree text and primary keys."""
+    def _gpu_prep(self, recs, db, codes, dedup, keep_override=None):
+        """K2 (+K3) and K5a on the device batch, then ltree text, primary keys
+        and display-attribute JSON per record."""
         n = len(recs)
         pks: List[Optional[str]] = [None] * n
         if not n:
-            return [], pks, None
+            return [], pks, None, []
         eng = self._engine
         d_end, d_code, d_status, _ = eng.record_prep(db, want_lcp=False)
-        d_keep = eng.pk_dedup(db, grouped=False) if dedup else None
+        if keep_override is not None:
+            keep = np.asarray(keep_override, dtype=np.uint8)
+        else:
+            d_keep = eng.pk_dedup(db, grouped=False) if dedup else None
+            keep = d_keep.cpu().numpy() if d_keep is not None else None
         code = d_code.cpu().numpy().view(np.uint32)
-        keep = d_keep.cpu().numpy() if d_keep is not None else None
         paths = eng.format_paths(np.asarray(codes, dtype=np.uint8), code)
+        disp = _display_texts(eng, db, d_end)
         # primary keys (short: text; long: K4 digests in one launch)
         items, idx = [], []
         for i, r in enumerate(recs):
@@ -417,9 +551,9 @@ class VCFVariantLoader(object):
                     pks[i] = self._pk_generator.generate_primary_keys([it])[0]
                 except ValueError as err:
                     recs[i][3] = err
-        return paths, pks, keep
+        return paths, pks, keep, disp
 
-    def _emit(self, parsed, recs, paths, pks, keep, errors):
+    def _emit(self, parsed, recs, paths, pks, keep, disp, errors):
         out = []
         ri = 0
         for li, p in enumerate(parsed):
@@ -444,12 +578,21 @@ class VCFVariantLoader(object):
                 r = recs[ri]
                 i = ri
                 ri += 1
+                # same order of failure as vcf_variant_loader.py:282-328: key, bin, FREQ
                 if r[3] is not None:
                     failed = r[3] if isinstance(r[3], Exception) else ValueError(str(r[3]))
                     break
                 path = paths[i]
                 if path is None:
                     failed = TypeError("'NoneType' object is not subscriptable")
+                    break
+                try:
+                    freq = _freq_str(entry, alt)
+                except Exception as err:  # noqa: BLE001 — raised by get_frequencies, as the reference
+                    failed = err
+                    break
+                if disp[i] is None:
+                    failed = ValueError("non-ASCII allele: outside the GPU path's contract")
                     break
                 pk = pks[i]
                 if keep is not None and not keep[i]:
@@ -458,8 +601,7 @@ class VCFVariantLoader(object):
                     self.add_copy_str("#".join([
                         "chr" + _xstr(v.chromosome), pk, _xstr(v.position), r[2], path,
                         _xstr(self._alg_invocation_id), _xstr(v.ref_snp_id, nullStr="NULL"),
-                        _xstr(v.is_multi_allelic, falseAsNull=True, nullStr="NULL"),
-                        "NULL", _freq_str(entry, alt)]))
+                        _xstr(v.is_multi_allelic, falseAsNull=True, nullStr="NULL"), disp[i], freq]))
                     self.increment_counter("variant")
                 mapping.append({"primary_key": pk, "bin_index": path})
             if failed is not None:
@@ -471,7 +613,6 @@ class VCFVariantLoader(object):
             out.append({v.id: mapping})
         return out
 
-
 class _LazyEntry:
     """Stands in for a parsed VcfEntryParser when only INFO FREQ may be needed."""
 
@@ -482,11 +623,20 @@ class _LazyEntry:
         self._e = None
 
     def get_frequencies(self, alt):
-        if "FREQ=" not in self._line:
+        if "FREQ" not in self._line:
             return None
         if self._e is None:
             self._e = VcfEntryParser(self._line)
         return self._e.get_frequencies(alt)
+
+
+def _display_texts(eng, db, d_end) -> List[Optional[str]]:
+    """K5a display-attribute JSON per record (None: non-ASCII alleles)."""
+    text, off, state = eng.display_attributes(db, d_end)
+    raw = text.cpu().numpy().tobytes().decode("ascii")
+    o = off.cpu().numpy()
+    st = state.cpu().numpy()
+    return [raw[o[i]:o[i + 1]] if st[i] == 0 else None for i in range(len(st))]
 
 
 def _select(b, idx):
@@ -503,9 +653,8 @@ def _next_line_start(recs, ri, li):
 
 
 def _freq_str(entry, alt):
+    """xstr(get_frequencies(alt), nullStr='NULL') (vcf_variant_loader.py:313,329);
+    exceptions propagate as in the reference."""
     import json
-    try:
-        f = entry.get_frequencies(alt)
-    except Exception:  # noqa: BLE001 — malformed FREQ: reference would raise; keep NULL
-        return "NULL"
+    f = entry.get_frequencies(alt)
     return "NULL" if f is None else json.dumps(f)

@@ -196,8 +196,11 @@ def vcf_text(n_lines: int, seed: int = 6, lengths=None, multi_frac: float = 0.1,
         alt = b",".join(alts).decode()
         rid = "rs%d" % rsn[i] if has_rs[i] else "."
         vc = "SNV" if u[i] < 0.8 else ("INDEL" if u[i] < 0.9 else "MNV")
-        inf = ("RS=%d;dbSNPBuildID=151;SSR=0;VC=%s;FREQ=1000Genomes:0.%04d,0.%04d"
-               % (rsn[i], vc, 10000 - fq[i], fq[i])) if info else "."
+        # FREQ: one value for REF and one per ALT (vcf_parser.py:213-220 indexes by ALT)
+        fr = "1000Genomes:0.%04d,0.%04d" % (10000 - fq[i], fq[i]) + (",." if multi[i] else "")
+        if fq[i] % 3 == 0:
+            fr += "|GnomAD:0.%04d,0.%04d" % (10000 - fq[i] // 2, fq[i] // 2) + (",0.0001" if multi[i] else "")
+        inf = ("RS=%d;dbSNPBuildID=151;SSR=0;VC=%s;FREQ=%s" % (rsn[i], vc, fr)) if info else "."
         out.append("%s\t%d\t%s\t%s\t%s\t.\t.\t%s" % (CHROM_NAMES[chrom[i]], pos[i], rid,
                                                     ref.decode(), alt, inf))
     return ("\n".join(out) + "\n").encode()

@@ -80,6 +80,10 @@ extern "C" {
 #define AVDB_CTR_DUPLICATES 21          /* records whose primary key repeats an earlier one */
 #define AVDB_CTR_HASH_COLLISIONS 22     /* fingerprint collisions resolved by byte compare */
 #define AVDB_CTR_LONG 23                /* records with ref_len + alt_len > max_seq_len */
+#define AVDB_CTR_COPY_ROWS 24           /* COPY rows written by avdb_vcf_format_write */
+#define AVDB_CTR_SKIPPED_ALTS 25        /* ALT '.' entries skipped (vcf_variant_loader.py:277-280) */
+#define AVDB_CTR_DUP_ROWS 26            /* records whose COPY row was dropped (keep == 0) */
+#define AVDB_CTR_HOST_LINES 27          /* lines left to the host renderer */
 #define AVDB_N_COUNTERS 32
 
 typedef struct avdb_ctx avdb_ctx;
@@ -210,6 +214,58 @@ int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t 
                   uint8_t* chrom, uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len,
                   uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line,
                   uint32_t* rec_alt, void* stream);
+
+/* ---- K5: the load driver's text outputs ---------------------------------
+ * Replaces the per-alt COPY row assembly of VCFVariantLoader.__parse_alt_alleles
+ * (vcf_variant_loader.py:320-343) — primary key (primary_key_generator.py:99-122),
+ * metaseq id, bin path, refSNP, multi-allelic flag, display attributes
+ * (variant_annotator.py:134-241) and INFO FREQ allele frequencies
+ * (vcf_parser.py:200-222), both as json.dumps text — and the .mapping line
+ * (Load/bin/load_vcf_file.py:116-117), for lines K0 tokenized and K2 (end,
+ * bin_code, status), K4 (digest, long keys; NULL if none) and K3 (keep; NULL =
+ * keep all) processed.
+ *   1. avdb_vcf_format_size : line_state[n_lines] and exclusive byte offsets
+ *      copy_off[n_lines+1] / map_off[n_lines+1] (totals in [n_lines]);
+ *      workspace of avdb_format_workspace_size(n_lines) bytes.
+ *   2. avdb_vcf_format_write: the texts into copy_out / map_out (8-byte aligned,
+ *      sized by the totals); counters[AVDB_CTR_COPY_ROWS..HOST_LINES] accumulated.
+ * line_state: AVDB_LINE_GPU rendered here; AVDB_LINE_HOST zero bytes — the host
+ * renders the line (text the GPU does not canonicalise, or a line on which the
+ * reference raises); AVDB_LINE_SKIP comment line ('#', load_vcf_file.py:103). */
+#define AVDB_LINE_GPU 0
+#define AVDB_LINE_HOST 1
+#define AVDB_LINE_SKIP 2
+#define AVDB_MAX_ALG_ID 64
+
+typedef struct avdb_format_opts {
+  const char* alg_id;     /* xstr(row_algorithm_id), host NUL-terminated; NULL = "" */
+  uint32_t max_seq_len;   /* primary_key_generator.py:53 (default 50) */
+  uint32_t reserved;
+} avdb_format_opts;
+
+int avdb_format_workspace_size(size_t n, size_t* bytes);
+int avdb_vcf_format_size(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                         const avdb_vcf_line* lines, const uint64_t* rec_off, const uint32_t* end,
+                         const uint32_t* bin_code, const uint8_t* status, const char* digest,
+                         const uint8_t* keep, const avdb_format_opts* opts, void* workspace,
+                         size_t workspace_bytes, uint64_t* copy_off, uint64_t* map_off,
+                         uint8_t* line_state, void* stream);
+int avdb_vcf_format_write(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                          const avdb_vcf_line* lines, const uint64_t* rec_off, const uint32_t* end,
+                          const uint32_t* bin_code, const uint8_t* status, const char* digest,
+                          const uint8_t* keep, const avdb_format_opts* opts, const uint64_t* copy_off,
+                          const uint64_t* map_off, const uint8_t* line_state, uint8_t* copy_out,
+                          uint8_t* map_out, uint64_t* counters, void* stream);
+/* get_display_attributes (variant_annotator.py:134-241) of a record batch as
+ * json.dumps text (ASCII alleles; json escaping applied).  end = K2's end.
+ * Call with out == NULL first: rec_state[i] (0 ok, 1 non-ASCII allele, 2 heap
+ * overrun) and exclusive offsets out_off[n+1]; then with out (8-byte aligned,
+ * out_off[n] bytes).  Contigs >= 25 get no label inside normalized_metaseq_id. */
+int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint32_t* end,
+                            const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                            const uint8_t* heap, size_t heap_bytes, size_t n, void* workspace,
+                            size_t workspace_bytes, uint64_t* out_off, uint8_t* out, uint8_t* rec_state,
+                            void* stream);
 
 /* ---- host-side formatting of kernel outputs -------------------------------
  * ltree path text (<= AVDB_MAX_PATH bytes).  Returns the length written (no

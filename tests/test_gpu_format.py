@@ -1,0 +1,158 @@
+"""K5 (COPY rows, .mapping lines, display attributes) on the GPU vs the
+reference's own load-driver output (tests/golden/vcf_load.tsv.gz,
+display_attrs.tsv.gz) and vs the oracle on synthetic dbSNP-shaped text.
+Text output: byte-exact."""
+
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from annotatedvdb_amd.chromosomes import CHROM_NAMES, length_table
+from oracle import avdb_oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def read_tsv(name):
+    with gzip.open(os.path.join(GOLDEN, name), "rt") as fh:
+        header = fh.readline().rstrip("\n").split("\t")
+        return [dict(zip(header, line.rstrip("\n").split("\t"))) for line in fh]
+
+
+def load_rows():
+    with gzip.open(os.path.join(GOLDEN, "vcf_load.tsv.gz"), "rt") as fh:
+        fh.readline()
+        out = []
+        for line in fh:
+            raw, err, mapping, copy = line.rstrip("\n").split("\t")
+            out.append((raw.replace("\\t", "\t"), err or None, json.loads(mapping), json.loads(copy)))
+        return out
+
+
+@pytest.fixture()
+def loader():
+    from annotatedvdb_amd.loaders import VCFVariantLoader
+    ld = VCFVariantLoader("dbSNP")
+    ld.initialize_pk_generator("GRCh38", None)
+    ld.initialize_bin_indexer(None)
+    ld.set_algorithm_invocation_id(1)
+    ld.initialize_copy_sql()
+    return ld
+
+
+def _display(engine, recs):
+    from annotatedvdb_amd.engine import pack_records
+    b = pack_records([r[0] for r in recs], [r[1] for r in recs], [r[2].encode() for r in recs],
+                     [r[3].encode() for r in recs])
+    end, _, _, _ = engine.record_prep(b, want_lcp=False)
+    text, off, state = engine.display_attributes(b, end)
+    raw = text.cpu().numpy().tobytes().decode("ascii")
+    o = off.cpu().numpy()
+    st = state.cpu().numpy()
+    return [raw[o[i]:o[i + 1]] if st[i] == 0 else None for i in range(len(recs))]
+
+
+def test_k5a_display_attributes_golden(engine):
+    rows = read_tsv("display_attrs.tsv.gz")
+    recs = [(CHROM_NAMES.index(r["chrom"]), int(r["pos"]), r["ref"], r["alt"]) for r in rows]
+    got = _display(engine, recs)
+    for r, g in zip(rows, got):
+        assert g == r["attributes"], r
+
+
+def test_k5a_display_attributes_escaping_vs_oracle(engine):
+    pairs = [('A"', 'A'), ("A\\", "AC\\"), ("A\tB", "A"), ("\x01", "\x7f"), ("AC", "A'"), ("<DEL>", "A"),
+             ("A", "<INS:ME>"), ("", "A"), ("A", ""), ("", ""), ("AT", "AT"), ("ATA", "ATA"), ("A", "*"),
+             ("CAG", "CAGCAGCAG"), ("C", "CAGCAG"), ("CA" * 80, "C"), ("G" + "TC" * 70, "G" + "TC" * 75)]
+    recs = [(i % 25, 1000 + i, r, a) for i, (r, a) in enumerate(pairs)]
+    got = _display(engine, recs)
+    for (c, p, r, a), g in zip(recs, got):
+        assert g == json.dumps(O.display_attributes(CHROM_NAMES[c], p, r, a)), (r, a)
+    # non-ASCII alleles are outside the contract: state 1, no text
+    assert _display(engine, [(0, 5, "A", "é")]) == [None]
+
+
+def test_k5b_load_driver_golden(engine, loader):
+    """Every golden line through the GPU load path: COPY buffer == the
+    reference's rows (all columns), .mapping text == the reference's lines."""
+    rows = load_rows()
+    text = ("\n".join(r[0] for r in rows) + "\n").encode()
+    loader.reset_copy_buffer()
+    mapping = loader.load_vcf_text(text, errors="record")
+    exp_copy = [c for r in rows for c in r[3]]
+    exp_map = [m for r in rows if r[1] is None for m in r[2]]
+    got_copy = loader.copy_buffer().getvalue().splitlines()
+    assert len(got_copy) == len(exp_copy)
+    for g, e in zip(got_copy, exp_copy):
+        assert g == e
+    assert mapping.splitlines() == exp_map
+    st = loader.last_load_stats
+    assert st["lines"] == len(rows)
+    # the rest: lines the reference fails on (7 %) and adversarial FREQ numbers / allele bytes
+    assert st["gpu_lines"] > 0.75 * len(rows), st
+
+
+def test_k5b_synthetic_vs_oracle(engine, loader):
+    """dbSNP-shaped synthetic text (FREQ on every line): every line rendered on
+    the GPU, byte-exact vs the oracle's restatement of the load driver."""
+    from annotatedvdb_amd import synth
+    text = synth.vcf_text(30000, seed=12)
+    lines = text.decode().splitlines()
+    loader.reset_copy_buffer()
+    mapping = loader.load_vcf_text(text)
+    assert loader.last_load_stats["host_lines"] == 0
+    exp_copy, exp_map = [], []
+    for ln in lines:
+        err, m, c = O.load_line(ln, length_table())
+        assert err is None
+        exp_copy += c
+        exp_map += m
+    assert loader.copy_buffer().getvalue().splitlines() == exp_copy
+    assert mapping.splitlines() == exp_map
+
+
+def test_k5b_dedup_and_counters(engine, loader):
+    rows = [r for r in load_rows() if r[1] is None][:1500]
+    text = ("\n".join(r[0] for r in rows) + "\n").encode()
+    loader.reset_copy_buffer()
+    before = {k: loader.get_count(k) for k in ("line", "variant", "duplicates", "skipped")}
+    loader.load_vcf_text(text, dedup=True)
+    got = loader.copy_buffer().getvalue().splitlines()
+    pks = [r.split("#")[1] for r in got]
+    assert len(pks) == len(set(pks))
+    all_rows = [c for r in rows for c in r[3]]
+    first = {}
+    for c in all_rows:
+        first.setdefault(c.split("#")[1], c)
+    assert got == list(first.values())
+    assert loader.get_count("variant") - before["variant"] == len(got)
+    assert loader.get_count("duplicates") - before["duplicates"] == len(all_rows) - len(got)
+    assert loader.get_count("line") - before["line"] == len(rows)
+
+
+def test_k5b_edge_lines(engine, loader):
+    text = (b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\n"
+            b"1\t10177\trs367896724\tA\tAC,.\t.\t.\tRS=367896724;FREQ=A:0.5,0.25,.\n"
+            b"chr2\t00500\t.\tG\tT,T\t.\t.\tRS=5;FREQ=B:0.9,0.00001,1e-05|C:1,0,00\n"
+            b"MT\t100\tid1\tC\tT\t.\t.\t.  \r\n"
+            b"X\t200\t.\tA\tG\t.\t.\tFREQ=D:0.1,0.0|E:0.2,.\n"
+            b"22\t2\t.\tAT\tAT\t.\t.\t.")
+    loader.reset_copy_buffer()
+    mapping = loader.load_vcf_text(text)
+    got_copy = loader.copy_buffer().getvalue().splitlines()
+    exp_copy, exp_map = [], []
+    for ln in text.decode().split("\n"):
+        if ln and not ln.startswith("#"):
+            err, m, c = O.load_line(ln, length_table())
+            assert err is None, ln
+            exp_copy += c
+            exp_map += m
+    assert got_copy == exp_copy
+    assert mapping.splitlines() == exp_map
+    with pytest.raises(IndexError):  # short FREQ list, as the reference
+        loader.load_vcf_text(b"1\t5\t.\tA\tG,T\t.\t.\tFREQ=A:0.5,0.25\n")
