@@ -14,9 +14,8 @@
 //     (load_vcf_file.py:116-117).
 //   SIZE pass (bytes per line) -> hipCUB exclusive scans -> WRITE pass, both the
 //   same templated code.  One lane per line, 256 consecutive lines per workgroup
-//   with their text staged in LDS (as K0).  Output goes through a per-lane 8-byte
-//   word buffer: aligned dwordx2 stores, byte stores only at the two ends of a
-//   lane's span.  A line the GPU does not render byte-exact (non-ASCII text,
+//   with their text staged in LDS (as K0); each lane writes its own contiguous
+//   span of both outputs (layout and alternatives measured: see Out below).  A line the GPU does not render byte-exact (non-ASCII text,
 //   allele bytes that need escaping, an unmappable record (TypeError), a key the
 //   reference cannot build (':' in an allele), malformed or non-canonical FREQ
 //   numbers, K0 host-resolved fields) is marked HOST and gets zero bytes; the
@@ -32,35 +31,28 @@
 namespace avdb {
 
 // ---------------------------------------------------------------------------
-// output sink: SIZE pass counts, WRITE pass stores through an aligned word
+// output sink: SIZE pass counts, WRITE pass stores
 // ---------------------------------------------------------------------------
+// WRITE pass: one global byte store per output byte (global_store_byte through
+// an address-space-1 pointer; flat stores were no faster).  A/B on MI355X, 2 M
+// dbSNP-shaped lines, 1.31 GB of text: byte stores 4.5 ms; an 8-byte register
+// word with aligned dwordx2 stores 12.1 ms (255 VGPRs, occupancy 1); a per-lane
+// 128-byte LDS ring flushing aligned 64-byte lines as dwordx4 stores 6.2 ms
+// (LDS-limited occupancy).  The pass is instruction-issue bound (per-byte
+// formatting work), not HBM bound: see DESIGN.md.
+typedef __attribute__((address_space(1))) uint8_t gbyte;
+
 template <bool WRITE>
 struct Out {
-  uint8_t* base;
-  uint64_t p, lo, word;
-  __device__ __forceinline__ Out(uint8_t* b, uint64_t at) : base(b), p(at), lo(at), word(0) {}
+  gbyte* base;
+  uint64_t p, lo;
+  bool bad;  // set by a formatter that cannot render its input (line goes to the host)
+  __device__ __forceinline__ Out(uint8_t* b, uint64_t at)
+      : base((gbyte*)b), p(at), lo(at), bad(false) {}
+  __device__ __forceinline__ uint32_t size() const { return uint32_t(p - lo); }
   __device__ __forceinline__ void put(uint32_t c) {
-    if constexpr (WRITE) {
-      word |= uint64_t(c & 0xFFu) << (8 * (p & 7));
-      if ((++p & 7) == 0) flush();
-    } else {
-      ++p;
-    }
-  }
-  __device__ __forceinline__ void flush() {  // the aligned word [p-8, p) is complete
-    const uint64_t a = p - 8;
-    if (a >= lo) {
-      *reinterpret_cast<uint64_t*>(base + a) = word;
-    } else {
-      for (uint64_t b = lo; b < p; ++b) base[b] = uint8_t(word >> (8 * (b - a)));
-    }
-    word = 0;
-  }
-  __device__ __forceinline__ void finish() {
-    if constexpr (WRITE) {
-      const uint64_t a = p & ~uint64_t(7);
-      for (uint64_t b = a > lo ? a : lo; b < p; ++b) base[b] = uint8_t(word >> (8 * (b - a)));
-    }
+    if constexpr (WRITE) base[p] = uint8_t(c);
+    ++p;
   }
   __device__ __forceinline__ void lit(const char* s) {
     while (*s) put(uint8_t(*s++));
@@ -69,7 +61,7 @@ struct Out {
     if constexpr (!WRITE) {
       p += n;
     } else {
-      for (uint32_t i = 0; i < n; ++i) put(s[i]);
+      for (uint32_t k = 0; k < n; ++k) put(s[k]);
     }
   }
   __device__ __forceinline__ void u32v(uint32_t v) {
@@ -98,8 +90,10 @@ __device__ __forceinline__ void chrom_name(O& o, uint32_t c) {
 }
 
 // ltree path of a bin code (generate_bin_index_references.py:54,60-61,74)
+// (noinline helpers take and return the sink by value: it stays in VGPRs
+// across the call instead of going through the scratch stack)
 template <class O>
-__device__ __noinline__ void bin_path(O& o, uint32_t c, uint32_t code) {
+__device__ __noinline__ O bin_path(O o, uint32_t c, uint32_t code) {
   o.lit("chr");
   chrom_name(o, c);
   const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
@@ -110,6 +104,7 @@ __device__ __noinline__ void bin_path(O& o, uint32_t c, uint32_t code) {
     o.lit(".B");
     o.u32v(l == 1 ? gl + 1 : (gl & 1u) + 1);
   }
+  return o;
 }
 
 // ---------------------------------------------------------------------------
@@ -175,7 +170,7 @@ __device__ __forceinline__ void al_trunc(O& o, const Al& a, uint32_t cap) {
 // chrom >= 25 writes no label in normalized_metaseq_id (the caller prepends it).
 // ---------------------------------------------------------------------------
 template <bool ESC, class O>
-__device__ __noinline__ void display_json(O& o, uint32_t chrom, uint32_t pos, uint32_t end, const uint8_t* ref,
+__device__ __noinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, const uint8_t* ref,
                              uint32_t r, const uint8_t* alt, uint32_t a) {
   const bool snv = r == 1u && a == 1u;
   uint32_t l = 0;  // common prefix (__normalize_alleles :100-107); SNVs untouched (:97-98)
@@ -278,6 +273,7 @@ __device__ __noinline__ void display_json(O& o, uint32_t chrom, uint32_t pos, ui
     o.put('"');
   }
   o.put('}');
+  return o;
 }
 
 // ---------------------------------------------------------------------------
@@ -289,25 +285,40 @@ __device__ __noinline__ void display_json(O& o, uint32_t chrom, uint32_t pos, ui
 // Anything else (signs, exponents, '_', spaces, nan/inf, > 15 significant
 // digits) returns false: the line is rendered by the host.
 // ---------------------------------------------------------------------------
-template <class O>
-__device__ __noinline__ bool json_number(O& o, const uint8_t* f, uint32_t n) {
+__device__ __forceinline__ bool number_plain(const uint8_t* f, uint32_t n) {
   if (n == 0 || n > 40) return false;
-  uint32_t dot = n;
+  uint32_t dot = n, f0 = n, l0 = 0;
   for (uint32_t i = 0; i < n; ++i) {
     if (f[i] == '.') {
       if (dot != n) return false;
       dot = i;
     } else if (!is_digit(f[i])) {
       return false;
+    } else if (f[i] != '0') {
+      if (f0 == n) f0 = i;
+      l0 = i;
     }
   }
+  if (dot == n) return true;                  // int
+  if (n == 1) return false;                   // "." alone
+  if (f0 == n) return true;                   // 0.0
+  const uint32_t nd = l0 - f0 + 1 - (f0 < dot && dot < l0 ? 1u : 0u);
+  return nd <= 15;                            // repr == these digits
+}
+
+template <class O>
+__device__ __noinline__ O json_number(O o, const uint8_t* f, uint32_t n) {
+  o.bad = !number_plain(f, n);
+  if (o.bad) return o;
+  uint32_t dot = n;
+  for (uint32_t i = 0; i < n; ++i)
+    if (f[i] == '.') dot = i;
   if (dot == n) {  // int
     uint32_t i = 0;
     while (i + 1 < n && f[i] == '0') ++i;
     o.bytes(f + i, n - i);
-    return true;
+    return o;
   }
-  if (n == 1) return false;  // "." alone
   // digits without the dot: S[k] = f[k < dot ? k : k + 1], ns = n - 1
   const uint32_t ns = n - 1;
   auto S = [&](uint32_t k) -> uint8_t { return f[k < dot ? k : k + 1]; };
@@ -318,9 +329,8 @@ __device__ __noinline__ bool json_number(O& o, const uint8_t* f, uint32_t n) {
       l0 = int32_t(k);
     }
   }
-  if (f0 < 0) { o.lit("0.0"); return true; }
+  if (f0 < 0) { o.lit("0.0"); return o; }
   const int32_t nd = l0 - f0 + 1;
-  if (nd > 15) return false;
   const int32_t e = int32_t(dot) - 1 - f0;  // decimal exponent of the first significant digit
   if (e >= -4 && e < 16) {
     if (e >= 0) {
@@ -348,7 +358,7 @@ __device__ __noinline__ bool json_number(O& o, const uint8_t* f, uint32_t n) {
     if (ae < 10) o.put('0');
     o.u32v(ae);
   }
-  return true;
+  return o;
 }
 
 // ---------------------------------------------------------------------------
@@ -435,7 +445,7 @@ __device__ bool freq_plain(const uint8_t* s, uint32_t v0, uint32_t v1) {
 // json.dumps text or NULL; false when the reference would raise or print a
 // number the GPU does not format
 template <class O>
-__device__ __noinline__ bool freq_json(O& o, const uint8_t* s, uint32_t v0, uint32_t v1, uint32_t k) {
+__device__ __noinline__ O freq_json(O o, const uint8_t* s, uint32_t v0, uint32_t v1, uint32_t k) {
   bool any = false;
   for (uint32_t p0 = v0; p0 <= v1;) {
     const uint32_t p1 = find_byte(s, p0, v1, '|');
@@ -445,7 +455,7 @@ __device__ __noinline__ bool freq_json(O& o, const uint8_t* s, uint32_t v0, uint
     uint32_t f0 = c1 + 1, idx = 0;
     while (idx < k) {
       const uint32_t cm = find_byte(s, f0, c2, ',');
-      if (cm == c2) return false;  // IndexError in the reference
+      if (cm == c2) { o.bad = true; return o; }  // IndexError in the reference
       f0 = cm + 1;
       ++idx;
     }
@@ -458,7 +468,8 @@ __device__ __noinline__ bool freq_json(O& o, const uint8_t* s, uint32_t v0, uint
       o.put('"');
       o.bytes(s + p0, c1 - p0);
       o.lit("\": {\"gmaf\": ");
-      if (!json_number(o, s + f0, fn)) return false;
+      o = json_number(o, s + f0, fn);
+      if (o.bad) return o;
       o.put('}');
       any = true;
     }
@@ -466,11 +477,11 @@ __device__ __noinline__ bool freq_json(O& o, const uint8_t* s, uint32_t v0, uint
   }
   if (any) o.put('}');
   else o.lit("NULL");
-  return true;
+  return o;
 }
 
 template <bool WRITE>
-__device__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, const uint8_t* s, size_t li,
+__device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, const uint8_t* s, size_t li,
                                Out<WRITE>& oc, Out<WRITE>& om, uint32_t* n_rows, uint32_t* n_skip,
                                uint32_t* n_dup) {
   if (L.flags & AVDB_VCF_COMMENT) return kLineSkip;
@@ -572,7 +583,7 @@ __device__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, cons
       oc.put(':');
       oc.bytes(alt, al);
       oc.put('#');
-      bin_path(oc, c, code);
+      oc = bin_path(oc, c, code);
       oc.put('#');
       oc.bytes(reinterpret_cast<const uint8_t*>(A.alg), A.alg_len);
       oc.put('#');
@@ -585,10 +596,11 @@ __device__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, cons
       oc.put('#');
       oc.lit(L.n_alt > 1 ? "True" : "NULL");
       oc.put('#');
-      display_json<false>(oc, c, L.pos, A.end[r], ref, rl, alt, al);
+      oc = display_json<false>(oc, c, L.pos, A.end[r], ref, rl, alt, al);
       oc.put('#');
       if (fq0 >= 0) {
-        if (!freq_json(oc, s, uint32_t(fq0), uint32_t(fq1), k)) return kLineHost;
+        oc = freq_json(oc, s, uint32_t(fq0), uint32_t(fq1), k);
+        if (oc.bad) return kLineHost;
       } else {
         oc.lit("NULL");
       }
@@ -597,8 +609,7 @@ __device__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, cons
     } else {
       // no COPY row, but the reference would still have evaluated FREQ
       if (fq0 >= 0) {
-        Out<false> probe(nullptr, 0);
-        if (!freq_json(probe, s, uint32_t(fq0), uint32_t(fq1), k)) return kLineHost;
+        if (freq_json(Out<false>(nullptr, 0), s, uint32_t(fq0), uint32_t(fq1), k).bad) return kLineHost;
       }
       ++dups;
     }
@@ -607,7 +618,7 @@ __device__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, cons
     om.lit("{'primary_key': '");
     pk(om);
     om.lit("', 'bin_index': '");
-    bin_path(om, c, code);
+    om = bin_path(om, c, code);
     om.lit("'}");
     ++nrec;
     ++r;
@@ -639,8 +650,6 @@ __global__ __launch_bounds__(kBlock) void k_vcf_format(FormatArgs A) {
         if (st == kLineGpu) {
           Out<true> oc(A.copy_out, A.copy_off[li]), om(A.map_out, A.map_off[li]);
           format_line<true>(A, L, s, li, oc, om, &rows, &skip, &dups);
-          oc.finish();
-          om.finish();
         } else if (st == kLineHost) {
           ++hosts;
         }
@@ -648,8 +657,8 @@ __global__ __launch_bounds__(kBlock) void k_vcf_format(FormatArgs A) {
         Out<false> oc(nullptr, 0), om(nullptr, 0);
         const uint8_t st = format_line<false>(A, L, s, li, oc, om, &rows, &skip, &dups);
         A.line_state[li] = st;
-        A.copy_off[li] = st == kLineGpu ? oc.p : 0;
-        A.map_off[li] = st == kLineGpu ? om.p : 0;
+        A.copy_off[li] = st == kLineGpu ? oc.size() : 0;
+        A.map_off[li] = st == kLineGpu ? om.size() : 0;
       }
     }
     __syncthreads();  // the window is reused by the next trip
@@ -689,8 +698,7 @@ __global__ __launch_bounds__(kBlock) void k_display(const uint8_t* __restrict__ 
     if constexpr (WRITE) {
       if (state[i]) continue;
       Out<true> w(out, out_off[i]);
-      display_json<true>(w, chrom[i], pos[i], end[i], heap + o, r, heap + o + r, a);
-      w.finish();
+      w = display_json<true>(w, chrom[i], pos[i], end[i], heap + o, r, heap + o + r, a);
     } else {
       uint8_t st = o + r + a > heap_bytes ? 2 : 0;
       for (uint32_t k = 0; k < r + a && !st; ++k)
@@ -698,9 +706,7 @@ __global__ __launch_bounds__(kBlock) void k_display(const uint8_t* __restrict__ 
       state[i] = st;
       uint64_t len = 0;
       if (!st) {
-        Out<false> w(nullptr, 0);
-        display_json<true>(w, chrom[i], pos[i], end[i], heap + o, r, heap + o + r, a);
-        len = w.p;
+        len = display_json<true>(Out<false>(nullptr, 0), chrom[i], pos[i], end[i], heap + o, r, heap + o + r, a).size();
       }
       out_off[i] = len;
     }

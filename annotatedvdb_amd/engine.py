@@ -166,6 +166,26 @@ class VcfBatch:
         return self.lines.cpu().numpy()[: self.n_lines * 80].view(VCF_LINE_DTYPE)
 
 
+class _Timer:
+    """Optional HIP-event pairs on the engine's stream (bench stage timing)."""
+
+    def __init__(self, events: Optional[dict], device):
+        self.events, self.device, self.cur = events, device, None
+
+    def start(self, name):
+        if self.events is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(self.device))
+            self.cur = (name, e)
+
+    def stop(self):
+        if self.events is not None and self.cur:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(self.device))
+            self.events.setdefault(self.cur[0], []).append((self.cur[1], e))
+            self.cur = None
+
+
 @dataclass
 class FormatResult:
     """Output of ``Engine.vcf_format`` (device tensors)."""
@@ -404,7 +424,7 @@ class Engine:
     def vcf_format(self, vb: "VcfBatch", end: torch.Tensor, code: torch.Tensor, status: torch.Tensor,
                    digest: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None,
                    alg_id="", max_seq_len: int = 50,
-                   counters: Optional[torch.Tensor] = None) -> "FormatResult":
+                   counters: Optional[torch.Tensor] = None, events: Optional[dict] = None) -> "FormatResult":
         """The load driver's COPY buffer and .mapping text for ``vb``'s lines
         (K5b: size pass, scans, one host sync for the totals, write pass)."""
         n = vb.n_lines
@@ -423,14 +443,19 @@ class Engine:
         kp = None if keep is None else N.ptr(keep)
         args = (self.ctx, tp, vb.text.numel(), n, N.ptr(vb.lines), N.ptr(vb.rec_off), N.ptr(end), N.ptr(code),
                 N.ptr(status), dg, kp, ctypes.byref(opts))
+        ev = _Timer(events, self.device)
+        ev.start("format_size")
         N.check("avdb_vcf_format_size", self.lib.avdb_vcf_format_size(
             *args, N.ptr(ws), ws.numel(), N.ptr(copy_off), N.ptr(map_off), N.ptr(state), s))
+        ev.stop()
         tot = torch.stack([copy_off[n], map_off[n]]).cpu().tolist()
         copy = self.empty(max(8, int(tot[0])), torch.uint8)
         mapping = self.empty(max(8, int(tot[1])), torch.uint8)
         ctr = counters if counters is not None else self.new_counters()
+        ev.start("format_write")
         N.check("avdb_vcf_format_write", self.lib.avdb_vcf_format_write(
             *args, N.ptr(copy_off), N.ptr(map_off), N.ptr(state), N.ptr(copy), N.ptr(mapping), N.ptr(ctr), s))
+        ev.stop()
         return FormatResult(copy=copy[: int(tot[0])], mapping=mapping[: int(tot[1])], copy_off=copy_off,
                             map_off=map_off, line_state=state[:n], counters=ctr)
 

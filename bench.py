@@ -51,6 +51,10 @@ WORKLOADS = {
                                   "GPU (K0 tokenizer: line split + field parse + multi-allelic explode)",
                 bytes_per=None, kernel="avdb_vcf (whole tokenizer)"),
 }
+WORKLOADS["load"] = dict(
+    n=8_388_608, desc="SURVEY 8f ranks 1-3: dbSNP-shaped VCF text -> COPY rows + .mapping lines on the GPU "
+                      "(K0 tokenize, K2 end+bin, K5 display attributes/FREQ/keys/paths as text)",
+    bytes_per=None, kernel="k_vcf_format<write>")
 VCF_TILE = 1 << 19  # distinct synthetic lines, tiled on the device to n
 
 
@@ -159,7 +163,7 @@ def main():
     elif a.workload in ("c3", "c4"):
         chrom, start, end = synth.spans(n, seed=(3 if a.workload == "c3" else 4) + seed, device=dev,
                                         pieces=pieces, mix=a.workload)
-    elif a.workload == "vcf":
+    elif a.workload in ("vcf", "load"):
         tile = synth.vcf_text(min(VCF_TILE, n), seed=6 + seed)
         reps = -(-n // min(VCF_TILE, n))
         text = torch.frombuffer(bytearray(tile), dtype=torch.uint8).to(dev).repeat(reps)
@@ -195,12 +199,22 @@ def main():
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
         elif a.workload == "vcf":
             timed("vcf_tokenize", record, lambda: eng.vcf_tokenize(text))
+        elif a.workload == "load":
+            box = {}
+            timed("vcf_tokenize", record, lambda: box.setdefault("vb", eng.vcf_tokenize(text)))
+            vb = box["vb"]
+            timed("record_prep", record, lambda: box.setdefault(
+                "prep", eng.record_prep(vb.records, want_lcp=False)))
+            end, code_, status_, _ = box["prep"]
+            fr = eng.vcf_format(vb, end, code_, status_, alg_id="1", events=evs if record else None)
+            last["fr"] = fr
         else:
             timed("record_prep", record, lambda: eng.record_prep(batch, want_lcp=False, hist=hist,
                                                                  counters=ctr))
             timed("pk_dedup", record, lambda: eng.pk_dedup(batch, grouped=True, counters=ctr))
             timed("vrs_digest", record, lambda: eng.vrs_digest(batch, 50))
 
+    last = {}
     for _ in range(a.warmup):
         step(False)
     hist.zero_()
@@ -218,9 +232,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, ri, device=dev)
     stage_ms = {k: float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])) for k, v in evs.items()}
-    kname = {"c5": "record_prep", "vcf": "vcf_tokenize"}.get(a.workload, "bin_assign")
+    kname = {"c5": "record_prep", "vcf": "vcf_tokenize", "load": "format_write"}.get(a.workload, "bin_assign")
     kern_ms = stage_ms[kname]
-    if a.workload == "vcf":
+    if a.workload in ("vcf", "load"):
         n_lines, n = n, n_rec  # the unit is emitted variant records (per-ALT rows)
     total_records = n * ri.world * a.steps
     value = total_records / elapsed
@@ -229,6 +243,13 @@ def main():
         # K2 algorithmic bytes per record: in chrom 1 + pos 4 + allele_off 8 + ref_len 4 +
         # alt_len 4 (+ the heap bytes it reads, bounded by the heap); out end 4 + code 4
         bytes_per_launch = n * (1 + 4 + 8 + 4 + 4 + 4 + 4) + heap_bytes
+    elif a.workload == "load":
+        # K5 write pass: text read once + line table (80 B) + rec_off (8) + both offset
+        # arrays (16) + line state (1) per line + end/code/status (9) per record, and
+        # the COPY + .mapping text written
+        fr = last["fr"]
+        out_bytes = int(fr.copy.numel()) + int(fr.mapping.numel())
+        bytes_per_launch = int(text.numel()) + 105 * n_lines + 9 * n + out_bytes
     elif a.workload == "vcf":
         # text read once + record SoA written (chrom 1, pos 4, allele_off 8, ref_len 4,
         # alt_len 4, ext_id 8, rec_line 4, rec_alt 4 = 37 B) + allele heap written
@@ -267,6 +288,15 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "cpu_baseline": cpu,
     }
+    if a.workload == "load":
+        fr = last["fr"]
+        out["dtype"] = "u8"
+        out["data"] = "synthetic dbSNP-shaped VCF text with INFO FREQ (numpy PCG64 lines tiled on the device)"
+        out["config"].update(host_lines=int(fr.counters[27].item()), lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
+                             copy_bytes_per_gpu=int(fr.copy.numel()), mapping_bytes_per_gpu=int(fr.mapping.numel()),
+                             records_checked=None)
+        out["roofline"]["note"] = ("achieved = K5 write-pass algorithmic bytes (text + line table + offsets "
+                                   "+ per-record inputs + COPY/.mapping text written) / its HIP-event time")
     if a.workload == "vcf":
         out["dtype"] = "u8"
         out["data"] = "synthetic dbSNP-shaped VCF text (numpy PCG64 lines tiled on the device)"
