@@ -77,6 +77,23 @@ _SAMPLE = None
 _TABLE = None
 
 
+def _cpu_load_worker(k):
+    """Reference-structured load path (oracle.load_line: VcfEntryParser-style parse,
+    per-alt key / end / cached bin lookup / FREQ / display attributes / COPY row +
+    .mapping line) over this worker's lines."""
+    from oracle import avdb_oracle as O
+    from annotatedvdb_amd.chromosomes import length_table
+    lines = _SAMPLE[k]
+    bi = O.PortBinIndex(_TABLE)
+    lens = length_table()
+    t0 = time.perf_counter()
+    recs = 0
+    for ln in lines:
+        _, _, rows = O.load_line(ln, lens, bin_index=bi)
+        recs += len(rows)
+    return recs, time.perf_counter() - t0
+
+
 def _cpu_worker(k):
     from oracle import avdb_oracle as O
     names, pos, ends = _SAMPLE[k]
@@ -105,6 +122,24 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
     except AttributeError:
         cores = os.cpu_count() or 1
     workers = max(1, min(16, cores))
+    if workload == "load":
+        # ~80 us per line in the port (calibrated: 0.82x the verbatim reference's time)
+        per = int(seconds_per_worker / 80e-6)
+        lines = synth.vcf_text(per * workers, seed=6).decode().splitlines()
+        _TABLE = O.BinTable(GRCH38_LENGTHS)
+        _SAMPLE = [lines[k * per:(k + 1) * per] for k in range(workers)]
+        ctx = mp.get_context("fork")
+        t0 = time.perf_counter()
+        with ctx.Pool(workers) as pool:
+            res = pool.map(_cpu_load_worker, range(workers))
+        wall = time.perf_counter() - t0
+        n = sum(r[0] for r in res)
+        return {"value": n / wall, "unit": "variants/s", "cores": workers, "kind": "port",
+                "sample": f"{per * workers:,} synthetic dbSNP-shaped VCF lines ({n:,} COPY rows), "
+                          f"{workers} processes x {per:,} lines; reference-structured loader port "
+                          f"(oracle/avdb_oracle.py load_line + PortBinIndex; 0.82x the verbatim "
+                          f"reference's per-line time, tools/calibrate_cpu_baseline.py), per-process "
+                          f"{np.mean([r[1] for r in res]):.2f} s"}
     per = int(seconds_per_worker / 0.9e-6)  # ~0.9 us per cached find_bin_index call
     total = per * workers
     if workload == "c2":
@@ -138,7 +173,7 @@ def main():
     # CPU baseline first, before this process touches the GPU (its worker
     # processes are forked and must not inherit an initialised HIP runtime)
     want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and ri.world == 1
-                                          and a.workload in ("c2", "c3"))
+                                          and a.workload in ("c2", "c3", "load"))
     cpu = cpu_baseline(a.workload, a.cpu_seconds) if (ri.rank == 0 and want_cpu) else None
     ri = D.init("nccl")
     dev = torch.device("cuda", ri.local)

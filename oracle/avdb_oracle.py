@@ -547,11 +547,14 @@ def parse_vcf_line(line: str) -> dict:
             "position": int(ent["pos"]), "info": ent["info"]}
 
 
-def load_line(line: str, lengths: Sequence[int], alg_id="1", max_len: int = MAX_SEQUENCE_LENGTH):
+def load_line(line: str, lengths: Sequence[int], alg_id="1", max_len: int = MAX_SEQUENCE_LENGTH,
+              bin_index: Optional["PortBinIndex"] = None):
     """One line of the load driver (load_vcf_file.py:101-119 ->
     VCFVariantLoader.parse_variant, vcf_variant_loader.py:259-391, short keys
     only).  Returns ``(error_type_name | None, mapping_lines, copy_rows)``;
-    on an error the rows written before it are returned too."""
+    on an error the rows written before it are returned too.  With
+    ``bin_index`` (a :class:`PortBinIndex`) the bin comes from the reference's
+    cached lookup structure (the CPU baseline), else from the closed form."""
     rows: List[str] = []
     try:
         v = parse_vcf_line(line.rstrip())
@@ -569,10 +572,13 @@ def load_line(line: str, lengths: Sequence[int], alg_id="1", max_len: int = MAX_
             chrm = v["chromosome"] if "chr" in v["chromosome"] else "chr" + v["chromosome"]
             name = chrm[3:] if chrm.startswith("chr") else None
             L = lengths[CHROM_NAMES.index(name)] if name in CHROM_NAMES else None
-            code, _ = bin_code(L, v["position"], end)
-            if code == BIN_NONE:
-                raise TypeError("'NoneType' object is not subscriptable")
-            path = format_bin_path(name, code)
+            if bin_index is not None:
+                path = bin_index.find_bin_index(v["chromosome"], v["position"], end)
+            else:
+                code, _ = bin_code(L, v["position"], end)
+                if code == BIN_NONE:
+                    raise TypeError("'NoneType' object is not subscriptable")
+                path = format_bin_path(name, code)
             freq = frequencies(v["info"], v["alt_field"], alt)
             rows.append(copy_row(v["chromosome"], v["position"], v["ref"], alt, pk, path, alg_id,
                                  v["ref_snp_id"], v["is_multi"], freq))

@@ -30,10 +30,41 @@ def run(bi, names, pos, ends):
     return time.perf_counter() - t0
 
 
+def calibrate_load(n_lines):
+    """Load path: the verbatim reference loader (parse_variant + the driver's
+    mapping print) vs oracle.load_line with the PortBinIndex, per line."""
+    import io
+    from AnnotatedVDB.Util.loaders import VCFVariantLoader
+    from annotatedvdb_amd.chromosomes import length_table
+    lines = synth.vcf_text(n_lines, seed=6).decode().splitlines()
+    ld = VCFVariantLoader("dbSNP")
+    ld.initialize_pk_generator("GRCh38", "/nonexistent")
+    ld.initialize_bin_indexer(None)
+    ld._alg_invocation_id = "1"
+    ld.initialize_copy_sql()
+    out = io.StringIO()
+    t0 = time.perf_counter()
+    for ln in lines:
+        for k, v in ld.parse_variant(ln).items():
+            print(k, v, sep="\t", file=out)
+    tr = time.perf_counter() - t0
+    bi = O.PortBinIndex(O.BinTable(GRCH38_LENGTHS))
+    lens = length_table()
+    t0 = time.perf_counter()
+    for ln in lines:
+        O.load_line(ln, lens, bin_index=bi)
+    tp = time.perf_counter() - t0
+    print(f"load: reference {tr / n_lines * 1e6:.2f} us/line ({n_lines / tr:,.0f} lines/s), "
+          f"port {tp / n_lines * 1e6:.2f} us/line ({n_lines / tp:,.0f} lines/s), port/ref time = {tp / tr:.3f}")
+
+
 def main():
     n = int(os.environ.get("N", 1_000_000))
     MG.install_stubs()
     MG.build_binindexref()
+    calibrate_load(int(os.environ.get("N_LINES", 100_000)))
+    if os.environ.get("LOAD_ONLY"):
+        return
     from AnnotatedVDB.BinIndex.bin_index import BinIndex
     table = O.BinTable(GRCH38_LENGTHS)
     for wl in ("c2", "c3"):
