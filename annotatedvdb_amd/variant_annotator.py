@@ -5,8 +5,8 @@
 End inference and the common prefix come from the K2 kernel
 (``avdb_record_prep``) — one launch per annotator, evaluated lazily and cached
 on the instance.  Batched use goes through ``engine.Engine.record_prep`` (what
-the loaders do).  ``get_display_attributes`` (:134-241) is a later scope row
- and raises ``NotImplementedError`` here.
+the loaders do).  ``get_display_attributes`` (:134-241) comes from K5a
+(``avdb_display_attributes``).
 """
 
 from __future__ import annotations
@@ -70,6 +70,26 @@ class VariantAnnotator(object):
         return self.__metaseqId
 
     def get_display_attributes(self, rsPosition=None):
-        raise NotImplementedError(
-            "display attributes (variant_annotator.py:134-241) are outside the bin/key hot path "
-            "(SURVEY.md §8f rank 3)")
+        """Display attributes (variant_annotator.py:134-241), computed by K5a
+        (``avdb_display_attributes``) on the GPU; the dict keeps the
+        reference's key order.  Alleles must be ASCII; the position an int (as
+        every caller passes it)."""
+        import json
+        from .chromosomes import CHROM_NAMES
+        from .engine import default_engine, pack_records
+        eng = default_engine()
+        label = _xstr(self.__chrom)
+        code = CHROM_NAMES.index(label) if label in CHROM_NAMES else 255
+        ref = self.__ref.encode("utf-8") if isinstance(self.__ref, str) else bytes(self.__ref)
+        alt = self.__alt.encode("utf-8") if isinstance(self.__alt, str) else bytes(self.__alt)
+        b = pack_records([code], [int(self.__position)], [ref], [alt])
+        end, _, _, lcp = eng.record_prep(b)
+        self.__prep = (int(end.cpu()[0]), int(lcp.cpu()[0]))
+        text, off, state = eng.display_attributes(b, end)
+        if int(state[0]) != 0:
+            raise ValueError("non-ASCII allele: outside the GPU path's contract")
+        attrs = json.loads(text.cpu().numpy().tobytes().decode("ascii"))
+        nm = attrs.get("normalized_metaseq_id")
+        if nm is not None and code == 255:  # the kernel leaves unknown contig labels to the host
+            attrs["normalized_metaseq_id"] = label + nm
+        return attrs

@@ -219,3 +219,13 @@ def test_loader_text_path_comments_and_edge_lines(loader):
         if ln and not ln.startswith("#"):
             host.append(loader.parse_variant(ln.rstrip()))
     assert host == outs
+
+
+def test_variant_annotator_display_attributes_matches_reference():
+    from annotatedvdb_amd.variant_annotator import VariantAnnotator
+    rows = read_tsv("display_attrs.tsv.gz")[:200]
+    for r in rows:
+        va = VariantAnnotator(r["ref"], r["alt"], r["chrom"], int(r["pos"]))
+        assert json.dumps(va.get_display_attributes()) == r["attributes"], r
+    va = VariantAnnotator("CAG", "C", "chrUn_KI270302v1", 100)  # label the kernel leaves to the host
+    assert va.get_display_attributes()["normalized_metaseq_id"] == "chrUn_KI270302v1:100:AG:-"
