@@ -390,6 +390,10 @@ struct FormatArgs {
   uint32_t max_seq_len;
   uint32_t alg_len;
   char alg[AVDB_MAX_ALG_ID];
+  const int32_t* match;  // --skipExisting (K6), optional
+  const uint8_t* match_kind;
+  const uint8_t* frag;
+  const uint64_t* frag_off;
 };
 
 // allele bytes the GPU writes verbatim into JSON and Python repr text: printable
@@ -535,10 +539,23 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
       continue;
     }
     if (!plain_allele(alt, al)) return kLineHost;
-    const uint32_t st = A.status[r];
-    if (st == AVDB_STATUS_UNKNOWN_CHROM || st == AVDB_STATUS_OUT_OF_RANGE) return kLineHost;
     const bool lng = rl + al > A.max_seq_len;
     if (lng && !A.digest) return kLineHost;
+    if (A.match) {  // --skipExisting: after the key (:282), before the bin (:310)
+      if (A.match_kind[r] == AVDB_MATCH_HOST) return kLineHost;
+      if (A.match[r] >= 0) {  // primaryKeyMapping += matchedVariant; skipped (:287-291)
+        const int32_t m = A.match[r];
+        if (nrec) om.lit(", ");
+        om.bytes(A.frag + A.frag_off[m], uint32_t(A.frag_off[m + 1] - A.frag_off[m]));
+        ++nrec;
+        ++skip;
+        ++r;
+        a0 = a1 + 1;
+        continue;
+      }
+    }
+    const uint32_t st = A.status[r];
+    if (st == AVDB_STATUS_UNKNOWN_CHROM || st == AVDB_STATUS_OUT_OF_RANGE) return kLineHost;
     const uint32_t code = A.code[r];
     const bool keep = !A.keep || A.keep[r];
     // altIndex = altAlleles.index(allele) + 1: the first equal ALT
@@ -758,6 +775,16 @@ static int fill_args(FormatArgs* A, avdb_ctx* ctx, const uint8_t* text, size_t t
   }
   memcpy(A->alg, alg, n);
   A->alg_len = uint32_t(n);
+  if (opts && opts->match) {
+    if (!opts->match_kind || !opts->frag_off) {
+      avdb_set_error("avdb_vcf_format: match needs match_kind and frag_off");
+      return AVDB_EINVAL;
+    }
+    A->match = opts->match;
+    A->match_kind = opts->match_kind;
+    A->frag = opts->frag;
+    A->frag_off = opts->frag_off;
+  }
   return AVDB_OK;
 }
 

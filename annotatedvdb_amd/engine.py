@@ -424,13 +424,17 @@ class Engine:
     def vcf_format(self, vb: "VcfBatch", end: torch.Tensor, code: torch.Tensor, status: torch.Tensor,
                    digest: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None,
                    alg_id="", max_seq_len: int = 50,
-                   counters: Optional[torch.Tensor] = None, events: Optional[dict] = None) -> "FormatResult":
+                   counters: Optional[torch.Tensor] = None, events: Optional[dict] = None,
+                   existing: Optional[tuple] = None) -> "FormatResult":
         """The load driver's COPY buffer and .mapping text for ``vb``'s lines
         (K5b: size pass, scans, one host sync for the totals, write pass)."""
         n = vb.n_lines
         s = self._stream()
         tp = N.ptr(vb.text) if vb.text.numel() else None
         opts = N.FormatOpts(str(alg_id).encode(), int(max_seq_len), 0)
+        if existing is not None:  # (match, kind, frag, frag_off) device tensors from keyset_probe
+            m, k, fr, fo = existing
+            opts.match, opts.match_kind, opts.frag, opts.frag_off = N.ptr(m), N.ptr(k), N.ptr(fr), N.ptr(fo)
         if len(opts.alg_id) >= N.MAX_ALG_ID:
             raise ValueError("algorithm id too long")
         sz = ctypes.c_size_t()
@@ -480,6 +484,35 @@ class Engine:
         if n:
             N.check("avdb_display_attributes", self.lib.avdb_display_attributes(*args, N.ptr(out), N.ptr(state), s))
         return out[:total], off, state[:n]
+
+    # -- K6: existing-variant key set ----------------------------------------
+    def keyset_build(self, keys: torch.Tensor, key_off: torch.Tensor) -> torch.Tensor:
+        """Hash table over the key strings (``keys`` bytes, ``key_off`` int64[n+1])."""
+        keys, key_off = self._dev(keys), self._dev(key_off)
+        n = key_off.numel() - 1
+        sz = ctypes.c_size_t()
+        self.lib.avdb_keyset_workspace_size(n, ctypes.byref(sz))
+        table = self.empty(int(sz.value), torch.uint8)
+        N.check("avdb_keyset_build", self.lib.avdb_keyset_build(
+            self.ctx, N.ptr(keys) if keys.numel() else None, N.ptr(key_off), n, N.ptr(table), table.numel(),
+            self._stream()))
+        return table
+
+    def keyset_probe(self, table: torch.Tensor, keys: torch.Tensor, key_off: torch.Tensor, b: RecordBatch,
+                     check_alt: bool = True, counters: Optional[torch.Tensor] = None):
+        """``(match int32[n], kind uint8[n])``: first equal key of each record's
+        metaseq id (then of the switched alleles with ``check_alt``)."""
+        b = b if b.device == self.device else b.to(self.device)
+        self._check_alleles(b)
+        n = b.n
+        match = self.empty(max(1, n), torch.int32)
+        kind = self.empty(max(1, n), torch.uint8)
+        N.check("avdb_keyset_probe", self.lib.avdb_keyset_probe(
+            self.ctx, N.ptr(table), table.numel(), N.ptr(keys) if keys.numel() else None, N.ptr(key_off),
+            key_off.numel() - 1, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
+            N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, 1 if check_alt else 0, N.ptr(match), N.ptr(kind),
+            N.ptr(counters), self._stream()))
+        return match[:n], kind[:n]
 
     # -- formatting (host) ---------------------------------------------------
     def format_path(self, chrom_code: int, code: int) -> Optional[str]:

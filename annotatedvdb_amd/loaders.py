@@ -23,9 +23,10 @@ semantics.  Exceptions match the reference at the same record: ``ValueError``
 when a key cannot be built (e.g. ``':'`` inside an allele breaks
 ``metaseqId.split(':')``, primary_key_generator.py:106, through the retry
 ladder :234-256), ``TypeError`` when the location has no bin
-(bin_index.py:75).  Database-backed features (``--skipExisting`` lookups, ADSP
-duplicate updates, ``update_existing``, COPY into Postgres) are outside the
-bin/key path and raise ``NotImplementedError``.  Display attributes come from
+(bin_index.py:75).  ``--skipExisting`` checks a key set of the rows already
+loaded (``existing.ExistingVariants``, K6) instead of the database; the other
+database-backed features (ADSP duplicate updates, ``update_existing``, COPY
+into Postgres) are outside the bin/key path and raise ``NotImplementedError``.  Display attributes come from
 K5a (``avdb_display_attributes``); alleles must be ASCII (VCF 4.x REF/ALT).
 """
 
@@ -75,9 +76,11 @@ class VCFVariantLoader(object):
         self._copy_fields = None
         self._copy_sql = None
         self._skip_existing = False
+        self._existing = None
         self._update_existing = False
         self._vcf_header_fields = None
         self.last_load_stats = None
+        self._match = None
         self._initialize_counters()
         self.initialize_copy_buffer()
         self.logger.info(type(self).__name__ + " initialized")
@@ -128,10 +131,30 @@ class VCFVariantLoader(object):
     def vcf_header_fields(self):
         return self._vcf_header_fields
 
-    def set_skip_existing(self, skipDuplicates, gusConfigFile=None):
-        if skipDuplicates:
-            raise NotImplementedError("--skipExisting checks the database (map_variants); out of scope")
-        self._skip_existing = False
+    def set_skip_existing(self, skipDuplicates, gusConfigFile=None, existing=None):
+        """``--skipExisting`` (variant_loader.py:159-162): the rows already loaded
+        come as an :class:`~annotatedvdb_amd.existing.ExistingVariants` key set
+        (an export of AnnotatedVDB.Variant) instead of a database connection."""
+        if skipDuplicates and existing is None:
+            raise NotImplementedError("--skipExisting needs the existing rows: pass existing=ExistingVariants(...) "
+                                      "(exported from AnnotatedVDB.Variant); there is no database here")
+        self._skip_existing = bool(skipDuplicates)
+        self._existing = existing if skipDuplicates else None
+
+    def is_duplicate(self, variantId, returnMatch=False):
+        """variant_loader.py:173-174 for a metaseq id, against the key set (K6)."""
+        from .chromosomes import CHROM_NAMES
+        from .engine import pack_records
+        if self._existing is None:
+            raise ValueError("set_skip_existing(True, existing=...) first")
+        c, p, r, a = variantId.split(":")
+        code = CHROM_NAMES.index(c) if c in CHROM_NAMES else 255
+        b = pack_records([code], [int(p)], [r.encode()], [a.encode()]).to(self._engine.device)
+        m, k = self._existing.probe(b)
+        k0 = int(m.cpu()[0]) if int(k.cpu()[0]) != 255 else self._existing.resolve_host(variantId)
+        if k0 < 0:
+            return None if returnMatch else False
+        return self._existing.payload(k0) if returnMatch else True
 
     def skip_existing(self):
         return self._skip_existing
@@ -418,8 +441,12 @@ class VCFVariantLoader(object):
         if db.n and bool(((db.ref_len + db.alt_len) > mx).any()) and self._pk_generator.has_sequence_digests():
             digest, _ = self._pk_generator._eng().vrs_digest(db, mx)
         keep = eng.pk_dedup(db, grouped=False) if dedup and db.n else None
+        ex = None
+        if self._existing is not None and db.n:  # --skipExisting: K6 hash join, consumed by K5
+            m, k = self._existing.probe(db)
+            ex = self._existing.format_args(m, k)
         fr = eng.vcf_format(vb, end, code, status, digest, keep, alg_id=_xstr(self._alg_invocation_id),
-                            max_seq_len=mx)
+                            max_seq_len=mx, existing=ex)
         state = fr.line_state.cpu().numpy()
         copy_off = fr.copy_off.cpu().numpy()
         map_off = fr.map_off.cpu().numpy()
@@ -535,6 +562,13 @@ class VCFVariantLoader(object):
         code = d_code.cpu().numpy().view(np.uint32)
         paths = eng.format_paths(np.asarray(codes, dtype=np.uint8), code)
         disp = _display_texts(eng, db, d_end)
+        self._match = None
+        if self._existing is not None:  # --skipExisting (K6)
+            m, k = self._existing.probe(db)
+            m, k = m.cpu().numpy(), k.cpu().numpy()
+            for i in np.nonzero(k == 255)[0]:
+                m[i] = self._existing.resolve_host(recs[i][2])
+            self._match = m
         # primary keys (short: text; long: K4 digests in one launch)
         items, idx = [], []
         for i, r in enumerate(recs):
@@ -582,6 +616,10 @@ class VCFVariantLoader(object):
                 if r[3] is not None:
                     failed = r[3] if isinstance(r[3], Exception) else ValueError(str(r[3]))
                     break
+                if self._match is not None and self._match[i] >= 0:  # vcf_variant_loader.py:285-291
+                    mapping += self._existing.payload(int(self._match[i]))
+                    self.increment_counter("skipped")
+                    continue
                 path = paths[i]
                 if path is None:
                     failed = TypeError("'NoneType' object is not subscriptable")

@@ -84,6 +84,7 @@ extern "C" {
 #define AVDB_CTR_SKIPPED_ALTS 25        /* ALT '.' entries skipped (vcf_variant_loader.py:277-280) */
 #define AVDB_CTR_DUP_ROWS 26            /* records whose COPY row was dropped (keep == 0) */
 #define AVDB_CTR_HOST_LINES 27          /* lines left to the host renderer */
+#define AVDB_CTR_EXISTING 28            /* records found in the existing-variant key set (K6) */
 #define AVDB_N_COUNTERS 32
 
 typedef struct avdb_ctx avdb_ctx;
@@ -241,6 +242,15 @@ typedef struct avdb_format_opts {
   const char* alg_id;     /* xstr(row_algorithm_id), host NUL-terminated; NULL = "" */
   uint32_t max_seq_len;   /* primary_key_generator.py:53 (default 50) */
   uint32_t reserved;
+  /* --skipExisting (optional, device; NULL = off): K6 match / kind per record and
+   * the .mapping text each existing key contributes (its match list, rendered
+   * once by the host): frag[frag_off[k] .. frag_off[k+1]).  A matched record gets
+   * no COPY row, its fragment in the .mapping line, and counts as skipped
+   * (vcf_variant_loader.py:285-291). */
+  const int32_t* match;
+  const uint8_t* match_kind;
+  const uint8_t* frag;
+  const uint64_t* frag_off;
 } avdb_format_opts;
 
 int avdb_format_workspace_size(size_t n, size_t* bytes);
@@ -266,6 +276,26 @@ int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
                             const uint8_t* heap, size_t heap_bytes, size_t n, void* workspace,
                             size_t workspace_bytes, uint64_t* out_off, uint8_t* out, uint8_t* rec_state,
                             void* stream);
+
+/* ---- K6: duplicate check against variants already loaded ---------------
+ * Replaces VariantRecord.exists / SQL map_variants(id, firstHitOnly, checkAltVariants)
+ * (Util/lib/python/database/variant.py:41,287-309) as used by --skipExisting
+ * (vcf_variant_loader.py:284-291).  The existing rows' metaseq ids form a key
+ * set: keys = concatenated bytes, key_off[n_keys+1] (device).  build fills a
+ * table of avdb_keyset_workspace_size(n_keys) bytes; probe writes per record
+ * match[i] = index of the first equal key or -1, and kind[i]: */
+#define AVDB_MATCH_NONE 0
+#define AVDB_MATCH_EXACT 1              /* chrom:pos:ref:alt */
+#define AVDB_MATCH_SWITCHED 2           /* chrom:pos:alt:ref (check_alt) */
+#define AVDB_MATCH_HOST 255             /* contig without a canonical label: caller resolves */
+int avdb_keyset_workspace_size(size_t n_keys, size_t* bytes);
+int avdb_keyset_build(avdb_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, size_t n_keys, void* table,
+                      size_t table_bytes, void* stream);
+int avdb_keyset_probe(avdb_ctx* ctx, const void* table, size_t table_bytes, const uint8_t* keys,
+                      const uint64_t* key_off, size_t n_keys, const uint8_t* chrom, const uint32_t* pos,
+                      const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                      const uint8_t* heap, size_t heap_bytes, size_t n, int check_alt, int32_t* match,
+                      uint8_t* kind, uint64_t* counters, void* stream);
 
 /* ---- host-side formatting of kernel outputs -------------------------------
  * ltree path text (<= AVDB_MAX_PATH bytes).  Returns the length written (no

@@ -547,8 +547,21 @@ def parse_vcf_line(line: str) -> dict:
             "position": int(ent["pos"]), "info": ent["info"]}
 
 
+def existing_match(existing: Dict[str, int], metaseq: str, check_alt: bool = True) -> int:
+    """--skipExisting lookup (VariantRecord.exists, database/variant.py:287-309 ->
+    map_variants(id, firstHitOnly=True, checkAltVariants=True), external SQL):
+    index of the first existing row with this metaseq id, else of the switched
+    alleles, else -1.  ``existing`` maps id -> first index."""
+    k = existing.get(metaseq, -1)
+    if k < 0 and check_alt:
+        c, p, r, a = metaseq.split(":")
+        k = existing.get(":".join((c, p, a, r)), -1)
+    return k
+
+
 def load_line(line: str, lengths: Sequence[int], alg_id="1", max_len: int = MAX_SEQUENCE_LENGTH,
-              bin_index: Optional["PortBinIndex"] = None):
+              bin_index: Optional["PortBinIndex"] = None, existing: Optional[Dict[str, int]] = None,
+              payloads: Optional[List[List[dict]]] = None):
     """One line of the load driver (load_vcf_file.py:101-119 ->
     VCFVariantLoader.parse_variant, vcf_variant_loader.py:259-391, short keys
     only).  Returns ``(error_type_name | None, mapping_lines, copy_rows)``;
@@ -568,6 +581,11 @@ def load_line(line: str, lengths: Sequence[int], alg_id="1", max_len: int = MAX_
             if is_long(v["ref"], alt, max_len):
                 raise ValueError("long allele: VRS digest (parity unpinned)")
             pk = primary_key(v["chromosome"], v["position"], v["ref"], alt, v["ref_snp_id"], max_len=max_len)
+            if existing is not None:  # vcf_variant_loader.py:285-291
+                k = existing_match(existing, ms)
+                if k >= 0:
+                    mapping += payloads[k]
+                    continue
             end, _ = infer_end(v["position"], v["ref"], alt)
             chrm = v["chromosome"] if "chr" in v["chromosome"] else "chr" + v["chromosome"]
             name = chrm[3:] if chrm.startswith("chr") else None
