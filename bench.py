@@ -240,8 +240,8 @@ def main():
             vb = box["vb"]
             timed("record_prep", record, lambda: box.setdefault(
                 "prep", eng.record_prep(vb.records, want_lcp=False)))
-            end, code_, status_, _ = box["prep"]
-            fr = eng.vcf_format(vb, end, code_, status_, alg_id="1", events=evs if record else None)
+            p_end, p_code, p_status, _ = box["prep"]
+            fr = eng.vcf_format(vb, p_end, p_code, p_status, alg_id="1", events=evs if record else None)
             last["fr"] = fr
         else:
             timed("record_prep", record, lambda: eng.record_prep(batch, want_lcp=False, hist=hist,

@@ -114,3 +114,15 @@ def test_synthetic_numpy_generators_shape():
     c, s, e = synth.np_spans(10000, seed=1)
     assert np.all(e >= s) and np.all(e <= lens[c])
     assert np.mean(e == s) > 0.4
+
+
+def test_bench_step_does_not_shadow_main_buffers():
+    """bench.py's step() closes over main()'s resident buffers; a local of the
+    same name anywhere in step() breaks every workload (UnboundLocalError)."""
+    import ast
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
+    tree = ast.parse(src)
+    main = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "main")
+    step = next(n for n in ast.walk(main) if isinstance(n, ast.FunctionDef) and n.name == "step")
+    stored = {n.id for n in ast.walk(step) if isinstance(n, ast.Name) and isinstance(n.ctx, ast.Store)}
+    assert not stored & {"chrom", "start", "end", "code", "hist", "ctr", "batch", "text", "eng"}, stored
