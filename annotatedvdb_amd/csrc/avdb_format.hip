@@ -490,20 +490,26 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
                                uint32_t* n_dup) {
   if (L.flags & AVDB_VCF_COMMENT) return kLineSkip;
   if ((L.flags & kHostFlags) || L.chrom >= 25) return kLineHost;
+  // Checks that only decide GPU vs HOST run in the SIZE pass; the WRITE pass
+  // only visits lines that passed them (line_state == GPU).
   // the reference decodes every line as UTF-8 (load_vcf_file.py:102): ASCII only here
-  for (uint32_t i = 0; i < L.len; ++i)
-    if (s[i] & 0x80) return kLineHost;
+  if constexpr (!WRITE) {
+    for (uint32_t i = 0; i < L.len; ++i)
+      if (s[i] & 0x80) return kLineHost;
+  }
   const uint32_t c = L.chrom;
   const uint32_t ref0 = L.field[3], rl = L.field[4] - 1 - ref0;
   const uint32_t alt0 = L.field[4], alt1 = L.field[5] - 1;
   const uint8_t* ref = s + ref0;
-  if (!plain_allele(ref, rl)) return kLineHost;
+  if (!WRITE && !plain_allele(ref, rl)) return kLineHost;
   // INFO: the last FREQ entry (dict keeps the last key); '#' or '\' in INFO are
   // rewritten by the reference before it splits (vcf_parser.py:101-103)
   const uint32_t i0 = L.field[7], i1 = L.field_end8;
   int64_t fq0 = -1, fq1 = -1;
-  for (uint32_t i = i0; i < i1; ++i)
-    if (s[i] == '#' || s[i] == '\\') return kLineHost;
+  if constexpr (!WRITE) {
+    for (uint32_t i = i0; i < i1; ++i)
+      if (s[i] == '#' || s[i] == '\\') return kLineHost;
+  }
   for (uint32_t e0 = i0; e0 <= i1;) {
     const uint32_t e1 = find_byte(s, e0, i1, ';');
     if (e1 - e0 >= 4 && s[e0] == 'F' && s[e0 + 1] == 'R' && s[e0 + 2] == 'E' && s[e0 + 3] == 'Q') {
@@ -512,7 +518,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
     }
     e0 = e1 + 1;
   }
-  if (fq0 >= 0 && !freq_plain(s, uint32_t(fq0), uint32_t(fq1))) return kLineHost;
+  if (!WRITE && fq0 >= 0 && !freq_plain(s, uint32_t(fq0), uint32_t(fq1))) return kLineHost;
   const bool has_rs = (L.flags & (AVDB_VCF_ID_RS | AVDB_VCF_INFO_RS)) != 0;
   // .mapping: variant id (vcf_parser.py:140-142) TAB '['
   if (L.flags & AVDB_VCF_ID_METASEQ) {
@@ -538,7 +544,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
       a0 = a1 + 1;
       continue;
     }
-    if (!plain_allele(alt, al)) return kLineHost;
+    if (!WRITE && !plain_allele(alt, al)) return kLineHost;
     const bool lng = rl + al > A.max_seq_len;
     if (lng && !A.digest) return kLineHost;
     if (A.match) {  // --skipExisting: after the key (:282), before the bin (:310)
