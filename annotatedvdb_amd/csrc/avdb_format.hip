@@ -41,6 +41,10 @@ namespace avdb {
 // (LDS-limited occupancy).  The pass is instruction-issue bound (per-byte
 // formatting work), not HBM bound: see DESIGN.md.
 typedef __attribute__((address_space(1))) uint8_t gbyte;
+// text the formatters read: the LDS-staged window (ds_read_u8) or global memory
+// (global_load_ubyte) — explicit address spaces instead of flat loads
+typedef const __attribute__((address_space(3))) uint8_t* lds_cp;
+typedef const __attribute__((address_space(1))) uint8_t* glb_cp;
 
 template <bool WRITE>
 struct Out {
@@ -57,7 +61,8 @@ struct Out {
   __device__ __forceinline__ void lit(const char* s) {
     while (*s) put(uint8_t(*s++));
   }
-  __device__ __forceinline__ void bytes(const uint8_t* s, uint32_t n) {
+  template <class CP>
+  __device__ __forceinline__ void bytes(CP s, uint32_t n) {
     if constexpr (!WRITE) {
       p += n;
     } else {
@@ -111,8 +116,8 @@ __device__ __noinline__ O bin_path(O o, uint32_t c, uint32_t code) {
 // JSON strings (json.dumps, ensure_ascii): '"' '\\' and the short escapes,
 // other bytes outside ' '..'~' as \u00XX (lowercase hex)
 // ---------------------------------------------------------------------------
-template <bool ESC, class O>
-__device__ __forceinline__ void jstr(O& o, const uint8_t* s, uint32_t n) {
+template <bool ESC, class O, class CP>
+__device__ __forceinline__ void jstr(O& o, CP s, uint32_t n) {
   if constexpr (!ESC) {
     o.bytes(s, n);
   } else {
@@ -141,21 +146,22 @@ __device__ __forceinline__ void jstr(O& o, const uint8_t* s, uint32_t n) {
 
 // an allele in its display form: bytes, or '-' for an empty normalized allele
 // (variant_annotator.py:111-116, snvDivMinus=True)
+template <class CP>
 struct Al {
-  const uint8_t* p;
+  CP p;
   uint32_t n;
   bool dash;
 };
 
-template <bool ESC, class O>
-__device__ __forceinline__ void al_str(O& o, const Al& a) {
+template <bool ESC, class O, class CP>
+__device__ __forceinline__ void al_str(O& o, const Al<CP>& a) {
   if (a.dash) o.put('-');
   else jstr<ESC>(o, a.p, a.n);
 }
 
 // truncate(s, cap) = s if len(s) <= cap else s[:cap] + '...' (variant_annotator.py:8-10)
-template <bool ESC, class O>
-__device__ __forceinline__ void al_trunc(O& o, const Al& a, uint32_t cap) {
+template <bool ESC, class O, class CP>
+__device__ __forceinline__ void al_trunc(O& o, const Al<CP>& a, uint32_t cap) {
   if (a.dash) { o.put('-'); return; }
   jstr<ESC>(o, a.p, a.n < cap ? a.n : cap);
   if (a.n > cap) o.lit("...");
@@ -169,9 +175,9 @@ __device__ __forceinline__ void al_trunc(O& o, const Al& a, uint32_t cap) {
 // whose update() lists display_allele and sequence_allele first.
 // chrom >= 25 writes no label in normalized_metaseq_id (the caller prepends it).
 // ---------------------------------------------------------------------------
-template <bool ESC, class O>
-__device__ __noinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, const uint8_t* ref,
-                             uint32_t r, const uint8_t* alt, uint32_t a) {
+template <bool ESC, class O, class CP>
+__device__ __noinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, CP ref, uint32_t r,
+                                       CP alt, uint32_t a) {
   const bool snv = r == 1u && a == 1u;
   uint32_t l = 0;  // common prefix (__normalize_alleles :100-107); SNVs untouched (:97-98)
   if (!snv) {
@@ -179,11 +185,11 @@ __device__ __noinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32
     while (l < m && ref[l] == alt[l]) ++l;
   }
   const uint32_t nr = r - l, na = a - l;
-  const Al nref{ref + l, nr, l > 0 && nr == 0}, nalt{alt + l, na, l > 0 && na == 0};
+  const Al<CP> nref{ref + l, nr, l > 0 && nr == 0}, nalt{alt + l, na, l > 0 && na == 0};
   uint32_t ls = pos, le = pos;
   int cls;  // 0 SNV, 1 inversion, 2 substitution, 3 indel, 4 indel (ins downstream), 5 ins/dup, 6 deletion
   bool dup = false;
-  const Al orig{r ? ref + 1 : ref, r ? r - 1 : 0, false};
+  const Al<CP> orig{r ? ref + 1 : ref, r ? r - 1 : 0, false};
   if (snv) {
     cls = 0;
   } else if (r == a) {  // MNV (:171-189)
@@ -245,7 +251,7 @@ __device__ __noinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32
     o.put('"');
   }
   const char* pre = dup ? "dup" : "ins";
-  const Al raw_ref{ref, r, false}, raw_alt{alt, a, false};
+  const Al<CP> raw_ref{ref, r, false}, raw_alt{alt, a, false};
   o.lit(", \"display_allele\": \"");
   switch (cls) {
     case 0: al_str<ESC>(o, raw_ref); o.put('>'); al_str<ESC>(o, raw_alt); break;
@@ -285,7 +291,8 @@ __device__ __noinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32
 // Anything else (signs, exponents, '_', spaces, nan/inf, > 15 significant
 // digits) returns false: the line is rendered by the host.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool number_plain(const uint8_t* f, uint32_t n) {
+template <class CP>
+__device__ __forceinline__ bool number_plain(CP f, uint32_t n) {
   if (n == 0 || n > 40) return false;
   uint32_t dot = n, f0 = n, l0 = 0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -306,8 +313,8 @@ __device__ __forceinline__ bool number_plain(const uint8_t* f, uint32_t n) {
   return nd <= 15;                            // repr == these digits
 }
 
-template <class O>
-__device__ __noinline__ O json_number(O o, const uint8_t* f, uint32_t n) {
+template <class O, class CP>
+__device__ __noinline__ O json_number(O o, CP f, uint32_t n) {
   o.bad = !number_plain(f, n);
   if (o.bad) return o;
   uint32_t dot = n;
@@ -399,7 +406,8 @@ struct FormatArgs {
 // allele bytes the GPU writes verbatim into JSON and Python repr text: printable
 // ASCII except '"' '\\' '\'' (escaped by json.dumps / repr) and ':' (breaks
 // metaseqId.split(':'), primary_key_generator.py:106)
-__device__ __forceinline__ bool plain_allele(const uint8_t* s, uint32_t n) {
+template <class CP>
+__device__ __forceinline__ bool plain_allele(CP s, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) {
     const uint8_t c = s[i];
     if (c < 0x20 || c > 0x7E || c == '"' || c == '\\' || c == '\'' || c == ':') return false;
@@ -407,14 +415,16 @@ __device__ __forceinline__ bool plain_allele(const uint8_t* s, uint32_t n) {
   return true;
 }
 
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+template <class CP>
+__device__ __forceinline__ bool bytes_eq(CP a, CP b, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)
     if (a[i] != b[i]) return false;
   return true;
 }
 
 // next separator at or after i in [i, e), or e
-__device__ __forceinline__ uint32_t find_byte(const uint8_t* s, uint32_t i, uint32_t e, uint8_t c) {
+template <class CP>
+__device__ __forceinline__ uint32_t find_byte(CP s, uint32_t i, uint32_t e, uint8_t c) {
   while (i < e && s[i] != c) ++i;
   return i;
 }
@@ -423,7 +433,8 @@ __device__ __forceinline__ uint32_t find_byte(const uint8_t* s, uint32_t i, uint
 // needs a ':' (pop.split(':')[1]), a JSON-plain name, and names must be unique
 // (the reference's dict comprehension keeps the last value at the first
 // position).
-__device__ bool freq_plain(const uint8_t* s, uint32_t v0, uint32_t v1) {
+template <class CP>
+__device__ bool freq_plain(CP s, uint32_t v0, uint32_t v1) {
   uint32_t np = 0;
   for (uint32_t p0 = v0; p0 <= v1; ++np) {
     const uint32_t p1 = find_byte(s, p0, v1, '|');
@@ -448,8 +459,8 @@ __device__ bool freq_plain(const uint8_t* s, uint32_t v0, uint32_t v1) {
 // allele_frequencies of ALT index k (1-based, altAlleles.index(allele) + 1) as
 // json.dumps text or NULL; false when the reference would raise or print a
 // number the GPU does not format
-template <class O>
-__device__ __noinline__ O freq_json(O o, const uint8_t* s, uint32_t v0, uint32_t v1, uint32_t k) {
+template <class O, class CP>
+__device__ __noinline__ O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint32_t k) {
   bool any = false;
   for (uint32_t p0 = v0; p0 <= v1;) {
     const uint32_t p1 = find_byte(s, p0, v1, '|');
@@ -484,8 +495,8 @@ __device__ __noinline__ O freq_json(O o, const uint8_t* s, uint32_t v0, uint32_t
   return o;
 }
 
-template <bool WRITE>
-__device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, const uint8_t* s, size_t li,
+template <bool WRITE, class CP>
+__device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, CP s, size_t li,
                                Out<WRITE>& oc, Out<WRITE>& om, uint32_t* n_rows, uint32_t* n_skip,
                                uint32_t* n_dup) {
   if (L.flags & AVDB_VCF_COMMENT) return kLineSkip;
@@ -500,7 +511,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   const uint32_t c = L.chrom;
   const uint32_t ref0 = L.field[3], rl = L.field[4] - 1 - ref0;
   const uint32_t alt0 = L.field[4], alt1 = L.field[5] - 1;
-  const uint8_t* ref = s + ref0;
+  const CP ref = s + ref0;
   if (!WRITE && !plain_allele(ref, rl)) return kLineHost;
   // INFO: the last FREQ entry (dict keeps the last key); '#' or '\' in INFO are
   // rewritten by the reference before it splits (vcf_parser.py:101-103)
@@ -537,7 +548,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   uint32_t nrec = 0, rows = 0, skip = 0, dups = 0;
   for (uint32_t a0 = alt0, ai = 0; a0 <= alt1; ++ai) {
     const uint32_t a1 = find_byte(s, a0, alt1, ',');
-    const uint8_t* alt = s + a0;
+    const CP alt = s + a0;
     const uint32_t al = a1 - a0;
     if (al == 1 && alt[0] == '.') {  // vcf_variant_loader.py:277-280
       ++skip;
@@ -666,23 +677,29 @@ __global__ __launch_bounds__(kBlock) void k_vcf_format(FormatArgs A) {
     const size_t li = base + threadIdx.x;
     if (li < A.n_lines) {
       const avdb_vcf_line L = A.lines[li];
-      const uint8_t* s = w.staged ? reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)
-                                  : A.text + L.start;
-      if constexpr (WRITE) {
-        const uint8_t st = A.line_state[li];
-        if (st == kLineGpu) {
-          Out<true> oc(A.copy_out, A.copy_off[li]), om(A.map_out, A.map_off[li]);
-          format_line<true>(A, L, s, li, oc, om, &rows, &skip, &dups);
-        } else if (st == kLineHost) {
-          ++hosts;
+      // the same formatter on the LDS window (ds_read) or, for an oversized
+      // window, on global memory
+      auto run = [&](auto s) {
+        if constexpr (WRITE) {
+          const uint8_t st = A.line_state[li];
+          if (st == kLineGpu) {
+            Out<true> oc(A.copy_out, A.copy_off[li]), om(A.map_out, A.map_off[li]);
+            format_line<true>(A, L, s, li, oc, om, &rows, &skip, &dups);
+          } else if (st == kLineHost) {
+            ++hosts;
+          }
+        } else {
+          Out<false> oc(nullptr, 0), om(nullptr, 0);
+          const uint8_t st = format_line<false>(A, L, s, li, oc, om, &rows, &skip, &dups);
+          A.line_state[li] = st;
+          A.copy_off[li] = st == kLineGpu ? oc.size() : 0;
+          A.map_off[li] = st == kLineGpu ? om.size() : 0;
         }
-      } else {
-        Out<false> oc(nullptr, 0), om(nullptr, 0);
-        const uint8_t st = format_line<false>(A, L, s, li, oc, om, &rows, &skip, &dups);
-        A.line_state[li] = st;
-        A.copy_off[li] = st == kLineGpu ? oc.size() : 0;
-        A.map_off[li] = st == kLineGpu ? om.size() : 0;
-      }
+      };
+      if (w.staged)
+        run((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)));
+      else
+        run((glb_cp)(A.text + L.start));
     }
     __syncthreads();  // the window is reused by the next trip
   }
@@ -721,7 +738,7 @@ __global__ __launch_bounds__(kBlock) void k_display(const uint8_t* __restrict__ 
     if constexpr (WRITE) {
       if (state[i]) continue;
       Out<true> w(out, out_off[i]);
-      w = display_json<true>(w, chrom[i], pos[i], end[i], heap + o, r, heap + o + r, a);
+      w = display_json<true>(w, chrom[i], pos[i], end[i], (glb_cp)(heap + o), r, (glb_cp)(heap + o + r), a);
     } else {
       uint8_t st = o + r + a > heap_bytes ? 2 : 0;
       for (uint32_t k = 0; k < r + a && !st; ++k)
@@ -729,7 +746,8 @@ __global__ __launch_bounds__(kBlock) void k_display(const uint8_t* __restrict__ 
       state[i] = st;
       uint64_t len = 0;
       if (!st) {
-        len = display_json<true>(Out<false>(nullptr, 0), chrom[i], pos[i], end[i], heap + o, r, heap + o + r, a).size();
+        len = display_json<true>(Out<false>(nullptr, 0), chrom[i], pos[i], end[i], (glb_cp)(heap + o), r,
+                                 (glb_cp)(heap + o + r), a).size();
       }
       out_off[i] = len;
     }
