@@ -41,10 +41,6 @@ namespace avdb {
 // (LDS-limited occupancy).  The pass is instruction-issue bound (per-byte
 // formatting work), not HBM bound: see DESIGN.md.
 typedef __attribute__((address_space(1))) uint8_t gbyte;
-// text the formatters read: the LDS-staged window (ds_read_u8) or global memory
-// (global_load_ubyte) — explicit address spaces instead of flat loads
-typedef const __attribute__((address_space(3))) uint8_t* lds_cp;
-typedef const __attribute__((address_space(1))) uint8_t* glb_cp;
 
 template <bool WRITE>
 struct Out {

@@ -13,6 +13,12 @@ __device__ __forceinline__ uint64_t zero_bytes_mask(uint64_t y) {  // bit 7 of e
 
 constexpr uint64_t kHiBits = 0x8080808080808080ull;
 
+// Text pointers with an explicit address space, so byte reads compile to
+// ds_read_u8 (LDS-staged window) or global_load_ubyte instead of flat loads.
+typedef const __attribute__((address_space(3))) uint8_t* lds_cp;
+typedef const __attribute__((address_space(3))) uint64_t* lds_cp64;
+typedef const __attribute__((address_space(1))) uint8_t* glb_cp;
+
 // 8 bytes at aligned address a (bytes outside [lo,hi) read as 0x00)
 __device__ __forceinline__ uint64_t text_word(uintptr_t a, const Heap& h) { return heap_word(a, h); }
 

@@ -187,7 +187,8 @@ __global__ __launch_bounds__(kBlock) void k_vcf_starts(const uint8_t* __restrict
 // contig code of a CHROM field (vcf_parser.py:133-150 + bin_index.py:64): plain
 // digits go through int(); 'MT' -> 'M'; every 'chr' removed in one left-to-right
 // pass (str.replace); then chr1..22, X, Y, M.  *host set for non-alphanumeric bytes.
-__device__ uint8_t chrom_code_of(const uint8_t* p, uint32_t n, bool* host) {
+template <class CP>
+__device__ uint8_t chrom_code_of(CP p, uint32_t n, bool* host) {
   *host = false;
   if (n == 0) return 255;
   bool digits = true;
@@ -226,7 +227,8 @@ __device__ uint8_t chrom_code_of(const uint8_t* p, uint32_t n, bool* host) {
 }
 
 // canonical refSNP number of "rs<N>" bytes (N without leading zeros, < 10^18), else 0
-__device__ uint64_t rs_number(const uint8_t* p, uint32_t n) {
+template <class CP>
+__device__ uint64_t rs_number(CP p, uint32_t n) {
   if (n < 3 || n > 20 || p[0] != 'r' || p[1] != 's' || p[2] == '0') return 0;
   uint64_t v = 0;
   for (uint32_t i = 2; i < n; ++i) {
@@ -241,8 +243,8 @@ constexpr uint64_t kSemi = 0x3B3B3B3B3B3B3B3Bull;
 
 // one line: s points at its first byte (LDS or global), len = bytes up to its
 // newline; word_at/mis give the same bytes as aligned 8-byte words (SWAR scans)
-template <class WordAt>
-__device__ __forceinline__ void parse_line(const uint8_t* s, const WordAt& word_at, uint32_t mis,
+template <class CP, class WordAt>
+__device__ __forceinline__ void parse_line(CP s, const WordAt& word_at, uint32_t mis,
                                            uint32_t len, avdb_vcf_line& L, uint64_t& recs,
                                            uint64_t& hbytes) {
     while (len && is_ws(s[len - 1])) --len;  // str.rstrip()
@@ -299,7 +301,7 @@ __device__ __forceinline__ void parse_line(const uint8_t* s, const WordAt& word_
         if (host) L.flags |= AVDB_VCF_CHROM_HOST;
         // POS: plain decimal < 2^32
         {
-          const uint8_t* p = s + L.field[1];
+          const CP p = s + L.field[1];
           const uint32_t n = fend(1) - L.field[1];
           uint64_t v = 0;
           bool ok = n > 0 && n <= 10;
@@ -310,7 +312,7 @@ __device__ __forceinline__ void parse_line(const uint8_t* s, const WordAt& word_
           if (ok && v <= 0xFFFFFFFFull) L.pos = uint32_t(v); else L.flags |= AVDB_VCF_BAD_POS;
         }
         // ID
-        const uint8_t* id = s + L.field[2];
+        const CP id = s + L.field[2];
         const uint32_t idn = fend(2) - L.field[2];
         {
           bool numlike = idn > 0, has_digit = false;
@@ -332,7 +334,7 @@ __device__ __forceinline__ void parse_line(const uint8_t* s, const WordAt& word_
           if (!L.ext_id) L.flags |= AVDB_VCF_EXT_HOST;
         } else {
           // INFO: last entry whose key is exactly "RS" (dict(...) keeps the last)
-          const uint8_t* inf = s + L.field[7];
+          const CP inf = s + L.field[7];
           const uint32_t f7 = L.field[7], e7 = fend(7);
           int64_t vs = -1, ve = -1;
           bool bare = false;
@@ -378,7 +380,7 @@ __device__ __forceinline__ void parse_line(const uint8_t* s, const WordAt& word_
         }
         // REF / ALT
         const uint32_t rlen = fend(3) - L.field[3];
-        const uint8_t* alt = s + L.field[4];
+        const CP alt = s + L.field[4];
         const uint32_t an = fend(4) - L.field[4];
         uint32_t a0 = 0;
         for (uint32_t i = 0; i <= an; ++i) {
@@ -420,11 +422,11 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
       const uint32_t mis = uint32_t((h.lo + L.start) & 7);
       if (w.staged) {
         const uint8_t* ls = reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0);
-        const uint64_t* lw = reinterpret_cast<const uint64_t*>(ls - mis);
-        parse_line(ls, [lw](uint32_t k) { return lw[k]; }, mis, raw, L, recs, hbytes);
+        const lds_cp64 lw = (lds_cp64)(reinterpret_cast<const uint64_t*>(ls - mis));
+        parse_line((lds_cp)ls, [lw](uint32_t k) { return lw[k]; }, mis, raw, L, recs, hbytes);
       } else {
         const uintptr_t la = h.lo + L.start - mis;
-        parse_line(text + L.start, [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); },
+        parse_line((glb_cp)(text + L.start), [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); },
                    mis, raw, L, recs, hbytes);
       }
       lines[li] = L;
@@ -435,7 +437,8 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
   }
 }
 
-__device__ __forceinline__ void emit_line(const uint8_t* s, const avdb_vcf_line& L, size_t li,
+template <class CP>
+__device__ __forceinline__ void emit_line(CP s, const avdb_vcf_line& L, size_t li,
                                           uint64_t r, uint64_t h, uint8_t* __restrict__ chrom,
                                           uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
                                           uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
@@ -444,9 +447,9 @@ __device__ __forceinline__ void emit_line(const uint8_t* s, const avdb_vcf_line&
     const uint32_t nfields = L.n_fields < 8 ? L.n_fields : 8;
     const uint32_t rend = L.field[4] - 1;
     const uint32_t aend = 5 < nfields ? L.field[5] - 1 : L.len;
-    const uint8_t* ref = s + L.field[3];
+    const CP ref = s + L.field[3];
     const uint32_t rlen = rend - L.field[3];
-    const uint8_t* alt = s + L.field[4];
+    const CP alt = s + L.field[4];
     const uint32_t an = aend - L.field[4];
     uint32_t a0 = 0, ai = 0;
     for (uint32_t i = 0; i <= an; ++i) {
@@ -493,11 +496,11 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
       const avdb_vcf_line L = lines[li];
       if (L.n_rec) {
         if (w.staged)
-          emit_line(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0), L, li,
+          emit_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)), L, li,
                     rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id, heap,
                     rec_line, rec_alt);
         else
-          emit_line(text + L.start, L, li, rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len,
+          emit_line((glb_cp)(text + L.start), L, li, rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len,
                     alt_len, ext_id, heap, rec_line, rec_alt);
       }
     }
