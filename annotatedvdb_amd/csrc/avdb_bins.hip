@@ -392,8 +392,9 @@ extern "C" int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   // K1 variants (records per lane-group 4V, groups in flight U, memory flags F);
   // the default was chosen by on-device A/B (tools/k1_geom.py)
   struct K1Var { int V, U, F; };
-  static const K1Var kVars[] = {{1, 2, 6}, {2, 1, 6}, {2, 2, 6}, {4, 1, 6}, {1, 2, 2}, {1, 4, 6}};
-  const K1Var kv = kVars[(ctx->k1_variant >= 0 && ctx->k1_variant < 6) ? ctx->k1_variant : 0];
+  static const K1Var kVars[] = {{1, 2, 6}, {2, 1, 6}, {2, 2, 6}, {4, 1, 6}, {1, 2, 2}, {1, 4, 6},
+                                 {1, 2, 7}, {1, 2, 4}, {1, 4, 4}, {2, 1, 4}, {1, 1, 4}};
+  const K1Var kv = kVars[(ctx->k1_variant >= 0 && ctx->k1_variant < 11) ? ctx->k1_variant : 0];
   const int R = 4 * kv.V;
   const bool vec = aligned(chrom, size_t(R)) && aligned(start, 16) && (!end || aligned(end, 16)) &&
                    aligned(bin_code, 16) && (!status || aligned(status, size_t(R))) && n >= size_t(R);
@@ -420,6 +421,11 @@ extern "C" int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32
       case 3: K1V(HE, HI, 4, 1, 6); break;                                   \
       case 4: K1V(HE, HI, 1, 2, 2); break;                                   \
       case 5: K1V(HE, HI, 1, 4, 6); break;                                   \
+      case 6: K1V(HE, HI, 1, 2, 7); break;                                   \
+      case 7: K1V(HE, HI, 1, 2, 4); break;                                   \
+      case 8: K1V(HE, HI, 1, 4, 4); break;                                   \
+      case 9: K1V(HE, HI, 2, 1, 4); break;                                   \
+      case 10: K1V(HE, HI, 1, 1, 4); break;                                  \
       default: K1V(HE, HI, 1, 2, 6); break;                                  \
     }                                                                        \
   } while (0)

@@ -7,8 +7,8 @@ from annotatedvdb_amd import synth
 from annotatedvdb_amd.engine import Engine
 
 VARIANTS = [dict(AVDB_K1_VARIANT=v, AVDB_K1_BLOCK=b, AVDB_K1_BLOCKS_PER_CU=p)
-            for (v, b, p) in [(0, 512, 4), (1, 512, 4), (1, 512, 3), (2, 512, 3), (3, 512, 3),
-                              (3, 512, 2), (5, 512, 4), (0, 256, 8), (4, 512, 4)]]
+            for (v, b, p) in [tuple(int(x) for x in t.split(",")) for t in os.environ.get(
+                "K1_VARIANTS", "0,512,4;1,512,4;1,512,3;2,512,3;3,512,3;3,512,2;5,512,4;0,256,8;4,512,4").split(";")]]
 
 def main():
     n = int(os.environ.get("N", 100_000_000)); reps = int(os.environ.get("REPS", 20))
@@ -27,14 +27,21 @@ def main():
         engs[0].bin_assign(chrom, start, None, want_status=False, hist=hist, counters=ctr, out_code=code)
         torch.cuda.synchronize()
     res = {}
+    # BACK2BACK=k: time k back-to-back launches per sample (the bench's steady
+    # state: each launch also pays for the previous one's write-back), else one
+    # launch per sample with a host sync in between
+    b2b = int(os.environ.get("BACK2BACK", "1"))
     for r in range(reps):
         for i, e in enumerate(engs):
             for wl in ("c2", "c3"):
                 cc, ss, ee = (chrom, start, None) if wl == "c2" else (c3, s3, end)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record(); e.bin_assign(cc, ss, ee, want_status=False, hist=hist, counters=ctr, out_code=code); b.record()
+                a.record()
+                for _ in range(b2b):
+                    e.bin_assign(cc, ss, ee, want_status=False, hist=hist, counters=ctr, out_code=code)
+                b.record()
                 b.synchronize()
-                res.setdefault((i, wl), []).append(a.elapsed_time(b))
+                res.setdefault((i, wl), []).append(a.elapsed_time(b) / b2b)
     for (i, wl), ts in sorted(res.items()):
         ms = float(np.median(ts[2:])); bpr = 9 if wl == "c2" else 13
         print(json.dumps({**VARIANTS[i], "workload": wl, "ms": round(ms, 4), "GBps": round(n * bpr / ms / 1e6, 1),
