@@ -443,6 +443,9 @@ class Engine:
         copy_off = self.empty(n + 1, torch.int64)
         map_off = self.empty(n + 1, torch.int64)
         state = self.empty(max(1, n), torch.uint8)
+        if end.numel() == 0:  # no records in this batch: the kernels never read them
+            end = code = self.empty(1, torch.int32)
+            status = self.empty(1, torch.uint8)
         dg = None if digest is None else N.ptr(digest)
         kp = None if keep is None else N.ptr(keep)
         args = (self.ctx, tp, vb.text.numel(), n, N.ptr(vb.lines), N.ptr(vb.rec_off), N.ptr(end), N.ptr(code),

@@ -398,10 +398,34 @@ class VCFVariantLoader(object):
         paths, pks, keep, disp = self._gpu_prep(recs, db if recs else None, codes, dedup)
         return self._emit(parsed, recs, paths, pks, keep, disp, errors)
 
-    def load_vcf_text(self, text, dedup: bool = False, errors: str = "raise") -> str:
-        """One batch of the load driver (Load/bin/load_vcf_file.py:101-119) on the
-        GPU: appends every COPY row to ``copy_buffer()`` and returns the
-        .mapping text (one ``id<TAB>[{...}]`` line per data line).
+    def load_vcf_text(self, text, dedup: bool = False, errors: str = "raise",
+                      batch_bytes: int = 256 << 20) -> str:
+        """The load driver (Load/bin/load_vcf_file.py:101-119) on the GPU for a
+        block of VCF text: appends every COPY row to ``copy_buffer()`` and
+        returns the .mapping text (one ``id<TAB>[{...}]`` line per data line).
+        Text larger than ``batch_bytes`` runs as consecutive device batches cut at
+        line boundaries (bounded HBM and host memory); ``dedup`` (keep-first per
+        primary key, our addition) applies within each batch."""
+        raw = bytes(text)
+        if len(raw) <= batch_bytes:
+            return self._load_vcf_batch(raw, dedup, errors)
+        out = []
+        i = 0
+        while i < len(raw):
+            j = min(len(raw), i + batch_bytes)
+            if j < len(raw):
+                k = raw.rfind(b"\n", i, j)
+                if k >= i:
+                    j = k + 1
+                else:  # one line longer than a batch
+                    k = raw.find(b"\n", j)
+                    j = len(raw) if k < 0 else k + 1
+            out.append(self._load_vcf_batch(raw[i:j], dedup, errors))
+            i = j
+        return "".join(out)
+
+    def _load_vcf_batch(self, raw: bytes, dedup: bool, errors: str) -> str:
+        """One device batch of :meth:`load_vcf_text`.
 
         K0 tokenizes, K2 infers ends and bins, K4 digests long keys, K3 marks
         in-batch duplicates when ``dedup``, and K5 writes both texts on the
@@ -417,7 +441,6 @@ class VCFVariantLoader(object):
             raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
         if self.is_adsp():
             raise NotImplementedError("ADSP loads check duplicates in the database (is_duplicate); out of scope")
-        raw = bytes(text)
         if not self.resume_load() or self._chromosome_map is not None or self._vcf_header_fields:
             lines = [ln.rstrip() for ln in raw.decode("utf-8").split("\n") if ln and not ln.startswith("#")]
             out = self.parse_variants(lines, errors=errors, dedup=dedup)
@@ -467,16 +490,17 @@ class VCFVariantLoader(object):
             return map_raw
         rec_off = vb.rec_off.cpu().numpy()
         keep_h = keep.cpu().numpy() if keep is not None else None
-        L = vb.lines[: n * 80].view(torch.uint8)
+        # the host lines' table rows in one transfer
+        Lh = vb.lines[: n * 80].view(n, 80)[torch.from_numpy(host).to(eng.device)].cpu().numpy()
+        Lh = Lh.view(np.uint64).reshape(len(host), 10)
         maps = []
         c0 = m0 = 0
-        for li in host.tolist():
+        for hi, li in enumerate(host.tolist()):
             # GPU text of the lines before this one
             self._copy_buffer.write(copy_raw[c0:copy_off[li]])
             maps.append(map_raw[m0:map_off[li]])
             c0, m0 = int(copy_off[li]), int(map_off[li])
-            rec = np.frombuffer(L[li * 80:(li + 1) * 80].cpu().numpy().tobytes(), dtype=np.uint64)
-            st, ln = int(rec[0]), int(rec[1] & 0xFFFFFFFF)
+            st, ln = int(Lh[hi, 0]), int(Lh[hi, 1] & 0xFFFFFFFF)
             line = raw[st:st + ln].decode("utf-8")
             kov = None if keep_h is None else keep_h[rec_off[li]:rec_off[li + 1]]
             try:

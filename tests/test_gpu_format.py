@@ -156,3 +156,19 @@ def test_k5b_edge_lines(engine, loader):
     assert mapping.splitlines() == exp_map
     with pytest.raises(IndexError):  # short FREQ list, as the reference
         loader.load_vcf_text(b"1\t5\t.\tA\tG,T\t.\t.\tFREQ=A:0.5,0.25\n")
+
+
+def test_k5b_batched_text_equals_single_batch(engine, loader):
+    """load_vcf_text cut into small device batches (line boundaries, including a
+    line longer than the batch) == one batch."""
+    rows = load_rows()[:1200]
+    text = ("\n".join(r[0] for r in rows) + "\n").encode()
+    loader.reset_copy_buffer()
+    m1 = loader.load_vcf_text(text, errors="record")
+    c1 = loader.copy_buffer().getvalue()
+    loader.reset_copy_buffer()
+    m2 = loader.load_vcf_text(text, errors="record", batch_bytes=20000)
+    assert (m2, loader.copy_buffer().getvalue()) == (m1, c1)
+    loader.reset_copy_buffer()
+    m3 = loader.load_vcf_text(text, errors="record", batch_bytes=50)  # every batch one line
+    assert (m3, loader.copy_buffer().getvalue()) == (m1, c1)
