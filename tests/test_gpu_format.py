@@ -172,3 +172,34 @@ def test_k5b_batched_text_equals_single_batch(engine, loader):
     loader.reset_copy_buffer()
     m3 = loader.load_vcf_text(text, errors="record", batch_bytes=50)  # every batch one line
     assert (m3, loader.copy_buffer().getvalue()) == (m1, c1)
+
+
+@pytest.mark.slow
+def test_k5b_bench_size_properties(engine):
+    """The load workload at bench size (8.4 M synthetic dbSNP lines): every line
+    rendered on the GPU, one COPY row per record with ten '#'-columns, one
+    .mapping line per line, and a sample of 3,000 lines byte-exact vs the oracle."""
+    from annotatedvdb_amd import synth
+    tile = synth.vcf_text(1 << 19, seed=6)
+    reps = 16
+    text = torch.frombuffer(bytearray(tile), dtype=torch.uint8).cuda().repeat(reps)
+    vb = engine.vcf_tokenize(text)
+    end, code, status, _ = engine.record_prep(vb.records, want_lcp=False)
+    fr = engine.vcf_format(vb, end, code, status, alg_id="1")
+    assert vb.n_lines == reps << 19
+    assert int(fr.counters[27]) == 0 and bool((fr.line_state == 0).all())
+    assert int(fr.counters[24]) == vb.records.n
+    copy = fr.copy.cpu().numpy()
+    mapping = fr.mapping.cpu().numpy()
+    assert int((copy == 10).sum()) == vb.records.n and int((mapping == 10).sum()) == vb.n_lines
+    assert int((copy == ord("#")).sum()) == 9 * vb.records.n
+    # sample vs the oracle (the text repeats every 2^19 lines)
+    lines = tile.decode().splitlines()
+    co = fr.copy_off.cpu().numpy()
+    mo = fr.map_off.cpu().numpy()
+    rng = np.random.default_rng(8)
+    for li in rng.choice(vb.n_lines, 3000, replace=False):
+        err, m, c = O.load_line(lines[li % len(lines)], length_table())
+        assert err is None
+        assert copy[co[li]:co[li + 1]].tobytes().decode() == "".join(x + "\n" for x in c)
+        assert mapping[mo[li]:mo[li + 1]].tobytes().decode() == "".join(x + "\n" for x in m)

@@ -280,3 +280,49 @@ def test_k4_vrs_digest_vs_oracle_serialisation(engine):
         alt = h["heap"][o + r:o + r + a].tobytes()
         exp = O.vrs_allele_digest(digs[h["chrom"][i]], int(h["pos"][i]), ref, alt)
         assert raw[i].tobytes().decode() == exp
+
+
+@pytest.mark.slow
+def test_c5_full_size_vs_c_oracle(engine):
+    """BASELINE config 5 at full per-GPU size (2.5e7 ADSP-style records): K2 end /
+    bin / status and K3 keep-first bit-exact vs the C oracle; the hash-path dedup
+    equals the grouped path; long-key digests on a sample vs the oracle's
+    serialisation (VRS layout itself unpinned)."""
+    import oracle
+    from annotatedvdb_amd import synth
+    n = 25_000_000
+    b = synth.alleles(n, seed=5)
+    end, code, status, _ = engine.record_prep(b, want_lcp=False)
+    h = {k: getattr(b, k).cpu().numpy() for k in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap",
+                                                  "ext_id")}
+    re_, rc, rl = (np.empty(n, dtype=np.uint32) for _ in range(3))
+    rs = np.empty(n, dtype=np.uint8)
+    lens = np.asarray(LENGTHS, dtype=np.uint32)
+    oracle.c_oracle().avdb_oracle_record_prep(
+        h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
+        h["alt_len"].ctypes.data, h["heap"].ctypes.data, n, lens.ctypes.data, len(lens),
+        re_.ctypes.data, rc.ctypes.data, rs.ctypes.data, rl.ctypes.data)
+    assert np.array_equal(u32(end), re_)
+    assert np.array_equal(u32(code), rc)
+    assert np.array_equal(status.cpu().numpy(), rs)
+    keep = np.empty(n, dtype=np.uint8)
+    ndup = oracle.c_oracle().avdb_oracle_dedup_grouped(
+        h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
+        h["alt_len"].ctypes.data, h["heap"].ctypes.data, h["ext_id"].ctypes.data, n, keep.ctypes.data)
+    kg = engine.pk_dedup(b, grouped=True)
+    assert np.array_equal(kg.cpu().numpy(), keep) and ndup > 0
+    kh = engine.pk_dedup(b, grouped=False)
+    assert torch.equal(kg, kh)
+    digs = ["%032d" % i for i in range(25)]
+    eng2 = type(engine)(0, sequence_digests=digs)
+    d, is_long = eng2.vrs_digest(b, 50)
+    il = is_long.cpu().numpy()
+    assert np.array_equal(il, (h["ref_len"].astype(np.int64) + h["alt_len"] > 50).astype(np.uint8))
+    rows = np.nonzero(il)[0]
+    sel = rows[np.random.default_rng(5).choice(len(rows), 300, replace=False)]
+    raw = d[torch.from_numpy(sel).cuda()].cpu().numpy()
+    for k, i in enumerate(sel):
+        o, r, a = int(h["allele_off"][i]), int(h["ref_len"][i]), int(h["alt_len"][i])
+        exp = O.vrs_allele_digest(digs[h["chrom"][i]], int(h["pos"][i]), h["heap"][o:o + r].tobytes(),
+                                  h["heap"][o + r:o + r + a].tobytes())
+        assert raw[k].tobytes().decode() == exp
