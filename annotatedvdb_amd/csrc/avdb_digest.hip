@@ -87,33 +87,58 @@ __device__ __forceinline__ uint32_t allele_blocks(uint32_t a) {
   return sha_blocks(uint64_t(kAlPrefix) + a + nA2);
 }
 
-__device__ __forceinline__ uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate right by a constant as two 32-bit funnel shifts (v_alignbit_b32),
+// instead of two 64-bit shifts and an or
+template <int N>
+__device__ __forceinline__ uint64_t rotr(uint64_t x) {
+  const uint32_t lo = uint32_t(x), hi = uint32_t(x >> 32);
+  uint32_t nlo, nhi;
+  if constexpr (N < 32) {
+    nlo = __builtin_amdgcn_alignbit(hi, lo, N);
+    nhi = __builtin_amdgcn_alignbit(lo, hi, N);
+  } else {
+    nlo = __builtin_amdgcn_alignbit(lo, hi, N - 32);
+    nhi = __builtin_amdgcn_alignbit(hi, lo, N - 32);
+  }
+  return (uint64_t(nhi) << 32) | nlo;
+}
 
-// One SHA-512 compression; state and schedule in registers.
+// bitwise select / majority per 32-bit half (v_bfi_b32)
+__device__ __forceinline__ uint64_t bsel(uint64_t m, uint64_t x, uint64_t y) {  // m ? x : y
+  return (m & x) | (~m & y);
+}
+
+template <bool SCHED>
+__device__ __forceinline__ void sha512_16(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t& e,
+                                          uint64_t& f, uint64_t& g, uint64_t& hh, uint64_t* w, int r) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint64_t wt;
+    if constexpr (!SCHED) {
+      wt = w[j];
+    } else {
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+      const uint64_t s0 = rotr<1>(w15) ^ rotr<8>(w15) ^ (w15 >> 7);
+      const uint64_t s1 = rotr<19>(w2) ^ rotr<61>(w2) ^ (w2 >> 6);
+      wt = w[j] + s0 + w[(j + 9) & 15] + s1;
+      w[j] = wt;
+    }
+    const uint64_t S1 = rotr<14>(e) ^ rotr<18>(e) ^ rotr<41>(e);
+    const uint64_t ch = bsel(e, f, g);
+    const uint64_t t1 = hh + S1 + ch + K512[r + j] + wt;
+    const uint64_t S0 = rotr<28>(a) ^ rotr<34>(a) ^ rotr<39>(a);
+    const uint64_t mj = bsel(a ^ b, c, b);  // majority(a, b, c)
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+  }
+}
+
+// One SHA-512 compression; state and schedule in registers.  The first 16
+// rounds (message words as given) are peeled off the scheduled 64.
 __device__ __forceinline__ void sha512_block(uint64_t* H, uint64_t* w) {
   uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], hh = H[7];
+  sha512_16<false>(a, b, c, d, e, f, g, hh, w, 0);
 #pragma unroll 1
-  for (int r = 0; r < 80; r += 16) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      uint64_t wt;
-      if (r == 0) {
-        wt = w[j];
-      } else {
-        const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-        const uint64_t s0 = rotr(w15, 1) ^ rotr(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr(w2, 19) ^ rotr(w2, 61) ^ (w2 >> 6);
-        wt = w[j] + s0 + w[(j + 9) & 15] + s1;
-        w[j] = wt;
-      }
-      const uint64_t S1 = rotr(e, 14) ^ rotr(e, 18) ^ rotr(e, 41);
-      const uint64_t ch = (e & f) ^ (~e & g);
-      const uint64_t t1 = hh + S1 + ch + K512[r + j] + wt;
-      const uint64_t S0 = rotr(a, 28) ^ rotr(a, 34) ^ rotr(a, 39);
-      const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
-    }
-  }
+  for (int r = 16; r < 80; r += 16) sha512_16<true>(a, b, c, d, e, f, g, hh, w, r);
   H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += hh;
 }
 
@@ -321,10 +346,11 @@ __device__ __forceinline__ uint8_t loc_byte(const LocMsg& m, uint32_t p) {
   return uint8_t(kLoc3[p]);
 }
 
-// 3 waves per SIMD (<= 168 VGPRs): the SHA-512 chains are latency-bound, so
+// 4 waves per SIMD (<= 128 VGPRs): the SHA-512 chains are latency-bound, so
 // occupancy is what the VALU pipe needs (rocprof: 1 VALU issue per ~12 cycles
 // per wave at 2 waves/SIMD)
-__global__ __launch_bounds__(kBlock, 3) void k_vrs_digest(
+constexpr int kDigestWavesPerSimd = 4;
+__global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
     const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
@@ -468,7 +494,8 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
                      max_seq_len, counts, list);
   AVDB_LAUNCH_CHECK("k_long_scatter");
   // persistent grid over the grouped list
-  hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * 3), dim3(kBlock), 0, s, chrom, pos, allele_off,
+  hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * kDigestWavesPerSimd), dim3(kBlock), 0, s, chrom, pos,
+                     allele_off,
                      ref_len, alt_len, heap, heap_bytes, list, total, ctx->d_seq_digest, ctx->tab.n,
                      digest_out);
   AVDB_LAUNCH_CHECK("k_vrs_digest");
