@@ -292,28 +292,46 @@ __global__ __launch_bounds__(kBlock) void k_bin_assign1(
 // variant_annotator.py:36-79 with lcp from __normalize_alleles (:82-121).
 // Allele bytes are compared 8 at a time (first mismatch via count-trailing-zeros
 // of the XOR); the inversion test reverses 8-byte chunks with a byte swap.
+// wr / wa are the first 8 bytes of ref / alt, loaded by the caller ahead of
+// time; alleles of up to 8 bytes (the bulk) need no further heap reads.
 __device__ __forceinline__ uint32_t infer_end(const Heap& h, uint64_t off, uint32_t r, uint32_t a,
-                                              uint32_t pos, uint32_t* lcp_out) {
+                                              uint32_t pos, uint64_t wr, uint64_t wa,
+                                              uint32_t* lcp_out) {
   if (r == 1u && a == 1u) { *lcp_out = 0; return pos; }        // SNV (:54-55)
   const uint64_t alt = off + r;
   const uint32_t m = r < a ? r : a;
-  uint32_t n = 0;                                              // lcp (:100-108)
-  while (n < m) {
-    const uint64_t x = (heap_u64(h, off + n) ^ heap_u64(h, alt + n)) & low_bytes_mask(m - n);
-    if (x) { n += uint32_t(__builtin_ctzll(x)) >> 3; break; }
-    n += 8;
+  uint32_t n;                                                  // lcp (:100-108)
+  const uint64_t x0 = (wr ^ wa) & low_bytes_mask(m < 8u ? m : 8u);
+  if (x0) {
+    n = uint32_t(__builtin_ctzll(x0)) >> 3;
+  } else if (m <= 8u) {
+    n = m;
+  } else {
+    n = 8;
+    while (n < m) {
+      const uint64_t x = (heap_u64(h, off + n) ^ heap_u64(h, alt + n)) & low_bytes_mask(m - n);
+      if (x) { n += uint32_t(__builtin_ctzll(x)) >> 3; break; }
+      n += 8;
+    }
+    if (n > m) n = m;
   }
-  if (n > m) n = m;
   *lcp_out = n;
   const uint32_t nr = r - n, na = a - n;
   if (r == a) {                                                // MNV (:57-65)
     bool inv = true;                                           // ref == alt[::-1]
-    for (uint32_t i = 0; i < r && inv; i += 8) {
-      const uint32_t c = r - i < 8 ? r - i : 8;
-      const uint64_t mk = low_bytes_mask(c);
-      const uint64_t fw = heap_u64(h, off + i) & mk;
-      const uint64_t bw = __builtin_bswap64(heap_u64(h, alt + (r - i - c)) & mk) >> (8 * (8 - c));
-      inv = fw == bw;
+    if (r <= 8u) {
+      if (r) {
+        const uint64_t mk = low_bytes_mask(r);
+        inv = (wr & mk) == (__builtin_bswap64(wa & mk) >> (8 * (8 - r)));
+      }
+    } else {
+      for (uint32_t i = 0; i < r && inv; i += 8) {
+        const uint32_t c = r - i < 8 ? r - i : 8;
+        const uint64_t mk = low_bytes_mask(c);
+        const uint64_t fw = heap_u64(h, off + i) & mk;
+        const uint64_t bw = __builtin_bswap64(heap_u64(h, alt + (r - i - c)) & mk) >> (8 * (8 - c));
+        inv = fw == bw;
+      }
     }
     return inv ? pos + r - 1u : pos + nr - 1u;
   }
@@ -321,6 +339,11 @@ __device__ __forceinline__ uint32_t infer_end(const Heap& h, uint64_t off, uint3
     return nr >= 1u ? pos + nr : (r > 1u ? pos + r - 1u : pos + 1u);
   return nr == 0u ? pos + r - 1u : pos + nr;                   // deletion (:77-79)
 }
+
+// Records per lane per pass: all their SoA loads, then all their first heap
+// words, are issued before any is consumed (the heap reads depend on
+// allele_off, so one record per lane leaves K2 latency-bound).
+constexpr int kPrepU = 4;
 
 template <bool HIST>
 __global__ __launch_bounds__(kBlock) void k_record_prep(
@@ -343,24 +366,44 @@ __global__ __launch_bounds__(kBlock) void k_record_prep(
   const size_t i0 = size_t(blockIdx.x) * per;
   const size_t i1 = i0 + per < n ? i0 + per : n;
   ErrCounters ec;
-  for (size_t base = i0; base < i1; base += kBlock) {
-    const size_t i = base + threadIdx.x;
-    uint32_t key = 0xFFFFFFFFu;
-    if (i < i1) {
-      const uint32_t c = chrom[i], p = pos[i];
-      uint32_t l;
-      const uint32_t e = infer_end(hp, allele_off[i], ref_len[i], alt_len[i], p, &l);
-      uint32_t cv;
-      const uint32_t s_k = classify(c, p, e, tab.n, s_len, &cv);
-      end_out[i] = e;
-      code[i] = cv;
-      if (status) status[i] = uint8_t(s_k);
-      if (lcp) lcp[i] = l;
-      if (ctrs) ec.add(s_k);
-      key = l8_key(c, p, cv, s_l8off);
+  for (size_t base = i0; base < i1; base += size_t(kBlock) * kPrepU) {
+    uint32_t c[kPrepU], p[kPrepU], r[kPrepU], a[kPrepU];
+    uint64_t off[kPrepU], wr[kPrepU], wa[kPrepU];
+#pragma unroll
+    for (int k = 0; k < kPrepU; ++k) {
+      const size_t i = base + size_t(k) * kBlock + threadIdx.x;
+      const size_t j = i < i1 ? i : i0;  // clamped: every lane loads in bounds
+      c[k] = chrom[j];
+      p[k] = pos[j];
+      off[k] = allele_off[j];
+      r[k] = ref_len[j];
+      a[k] = alt_len[j];
     }
-    if (HIST) wave_hist_add(key, hist);
-    if (ctrs) ec.tick(s_ctr);
+#pragma unroll
+    for (int k = 0; k < kPrepU; ++k) {
+      const bool snv = r[k] == 1u && a[k] == 1u;
+      wr[k] = snv ? 0 : heap_u64(hp, off[k]);
+      wa[k] = snv ? 0 : heap_u64(hp, off[k] + r[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kPrepU; ++k) {
+      const size_t i = base + size_t(k) * kBlock + threadIdx.x;
+      uint32_t key = 0xFFFFFFFFu;
+      if (i < i1) {
+        uint32_t l;
+        const uint32_t e = infer_end(hp, off[k], r[k], a[k], p[k], wr[k], wa[k], &l);
+        uint32_t cv;
+        const uint32_t s_k = classify(c[k], p[k], e, tab.n, s_len, &cv);
+        end_out[i] = e;
+        code[i] = cv;
+        if (status) status[i] = uint8_t(s_k);
+        if (lcp) lcp[i] = l;
+        if (ctrs) ec.add(s_k);
+        key = l8_key(c[k], p[k], cv, s_l8off);
+      }
+      if (HIST) wave_hist_add(key, hist);
+      if (ctrs) ec.tick(s_ctr);
+    }
   }
   if (ctrs) ec.finish(s_ctr);
   publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);

@@ -80,9 +80,18 @@ __device__ __forceinline__ uint64_t heap_word(uintptr_t a, const Heap& h) {  // 
   return v;
 }
 
+// One unaligned 8-byte global load (global_load_dwordx2: gfx950 runs in
+// unaligned-access mode, and the compiler emits it for a packed struct).
+struct __attribute__((packed)) U64u {
+  uint64_t v;
+};
+typedef const __attribute__((address_space(1))) U64u* g_u64u;
+
 // little-endian 8 bytes starting at heap offset p (bytes past the heap read 0)
 __device__ __forceinline__ uint64_t heap_u64(const Heap& h, uint64_t p) {
   const uintptr_t addr = h.lo + p;
+  if (addr + 8 <= h.hi) return reinterpret_cast<g_u64u>(addr)->v;
+  // within 8 bytes of the heap end: aligned words, zero fill
   const uintptr_t a = addr & ~uintptr_t(7);
   const uint32_t sh = uint32_t(addr & 7) * 8;
   const uint64_t lo = heap_word(a, h);

@@ -279,8 +279,16 @@ def main():
 
     if a.workload == "c5":
         # K2 algorithmic bytes per record: in chrom 1 + pos 4 + allele_off 8 + ref_len 4 +
-        # alt_len 4 (+ the heap bytes it reads, bounded by the heap); out end 4 + code 4
-        bytes_per_launch = n * (1 + 4 + 8 + 4 + 4 + 4 + 4) + heap_bytes
+        # alt_len 4, out end 4 + code 4 + status 1 (= 30 B), plus the allele bytes end
+        # inference must read: through the first ref/alt mismatch (lcp + 1, capped at each
+        # allele's length) for every non-SNV record.  The inversion test of equal-length
+        # alleles may read further; that is not counted (a lower bound).
+        _, _, _, lcp = eng.record_prep(batch, want_lcp=True)
+        rl, al = batch.ref_len.long(), batch.alt_len.long()
+        need = (torch.minimum(lcp.long() + 1, rl) + torch.minimum(lcp.long() + 1, al))
+        need = torch.where((rl == 1) & (al == 1), torch.zeros_like(need), need)
+        bytes_per_launch = n * 30 + int(need.sum().item())
+        del lcp, need, rl, al
     elif a.workload == "load":
         # K5 write pass: text read once + line table (80 B) + rec_off (8) + both offset
         # arrays (16) + line state (1) per line + end/code/status (9) per record, and
