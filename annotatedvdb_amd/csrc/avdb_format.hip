@@ -15,7 +15,8 @@
 //   SIZE pass (bytes per line) -> hipCUB exclusive scans -> WRITE pass, both the
 //   same templated code.  One lane per line, 256 consecutive lines per workgroup
 //   with their text staged in LDS (as K0); each lane writes its own contiguous
-//   span of both outputs (layout and alternatives measured: see Out below).  A line the GPU does not render byte-exact (non-ASCII text,
+//   span of both outputs (sink and alternatives measured: see Out below).  A
+//   line the GPU does not render byte-exact (non-ASCII text,
 //   allele bytes that need escaping, an unmappable record (TypeError), a key the
 //   reference cannot build (':' in an allele), malformed or non-canonical FREQ
 //   numbers, K0 host-resolved fields) is marked HOST and gets zero bytes; the
@@ -27,20 +28,44 @@
 
 #include <hipcub/hipcub.hpp>
 #include <string.h>
+#include <type_traits>
 
 namespace avdb {
 
 // ---------------------------------------------------------------------------
 // output sink: SIZE pass counts, WRITE pass stores
 // ---------------------------------------------------------------------------
-// WRITE pass: one global byte store per output byte (global_store_byte through
-// an address-space-1 pointer; flat stores were no faster).  A/B on MI355X, 2 M
-// dbSNP-shaped lines, 1.31 GB of text: byte stores 4.5 ms; an 8-byte register
-// word with aligned dwordx2 stores 12.1 ms (255 VGPRs, occupancy 1); a per-lane
-// 128-byte LDS ring flushing aligned 64-byte lines as dwordx4 stores 6.2 ms
-// (LDS-limited occupancy).  The pass is instruction-issue bound (per-byte
-// formatting work), not HBM bound: see DESIGN.md.
+// WRITE pass sink: each lane's bytes are packed into a 64-bit register word and
+// stored 8 at a time (an unaligned global_store_dwordx2; gfx950 runs in
+// unaligned mode), the tail (< 8 bytes) byte by byte at the end of the line.
+// The lanes of a wave write 64 different lines, so every store instruction
+// touches up to 64 cache lines: what costs is the number of lane-stores, not
+// bytes.  A/B on MI355X, 8.39 M dbSNP-shaped lines, 5.25 GB written (write
+// pass; size pass 5.1 ms; tools/k5_ab.sh):
+//   byte stores, noinline helpers, 3 waves/SIMD            15.0 ms
+//   same, stores made coalesced (wrong output; the floor)     4.6 ms
+//   8-byte word, noinline helpers, 3 waves/SIMD             9.7 ms
+//   8-byte word, inlined helpers, 3 waves/SIMD              9.3 ms
+//   8-byte word, inlined helpers, 4 waves/SIMD (this)       8.1 ms
+//   16-byte word (two u64), 2 waves/SIMD (VGPR-bound)      17.4 ms
+//   per-lane LDS ring (32/64 B per stream) flushing 16-byte
+//     chunks at convergent points, 2 waves/SIMD             13.4 / 17.7 ms
+// Occupancy decides: the pass is latency-bound on LDS text reads and store
+// back-pressure, so 4 waves/SIMD (launch bound; ~120 B of spills) beats every
+// wider sink that costs registers or LDS.
 typedef __attribute__((address_space(1))) uint8_t gbyte;
+typedef __attribute__((address_space(1))) U64u* gw_u64u;
+constexpr int kFormatWaves = 4;  // per SIMD: the text window's LDS allows 4 workgroups per CU
+
+// decimal digits of v as nibbles, most significant digit in the lowest nibble
+// (registers only: a local char array would live in scratch memory)
+__device__ __forceinline__ uint64_t dec_nibbles(uint32_t v, uint32_t* ndig) {
+  uint64_t d = 0;
+  uint32_t k = 0;
+  do { d = (d << 4) | (v % 10u); v /= 10u; ++k; } while (v);
+  *ndig = k;
+  return d;
+}
 
 template <bool WRITE>
 struct Out {
@@ -50,9 +75,30 @@ struct Out {
   __device__ __forceinline__ Out(uint8_t* b, uint64_t at)
       : base((gbyte*)b), p(at), lo(at), bad(false) {}
   __device__ __forceinline__ uint32_t size() const { return uint32_t(p - lo); }
+  struct Pending {  // WRITE: bytes [p-k, p) not yet stored
+    uint64_t w = 0;
+    uint32_t k = 0;
+  };
+  struct None {};
+  [[no_unique_address]] std::conditional_t<WRITE, Pending, None> pend;
   __device__ __forceinline__ void put(uint32_t c) {
-    if constexpr (WRITE) base[p] = uint8_t(c);
+    if constexpr (WRITE) {
+      pend.w |= uint64_t(c & 0xFFu) << (8 * pend.k);
+      if (++pend.k == 8) {
+        reinterpret_cast<gw_u64u>(base + p - 7)->v = pend.w;
+        pend.w = 0;
+        pend.k = 0;
+      }
+    }
     ++p;
+  }
+  // end of the line: store the buffered tail
+  __device__ __forceinline__ void finish() {
+    if constexpr (WRITE) {
+      for (uint32_t j = 0; j < pend.k; ++j) base[p - pend.k + j] = uint8_t(pend.w >> (8 * j));
+      pend.w = 0;
+      pend.k = 0;
+    }
   }
   __device__ __forceinline__ void lit(const char* s) {
     while (*s) put(uint8_t(*s++));
@@ -66,17 +112,25 @@ struct Out {
     }
   }
   __device__ __forceinline__ void u32v(uint32_t v) {
-    char t[10];
-    int k = 0;
-    do { t[k++] = char('0' + v % 10u); v /= 10u; } while (v);
-    while (k) put(uint8_t(t[--k]));
+    uint32_t k;
+    uint64_t d = dec_nibbles(v, &k);
+    for (; k; --k, d >>= 4) put(uint32_t('0' + (d & 15u)));
   }
   __device__ __forceinline__ void u64v(uint64_t v) {
     if (v <= 0xFFFFFFFFull) { u32v(uint32_t(v)); return; }
-    char t[20];
-    int k = 0;
-    do { t[k++] = char('0' + v % 10u); v /= 10u; } while (v);
-    while (k) put(uint8_t(t[--k]));
+    const uint64_t q = v / 1000000000ull;
+    if (q <= 0xFFFFFFFFull) {
+      u32v(uint32_t(q));
+    } else {
+      u32v(uint32_t(q / 1000000000ull));
+      dec9(uint32_t(q % 1000000000ull));
+    }
+    dec9(uint32_t(v % 1000000000ull));
+  }
+  __device__ __forceinline__ void dec9(uint32_t v) {  // exactly 9 digits, zero-padded
+    uint64_t d = 0;
+    for (int i = 0; i < 9; ++i) { d = (d << 4) | (v % 10u); v /= 10u; }
+    for (int i = 0; i < 9; ++i, d >>= 4) put(uint32_t('0' + (d & 15u)));
   }
 };
 
@@ -90,11 +144,11 @@ __device__ __forceinline__ void chrom_name(O& o, uint32_t c) {
   else o.u32v(c);  // contigs beyond the human 25: numeric label (matches avdb_format_bin_path)
 }
 
-// ltree path of a bin code (generate_bin_index_references.py:54,60-61,74)
-// (noinline helpers take and return the sink by value: it stays in VGPRs
-// across the call instead of going through the scratch stack)
+// ltree path of a bin code (generate_bin_index_references.py:54,60-61,74).
+// Helpers take and return the sink by value (never by reference: a sink whose
+// address escapes lives in scratch memory); all are inlined (see the A/B above).
 template <class O>
-__device__ __noinline__ O bin_path(O o, uint32_t c, uint32_t code) {
+__device__ __forceinline__ O bin_path(O o, uint32_t c, uint32_t code) {
   o.lit("chr");
   chrom_name(o, c);
   const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
@@ -172,7 +226,7 @@ __device__ __forceinline__ void al_trunc(O& o, const Al<CP>& a, uint32_t cap) {
 // chrom >= 25 writes no label in normalized_metaseq_id (the caller prepends it).
 // ---------------------------------------------------------------------------
 template <bool ESC, class O, class CP>
-__device__ __noinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, CP ref, uint32_t r,
+__device__ __forceinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, CP ref, uint32_t r,
                                        CP alt, uint32_t a) {
   const bool snv = r == 1u && a == 1u;
   uint32_t l = 0;  // common prefix (__normalize_alleles :100-107); SNVs untouched (:97-98)
@@ -310,7 +364,7 @@ __device__ __forceinline__ bool number_plain(CP f, uint32_t n) {
 }
 
 template <class O, class CP>
-__device__ __noinline__ O json_number(O o, CP f, uint32_t n) {
+__device__ __forceinline__ O json_number(O o, CP f, uint32_t n) {
   o.bad = !number_plain(f, n);
   if (o.bad) return o;
   uint32_t dot = n;
@@ -456,7 +510,7 @@ __device__ bool freq_plain(CP s, uint32_t v0, uint32_t v1) {
 // json.dumps text or NULL; false when the reference would raise or print a
 // number the GPU does not format
 template <class O, class CP>
-__device__ __noinline__ O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint32_t k) {
+__device__ __forceinline__ O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint32_t k) {
   bool any = false;
   for (uint32_t p0 = v0; p0 <= v1;) {
     const uint32_t p1 = find_byte(s, p0, v1, '|');
@@ -491,9 +545,9 @@ __device__ __noinline__ O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint32_
   return o;
 }
 
-template <bool WRITE, class CP>
+template <bool WRITE, class O, class CP>
 __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, CP s, size_t li,
-                               Out<WRITE>& oc, Out<WRITE>& om, uint32_t* n_rows, uint32_t* n_skip,
+                               O& oc, O& om, uint32_t* n_rows, uint32_t* n_skip,
                                uint32_t* n_dup) {
   if (L.flags & AVDB_VCF_COMMENT) return kLineSkip;
   if ((L.flags & kHostFlags) || L.chrom >= 25) return kLineHost;
@@ -579,7 +633,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
       b0 = b1 + 1;
     }
     // primary key (primary_key_generator.py:106-122)
-    auto pk = [&](Out<WRITE>& o) {
+    auto pk = [&](O& o) {
       chrom_name(o, c);
       o.put(':');
       o.u32v(L.pos);
@@ -662,7 +716,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
 }
 
 template <bool WRITE>
-__global__ __launch_bounds__(kBlock) void k_vcf_format(FormatArgs A) {
+__global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs A) {
   __shared__ u32x4 s_text[kStage / 16];
   const Heap h = make_heap(A.text, A.text_bytes);
   uint32_t rows = 0, skip = 0, dups = 0, hosts = 0;
@@ -681,6 +735,8 @@ __global__ __launch_bounds__(kBlock) void k_vcf_format(FormatArgs A) {
           if (st == kLineGpu) {
             Out<true> oc(A.copy_out, A.copy_off[li]), om(A.map_out, A.map_off[li]);
             format_line<true>(A, L, s, li, oc, om, &rows, &skip, &dups);
+            oc.finish();
+            om.finish();
           } else if (st == kLineHost) {
             ++hosts;
           }
@@ -735,6 +791,7 @@ __global__ __launch_bounds__(kBlock) void k_display(const uint8_t* __restrict__ 
       if (state[i]) continue;
       Out<true> w(out, out_off[i]);
       w = display_json<true>(w, chrom[i], pos[i], end[i], (glb_cp)(heap + o), r, (glb_cp)(heap + o + r), a);
+      w.finish();
     } else {
       uint8_t st = o + r + a > heap_bytes ? 2 : 0;
       for (uint32_t k = 0; k < r + a && !st; ++k)

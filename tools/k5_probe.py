@@ -20,3 +20,8 @@ for it in range(4):
     print("lines %d  size %.3f ms  write %.3f ms  out %.0f MB  write-rate %.1f GB/s  host_lines %d" % (
         vb.n_lines, t["format_size"], t["format_write"], out / 1e6, out / t["format_write"] / 1e6,
         int(fr.counters[27])), flush=True)
+def cks(t):
+    t = t.to(torch.int64)
+    w = torch.arange(t.numel(), device=t.device, dtype=torch.int64) % 251 + 1
+    return int(t.sum()), int((t * w).sum())
+print("checksum copy", cks(fr.copy), "mapping", cks(fr.mapping), flush=True)
