@@ -67,6 +67,12 @@ __device__ __forceinline__ uint64_t dec_nibbles(uint32_t v, uint32_t* ndig) {
   return d;
 }
 
+__device__ __forceinline__ uint32_t ndigits(uint32_t v) {  // decimal digits
+  uint32_t k = 1;
+  while (v >= 10u) { v /= 10u; ++k; }
+  return k;
+}
+
 template <bool WRITE>
 struct Out {
   gbyte* base;
@@ -112,6 +118,10 @@ struct Out {
     }
   }
   __device__ __forceinline__ void u32v(uint32_t v) {
+    if constexpr (!WRITE) {
+      p += ndigits(v);
+      return;
+    }
     uint32_t k;
     uint64_t d = dec_nibbles(v, &k);
     for (; k; --k, d >>= 4) put(uint32_t('0' + (d & 15u)));
@@ -128,6 +138,10 @@ struct Out {
     dec9(uint32_t(v % 1000000000ull));
   }
   __device__ __forceinline__ void dec9(uint32_t v) {  // exactly 9 digits, zero-padded
+    if constexpr (!WRITE) {
+      p += 9;
+      return;
+    }
     uint64_t d = 0;
     for (int i = 0; i < 9; ++i) { d = (d << 4) | (v % 10u); v /= 10u; }
     for (int i = 0; i < 9; ++i, d >>= 4) put(uint32_t('0' + (d & 15u)));
@@ -456,13 +470,14 @@ struct FormatArgs {
 // allele bytes the GPU writes verbatim into JSON and Python repr text: printable
 // ASCII except '"' '\\' '\'' (escaped by json.dumps / repr) and ':' (breaks
 // metaseqId.split(':'), primary_key_generator.py:106)
+// (SWAR, 8 bytes per step: bytes >= 0x80, < 0x20, 0x7F and the four specials)
 template <class CP>
 __device__ __forceinline__ bool plain_allele(CP s, uint32_t n) {
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint8_t c = s[i];
-    if (c < 0x20 || c > 0x7E || c == '"' || c == '\\' || c == '\'' || c == ':') return false;
-  }
-  return true;
+  return swar_find(s, n, [](uint64_t x) {
+           const uint64_t lt20 = ~((x & 0x7F7F7F7F7F7F7F7Full) + 0x6060606060606060ull) & kHiBits;
+           return (x & kHiBits) | lt20 | bytes_eq_mask(x, 0x7F) | bytes_eq_mask(x, '"') |
+                  bytes_eq_mask(x, '\\') | bytes_eq_mask(x, '\'') | bytes_eq_mask(x, ':');
+         }) == n;
 }
 
 template <class CP>
@@ -475,8 +490,8 @@ __device__ __forceinline__ bool bytes_eq(CP a, CP b, uint32_t n) {
 // next separator at or after i in [i, e), or e
 template <class CP>
 __device__ __forceinline__ uint32_t find_byte(CP s, uint32_t i, uint32_t e, uint8_t c) {
-  while (i < e && s[i] != c) ++i;
-  return i;
+  if (i >= e) return i;
+  return i + swar_find(s + i, e - i, [c](uint64_t x) { return bytes_eq_mask(x, c); });
 }
 
 // FREQ value [v0, v1) of the line: is it one the GPU renders?  Every population
@@ -555,8 +570,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   // only visits lines that passed them (line_state == GPU).
   // the reference decodes every line as UTF-8 (load_vcf_file.py:102): ASCII only here
   if constexpr (!WRITE) {
-    for (uint32_t i = 0; i < L.len; ++i)
-      if (s[i] & 0x80) return kLineHost;
+    if (swar_find(s, L.len, [](uint64_t x) { return x & kHiBits; }) != L.len) return kLineHost;
   }
   const uint32_t c = L.chrom;
   const uint32_t ref0 = L.field[3], rl = L.field[4] - 1 - ref0;
@@ -568,8 +582,10 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   const uint32_t i0 = L.field[7], i1 = L.field_end8;
   int64_t fq0 = -1, fq1 = -1;
   if constexpr (!WRITE) {
-    for (uint32_t i = i0; i < i1; ++i)
-      if (s[i] == '#' || s[i] == '\\') return kLineHost;
+    if (i1 > i0 && swar_find(s + i0, i1 - i0, [](uint64_t x) {
+          return bytes_eq_mask(x, '#') | bytes_eq_mask(x, '\\');
+        }) != i1 - i0)
+      return kLineHost;
   }
   for (uint32_t e0 = i0; e0 <= i1;) {
     const uint32_t e1 = find_byte(s, e0, i1, ';');

@@ -19,6 +19,38 @@ typedef const __attribute__((address_space(3))) uint8_t* lds_cp;
 typedef const __attribute__((address_space(3))) uint64_t* lds_cp64;
 typedef const __attribute__((address_space(1))) uint8_t* glb_cp;
 
+typedef const __attribute__((address_space(1))) uint64_t* glb_cp64;
+
+// the 8-byte-word pointer of the same address space as a text pointer
+template <class CP> struct Word64;
+template <> struct Word64<lds_cp> { typedef lds_cp64 T; };
+template <> struct Word64<glb_cp> { typedef glb_cp64 T; };
+
+// SWAR scan of s[0, n) eight bytes at a time (aligned words: an aligned word
+// holding a byte of the text never leaves its LDS window / global page).  F maps a
+// word to a mask with bit 7 set in every flagged byte; returns the index of the
+// first flagged byte, or n.
+template <class CP, class F>
+__device__ __forceinline__ uint32_t swar_find(CP s, uint32_t n, F f) {
+  if (n == 0) return 0;
+  const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(s)) & 7u;
+  const typename Word64<CP>::T w = reinterpret_cast<typename Word64<CP>::T>(s - mis);
+  const uint32_t total = n + mis;
+  uint64_t m = f(w[0]) & (~0ull << (8 * mis));
+  uint32_t base = 0;
+  while (!m) {
+    base += 8;
+    if (base >= total) return n;
+    m = f(w[base >> 3]);
+  }
+  const uint32_t at = base + (uint32_t(__builtin_ctzll(m)) >> 3);
+  return at >= total ? n : at - mis;
+}
+
+__device__ __forceinline__ uint64_t bytes_eq_mask(uint64_t x, uint8_t c) {
+  return zero_bytes_mask(x ^ (0x0101010101010101ull * c));
+}
+
 // 8 bytes at aligned address a (bytes outside [lo,hi) read as 0x00)
 __device__ __forceinline__ uint64_t text_word(uintptr_t a, const Heap& h) { return heap_word(a, h); }
 
