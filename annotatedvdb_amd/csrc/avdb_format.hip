@@ -87,17 +87,22 @@ struct Out {
   };
   struct None {};
   [[no_unique_address]] std::conditional_t<WRITE, Pending, None> pend;
-  __device__ __forceinline__ void put(uint32_t c) {
+  // append t (1..8) bytes, little-endian in x (bytes of x at and above t are 0)
+  __device__ __forceinline__ void append(uint64_t x, uint32_t t) {
     if constexpr (WRITE) {
-      pend.w |= uint64_t(c & 0xFFu) << (8 * pend.k);
-      if (++pend.k == 8) {
-        reinterpret_cast<gw_u64u>(base + p - 7)->v = pend.w;
-        pend.w = 0;
-        pend.k = 0;
+      const uint32_t k = pend.k;  // 0..7
+      pend.w |= x << (8 * k);
+      if (k + t >= 8) {
+        reinterpret_cast<gw_u64u>(base + p - k)->v = pend.w;
+        pend.w = k ? x >> (64 - 8 * k) : 0ull;
+        pend.k = k + t - 8;
+      } else {
+        pend.k = k + t;
       }
     }
-    ++p;
+    p += t;
   }
+  __device__ __forceinline__ void put(uint32_t c) { append(c & 0xFFu, 1); }
   // end of the line: store the buffered tail
   __device__ __forceinline__ void finish() {
     if constexpr (WRITE) {
@@ -106,16 +111,42 @@ struct Out {
       pend.k = 0;
     }
   }
+  // (literal strings: the length and the 8-byte chunks fold at compile time)
   __device__ __forceinline__ void lit(const char* s) {
-    while (*s) put(uint8_t(*s++));
+    uint32_t n = 0;
+    while (s[n]) ++n;
+    for (uint32_t i = 0; i < n; i += 8) {
+      const uint32_t t = n - i < 8u ? n - i : 8u;
+      uint64_t x = 0;
+      for (uint32_t j = 0; j < t; ++j) x |= uint64_t(uint8_t(s[i + j])) << (8 * j);
+      append(x, t);
+    }
   }
   template <class CP>
   __device__ __forceinline__ void bytes(CP s, uint32_t n) {
     if constexpr (!WRITE) {
       p += n;
+    } else if constexpr (std::is_same_v<CP, lds_cp> || std::is_same_v<CP, glb_cp>) {
+      // aligned 8-byte text words, up to 8 bytes per append
+      const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(s)) & 7u;
+      const typename Word64<CP>::T w = reinterpret_cast<typename Word64<CP>::T>(s - mis);
+      for (uint32_t i = 0; i < n;) {
+        const uint32_t q = mis + i, o = q & 7u;
+        const uint32_t t = (8u - o) < (n - i) ? 8u - o : n - i;
+        append((w[q >> 3] >> (8 * o)) & low_bytes_mask(t), t);
+        i += t;
+      }
     } else {
       for (uint32_t k = 0; k < n; ++k) put(s[k]);
     }
+  }
+  // up to 8 decimal digits given as nibbles (most significant lowest) -> ASCII
+  __device__ __forceinline__ void digits8(uint64_t d, uint32_t k) {
+    uint64_t y = d & 0xFFFFFFFFull;
+    y = (y | (y << 16)) & 0x0000FFFF0000FFFFull;
+    y = (y | (y << 8)) & 0x00FF00FF00FF00FFull;
+    y = (y | (y << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    append((y + 0x3030303030303030ull) & low_bytes_mask(k), k);
   }
   __device__ __forceinline__ void u32v(uint32_t v) {
     if constexpr (!WRITE) {
@@ -123,8 +154,13 @@ struct Out {
       return;
     }
     uint32_t k;
-    uint64_t d = dec_nibbles(v, &k);
-    for (; k; --k, d >>= 4) put(uint32_t('0' + (d & 15u)));
+    const uint64_t d = dec_nibbles(v, &k);
+    if (k > 8) {
+      digits8(d, 8);
+      digits8(d >> 32, k - 8);
+    } else {
+      digits8(d, k);
+    }
   }
   __device__ __forceinline__ void u64v(uint64_t v) {
     if (v <= 0xFFFFFFFFull) { u32v(uint32_t(v)); return; }
@@ -144,7 +180,8 @@ struct Out {
     }
     uint64_t d = 0;
     for (int i = 0; i < 9; ++i) { d = (d << 4) | (v % 10u); v /= 10u; }
-    for (int i = 0; i < 9; ++i, d >>= 4) put(uint32_t('0' + (d & 15u)));
+    digits8(d, 8);
+    digits8(d >> 32, 1);
   }
 };
 
