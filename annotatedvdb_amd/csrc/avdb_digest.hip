@@ -76,8 +76,8 @@ constexpr uint32_t nA2 = sizeof(AL2) - 1;
 constexpr uint32_t kAlPrefix = nA0 + AVDB_DIGEST_CHARS + nA1;  // ALT starts here
 static_assert(kAlPrefix == 68, "allele prefix");
 
-constexpr int kLongBuckets = 64;
-constexpr int kCompactGrid = 1024;  // 4 workgroups per CU for the streaming passes
+constexpr int kLongBuckets = 32;  // allele-message block counts (the last bucket takes the rest)
+constexpr int kCompactGrid = 2048;  // 8 workgroups per CU for the streaming passes
 
 __device__ __forceinline__ uint32_t sha_blocks(uint64_t msg_bytes) {
   return uint32_t((msg_bytes + 17 + 127) / 128);
@@ -254,6 +254,53 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t a) {
   return nb < kLongBuckets ? nb : kLongBuckets - 1;
 }
 
+// f(i, ref_len, alt_len) for every record of this workgroup's contiguous chunk;
+// 4 records per lane per step through 16-byte loads when VEC (the chunk size is
+// a multiple of 4, so the loads are aligned when the arrays are)
+template <bool VEC, class F>
+__device__ __forceinline__ void for_chunk_records(const uint32_t* __restrict__ rl,
+                                                  const uint32_t* __restrict__ al, size_t n, F f) {
+  const size_t per = (((n + gridDim.x - 1) / gridDim.x) + 3) & ~size_t(3);
+  const size_t i0 = size_t(blockIdx.x) * per;
+  const size_t i1 = i0 + per < n ? i0 + per : n;
+  if constexpr (VEC) {
+    // two groups per lane per step, both loaded before either is used
+    const size_t step = 4 * size_t(blockDim.x);
+    for (size_t j = i0 + 4 * size_t(threadIdx.x); j < i1; j += 2 * step) {
+      const size_t j2 = j + step;
+      u32x4 r0{}, a0{}, r1{}, a1{};
+      const bool full0 = j + 4 <= i1, full1 = j2 + 4 <= i1;
+      if (full0) {
+        r0 = *reinterpret_cast<const u32x4*>(rl + j);
+        a0 = *reinterpret_cast<const u32x4*>(al + j);
+      }
+      if (full1) {
+        r1 = *reinterpret_cast<const u32x4*>(rl + j2);
+        a1 = *reinterpret_cast<const u32x4*>(al + j2);
+      }
+      if (full0) {
+        f(j, r0.x, a0.x);
+        f(j + 1, r0.y, a0.y);
+        f(j + 2, r0.z, a0.z);
+        f(j + 3, r0.w, a0.w);
+      } else {
+        for (size_t k = j; k < i1; ++k) f(k, rl[k], al[k]);
+      }
+      if (full1) {
+        f(j2, r1.x, a1.x);
+        f(j2 + 1, r1.y, a1.y);
+        f(j2 + 2, r1.z, a1.z);
+        f(j2 + 3, r1.w, a1.w);
+      } else {
+        for (size_t k = j2; k < i1; ++k) f(k, rl[k], al[k]);
+      }
+    }
+  } else {
+    for (size_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) f(i, rl[i], al[i]);
+  }
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_long_hist(const uint32_t* __restrict__ rl,
                                                       const uint32_t* __restrict__ al, size_t n,
                                                       uint32_t max_len, uint8_t* __restrict__ is_long,
@@ -261,50 +308,83 @@ __global__ __launch_bounds__(kBlock) void k_long_hist(const uint32_t* __restrict
   __shared__ uint32_t s_cnt[kLongBuckets];
   if (threadIdx.x < kLongBuckets) s_cnt[threadIdx.x] = 0;
   __syncthreads();
-  const size_t per = (n + gridDim.x - 1) / gridDim.x;
-  const size_t i0 = size_t(blockIdx.x) * per;
-  const size_t i1 = i0 + per < n ? i0 + per : n;
-  for (size_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const uint32_t a = al[i];
-    const bool lg = is_long_rec(rl[i], a, max_len);
-    if (is_long) is_long[i] = lg;
+  // (VEC: the four is_long bytes of a group leave as one 32-bit store)
+  uint32_t flags = 0;
+  for_chunk_records<VEC>(rl, al, n, [&](size_t i, uint32_t r, uint32_t a) {
+    const bool lg = is_long_rec(r, a, max_len);
+    if (VEC && is_long) {
+      flags |= uint32_t(lg) << (8 * (i & 3));
+      if ((i & 3) == 3) {
+        *reinterpret_cast<uint32_t*>(is_long + (i - 3)) = flags;
+        flags = 0;
+      }
+    } else if (is_long) {
+      is_long[i] = lg;
+    }
     if (lg) atomicAdd(&s_cnt[bucket_of(a)], 1u);
+  });
+  if (VEC && is_long) {  // a chunk ending inside a group (n % 4 != 0): its lane stores the rest
+    const size_t per = (((n + gridDim.x - 1) / gridDim.x) + 3) & ~size_t(3);
+    const size_t i0 = size_t(blockIdx.x) * per;
+    const size_t i1 = i0 + per < n ? i0 + per : n;
+    const size_t jt = i1 & ~size_t(3);
+    if ((i1 & 3) && jt >= i0 && ((jt - i0) / 4) % blockDim.x == threadIdx.x)
+      for (size_t k = jt; k < i1; ++k) is_long[k] = uint8_t(flags >> (8 * (k & 3)));
   }
   __syncthreads();
   if (threadIdx.x < kLongBuckets) counts[threadIdx.x * gridDim.x + blockIdx.x] = s_cnt[threadIdx.x];
 }
 
-// exclusive scan of m = kLongBuckets * G counts by one 1024-thread workgroup
-__global__ __launch_bounds__(1024) void k_long_scan(uint32_t* __restrict__ counts, uint32_t m,
-                                                    unsigned int* __restrict__ total) {
-  __shared__ uint32_t s_part[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = (m + 1023) / 1024;
-  uint32_t sum = 0;
-  for (uint32_t k = 0; k < per; ++k) {
-    const uint32_t idx = t * per + k;
-    if (idx < m) sum += counts[idx];
+// exclusive scan of the kLongBuckets * kCompactGrid counts by one 1024-thread
+// workgroup: wave w owns a contiguous 1/16 of the array and reads it coalesced
+// (lane l takes 16-byte word l of every 256-count step), all loads issued first
+constexpr uint32_t kScanN = kLongBuckets * kCompactGrid;
+constexpr uint32_t kScanSteps = kScanN / 16 / 256;
+static_assert(kScanN % (16 * 256) == 0, "k_long_scan layout");
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t u = __shfl_up(v, d, kWave);
+    if (lane >= d) v += u;
   }
-  s_part[t] = sum;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-    const uint32_t v = t >= d ? s_part[t - d] : 0u;
-    __syncthreads();
-    s_part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = s_part[t] - sum;  // exclusive prefix of this thread's slice
-  for (uint32_t k = 0; k < per; ++k) {
-    const uint32_t idx = t * per + k;
-    if (idx < m) {
-      const uint32_t c = counts[idx];
-      counts[idx] = run;
-      run += c;
-    }
-  }
-  if (t == 1023) *total = s_part[1023];
+  return v;
 }
 
+__global__ __launch_bounds__(1024) void k_long_scan(uint32_t* __restrict__ counts,
+                                                    unsigned int* __restrict__ total) {
+  __shared__ uint32_t s_wave[16];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  u32x4* seg = reinterpret_cast<u32x4*>(counts + size_t(wv) * (kScanN / 16));
+  u32x4 v[kScanSteps];
+#pragma unroll
+  for (uint32_t k = 0; k < kScanSteps; ++k) v[k] = seg[k * 64 + lane];
+  uint32_t tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanSteps; ++k) tot += v[k].x + v[k].y + v[k].z + v[k].w;
+  const uint32_t wsum = __shfl(wave_incl_scan(tot), 63, kWave);
+  if (lane == 0) s_wave[wv] = wsum;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t w = 0; w < wv; ++w) base += s_wave[w];
+#pragma unroll
+  for (uint32_t k = 0; k < kScanSteps; ++k) {
+    const uint32_t ls = v[k].x + v[k].y + v[k].z + v[k].w;
+    const uint32_t incl = wave_incl_scan(ls);
+    uint32_t run = base + incl - ls;
+    u32x4 o;
+    o.x = run; run += v[k].x;
+    o.y = run; run += v[k].y;
+    o.z = run; run += v[k].z;
+    o.w = run;
+    seg[k * 64 + lane] = o;
+    base += __shfl(incl, 63, kWave);
+  }
+  if (threadIdx.x == 1023) *total = base;
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_long_scatter(const uint32_t* __restrict__ rl,
                                                          const uint32_t* __restrict__ al, size_t n,
                                                          uint32_t max_len,
@@ -313,13 +393,9 @@ __global__ __launch_bounds__(kBlock) void k_long_scatter(const uint32_t* __restr
   __shared__ uint32_t s_cur[kLongBuckets];
   if (threadIdx.x < kLongBuckets) s_cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
   __syncthreads();
-  const size_t per = (n + gridDim.x - 1) / gridDim.x;
-  const size_t i0 = size_t(blockIdx.x) * per;
-  const size_t i1 = i0 + per < n ? i0 + per : n;
-  for (size_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const uint32_t a = al[i];
-    if (is_long_rec(rl[i], a, max_len)) list[atomicAdd(&s_cur[bucket_of(a)], 1u)] = uint32_t(i);
-  }
+  for_chunk_records<VEC>(rl, al, n, [&](size_t i, uint32_t r, uint32_t a) {
+    if (is_long_rec(r, a, max_len)) list[atomicAdd(&s_cur[bucket_of(a)], 1u)] = uint32_t(i);
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -479,19 +555,32 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
     avdb_set_error("avdb_vrs_digest: workspace of %zu bytes required", need);
     return AVDB_ERANGE;
   }
+  if (reinterpret_cast<uintptr_t>(workspace) % 16) {
+    avdb_set_error("avdb_vrs_digest: workspace must be 16-byte aligned");
+    return AVDB_EINVAL;
+  }
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   auto* total = static_cast<unsigned int*>(workspace);
   auto* counts = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + 256);
   auto* list = counts + size_t(kLongBuckets) * kCompactGrid;
-  hipLaunchKernelGGL(k_long_hist, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
-                     max_seq_len, is_long, counts);
+  const bool vec = (reinterpret_cast<uintptr_t>(ref_len) | reinterpret_cast<uintptr_t>(alt_len)) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(is_long) % 4 == 0;
+  if (vec)
+    hipLaunchKernelGGL(k_long_hist<true>, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
+                       max_seq_len, is_long, counts);
+  else
+    hipLaunchKernelGGL(k_long_hist<false>, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
+                       max_seq_len, is_long, counts);
   AVDB_LAUNCH_CHECK("k_long_hist");
-  hipLaunchKernelGGL(k_long_scan, dim3(1), dim3(1024), 0, s, counts,
-                     uint32_t(kLongBuckets * kCompactGrid), total);
+  hipLaunchKernelGGL(k_long_scan, dim3(1), dim3(1024), 0, s, counts, total);
   AVDB_LAUNCH_CHECK("k_long_scan");
-  hipLaunchKernelGGL(k_long_scatter, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
-                     max_seq_len, counts, list);
+  if (vec)
+    hipLaunchKernelGGL(k_long_scatter<true>, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
+                       max_seq_len, counts, list);
+  else
+    hipLaunchKernelGGL(k_long_scatter<false>, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
+                       max_seq_len, counts, list);
   AVDB_LAUNCH_CHECK("k_long_scatter");
   // persistent grid over the grouped list
   hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * kDigestWavesPerSimd), dim3(kBlock), 0, s, chrom, pos,

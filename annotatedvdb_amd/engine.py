@@ -334,12 +334,13 @@ class Engine:
     # -- K4 ----------------------------------------------------------------
     def vrs_digest(self, b: RecordBatch, max_seq_len: int = 50,
                    workspace: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Returns ``(digests uint8[n,32], is_long uint8[n])``; rows that are not
-        long are left zero."""
+        """Returns ``(digests uint8[n,32], is_long uint8[n])``.  Only the rows
+        with ``is_long`` set are written (the rest are unspecified: zero-filling
+        32 bytes per record would cost more HBM traffic than the digests)."""
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
-        dig = torch.zeros((n, N.DIGEST_CHARS), dtype=torch.uint8, device=self.device)
+        dig = torch.empty((n, N.DIGEST_CHARS), dtype=torch.uint8, device=self.device)
         is_long = self.empty(n, torch.uint8)
         sz = ctypes.c_size_t()
         self.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))

@@ -153,7 +153,7 @@ int avdb_sha512t24u(avdb_ctx* ctx, const uint8_t* data, const uint64_t* off, con
  * digest of interval (pos-1, pos-1+ref_len] and literal state ALT, written to
  * digest_out[i*32..] (other rows untouched); is_long[i] set 0/1 if non-NULL.
  * Long rows are compacted into `workspace` (avdb_vrs_digest_workspace_size()
- * bytes, device) first.  PARITY UNPINNED. */
+ * bytes, device, 16-byte aligned) first.  PARITY UNPINNED. */
 int avdb_vrs_digest_workspace_size(size_t n, size_t* bytes);
 int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                     const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,

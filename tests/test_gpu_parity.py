@@ -282,6 +282,19 @@ def test_k4_vrs_digest_vs_oracle_serialisation(engine):
         assert raw[i].tobytes().decode() == exp
 
 
+def test_k4_is_long_ragged_batch(engine):
+    """is_long / digests for batch sizes that end inside a 4-record group (the
+    compaction kernels' 16-byte-load path stores is_long 4 bytes at a time)."""
+    from annotatedvdb_amd import synth
+    digs = ["%032d" % i for i in range(25)]
+    eng2 = type(engine)(0, sequence_digests=digs)
+    for n in (1, 3, 4097, 20003):
+        b = synth.alleles(n, seed=45 + n, long_frac=0.3)
+        d, is_long = eng2.vrs_digest(b, 50)
+        r, a = b.ref_len.cpu().numpy().astype(np.int64), b.alt_len.cpu().numpy()
+        assert np.array_equal(is_long.cpu().numpy(), (r + a > 50).astype(np.uint8)), n
+
+
 @pytest.mark.slow
 def test_c5_full_size_vs_c_oracle(engine):
     """BASELINE config 5 at full per-GPU size (2.5e7 ADSP-style records): K2 end /
