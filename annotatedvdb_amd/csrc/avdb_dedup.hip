@@ -47,6 +47,74 @@ __device__ __forceinline__ bool wave_heap_equal(const Heap& h, uint64_t p, uint6
   return true;
 }
 
+// Keep bit of record i: the nearest earlier record of its (chrom,pos) run with
+// the same lengths and external id is compared; short candidates in-lane, long
+// ones queued for the whole wave.  Earlier run members are scanned in order, so
+// the first equal one decides (keep-first).  scan == false (record i-1 is known
+// to be outside the run) skips the scan.  Every lane of the wave must call it
+// together (ballots).
+__device__ __forceinline__ uint8_t dedup_record(const Heap& h, const uint8_t* __restrict__ chrom,
+                                                const uint32_t* __restrict__ pos,
+                                                const uint64_t* __restrict__ off,
+                                                const uint32_t* __restrict__ rl,
+                                                const uint32_t* __restrict__ al,
+                                                const uint64_t* __restrict__ ext, size_t i, bool live,
+                                                bool scan) {
+  uint8_t k = 1;
+  size_t j = i;
+  uint32_t L = 0;
+  bool pending = false;
+  if (live && scan) {
+    const uint8_t c = chrom[i];
+    const uint32_t p = pos[i];
+    const uint32_t r = rl[i], a = al[i];
+    const uint64_t e = ext ? ext[i] : 0;
+    L = r + a;
+    while (j-- > 0) {
+      if (chrom[j] != c || pos[j] != p) break;
+      if (rl[j] != r || al[j] != a || (ext && ext[j] != e)) continue;
+      if (L > kCoopBytes) { pending = true; break; }
+      if (heap_equal(h, off[i], off[j], L)) { k = 0; break; }
+    }
+  }
+  // long candidates: one cooperative compare per queued lane; a mismatch sends
+  // that lane on to its next candidate (rare: equal lengths at one position)
+  uint64_t q = __ballot(pending);
+  while (q) {
+    const int l = __ffsll((unsigned long long)q) - 1;
+    const uint64_t pi = __shfl(live ? off[i] : 0ull, l, kWave);
+    const uint64_t pj = __shfl(pending ? off[j] : 0ull, l, kWave);
+    const uint32_t Ll = __shfl(L, l, kWave);
+    const bool eq = wave_heap_equal(h, pi, pj, Ll);
+    if (__lane_id() == l) {
+      if (eq) {
+        k = 0;
+        pending = false;
+      } else {  // continue this lane's scan past j
+        pending = false;
+        const uint8_t c = chrom[i];
+        const uint32_t p = pos[i];
+        const uint32_t r = rl[i], a = al[i];
+        const uint64_t e = ext ? ext[i] : 0;
+        while (j-- > 0) {
+          if (chrom[j] != c || pos[j] != p) break;
+          if (rl[j] != r || al[j] != a || (ext && ext[j] != e)) continue;
+          pending = true;
+          break;
+        }
+      }
+    }
+    q = __ballot(pending);
+  }
+  return k;
+}
+
+__device__ __forceinline__ void count_dups(uint32_t dups, unsigned long long* g_ctr) {
+  if (!g_ctr) return;
+  for (int d = 32; d > 0; d >>= 1) dups += __shfl_down(dups, d, kWave);
+  if (__lane_id() == 0 && dups) atomicAdd(&g_ctr[AVDB_CTR_DUPLICATES], (unsigned long long)dups);
+}
+
 __global__ __launch_bounds__(kBlock) void k_dedup_grouped(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
@@ -60,65 +128,114 @@ __global__ __launch_bounds__(kBlock) void k_dedup_grouped(
   for (size_t base = size_t(blockIdx.x) * blockDim.x; base < n; base += stride) {
     const size_t i = base + threadIdx.x;
     const bool live = i < n;
-    uint8_t k = 1;
-    // candidate: the nearest earlier record of this (chrom,pos) run with the same
-    // lengths and external id; short candidates are compared in-lane, long ones
-    // are queued for the whole wave.  Earlier run members are scanned in order,
-    // so the first equal one decides (keep-first).
-    size_t j = i;
-    uint32_t L = 0;
-    bool pending = false;
-    if (live) {
-      const uint8_t c = chrom[i];
-      const uint32_t p = pos[i];
-      const uint32_t r = rl[i], a = al[i];
-      const uint64_t e = ext ? ext[i] : 0;
-      L = r + a;
-      while (j-- > 0) {
-        if (chrom[j] != c || pos[j] != p) break;
-        if (rl[j] != r || al[j] != a || (ext && ext[j] != e)) continue;
-        if (L > kCoopBytes) { pending = true; break; }
-        if (heap_equal(h, off[i], off[j], L)) { k = 0; break; }
-      }
-    }
-    // long candidates: one cooperative compare per queued lane; a mismatch sends
-    // that lane on to its next candidate (rare: equal lengths at one position)
-    uint64_t q = __ballot(pending);
-    while (q) {
-      const int l = __ffsll((unsigned long long)q) - 1;
-      const uint64_t pi = __shfl(live ? off[i] : 0ull, l, kWave);
-      const uint64_t pj = __shfl(pending ? off[j] : 0ull, l, kWave);
-      const uint32_t Ll = __shfl(L, l, kWave);
-      const bool eq = wave_heap_equal(h, pi, pj, Ll);
-      if (__lane_id() == l) {
-        if (eq) {
-          k = 0;
-          pending = false;
-        } else {  // continue this lane's scan past j
-          pending = false;
-          const uint8_t c = chrom[i];
-          const uint32_t p = pos[i];
-          const uint32_t r = rl[i], a = al[i];
-          const uint64_t e = ext ? ext[i] : 0;
-          while (j-- > 0) {
-            if (chrom[j] != c || pos[j] != p) break;
-            if (rl[j] != r || al[j] != a || (ext && ext[j] != e)) continue;
-            pending = true;
-            break;
-          }
-        }
-      }
-      q = __ballot(pending);
-    }
+    const uint8_t k = dedup_record(h, chrom, pos, off, rl, al, ext, i, live, true);
     if (live) {
       keep[i] = k;
       dups += 1u - k;
     }
   }
-  if (g_ctr) {
-    for (int d = 32; d > 0; d >>= 1) dups += __shfl_down(dups, d, kWave);
-    if (__lane_id() == 0 && dups) atomicAdd(&g_ctr[AVDB_CTR_DUPLICATES], (unsigned long long)dups);
+  count_dups(dups, g_ctr);
+}
+
+// Vector form (aligned arrays): 4 consecutive records per lane from 16-byte
+// loads.  A record whose predecessor (same lane, the previous lane via a
+// shuffle, or one load for lane 0) has another (chrom,pos) is kept without
+// touching memory again — the common case; the rest go through dedup_record.
+__global__ __launch_bounds__(kBlock) void k_dedup_grouped4(
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
+    const uint64_t* __restrict__ ext, size_t n, uint8_t* __restrict__ keep,
+    unsigned long long* __restrict__ g_ctr) {
+  const Heap h = make_heap(heap, heap_bytes);
+  const size_t ngroups = (n + 3) / 4;
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  uint32_t dups = 0;
+  for (size_t base = size_t(blockIdx.x) * blockDim.x; base < ngroups; base += stride) {
+    const size_t g = base + threadIdx.x;
+    const size_t i0 = 4 * g;
+    const bool full = i0 + 4 <= n;
+    uint32_t c4 = 0;
+    u32x4 p4{};
+    if (full) {
+      c4 = *reinterpret_cast<const uint32_t*>(chrom + i0);
+      p4 = *reinterpret_cast<const u32x4*>(pos + i0);
+    } else if (i0 < n) {
+      for (uint32_t t = 0; t < 4 && i0 + t < n; ++t) {
+        c4 |= uint32_t(chrom[i0 + t]) << (8 * t);
+        p4[t] = pos[i0 + t];
+      }
+    }
+    // predecessor of record i0: the previous lane's last record, or a load
+    uint32_t pc = __shfl_up(c4 >> 24, 1, kWave), pp = __shfl_up(p4.w, 1, kWave);
+    if (__lane_id() == 0 && i0 > 0 && i0 - 1 < n) {
+      pc = chrom[i0 - 1];
+      pp = pos[i0 - 1];
+    }
+    bool same[4];
+    same[0] = i0 > 0 && (c4 & 0xFFu) == pc && p4.x == pp;
+    same[1] = ((c4 >> 8) & 0xFFu) == (c4 & 0xFFu) && p4.y == p4.x;
+    same[2] = ((c4 >> 16) & 0xFFu) == ((c4 >> 8) & 0xFFu) && p4.z == p4.y;
+    same[3] = (c4 >> 24) == ((c4 >> 16) & 0xFFu) && p4.w == p4.z;
+    uint32_t k4 = 0x01010101u;
+    const bool any = i0 < n && (same[0] || same[1] || same[2] || same[3]);
+    if (__ballot(any)) {
+      // The usual case: the record equals its immediate predecessor.  All four
+      // records' lengths / ids / offsets (and the predecessor's) are loaded at
+      // once and the short byte compares issued together; a record the
+      // predecessor does not settle goes through dedup_record below.
+      uint32_t r[5] = {0, 0, 0, 0, 0}, a[5] = {0, 0, 0, 0, 0};
+      uint64_t e[5] = {0, 0, 0, 0, 0}, o[5] = {0, 0, 0, 0, 0};
+      if (any) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const size_t i = i0 + t < n ? i0 + t : n - 1;
+          r[t + 1] = rl[i];
+          a[t + 1] = al[i];
+          e[t + 1] = ext ? ext[i] : 0;
+          o[t + 1] = off[i];
+        }
+        if (same[0]) {
+          r[0] = rl[i0 - 1];
+          a[0] = al[i0 - 1];
+          e[0] = ext ? ext[i0 - 1] : 0;
+          o[0] = off[i0 - 1];
+        }
+      }
+      uint32_t unresolved = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (!(any && same[t] && i0 + t < n)) continue;
+        const uint32_t L = r[t + 1] + a[t + 1];
+        if (r[t + 1] == r[t] && a[t + 1] == a[t] && e[t + 1] == e[t] && L <= kCoopBytes &&
+            heap_equal(h, o[t + 1], o[t], L))
+          k4 &= ~(1u << (8 * t));
+        else
+          unresolved |= 1u << t;
+      }
+      if (__ballot(unresolved != 0)) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const size_t i = i0 + t;
+          const bool live = i < n;
+          const uint8_t k =
+              dedup_record(h, chrom, pos, off, rl, al, ext, i, live, live && ((unresolved >> t) & 1u));
+          if (!k) k4 &= ~(1u << (8 * t));
+        }
+      }
+    }
+    if (full) {
+      *reinterpret_cast<uint32_t*>(keep + i0) = k4;
+      dups += 4u - __popc(k4);
+    } else {
+      for (uint32_t t = 0; t < 4 && i0 + t < n; ++t) {
+        const uint8_t k = uint8_t((k4 >> (8 * t)) & 1u);
+        keep[i0 + t] = k;
+        dups += 1u - k;
+      }
+    }
   }
+  count_dups(dups, g_ctr);
 }
 
 // 64-bit fingerprint of (chrom, pos, ext, ref_len, alt_len, bytes)
@@ -238,9 +355,18 @@ extern "C" int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t
   auto* ctr = reinterpret_cast<unsigned long long*>(counters);
   const unsigned grid = stream_grid(n, kBlock * 4, 4096);
   if (grouped) {
-    hipLaunchKernelGGL(k_dedup_grouped, dim3(grid), dim3(kBlock), 0, s, chrom, pos, allele_off,
-                       ref_len, alt_len, heap, heap_bytes, ext_id, n, keep, ctr);
-    AVDB_LAUNCH_CHECK("k_dedup_grouped");
+    const bool vec = (reinterpret_cast<uintptr_t>(chrom) | reinterpret_cast<uintptr_t>(keep)) % 4 == 0 &&
+                     reinterpret_cast<uintptr_t>(pos) % 16 == 0;
+    if (vec) {
+      const unsigned grid4 = stream_grid((n + 3) / 4, kBlock * 2, 4096);
+      hipLaunchKernelGGL(k_dedup_grouped4, dim3(grid4), dim3(kBlock), 0, s, chrom, pos, allele_off,
+                         ref_len, alt_len, heap, heap_bytes, ext_id, n, keep, ctr);
+      AVDB_LAUNCH_CHECK("k_dedup_grouped4");
+    } else {
+      hipLaunchKernelGGL(k_dedup_grouped, dim3(grid), dim3(kBlock), 0, s, chrom, pos, allele_off,
+                         ref_len, alt_len, heap, heap_bytes, ext_id, n, keep, ctr);
+      AVDB_LAUNCH_CHECK("k_dedup_grouped");
+    }
     return AVDB_OK;
   }
   size_t need = 0;

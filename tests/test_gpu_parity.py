@@ -226,6 +226,28 @@ def test_k3_dedup_grouped_and_hash(engine):
     assert int(ctr[21]) == ndup and int(ctr[22]) == 0
 
 
+def test_k3_dedup_ragged_long_and_unaligned(engine):
+    """Grouped dedup at sizes ending inside a 4-record group, with long duplicate
+    alleles (wave-cooperative compares) and dense duplicate runs crossing lane,
+    wave and workgroup boundaries; then the same records through unaligned array
+    views (the one-record-per-lane kernel)."""
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.engine import RecordBatch
+    for n in (1, 2, 5, 255, 257, 1031, 70001):
+        b = synth.alleles(n, seed=60 + n, long_frac=0.3, dup_frac=0.3)
+        exp, ndup = _oracle_keep(b)
+        ctr = engine.new_counters()
+        keep = engine.pk_dedup(b, grouped=True, counters=ctr)
+        assert np.array_equal(keep.cpu().numpy(), exp), n
+        assert int(ctr[21]) == ndup
+    # views starting one record in: pos / chrom / keep lose their 16- and 4-byte alignment
+    b = synth.alleles(20001, seed=71, long_frac=0.3, dup_frac=0.3)
+    v = RecordBatch(**{f: (getattr(b, f)[1:] if f != "heap" else b.heap)
+                       for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap", "ext_id")})
+    exp, _ = _oracle_keep(v)
+    assert np.array_equal(engine.pk_dedup(v, grouped=True).cpu().numpy(), exp)
+
+
 def test_k3_dedup_small_cases(engine):
     from annotatedvdb_amd.engine import pack_records
     recs = [(0, 5, "A", "G", 0), (0, 5, "A", "T", 0), (0, 5, "A", "G", 0), (0, 5, "A", "G", 7),
