@@ -183,10 +183,6 @@ __device__ __forceinline__ uint32_t ndigits(uint32_t v) {
   return d;
 }
 
-__device__ __forceinline__ uint8_t digit_at(uint32_t v, uint32_t d, uint32_t k) {  // k-th of d digits
-  for (uint32_t i = k + 1; i < d; ++i) v /= 10u;
-  return uint8_t('0' + v % 10u);
-}
 
 __device__ __forceinline__ void store_digest(char* o, const uint64_t* cw) {
   if ((reinterpret_cast<uintptr_t>(o) & 7) == 0) {
@@ -401,25 +397,166 @@ __global__ __launch_bounds__(kBlock) void k_long_scatter(const uint32_t* __restr
 // ---------------------------------------------------------------------------
 // VRS Allele digest per long record
 // ---------------------------------------------------------------------------
-struct LocMsg {
-  uint32_t E, S, dE, dS, T;
-  const char* dig;  // 32 refget chars of the contig
+// Message words of one 128-byte block, produced by appending <= 8 bytes at a
+// time (little-endian in a 64-bit accumulator); the words of block `blk` go to
+// this lane's LDS slot as the big-endian values SHA-512 consumes.
+struct MsgSink {
+  uint64_t* slot;  // [word][lane]
+  uint32_t jlo;    // first word of the block being built
+  uint32_t j = 0;  // index of the word being filled
+  uint32_t k = 0;  // bytes pending in w
+  uint64_t w = 0;
+  __device__ __forceinline__ MsgSink(uint64_t* sl, uint32_t blk) : slot(sl), jlo(16 * blk) {}
+  __device__ __forceinline__ void word(uint64_t v) {  // v: the big-endian word value
+    if (j - jlo < 16u) slot[(j - jlo) * kBlock] = v;
+    ++j;
+  }
+  __device__ __forceinline__ void append(uint64_t x, uint32_t t) {  // 1 <= t <= 8
+    w |= x << (8 * k);
+    if (k + t >= 8) {
+      word(__builtin_bswap64(w));
+      w = k ? x >> (64 - 8 * k) : 0ull;
+      k = k + t - 8;
+    } else {
+      k += t;
+    }
+  }
+  // (string literals: the length and the chunks fold at compile time)
+  __device__ __forceinline__ void lit(const char* s) {
+    uint32_t n = 0;
+    while (s[n]) ++n;
+    for (uint32_t i = 0; i < n; i += 8) {
+      const uint32_t t = n - i < 8u ? n - i : 8u;
+      uint64_t x = 0;
+      for (uint32_t q = 0; q < t; ++q) x |= uint64_t(uint8_t(s[i + q])) << (8 * q);
+      append(x, t);
+    }
+  }
+  __device__ __forceinline__ void digits(uint32_t v) {  // decimal, no leading zeros
+    uint64_t d = 0;
+    uint32_t nd = 0;
+    do { d = (d << 4) | (v % 10u); v /= 10u; ++nd; } while (v);
+    for (uint32_t h = 0; h < nd; h += 8, d >>= 32) {  // nibbles -> ASCII bytes
+      uint64_t y = d & 0xFFFFFFFFull;
+      y = (y | (y << 16)) & 0x0000FFFF0000FFFFull;
+      y = (y | (y << 8)) & 0x00FF00FF00FF00FFull;
+      y = (y | (y << 4)) & 0x0F0F0F0F0F0F0F0Full;
+      const uint32_t t = nd - h < 8u ? nd - h : 8u;
+      append((y + 0x3030303030303030ull) & low_bytes_mask(t), t);
+    }
+  }
+  // SHA padding for a T-byte message of nb blocks: 0x80, zeros, 128-bit length
+  __device__ __forceinline__ void finish(uint64_t T, uint32_t nb) {
+    append(0x80, 1);
+    if (k) {
+      word(__builtin_bswap64(w));
+      w = 0;
+      k = 0;
+    }
+    const uint32_t last = nb * 16 - 1;
+    while (j < last - 1) word(0);
+    word(0);
+    word(T * 8);
+  }
 };
 
-__device__ __forceinline__ uint8_t loc_byte(const LocMsg& m, uint32_t p) {
-  if (p < nL0) return uint8_t(kLoc0[p]);
-  p -= nL0;
-  if (p < m.dE) return digit_at(m.E, m.dE, p);
-  p -= m.dE;
-  if (p < nL1) return uint8_t(kLoc1[p]);
-  p -= nL1;
-  if (p < m.dS) return digit_at(m.S, m.dS, p);
-  p -= m.dS;
-  if (p < nL2) return uint8_t(kLoc2[p]);
-  p -= nL2;
-  if (p < AVDB_DIGEST_CHARS) return uint8_t(m.dig[p]);
-  p -= AVDB_DIGEST_CHARS;
-  return uint8_t(kLoc3[p]);
+// the VRS SequenceLocation serialisation of interval (S, E] on a contig whose 32
+// refget chars are dig (4 little-endian words), block `blk` of its 2
+__device__ __forceinline__ void location_block(uint64_t* slot, uint32_t blk, uint32_t S, uint32_t E,
+                                               const uint64_t* dig, uint64_t T) {
+  MsgSink m(slot, blk);
+  m.lit(LOC0);
+  m.digits(E);
+  m.lit(LOC1);
+  m.digits(S);
+  m.lit(LOC2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) m.append(dig[q], 8);
+  m.lit(LOC3);
+  m.finish(T, sha_blocks(T));
+}
+
+// compile-time little-endian 8-byte chunk of a string literal (zero past its end)
+template <size_t N>
+__device__ __forceinline__ uint64_t lit_word(const char (&s)[N], int at) {
+  uint64_t x = 0;
+  for (int q = 0; q < 8; ++q)
+    if (at + q >= 0 && at + q < int(N) - 1) x |= uint64_t(uint8_t(s[at + q])) << (8 * q);
+  return x;
+}
+
+// prefix bytes [8K, 8K+8) of the Allele message (those below kAlPrefix), little-endian
+template <int K>
+__device__ __forceinline__ uint64_t prefix_word(const uint64_t* locw) {
+  constexpr int p = 8 * K, c_lo = int(nA0), c_hi = int(nA0) + AVDB_DIGEST_CHARS;
+  uint64_t le = lit_word(AL0, p) | lit_word(AL1, p - c_hi);
+  constexpr int c0 = p > c_lo ? p : c_lo, c1 = p + 8 < c_hi ? p + 8 : c_hi;
+  if constexpr (c0 < c1) {
+    constexpr int ci = c0 - c_lo, wi = ci >> 3, bo = ci & 7;
+    uint64_t x = locw[wi] >> (8 * bo);
+    if constexpr (bo != 0 && wi + 1 < 4) x |= locw[wi + 1] << (64 - 8 * bo);
+    le |= (x & low_bytes_mask(uint32_t(c1 - c0))) << (8 * (c0 - p));
+  }
+  if constexpr (p + 8 > int(kAlPrefix)) le &= low_bytes_mask(uint32_t(int(kAlPrefix) - p));
+  return le;
+}
+
+// The Allele serialisation AL0 + <32 location chars> + AL1 + ALT + AL2: message
+// word jw (0-based, big-endian value) of a TA-byte message in nb blocks.
+// Prefix words (0..8) come from the literals and the location chars, ALT words
+// from one 8-byte heap load, the suffix from AL2 + 0x80 as literal chunks.
+__device__ __forceinline__ uint64_t allele_word(uint32_t jw, const uint64_t* locw, const Heap& hp,
+                                                uint64_t altoff, uint32_t a, uint64_t TA, uint32_t nb) {
+  const uint32_t last = nb * 16 - 1;
+  if (jw == last) return TA * 8;
+  if (jw == last - 1) return 0;
+  const uint64_t p = uint64_t(jw) * 8;       // first message byte of the word
+  const uint64_t Q = uint64_t(kAlPrefix) + a;  // first suffix byte
+  uint64_t le = 0;
+  // prefix: AL0 | 32 location chars | AL1 (68 bytes, words 0..8)
+  if (p < kAlPrefix) {
+    switch (jw) {
+      case 0: le = prefix_word<0>(locw); break;
+      case 1: le = prefix_word<1>(locw); break;
+      case 2: le = prefix_word<2>(locw); break;
+      case 3: le = prefix_word<3>(locw); break;
+      case 4: le = prefix_word<4>(locw); break;
+      case 5: le = prefix_word<5>(locw); break;
+      case 6: le = prefix_word<6>(locw); break;
+      case 7: le = prefix_word<7>(locw); break;
+      default: le = prefix_word<8>(locw); break;
+    }
+  }
+  // ALT bytes [max(p, 68), min(p + 8, Q))
+  const uint64_t q0 = p > kAlPrefix ? p : uint64_t(kAlPrefix);
+  const uint64_t q1 = p + 8 < Q ? p + 8 : Q;
+  if (q0 < q1) {
+    const uint32_t sh = uint32_t(q0 - p), nbytes = uint32_t(q1 - q0);
+    le |= (heap_u64(hp, altoff + (q0 - kAlPrefix)) & low_bytes_mask(nbytes)) << (8 * sh);
+  }
+  // suffix AL2 + 0x80 (then zeros) from byte Q on
+  if (p + 8 > Q) {
+    const uint64_t s0 = p > Q ? p : Q;
+    const uint32_t sh = uint32_t(s0 - p);
+    const uint64_t d = s0 - Q;  // suffix offset of byte s0
+    uint64_t x = 0;
+    if (d < uint64_t(nA2) + 1) {
+      constexpr int kSufWords = (nA2 + 1 + 7) / 8;
+      // 8 suffix bytes from offset d (AL2 then 0x80), assembled from literal chunks
+      const uint32_t wi = uint32_t(d) >> 3, bo = uint32_t(d) & 7u;
+      uint64_t lo = 0, hi = 0;
+#pragma unroll
+      for (int q = 0; q <= kSufWords; ++q) {
+        const uint64_t c = lit_word(AL2, 8 * q) |
+                           ((nA2 >= 8 * q && nA2 < 8 * q + 8) ? uint64_t(0x80) << (8 * (nA2 - 8 * q)) : 0ull);
+        if (uint32_t(q) == wi) lo = c;
+        if (uint32_t(q) == wi + 1) hi = c;
+      }
+      x = bo ? (lo >> (8 * bo)) | (hi << (64 - 8 * bo)) : lo;
+    }
+    le |= sh ? (x << (8 * sh)) : x;
+  }
+  return __builtin_bswap64(le);
 }
 
 // 4 waves per SIMD (<= 128 VGPRs): the SHA-512 chains are latency-bound, so
@@ -446,52 +583,27 @@ __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
       continue;
     }
     // gnomAD chr-pos-ref-alt -> interbase interval (pos-1, pos-1+len(ref)]
-    LocMsg lm;
-    lm.S = pos[i] - 1u;
-    lm.E = lm.S + r;
-    lm.dE = ndigits(lm.E);
-    lm.dS = ndigits(lm.S);
-    lm.T = nL0 + lm.dE + nL1 + lm.dS + nL2 + AVDB_DIGEST_CHARS + nL3;
-    lm.dig = seq_digest + size_t(c) * AVDB_DIGEST_CHARS;
+    const uint32_t S = pos[i] - 1u, E = S + r;
+    const uint64_t TL = uint64_t(nL0 + nL1 + nL2 + nL3 + AVDB_DIGEST_CHARS) + ndigits(E) + ndigits(S);
+    const uint32_t nbL = sha_blocks(TL);  // 2 for every 32-bit position
+    const uint64_t* dg = reinterpret_cast<const uint64_t*>(seq_digest + size_t(c) * AVDB_DIGEST_CHARS);
+    const uint64_t dig[4] = {dg[0], dg[1], dg[2], dg[3]};
     const uint64_t altoff = off[i] + r;
     const uint64_t TA = uint64_t(kAlPrefix) + a + nA2;
     const uint32_t nbA = sha_blocks(TA);
-    const uint32_t nbL = sha_blocks(lm.T);  // 2 for every 32-bit position
     uint64_t H[8], locw[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 8; ++k) H[k] = kIV[k];
     uint64_t* slot = &s_w[threadIdx.x];  // this lane's 16 message words, [word][lane]
     for (uint32_t b = 0; b < nbL + nbA; ++b) {
-      // build the block's 16 words (not unrolled: keeps the register budget for
-      // the compression), then reload them with static indices
+      // build the block's 16 words in LDS, then reload them with static indices
+      if (b < nbL) {
+        location_block(slot, b, S, E, dig, TL);
+      } else {
+        const uint32_t ab = b - nbL;
 #pragma unroll 1
-      for (int j = 0; j < 16; ++j) {
-        uint64_t x = 0;
-        if (b < nbL) {  // SequenceLocation message
-          const uint32_t p = b * 128 + 8 * j;
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t q = p + k;
-            x = (x << 8) | (q < lm.T ? loc_byte(lm, q) : pad_byte(q, lm.T, nbL));
-          }
-        } else {  // Allele message
-          const uint64_t p = uint64_t(b - nbL) * 128 + 8 * j;
-          if (p >= kAlPrefix && p + 8 <= kAlPrefix + uint64_t(a)) {
-            x = __builtin_bswap64(heap_u64(hp, altoff + (p - kAlPrefix)));
-          } else {
-            for (int k = 0; k < 8; ++k) {
-              const uint64_t q = p + k;
-              uint8_t by;
-              if (q < nA0) by = uint8_t(kAl0[q]);
-              else if (q < nA0 + AVDB_DIGEST_CHARS) by = word_char(locw, uint32_t(q - nA0));
-              else if (q < kAlPrefix) by = uint8_t(kAl1[q - nA0 - AVDB_DIGEST_CHARS]);
-              else if (q < kAlPrefix + uint64_t(a)) by = heap[altoff + (q - kAlPrefix)];
-              else if (q < TA) by = uint8_t(kAl2[q - kAlPrefix - a]);
-              else by = pad_byte(q, TA, nbA);
-              x = (x << 8) | by;
-            }
-          }
-        }
-        slot[j * kBlock] = x;
+        for (uint32_t j = 0; j < 16; ++j)
+          slot[j * kBlock] = allele_word(16 * ab + j, locw, hp, altoff, a, TA, nbA);
       }
       uint64_t w[16];
 #pragma unroll
