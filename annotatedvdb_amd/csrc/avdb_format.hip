@@ -73,6 +73,27 @@ __device__ __forceinline__ uint32_t ndigits(uint32_t v) {  // decimal digits
   return k;
 }
 
+// a decimal number as ASCII text in registers (up to 16 digits), so a value
+// printed several times per line is converted once
+struct Dec {
+  uint64_t lo, hi;  // digits 0..7 and 8..15, little-endian bytes
+  uint32_t n;
+};
+
+__device__ __forceinline__ uint64_t nibbles_to_ascii(uint64_t d, uint32_t k) {  // k <= 8
+  uint64_t y = d & 0xFFFFFFFFull;
+  y = (y | (y << 16)) & 0x0000FFFF0000FFFFull;
+  y = (y | (y << 8)) & 0x00FF00FF00FF00FFull;
+  y = (y | (y << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  return (y + 0x3030303030303030ull) & low_bytes_mask(k);
+}
+
+__device__ __forceinline__ Dec dec_text(uint32_t v) {
+  uint32_t k;
+  const uint64_t d = dec_nibbles(v, &k);
+  return Dec{nibbles_to_ascii(d, k < 8 ? k : 8), k > 8 ? nibbles_to_ascii(d >> 32, k - 8) : 0ull, k};
+}
+
 template <bool WRITE>
 struct Out {
   gbyte* base;
@@ -141,12 +162,14 @@ struct Out {
     }
   }
   // up to 8 decimal digits given as nibbles (most significant lowest) -> ASCII
-  __device__ __forceinline__ void digits8(uint64_t d, uint32_t k) {
-    uint64_t y = d & 0xFFFFFFFFull;
-    y = (y | (y << 16)) & 0x0000FFFF0000FFFFull;
-    y = (y | (y << 8)) & 0x00FF00FF00FF00FFull;
-    y = (y | (y << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    append((y + 0x3030303030303030ull) & low_bytes_mask(k), k);
+  __device__ __forceinline__ void digits8(uint64_t d, uint32_t k) { append(nibbles_to_ascii(d, k), k); }
+  __device__ __forceinline__ void dec(const Dec& t) {
+    if constexpr (!WRITE) {
+      p += t.n;
+    } else {
+      append(t.lo, t.n < 8 ? t.n : 8);
+      if (t.n > 8) append(t.hi, t.n - 8);
+    }
   }
   __device__ __forceinline__ void u32v(uint32_t v) {
     if constexpr (!WRITE) {
@@ -188,14 +211,16 @@ struct Out {
 // contig label (Util/lib/python/enums/chromosomes.py:9-38 order)
 template <class O>
 __device__ __forceinline__ void chrom_name(O& o, uint32_t c) {
-  if (c < 22) o.u32v(c + 1);
+  if (c < 9) o.put('1' + c);
+  else if (c < 22) o.append(uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8), 2);
   else if (c == 22) o.put('X');
   else if (c == 23) o.put('Y');
   else if (c == 24) o.put('M');
   else o.u32v(c);  // contigs beyond the human 25: numeric label (matches avdb_format_bin_path)
 }
 
-// ltree path of a bin code (generate_bin_index_references.py:54,60-61,74).
+// ltree path of a bin code (generate_bin_index_references.py:54,60-61,74): one
+// 6- or 7-byte append per level (".L<l>.B<b>").
 // Helpers take and return the sink by value (never by reference: a sink whose
 // address escapes lives in scratch memory); all are inlined (see the A/B above).
 template <class O>
@@ -205,10 +230,17 @@ __device__ __forceinline__ O bin_path(O o, uint32_t c, uint32_t code) {
   const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
   for (uint32_t l = 1; l <= level; ++l) {
     const uint32_t gl = g >> (level - l);
-    o.lit(".L");
-    o.u32v(l);
-    o.lit(".B");
-    o.u32v(l == 1 ? gl + 1 : (gl & 1u) + 1);
+    const uint32_t b = l == 1 ? gl + 1 : (gl & 1u) + 1;
+    if (b >= 10) {  // L1 of a contig longer than 576 Mb (custom chromosome tables)
+      o.lit(".L");
+      o.u32v(l);
+      o.lit(".B");
+      o.u32v(b);
+    } else if (l < 10) {
+      o.append(0x000000422E004C2Eull | (uint64_t('0' + l) << 16) | (uint64_t('0' + b) << 40), 6);
+    } else {
+      o.append(0x00422E00314C2Eull | (uint64_t('0' + l - 10) << 24) | (uint64_t('0' + b) << 48), 7);
+    }
   }
   return o;
 }
@@ -634,11 +666,14 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   }
   if (!WRITE && fq0 >= 0 && !freq_plain(s, uint32_t(fq0), uint32_t(fq1))) return kLineHost;
   const bool has_rs = (L.flags & (AVDB_VCF_ID_RS | AVDB_VCF_INFO_RS)) != 0;
+  Dec posd;  // POS is printed up to 5 times per ALT
+  if constexpr (WRITE) posd = dec_text(L.pos);
+  else posd = Dec{0, 0, ndigits(L.pos)};
   // .mapping: variant id (vcf_parser.py:140-142) TAB '['
   if (L.flags & AVDB_VCF_ID_METASEQ) {
     chrom_name(om, c);
     om.put(':');
-    om.u32v(L.pos);
+    om.dec(posd);
     om.put(':');
     om.bytes(ref, rl);
     om.put(':');
@@ -689,7 +724,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
     auto pk = [&](O& o) {
       chrom_name(o, c);
       o.put(':');
-      o.u32v(L.pos);
+      o.dec(posd);
       o.put(':');
       if (lng) {
         o.bytes(reinterpret_cast<const uint8_t*>(A.digest) + 32 * r, AVDB_DIGEST_CHARS);
@@ -710,11 +745,11 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
       oc.put('#');
       pk(oc);
       oc.put('#');
-      oc.u32v(L.pos);
+      oc.dec(posd);
       oc.put('#');
       chrom_name(oc, c);
       oc.put(':');
-      oc.u32v(L.pos);
+      oc.dec(posd);
       oc.put(':');
       oc.bytes(ref, rl);
       oc.put(':');
