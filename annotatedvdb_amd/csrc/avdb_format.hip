@@ -310,7 +310,7 @@ __device__ __forceinline__ void al_trunc(O& o, const Al<CP>& a, uint32_t cap) {
 // ---------------------------------------------------------------------------
 template <bool ESC, class O, class CP>
 __device__ __forceinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, CP ref, uint32_t r,
-                                       CP alt, uint32_t a) {
+                                       CP alt, uint32_t a, Dec posd = Dec{0, 0, 0}) {
   const bool snv = r == 1u && a == 1u;
   uint32_t l = 0;  // common prefix (__normalize_alleles :100-107); SNVs untouched (:97-98)
   if (!snv) {
@@ -350,14 +350,17 @@ __device__ __forceinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uin
     le = end;
   }
   o.lit("{\"location_start\": ");
-  o.u32v(ls);
+  if (posd.n && ls == pos) o.dec(posd);  // posd: POS as text, when the caller has it
+  else o.u32v(ls);
   o.lit(", \"location_end\": ");
-  o.u32v(le);
+  if (posd.n && le == pos) o.dec(posd);
+  else o.u32v(le);
   if (!snv && l > 0) {  // normalized id differs from the metaseq id iff a prefix was trimmed
     o.lit(", \"normalized_metaseq_id\": \"");
     if (chrom < 25) chrom_name(o, chrom);
     o.put(':');
-    o.u32v(pos);
+    if (posd.n) o.dec(posd);
+    else o.u32v(pos);
     o.put(':');
     al_str<ESC>(o, nref);
     o.put(':');
@@ -666,7 +669,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   }
   if (!WRITE && fq0 >= 0 && !freq_plain(s, uint32_t(fq0), uint32_t(fq1))) return kLineHost;
   const bool has_rs = (L.flags & (AVDB_VCF_ID_RS | AVDB_VCF_INFO_RS)) != 0;
-  Dec posd;  // POS is printed up to 5 times per ALT
+  Dec posd;  // POS is printed up to 7 times per ALT
   if constexpr (WRITE) posd = dec_text(L.pos);
   else posd = Dec{0, 0, ndigits(L.pos)};
   // .mapping: variant id (vcf_parser.py:140-142) TAB '['
@@ -768,7 +771,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
       oc.put('#');
       oc.lit(L.n_alt > 1 ? "True" : "NULL");
       oc.put('#');
-      oc = display_json<false>(oc, c, L.pos, A.end[r], ref, rl, alt, al);
+      oc = display_json<false>(oc, c, L.pos, A.end[r], ref, rl, alt, al, posd);
       oc.put('#');
       if (fq0 >= 0) {
         oc = freq_json(oc, s, uint32_t(fq0), uint32_t(fq1), k);
