@@ -559,10 +559,11 @@ __device__ __forceinline__ uint64_t allele_word(uint32_t jw, const uint64_t* loc
   return __builtin_bswap64(le);
 }
 
-// 4 waves per SIMD (<= 128 VGPRs): the SHA-512 chains are latency-bound, so
+// 3 waves per SIMD (<= 168 VGPRs): the SHA-512 chains are latency-bound, so
 // occupancy is what the VALU pipe needs (rocprof: 1 VALU issue per ~12 cycles
-// per wave at 2 waves/SIMD)
-constexpr int kDigestWavesPerSimd = 4;
+// per wave at 2 waves/SIMD); at 4 (<= 128 VGPRs) the message builders spill:
+// C5 A/B (tools/lib_ab.sh) 1.81 ms at 3 vs 1.90 ms at 4.
+constexpr int kDigestWavesPerSimd = 3;
 __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
