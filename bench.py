@@ -94,6 +94,29 @@ def _cpu_load_worker(k):
     return recs, time.perf_counter() - t0
 
 
+def _cpu_c5_worker(k):
+    """Reference-structured C5 path per record: end inference (VariantAnnotator),
+    cached bin lookup (BinIndex), primary key (short join, or the VRS Allele digest
+    through hashlib SHA-512 for long alleles), keep-first dedup on the key."""
+    from oracle import avdb_oracle as O
+    names, pos, refs, alts, exts, digs = _SAMPLE[k]
+    bi = O.PortBinIndex(_TABLE)
+    t0 = time.perf_counter()
+    seen = set()
+    for c, p, ref, alt, e in zip(names, pos, refs, alts, exts):
+        end, _ = O.infer_end(p, ref, alt)
+        try:
+            bi.find_bin_index(c, p, end)
+        except TypeError:  # unmappable (the GPU leg's status 2), as bin_index.py:75 raises
+            pass
+        dg = O.vrs_allele_digest(digs[c], p, ref, alt) if len(ref) + len(alt) > 50 else None
+        pk = O.primary_key(c[3:] if c.startswith("chr") else c, p, ref, alt, e, digest=dg)
+        if pk in seen:
+            continue
+        seen.add(pk)
+    return len(pos), time.perf_counter() - t0
+
+
 def _cpu_worker(k):
     from oracle import avdb_oracle as O
     names, pos, ends = _SAMPLE[k]
@@ -140,6 +163,32 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
                           f"(oracle/avdb_oracle.py load_line + PortBinIndex; 0.82x the verbatim "
                           f"reference's per-line time, tools/calibrate_cpu_baseline.py), per-process "
                           f"{np.mean([r[1] for r in res]):.2f} s"}
+    if workload == "c5":
+        # ADSP-style records generated on the CPU (same generator, CPU stream)
+        per = int(seconds_per_worker / 6e-6)  # ~5.6 us per record in the port
+        b = synth.alleles(per * workers, seed=5, device="cpu")
+        heap = b.heap.numpy().tobytes()
+        off, rl, al = b.allele_off.numpy(), b.ref_len.numpy(), b.alt_len.numpy()
+        names = [CHROM_NAMES[c] for c in b.chrom.numpy().tolist()]
+        pos = b.pos.numpy().tolist()
+        refs = [heap[o:o + r].decode() for o, r in zip(off.tolist(), rl.tolist())]
+        alts = [heap[o + r:o + r + a].decode() for o, r, a in zip(off.tolist(), rl.tolist(), al.tolist())]
+        exts = ["rs%d" % e if e else None for e in b.ext_id.numpy().tolist()]
+        digs = {n: "%032d" % i for i, n in enumerate(CHROM_NAMES)}  # as the GPU leg's refget ids
+        _TABLE = O.BinTable(GRCH38_LENGTHS)
+        _SAMPLE = [(names[k * per:(k + 1) * per], pos[k * per:(k + 1) * per], refs[k * per:(k + 1) * per],
+                    alts[k * per:(k + 1) * per], exts[k * per:(k + 1) * per], digs) for k in range(workers)]
+        ctx = mp.get_context("fork")
+        t0 = time.perf_counter()
+        with ctx.Pool(workers) as pool:
+            res = pool.map(_cpu_c5_worker, range(workers))
+        wall = time.perf_counter() - t0
+        n = sum(r[0] for r in res)
+        return {"value": n / wall, "unit": "variants/s", "cores": workers, "kind": "port",
+                "sample": f"{n:,} ADSP-style records (C5 generator on the CPU), {workers} processes x "
+                          f"{per:,} records; reference-structured end inference + PortBinIndex + primary "
+                          f"key (hashlib SHA-512 VRS digests for long alleles) + keep-first dedup "
+                          f"(oracle/avdb_oracle.py), per-process {np.mean([r[1] for r in res]):.2f} s"}
     per = int(seconds_per_worker / 0.9e-6)  # ~0.9 us per cached find_bin_index call
     total = per * workers
     if workload == "c2":
@@ -173,7 +222,7 @@ def main():
     # CPU baseline first, before this process touches the GPU (its worker
     # processes are forked and must not inherit an initialised HIP runtime)
     want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and ri.world == 1
-                                          and a.workload in ("c2", "c3", "load"))
+                                          and a.workload in ("c2", "c3", "c5", "load"))
     cpu = cpu_baseline(a.workload, a.cpu_seconds) if (ri.rank == 0 and want_cpu) else None
     ri = D.init("nccl")
     dev = torch.device("cuda", ri.local)
