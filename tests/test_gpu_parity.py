@@ -147,6 +147,32 @@ def test_k1_full_size_c3_vs_c_oracle(engine):
     assert np.array_equal(status.cpu().numpy(), rs)
 
 
+@pytest.mark.slow
+def test_k1_c4_one_billion_vs_c_oracle(engine):
+    """BASELINE config 4's whole job on one GPU, shard by shard: the 8 ranks'
+    length-balanced pieces x 1.25e8 mixed records (1e9 in all, the bench's own
+    generator and seeds), every bin code and status bit-exact vs the C oracle."""
+    import oracle
+    from annotatedvdb_amd import shard, synth
+    n = 125_000_000
+    lens = np.asarray(LENGTHS, dtype=np.uint32)
+    plan = shard.plan(8)
+    total = 0
+    for rank in range(8):
+        chrom, start, end = synth.spans(n, seed=4 + 1000 * rank, pieces=plan[rank], mix="c4")
+        code, status = engine.bin_assign(chrom, start, end)
+        hc, hs, he = chrom.cpu().numpy(), start.cpu().numpy(), end.cpu().numpy()
+        rc = np.empty(n, dtype=np.uint32)
+        rs = np.empty(n, dtype=np.uint8)
+        oracle.c_oracle().avdb_oracle_bin_assign(hc.ctypes.data, hs.ctypes.data, he.ctypes.data, n,
+                                                lens.ctypes.data, len(lens), rc.ctypes.data, rs.ctypes.data)
+        assert np.array_equal(u32(code), rc), rank
+        assert np.array_equal(status.cpu().numpy(), rs), rank
+        total += n
+        del chrom, start, end, code, status, hc, hs, he, rc, rs
+    assert total == 1_000_000_000
+
+
 # ---------------------------------------------------------------------------
 # K2 record prep (end inference + bin)
 # ---------------------------------------------------------------------------
