@@ -344,6 +344,39 @@ def test_k4_is_long_ragged_batch(engine):
 
 
 @pytest.mark.slow
+def test_c5_all_shards_vs_c_oracle(engine):
+    """BASELINE config 5's whole job (8 ranks x 2.5e7 ADSP-style records, the
+    bench's generator, seeds and pieces) on one GPU: end / bin / status (K2) and
+    keep-first (K3) bit-exact vs the C oracle for all 2e8 records."""
+    import oracle
+    from annotatedvdb_amd import shard, synth
+    n = 25_000_000
+    lens = np.asarray(LENGTHS, dtype=np.uint32)
+    plan = shard.plan(8)
+    for rank in range(8):
+        b = synth.alleles(n, seed=5 + 1000 * rank, pieces=plan[rank])
+        end, code, status, _ = engine.record_prep(b, want_lcp=False)
+        keep = engine.pk_dedup(b, grouped=True)
+        h = {k: getattr(b, k).cpu().numpy() for k in ("chrom", "pos", "allele_off", "ref_len", "alt_len",
+                                                      "heap", "ext_id")}
+        re_, rc, rl = (np.empty(n, dtype=np.uint32) for _ in range(3))
+        rs = np.empty(n, dtype=np.uint8)
+        oracle.c_oracle().avdb_oracle_record_prep(
+            h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
+            h["alt_len"].ctypes.data, h["heap"].ctypes.data, n, lens.ctypes.data, len(lens),
+            re_.ctypes.data, rc.ctypes.data, rs.ctypes.data, rl.ctypes.data)
+        assert np.array_equal(u32(end), re_), rank
+        assert np.array_equal(u32(code), rc), rank
+        assert np.array_equal(status.cpu().numpy(), rs), rank
+        ek = np.empty(n, dtype=np.uint8)
+        oracle.c_oracle().avdb_oracle_dedup_grouped(
+            h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
+            h["alt_len"].ctypes.data, h["heap"].ctypes.data, h["ext_id"].ctypes.data, n, ek.ctypes.data)
+        assert np.array_equal(keep.cpu().numpy(), ek), rank
+        del b, end, code, status, keep, h
+
+
+@pytest.mark.slow
 def test_c5_full_size_vs_c_oracle(engine):
     """BASELINE config 5 at full per-GPU size (2.5e7 ADSP-style records): K2 end /
     bin / status and K3 keep-first bit-exact vs the C oracle; the hash-path dedup
