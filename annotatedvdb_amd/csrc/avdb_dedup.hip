@@ -238,6 +238,115 @@ __global__ __launch_bounds__(kBlock) void k_dedup_grouped4(
   count_dups(dups, g_ctr);
 }
 
+// Two-phase grouped dedup (aligned arrays + a workspace of kListHead + 4n bytes).
+// Phase A streams chrom/pos 4 records per lane, writes keep = 1 for every
+// record, and lists the records that share their predecessor's (chrom,pos) —
+// the only ones that can repeat an earlier key.  Each workgroup owns a
+// contiguous chunk of groups and lists its suspects in its own slice of the
+// list (one LDS atomic per wave; a single device-wide counter serialises at
+// ~90 atomics/us, which cost 1 ms here).  Phase B runs the same workgroup
+// count: workgroup b gives each of its chunk's suspects a lane of its own for
+// the run scan, so a suspect's dependent memory round trips are paid once per
+// 64 suspects instead of once per wave of mostly unique records.
+constexpr int kListGridMax = 4096;
+constexpr size_t kListHead = 4 * kListGridMax;  // per-workgroup suspect counts
+
+__device__ __forceinline__ void chunk_of(size_t items, size_t* lo, size_t* hi) {
+  const size_t per = (items + gridDim.x - 1) / gridDim.x;
+  const size_t a = size_t(blockIdx.x) * per;
+  *lo = a < items ? a : items;
+  *hi = a + per < items ? a + per : items;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dedup_mark4(const uint8_t* __restrict__ chrom,
+                                                        const uint32_t* __restrict__ pos, size_t n,
+                                                        uint8_t* __restrict__ keep,
+                                                        uint32_t* __restrict__ counts,
+                                                        uint32_t* __restrict__ list) {
+  __shared__ uint32_t s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  size_t g0, g1;
+  chunk_of((n + 3) / 4, &g0, &g1);
+  uint32_t* mine = list + 4 * g0;
+  for (size_t base = g0; base < g1; base += blockDim.x) {
+    const size_t g = base + threadIdx.x;
+    const size_t i0 = 4 * g;
+    const bool live = g < g1;
+    const bool full = live && i0 + 4 <= n;
+    uint32_t c4 = 0;
+    u32x4 p4{};
+    if (full) {
+      c4 = *reinterpret_cast<const uint32_t*>(chrom + i0);
+      p4 = *reinterpret_cast<const u32x4*>(pos + i0);
+    } else if (live) {
+      for (uint32_t t = 0; t < 4 && i0 + t < n; ++t) {
+        c4 |= uint32_t(chrom[i0 + t]) << (8 * t);
+        p4[t] = pos[i0 + t];
+      }
+    }
+    uint32_t pc = __shfl_up(c4 >> 24, 1, kWave), pp = __shfl_up(p4.w, 1, kWave);
+    if (__lane_id() == 0 && live && i0 > 0) {
+      pc = chrom[i0 - 1];
+      pp = pos[i0 - 1];
+    }
+    uint32_t same = 0;
+    same |= uint32_t(i0 > 0 && (c4 & 0xFFu) == pc && p4.x == pp);
+    same |= uint32_t(((c4 >> 8) & 0xFFu) == (c4 & 0xFFu) && p4.y == p4.x) << 1;
+    same |= uint32_t(((c4 >> 16) & 0xFFu) == ((c4 >> 8) & 0xFFu) && p4.z == p4.y) << 2;
+    same |= uint32_t((c4 >> 24) == ((c4 >> 16) & 0xFFu) && p4.w == p4.z) << 3;
+    if (!full) same &= (live && i0 < n) ? (1u << uint32_t(n - i0 < 4 ? n - i0 : 4)) - 1u : 0u;
+    // wave-aggregated append of this lane's suspects to the workgroup's slice
+    const uint32_t cnt = __popc(same);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t u = __shfl_up(incl, d, kWave);
+      if (__lane_id() >= d) incl += u;
+    }
+    const uint32_t total = __shfl(incl, kWave - 1, kWave);
+    if (total) {
+      uint32_t at = 0;
+      if (__lane_id() == kWave - 1) at = atomicAdd(&s_cnt, total);
+      at = __shfl(at, kWave - 1, kWave) + incl - cnt;
+      for (uint32_t m = same; m; m &= m - 1) mine[at++] = uint32_t(i0 + __builtin_ctz(m));
+    }
+    if (full) {
+      *reinterpret_cast<uint32_t*>(keep + i0) = 0x01010101u;
+    } else if (live) {
+      for (uint32_t t = 0; t < 4 && i0 + t < n; ++t) keep[i0 + t] = 1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dedup_resolve_list(
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
+    const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
+    const uint64_t* __restrict__ ext, size_t n, const uint32_t* __restrict__ counts,
+    const uint32_t* __restrict__ list, uint8_t* __restrict__ keep, unsigned long long* __restrict__ g_ctr) {
+  const Heap h = make_heap(heap, heap_bytes);
+  size_t g0, g1;
+  chunk_of((n + 3) / 4, &g0, &g1);
+  const uint32_t* mine = list + 4 * g0;
+  const uint32_t cnt = counts[blockIdx.x];
+  uint32_t dups = 0;
+  // wave-uniform trip count (dedup_record's cooperative compares need the whole wave)
+  for (uint32_t base = 0; base < cnt; base += blockDim.x) {
+    const uint32_t t = base + threadIdx.x;
+    const bool live = t < cnt;
+    const size_t i = live ? mine[t] : 0;
+    const uint8_t k = dedup_record(h, chrom, pos, off, rl, al, ext, i, live, live);
+    if (live && !k) {
+      keep[i] = 0;
+      ++dups;
+    }
+  }
+  count_dups(dups, g_ctr);
+}
+
 // 64-bit fingerprint of (chrom, pos, ext, ref_len, alt_len, bytes)
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
@@ -357,8 +466,17 @@ extern "C" int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t
   if (grouped) {
     const bool vec = (reinterpret_cast<uintptr_t>(chrom) | reinterpret_cast<uintptr_t>(keep)) % 4 == 0 &&
                      reinterpret_cast<uintptr_t>(pos) % 16 == 0;
-    if (vec) {
-      const unsigned grid4 = stream_grid((n + 3) / 4, kBlock * 2, 4096);
+    const unsigned grid4 = stream_grid((n + 3) / 4, kBlock * 2, kListGridMax);
+    if (vec && workspace && workspace_bytes >= kListHead + 4 * ((n + 3) & ~size_t(3)) &&
+        reinterpret_cast<uintptr_t>(workspace) % 16 == 0) {
+      auto* counts = static_cast<uint32_t*>(workspace);
+      auto* list = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + kListHead);
+      hipLaunchKernelGGL(k_dedup_mark4, dim3(grid4), dim3(kBlock), 0, s, chrom, pos, n, keep, counts, list);
+      AVDB_LAUNCH_CHECK("k_dedup_mark4");
+      hipLaunchKernelGGL(k_dedup_resolve_list, dim3(grid4), dim3(kBlock), 0, s, chrom, pos, allele_off,
+                         ref_len, alt_len, heap, heap_bytes, ext_id, n, counts, list, keep, ctr);
+      AVDB_LAUNCH_CHECK("k_dedup_resolve_list");
+    } else if (vec) {
       hipLaunchKernelGGL(k_dedup_grouped4, dim3(grid4), dim3(kBlock), 0, s, chrom, pos, allele_off,
                          ref_len, alt_len, heap, heap_bytes, ext_id, n, keep, ctr);
       AVDB_LAUNCH_CHECK("k_dedup_grouped4");

@@ -319,7 +319,11 @@ class Engine:
         keep = self.empty(n, torch.uint8)
         ws = None
         ws_bytes = 0
-        if not grouped:
+        if grouped:  # optional list of same-position records (two-phase run scan)
+            ws_bytes = 16384 + 4 * ((n + 3) & ~3)
+            ws = workspace if workspace is not None and workspace.numel() >= ws_bytes else \
+                self.empty(ws_bytes, torch.uint8)
+        else:
             sz = ctypes.c_size_t()
             self.lib.avdb_pk_dedup_workspace_size(n, ctypes.byref(sz))
             ws_bytes = int(sz.value)

@@ -133,8 +133,10 @@ int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
  * keep[i] = 1 iff no j < i has the same primary key chr:pos:ref:alt[:ext]
  * (primary_key_generator.py:99-122; equal keys <=> equal (chrom,pos,ref,alt,ext_id)).
  * grouped != 0 promises records with equal (chrom,pos) are contiguous (any
- * position-sorted VCF): a run scan, no workspace.  grouped == 0: hash path,
- * needs `workspace` of avdb_pk_dedup_workspace_size() bytes (device).
+ * position-sorted VCF): a run scan; a 16-byte-aligned `workspace` of at least
+ * 16384 + 4*round_up(n, 4) bytes (optional) lets it list the records that share
+ * their predecessor's position and resolve only those (faster).  grouped == 0: hash
+ * path, needs `workspace` of avdb_pk_dedup_workspace_size() bytes (device).
  * counters[AVDB_CTR_DUPLICATES / _HASH_COLLISIONS] accumulated if non-NULL. */
 int avdb_pk_dedup_workspace_size(size_t n, size_t* bytes);
 int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
