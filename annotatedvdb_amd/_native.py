@@ -50,6 +50,7 @@ CTR_HOST_LINES = 27
 CTR_EXISTING = 28
 MATCH_NONE, MATCH_EXACT, MATCH_SWITCHED, MATCH_HOST = 0, 1, 2, 255
 LINE_GPU, LINE_HOST, LINE_SKIP = 0, 1, 2
+KEY_OK, KEY_HOST, KEY_NEED_DIGEST = 0, 1, 2
 MAX_ALG_ID = 64
 
 
@@ -72,6 +73,7 @@ EXPORTED_SYMBOLS = [
     "avdb_format_workspace_size", "avdb_vcf_format_size", "avdb_vcf_format_write",
     "avdb_display_attributes",
     "avdb_keyset_workspace_size", "avdb_keyset_build", "avdb_keyset_probe",
+    "avdb_primary_keys",
 ]
 
 
@@ -127,6 +129,7 @@ def _sig(lib):
     f.avdb_keyset_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_build.argtypes = [P, P, P, SZ, P, SZ, P]
     f.avdb_keyset_probe.argtypes = [P, P, SZ, P, P, SZ, P, P, P, P, P, P, SZ, SZ, I32, P, P, P, P]
+    f.avdb_primary_keys.argtypes = [P, P, P, P, P, P, P, SZ, P, P, P, SZ, U32, P, SZ, P, P, P, SZ, P, SZ, P, P]
     for name in EXPORTED_SYMBOLS:
         if name not in ("avdb_last_error",):
             getattr(f, name).restype = I32

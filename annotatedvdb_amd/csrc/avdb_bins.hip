@@ -409,6 +409,165 @@ __global__ __launch_bounds__(kBlock) void k_record_prep(
   publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
 }
 
+// K2, vector form (K1's memory discipline): each lane takes 4 consecutive
+// records per group through 16-byte loads (chrom as one u32 of 4 codes, pos /
+// ref_len / alt_len as u32x4, allele_off as two u64x2), UNROLL groups in flight;
+// then all heap peeks of its non-SNV records are issued before any is used;
+// end / code leave as u32x4 stores, status as one u32.  Consecutive lanes hold
+// consecutive records, so a wave's heap peeks fall in one contiguous stretch of
+// the heap.  Grid-stride over a resident grid, as K1.
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+template <bool HIST, int UNROLL>
+__global__ __launch_bounds__(kK1Block) void k_record_prep4(
+    const uint32_t* __restrict__ chromv, const u32x4* __restrict__ pos4, const u64x2* __restrict__ off2,
+    const u32x4* __restrict__ rl4, const u32x4* __restrict__ al4, const uint8_t* __restrict__ heap,
+    size_t heap_bytes, size_t ngroups, u32x4* __restrict__ end4, u32x4* __restrict__ code4,
+    uint32_t* __restrict__ statusv, u32x4* __restrict__ lcp4, ChromTable tab, uint32_t* __restrict__ g_hist,
+    unsigned long long* __restrict__ g_ctr, int lds_hist,
+    // scalar tail [tail_begin, n): block 0, wave 0
+    const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ rl, const uint32_t* __restrict__ al, size_t tail_begin, size_t n,
+    uint32_t* __restrict__ end_out, uint32_t* __restrict__ code, uint8_t* __restrict__ status,
+    uint32_t* __restrict__ lcp) {
+  const Heap hp = make_heap(heap, heap_bytes);
+  extern __shared__ uint32_t s_hist[];
+  __shared__ uint32_t s_len[AVDB_MAX_CHROM];
+  __shared__ uint32_t s_l8off[AVDB_MAX_CHROM];
+  __shared__ unsigned long long s_ctr[AVDB_N_COUNTERS];
+  const bool use_lds = HIST && lds_hist;
+  stage_table(tab, s_len, s_l8off, s_ctr, s_hist, use_lds);
+  uint32_t* hist = use_lds ? s_hist : g_hist;
+  const bool ctrs = g_ctr != nullptr;
+  const int n_chrom = tab.n;
+  const size_t bdim = blockDim.x;
+  uint32_t err = 0, nrec = 0;
+  int since_flush = 0;
+  uint32_t run_key = 0xFFFFFFFFu, run_cnt = 0;
+  for (size_t base = size_t(blockIdx.x) * bdim * UNROLL; base < ngroups; base += size_t(gridDim.x) * bdim * UNROLL) {
+    uint32_t cw[UNROLL];
+    u32x4 p4[UNROLL], r4[UNROLL], a4[UNROLL];
+    u64x2 o01[UNROLL], o23[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const size_t j = base + size_t(u) * bdim + threadIdx.x;
+      const size_t jj = j < ngroups ? j : 0;  // clamped: every lane loads in bounds
+      cw[u] = __builtin_nontemporal_load(&chromv[jj]);
+      p4[u] = __builtin_nontemporal_load(&pos4[jj]);
+      o01[u] = __builtin_nontemporal_load(&off2[2 * jj]);
+      o23[u] = __builtin_nontemporal_load(&off2[2 * jj + 1]);
+      r4[u] = __builtin_nontemporal_load(&rl4[jj]);
+      a4[u] = __builtin_nontemporal_load(&al4[jj]);
+    }
+    // first 8 bytes of ref and alt of every non-SNV record, all issued first
+    uint64_t wr[UNROLL][4], wa[UNROLL][4];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t o = k < 2 ? o01[u][k] : o23[u][k - 2];
+        const bool snv = r4[u][k] == 1u && a4[u][k] == 1u;
+        wr[u][k] = snv ? 0 : heap_u64(hp, o);
+        wa[u][k] = snv ? 0 : heap_u64(hp, o + r4[u][k]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const size_t j = base + size_t(u) * bdim + threadIdx.x;
+      const bool live = j < ngroups;
+      u32x4 e, cv, l;
+      uint32_t stw = 0, key[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t o = k < 2 ? o01[u][k] : o23[u][k - 2];
+        const uint32_t c = (cw[u] >> (8 * k)) & 0xFFu, p = p4[u][k];
+        uint32_t lk;
+        const uint32_t ek = infer_end(hp, o, r4[u][k], a4[u][k], p, wr[u][k], wa[u][k], &lk);
+        uint32_t ck;
+        const uint32_t s_k = classify(c, p, ek, n_chrom, s_len, &ck);
+        e[k] = ek;
+        cv[k] = ck;
+        l[k] = lk;
+        stw |= s_k << (8 * k);
+        key[k] = live ? l8_key(c, p, ck, s_l8off) : 0xFFFFFFFFu;
+      }
+      if (ctrs && live) {
+        nrec += 4;
+        if (stw) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t s_k = (stw >> (8 * k)) & 0xFFu;
+            err += s_k ? (1u << (8 * (s_k - 1))) : 0u;
+          }
+        }
+      }
+      if (HIST) {  // as K1: wave-uniform runs of one key cost one LDS atomic per run
+        const bool same = key[1] == key[0] && key[2] == key[0] && key[3] == key[0];
+        const uint32_t lk = same ? key[0] : 0xFFFFFFFEu;
+        const uint32_t first = __builtin_amdgcn_readfirstlane(lk);
+        const uint64_t ok = __ballot(!live || lk == first);
+        if (ok == ~0ull && first < 0xFFFFFFFEu) {
+          const uint32_t cnt = 4u * uint32_t(__popcll(__ballot(live)));
+          if (first == run_key) {
+            run_cnt += cnt;
+          } else {
+            if (run_cnt && __lane_id() == 0) atomicAdd(&hist[run_key], run_cnt);
+            run_key = first;
+            run_cnt = cnt;
+          }
+        } else if (!(ok == ~0ull && first == 0xFFFFFFFFu)) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) wave_hist_add(key[k], hist);
+        }
+      }
+      if (live) {
+        __builtin_nontemporal_store(e, &end4[j]);
+        __builtin_nontemporal_store(cv, &code4[j]);
+        if (statusv) __builtin_nontemporal_store(stw, &statusv[j]);
+        if (lcp4) lcp4[j] = l;
+      }
+    }
+    if (ctrs && ++since_flush == 255 / (UNROLL * 4)) {  // 8-bit error fields never wrap
+      flush_errors(err, s_ctr);
+      since_flush = 0;
+    }
+  }
+  if (HIST && run_cnt && __lane_id() == 0) atomicAdd(&hist[run_key], run_cnt);
+  // scalar tail (< 4 records)
+  if (blockIdx.x == 0 && threadIdx.x < kWave) {
+    const size_t i = tail_begin + threadIdx.x;
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < n) {
+      const uint32_t r = rl[i], a = al[i], p = pos[i], c = chrom[i];
+      const uint64_t o = off[i];
+      const bool snv = r == 1u && a == 1u;
+      uint32_t l, cv;
+      const uint32_t e = infer_end(hp, o, r, a, p, snv ? 0 : heap_u64(hp, o), snv ? 0 : heap_u64(hp, o + r), &l);
+      const uint32_t s_k = classify(c, p, e, n_chrom, s_len, &cv);
+      end_out[i] = e;
+      code[i] = cv;
+      if (status) status[i] = uint8_t(s_k);
+      if (lcp) lcp[i] = l;
+      nrec += 1;
+      err += s_k ? (1u << (8 * (s_k - 1))) : 0u;
+      key = l8_key(c, p, cv, s_l8off);
+    }
+    if (HIST) wave_hist_add(key, hist);
+  }
+  if (ctrs) {
+    flush_errors(err, s_ctr);
+    for (int d = 32; d > 0; d >>= 1) nrec += __shfl_down(nrec, d, kWave);
+    if (__lane_id() == 0 && nrec) atomicAdd(&s_ctr[AVDB_CTR_RECORDS], (unsigned long long)nrec);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long bad = s_ctr[AVDB_CTR_STATUS0 + 1] + s_ctr[AVDB_CTR_STATUS0 + 2] +
+                                     s_ctr[AVDB_CTR_STATUS0 + 3];
+      s_ctr[AVDB_CTR_STATUS0] = s_ctr[AVDB_CTR_RECORDS] - bad;
+    }
+  }
+  publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
+}
+
 }  // namespace avdb
 
 using namespace avdb;
@@ -508,6 +667,29 @@ extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint3
   const int lds_hist = hist && ctx->tab.n_l8 <= uint32_t(kMaxLdsHistBins);
   const size_t shm = lds_hist ? size_t(ctx->tab.n_l8) * 4 : 0;
   auto* ctr = reinterpret_cast<unsigned long long*>(counters);
+  const bool vec = ctx->k2_vector && n >= 4 && aligned(chrom, 4) && aligned(pos, 16) && aligned(allele_off, 16) &&
+                   aligned(ref_len, 16) && aligned(alt_len, 16) && aligned(end_out, 16) && aligned(bin_code, 16) &&
+                   (!status || aligned(status, 4)) && (!lcp || aligned(lcp, 16));
+  if (vec) {
+    constexpr int U = 2;
+    const size_t ngroups = n / 4;
+    const unsigned bdim = unsigned(kK1Block);
+    const unsigned grid = stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k1_blocks_per_cu));
+#define K2V(HI)                                                                                           \
+  hipLaunchKernelGGL((k_record_prep4<HI, U>), dim3(grid), dim3(bdim), shm, s,                            \
+                     reinterpret_cast<const uint32_t*>(chrom), reinterpret_cast<const u32x4*>(pos),      \
+                     reinterpret_cast<const u64x2*>(allele_off), reinterpret_cast<const u32x4*>(ref_len), \
+                     reinterpret_cast<const u32x4*>(alt_len), heap, heap_bytes, ngroups,                  \
+                     reinterpret_cast<u32x4*>(end_out), reinterpret_cast<u32x4*>(bin_code),              \
+                     reinterpret_cast<uint32_t*>(status), reinterpret_cast<u32x4*>(lcp), ctx->tab, hist_l8, \
+                     ctr, lds_hist, chrom, pos, allele_off, ref_len, alt_len, ngroups * 4, n, end_out,   \
+                     bin_code, status, lcp)
+    if (hist) K2V(true);
+    else K2V(false);
+#undef K2V
+    AVDB_LAUNCH_CHECK("k_record_prep4");
+    return AVDB_OK;
+  }
   const unsigned grid = stream_grid(n, kBlock * 8, 2048);
   if (hist)
     hipLaunchKernelGGL((k_record_prep<true>), dim3(grid), dim3(kBlock), shm, s, chrom, pos,

@@ -93,6 +93,10 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     const int v = atoi(s);
     if (v == 256 || v == 512) c->k1_block = v;
   }
+  // K2 vector form (4 records per lane from 16-byte loads) when the arrays are
+  // aligned; AVDB_K2_VECTOR=0 keeps the one-record-per-lane form (A/B)
+  c->k2_vector = true;
+  if (const char* s = getenv("AVDB_K2_VECTOR")) c->k2_vector = atoi(s) != 0;
   *out = c;
   return AVDB_OK;
 }

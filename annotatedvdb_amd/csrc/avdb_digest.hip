@@ -103,9 +103,35 @@ __device__ __forceinline__ uint64_t rotr(uint64_t x) {
   return (uint64_t(nhi) << 32) | nlo;
 }
 
-// bitwise select / majority per 32-bit half (v_bfi_b32)
-__device__ __forceinline__ uint64_t bsel(uint64_t m, uint64_t x, uint64_t y) {  // m ? x : y
-  return (m & x) | (~m & y);
+// gfx950 v_bitop3_b32: any 3-input bitwise function in one instruction per
+// 32-bit half (truth table over inputs 0xF0, 0xCC, 0xAA).  xor3 folds the three
+// rotations of Sigma/sigma, and Ch / Maj are single selects.
+constexpr unsigned kXor3 = 0x96;  // x ^ y ^ z
+constexpr unsigned kCh = 0xCA;    // x ? y : z
+constexpr unsigned kMaj = 0xE8;   // majority(x, y, z)
+template <unsigned LUT>
+__device__ __forceinline__ uint64_t bop3(uint64_t x, uint64_t y, uint64_t z) {
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32(uint32_t(x), uint32_t(y), uint32_t(z), LUT);
+  const uint32_t hi =
+      __builtin_amdgcn_bitop3_b32(uint32_t(x >> 32), uint32_t(y >> 32), uint32_t(z >> 32), LUT);
+  return (uint64_t(hi) << 32) | lo;
+}
+
+// 64-bit logical shift right by a constant < 32: one funnel shift + one shift
+template <int N>
+__device__ __forceinline__ uint64_t shr(uint64_t x) {
+  const uint32_t lo = uint32_t(x), hi = uint32_t(x >> 32);
+  return (uint64_t(hi >> N) << 32) | __builtin_amdgcn_alignbit(hi, lo, N);
+}
+
+// 64-bit add as one v_lshl_add_u64.  Written as inline asm because operands
+// assembled from two 32-bit halves (bop3 results) are otherwise split by the
+// compiler into a 64-bit add of the low half plus a 32-bit add of the high
+// halves and register moves (~5 extra instructions per round).
+__device__ __forceinline__ uint64_t add64(uint64_t x, uint64_t y) {
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
 }
 
 template <bool SCHED>
@@ -118,17 +144,18 @@ __device__ __forceinline__ void sha512_16(uint64_t& a, uint64_t& b, uint64_t& c,
       wt = w[j];
     } else {
       const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-      const uint64_t s0 = rotr<1>(w15) ^ rotr<8>(w15) ^ (w15 >> 7);
-      const uint64_t s1 = rotr<19>(w2) ^ rotr<61>(w2) ^ (w2 >> 6);
-      wt = w[j] + s0 + w[(j + 9) & 15] + s1;
+      const uint64_t s0 = bop3<kXor3>(rotr<1>(w15), rotr<8>(w15), shr<7>(w15));
+      const uint64_t s1 = bop3<kXor3>(rotr<19>(w2), rotr<61>(w2), shr<6>(w2));
+      wt = add64(add64(w[j], w[(j + 9) & 15]), add64(s0, s1));
       w[j] = wt;
     }
-    const uint64_t S1 = rotr<14>(e) ^ rotr<18>(e) ^ rotr<41>(e);
-    const uint64_t ch = bsel(e, f, g);
-    const uint64_t t1 = hh + S1 + ch + K512[r + j] + wt;
-    const uint64_t S0 = rotr<28>(a) ^ rotr<34>(a) ^ rotr<39>(a);
-    const uint64_t mj = bsel(a ^ b, c, b);  // majority(a, b, c)
-    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    // hh + K + w does not depend on this round's e/a: off the critical path
+    const uint64_t hkw = hh + (K512[r + j] + wt);
+    const uint64_t S1 = bop3<kXor3>(rotr<14>(e), rotr<18>(e), rotr<41>(e));
+    const uint64_t t1 = add64(hkw, add64(S1, bop3<kCh>(e, f, g)));
+    const uint64_t S0 = bop3<kXor3>(rotr<28>(a), rotr<34>(a), rotr<39>(a));
+    const uint64_t mj = bop3<kMaj>(a, b, c);
+    hh = g; g = f; f = e; e = add64(d, t1); d = c; c = b; b = a; a = add64(t1, add64(S0, mj));
   }
 }
 
@@ -501,69 +528,58 @@ __device__ __forceinline__ uint64_t prefix_word(const uint64_t* locw) {
   return le;
 }
 
-// The Allele serialisation AL0 + <32 location chars> + AL1 + ALT + AL2: message
-// word jw (0-based, big-endian value) of a TA-byte message in nb blocks.
-// Prefix words (0..8) come from the literals and the location chars, ALT words
-// from one 8-byte heap load, the suffix from AL2 + 0x80 as literal chunks.
-__device__ __forceinline__ uint64_t allele_word(uint32_t jw, const uint64_t* locw, const Heap& hp,
-                                                uint64_t altoff, uint32_t a, uint64_t TA, uint32_t nb) {
-  const uint32_t last = nb * 16 - 1;
-  if (jw == last) return TA * 8;
-  if (jw == last - 1) return 0;
-  const uint64_t p = uint64_t(jw) * 8;       // first message byte of the word
-  const uint64_t Q = uint64_t(kAlPrefix) + a;  // first suffix byte
-  uint64_t le = 0;
-  // prefix: AL0 | 32 location chars | AL1 (68 bytes, words 0..8)
-  if (p < kAlPrefix) {
-    switch (jw) {
-      case 0: le = prefix_word<0>(locw); break;
-      case 1: le = prefix_word<1>(locw); break;
-      case 2: le = prefix_word<2>(locw); break;
-      case 3: le = prefix_word<3>(locw); break;
-      case 4: le = prefix_word<4>(locw); break;
-      case 5: le = prefix_word<5>(locw); break;
-      case 6: le = prefix_word<6>(locw); break;
-      case 7: le = prefix_word<7>(locw); break;
-      default: le = prefix_word<8>(locw); break;
-    }
-  }
-  // ALT bytes [max(p, 68), min(p + 8, Q))
-  const uint64_t q0 = p > kAlPrefix ? p : uint64_t(kAlPrefix);
-  const uint64_t q1 = p + 8 < Q ? p + 8 : Q;
-  if (q0 < q1) {
-    const uint32_t sh = uint32_t(q0 - p), nbytes = uint32_t(q1 - q0);
-    le |= (heap_u64(hp, altoff + (q0 - kAlPrefix)) & low_bytes_mask(nbytes)) << (8 * sh);
-  }
-  // suffix AL2 + 0x80 (then zeros) from byte Q on
-  if (p + 8 > Q) {
-    const uint64_t s0 = p > Q ? p : Q;
-    const uint32_t sh = uint32_t(s0 - p);
-    const uint64_t d = s0 - Q;  // suffix offset of byte s0
-    uint64_t x = 0;
-    if (d < uint64_t(nA2) + 1) {
-      constexpr int kSufWords = (nA2 + 1 + 7) / 8;
-      // 8 suffix bytes from offset d (AL2 then 0x80), assembled from literal chunks
-      const uint32_t wi = uint32_t(d) >> 3, bo = uint32_t(d) & 7u;
-      uint64_t lo = 0, hi = 0;
+// The Allele serialisation AL0 + <32 location chars> + AL1 + ALT + AL2, then SHA
+// padding: the 16 big-endian message words of block `ab` (uniform across the
+// wave: lanes are grouped by block count), built in registers with no branch
+// on the lane's ALT length.  A word is the OR of three masked sources:
+//   prefix  words 0..8 of block 0 (literals + the location chars; static j)
+//   ALT     one unaligned 8-byte heap load, masked to the bytes before Q
+//   suffix  an 8-byte window of (8 zero bytes | AL2 | 0x80 | zeros) read from
+//           the LDS table s_suf at the word's offset from Q (clamped: the
+//           windows outside the suffix are zero)
+// and the final block's last word is the message length in bits.
+constexpr int kSufTab = 72;  // windows at offsets -8 .. 63 from the suffix start
+__device__ __forceinline__ void allele_block(uint64_t* w, uint32_t ab, const uint64_t* locw, const Heap& hp,
+                                             uint64_t altoff, uint32_t a, uint64_t TA, uint32_t nb,
+                                             const uint64_t* s_suf) {
+  const int64_t Q = int64_t(kAlPrefix) + a;  // first suffix byte
 #pragma unroll
-      for (int q = 0; q <= kSufWords; ++q) {
-        const uint64_t c = lit_word(AL2, 8 * q) |
-                           ((nA2 >= 8 * q && nA2 < 8 * q + 8) ? uint64_t(0x80) << (8 * (nA2 - 8 * q)) : 0ull);
-        if (uint32_t(q) == wi) lo = c;
-        if (uint32_t(q) == wi + 1) hi = c;
+  for (int j = 0; j < 16; ++j) {
+    const int64_t p = int64_t(ab) * 128 + 8 * j;  // first message byte of the word
+    uint64_t le = 0;
+    if (j <= 8 && ab == 0) {
+      switch (j) {
+        case 0: le = prefix_word<0>(locw); break;
+        case 1: le = prefix_word<1>(locw); break;
+        case 2: le = prefix_word<2>(locw); break;
+        case 3: le = prefix_word<3>(locw); break;
+        case 4: le = prefix_word<4>(locw); break;
+        case 5: le = prefix_word<5>(locw); break;
+        case 6: le = prefix_word<6>(locw); break;
+        case 7: le = prefix_word<7>(locw); break;
+        default: le = prefix_word<8>(locw); break;
       }
-      x = bo ? (lo >> (8 * bo)) | (hi << (64 - 8 * bo)) : lo;
     }
-    le |= sh ? (x << (8 * sh)) : x;
+    if (p + 8 > int64_t(kAlPrefix) && p < Q) {
+      // block 0 word 8 holds prefix bytes 64..67 then ALT bytes 0..3
+      const uint64_t x = (j == 8 && ab == 0) ? heap_u64(hp, altoff) << 32
+                                               : heap_u64(hp, altoff + uint64_t(p - int64_t(kAlPrefix)));
+      le |= Q - p < 8 ? x & low_bytes_mask(uint32_t(Q - p)) : x;
+    }
+    int64_t t = p - Q + 8;
+    t = t < 0 ? 0 : (t > kSufTab - 1 ? kSufTab - 1 : t);
+    le |= s_suf[t];
+    w[j] = __builtin_bswap64(le);
   }
-  return __builtin_bswap64(le);
+  if (ab + 1 == nb) w[15] = TA * 8;  // (w[14], the high length word, is 0 from the table)
 }
 
-// 3 waves per SIMD (<= 168 VGPRs): the SHA-512 chains are latency-bound, so
-// occupancy is what the VALU pipe needs (rocprof: 1 VALU issue per ~12 cycles
-// per wave at 2 waves/SIMD); at 4 (<= 128 VGPRs) the message builders spill:
-// C5 A/B (tools/lib_ab.sh) 1.81 ms at 3 vs 1.90 ms at 4.
-constexpr int kDigestWavesPerSimd = 3;
+// Waves per SIMD (launch bound and persistent grid).  3: <= 168 VGPRs, no
+// spills; the SHA-512 chains are latency-bound, so occupancy feeds the VALU.
+#ifndef AVDB_DIGEST_WAVES
+#define AVDB_DIGEST_WAVES 3
+#endif
+constexpr int kDigestWavesPerSimd = AVDB_DIGEST_WAVES;
 __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
@@ -571,6 +587,17 @@ __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     const uint32_t* __restrict__ list, const unsigned int* __restrict__ count,
     const char* __restrict__ seq_digest, int n_chrom, char* __restrict__ out) {
   __shared__ uint64_t s_w[16 * kBlock];
+  __shared__ uint64_t s_suf[kSufTab];
+  if (threadIdx.x < kSufTab) {  // 8-byte windows of (8 zero bytes | AL2 | 0x80 | zeros)
+    uint64_t x = 0;
+    for (int q = 0; q < 8; ++q) {
+      const int z = int(threadIdx.x) + q - 8;  // suffix byte index
+      const uint32_t by = (z >= 0 && z < int(nA2)) ? uint8_t(kAl2[z]) : (z == int(nA2) ? 0x80u : 0u);
+      x |= uint64_t(by) << (8 * q);
+    }
+    s_suf[threadIdx.x] = x;
+  }
+  __syncthreads();
   const Heap hp = make_heap(heap, heap_bytes);
   const unsigned int cnt = *count;
   const size_t stride = size_t(gridDim.x) * blockDim.x;
@@ -596,19 +623,18 @@ __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
 #pragma unroll
     for (int k = 0; k < 8; ++k) H[k] = kIV[k];
     uint64_t* slot = &s_w[threadIdx.x];  // this lane's 16 message words, [word][lane]
+    // One compression site (code size): SequenceLocation blocks take their
+    // words from this lane's LDS slot, Allele blocks build them in registers;
+    // b is uniform across the wave, so the branch does not diverge.
     for (uint32_t b = 0; b < nbL + nbA; ++b) {
-      // build the block's 16 words in LDS, then reload them with static indices
+      uint64_t w[16];
       if (b < nbL) {
         location_block(slot, b, S, E, dig, TL);
-      } else {
-        const uint32_t ab = b - nbL;
-#pragma unroll 1
-        for (uint32_t j = 0; j < 16; ++j)
-          slot[j * kBlock] = allele_word(16 * ab + j, locw, hp, altoff, a, TA, nbA);
-      }
-      uint64_t w[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) w[j] = slot[j * kBlock];
+        for (int j = 0; j < 16; ++j) w[j] = slot[j * kBlock];
+      } else {
+        allele_block(w, b - nbL, locw, hp, altoff, a, TA, nbA, s_suf);
+      }
       sha512_block(H, w);
       if (b + 1 == nbL) {  // location digest done: its chars feed the Allele blob
         t24u_words(H, locw);

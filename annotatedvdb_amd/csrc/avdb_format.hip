@@ -900,6 +900,95 @@ __global__ __launch_bounds__(kBlock) void k_display(const uint8_t* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// K7: primary keys (+ ltree bin paths) of a record batch; one lane per record.
+// SIZE needs only the SoA (lengths, pos, ext): it never reads the heap, so it
+// is a cheap streaming pass; WRITE renders the text and checks the allele bytes.
+// ---------------------------------------------------------------------------
+struct KeyArgs {
+  const uint8_t* chrom;
+  const uint32_t* pos;
+  const uint64_t* off;
+  const uint32_t* rl;
+  const uint32_t* al;
+  const uint8_t* heap;
+  const uint64_t* ext;
+  const uint32_t* code;   // nullable: no paths
+  const char* digest;     // nullable: long records get state NEED_DIGEST
+  size_t heap_bytes, n, key_cap, path_cap;
+  uint32_t max_seq_len;
+  int32_t n_chrom;
+  uint64_t* key_off;
+  uint64_t* path_off;
+  uint8_t* key_out;
+  uint8_t* path_out;
+  uint8_t* state;
+};
+
+// ':' in an allele (the reference's metaseq split raises ValueError,
+// primary_key_generator.py:106) or a non-ASCII byte (outside the contract)
+template <class CP>
+__device__ __forceinline__ bool key_allele_ok(CP s, uint32_t n) {
+  return swar_find(s, n, [](uint64_t x) { return (x & kHiBits) | bytes_eq_mask(x, ':'); }) == n;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void k_record_keys(KeyArgs A) {
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < A.n; i += size_t(gridDim.x) * blockDim.x) {
+    const uint32_t c = A.chrom[i], p = A.pos[i], r = A.rl[i], a = A.al[i];
+    const uint64_t e = A.ext ? A.ext[i] : 0ull;
+    const bool lng = uint64_t(r) + a > A.max_seq_len;
+    // SoA-decidable states; the WRITE pass adds the allele-byte checks
+    uint8_t st = AVDB_KEY_OK;
+    if (c >= uint32_t(A.n_chrom) || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
+    else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
+    auto key = [&](auto o) {  // primary_key_generator.py:106-122
+      chrom_name(o, c);
+      o.put(':');
+      o.u32v(p);
+      o.put(':');
+      if (lng) {  // only reached with a digest array (st == OK)
+        o.bytes((glb_cp)(A.digest + 32 * i), AVDB_DIGEST_CHARS);
+      } else {
+        const uint64_t off = A.off[i];
+        o.bytes((glb_cp)(A.heap + off), r);
+        o.put(':');
+        o.bytes((glb_cp)(A.heap + off + r), a);
+      }
+      if (e && !(e >> 63)) {
+        o.lit(":rs");
+        o.u64v(e);
+      }
+      return o;
+    };
+    if constexpr (WRITE) {
+      if (st == AVDB_KEY_OK && !lng) {
+        const uint64_t off = A.off[i];
+        if (off + r + a > A.heap_bytes || !key_allele_ok((glb_cp)(A.heap + off), r + a)) st = AVDB_KEY_HOST;
+      }
+      if (st == AVDB_KEY_OK && A.key_off[i + 1] <= A.key_cap) {  // (cap: never write past the buffer)
+        Out<true> o = key(Out<true>(A.key_out, A.key_off[i]));
+        o.finish();
+      }
+      if (A.code) {
+        const uint32_t cd = A.code[i];
+        if (cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom) && A.path_off[i + 1] <= A.path_cap) {
+          Out<true> o = bin_path(Out<true>(A.path_out, A.path_off[i]), c, cd);
+          o.finish();
+        }
+      }
+      A.state[i] = st;
+    } else {
+      A.key_off[i] = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;
+      if (A.code) {
+        const uint32_t cd = A.code[i];
+        A.path_off[i] = (cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom))
+                            ? bin_path(Out<false>(nullptr, 0), c, cd).size() : 0;
+      }
+    }
+  }
+}
+
 }  // namespace avdb
 
 using namespace avdb;
@@ -1075,5 +1164,79 @@ extern "C" int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, cons
   hipLaunchKernelGGL(k_display<true>, dim3(grid), dim3(kBlock), 0, s, chrom, pos, end, allele_off, ref_len,
                      alt_len, heap, heap_bytes, n, out_off, out, rec_state);
   AVDB_LAUNCH_CHECK("k_display<write>");
+  return AVDB_OK;
+}
+
+extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                 const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                                 const uint8_t* heap, size_t heap_bytes, const uint64_t* ext_id,
+                                 const uint32_t* bin_code, const char* digest, size_t n, uint32_t max_seq_len,
+                                 void* workspace, size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off,
+                                 uint8_t* key_out, size_t key_cap, uint8_t* path_out, size_t path_cap,
+                                 uint8_t* key_state, void* stream) {
+  if (!ctx || !key_off || (bin_code && !path_off)) {
+    avdb_set_error("avdb_primary_keys: null argument");
+    return AVDB_EINVAL;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  KeyArgs A;
+  memset(&A, 0, sizeof(A));
+  A.chrom = chrom;
+  A.pos = pos;
+  A.off = allele_off;
+  A.rl = ref_len;
+  A.al = alt_len;
+  A.heap = heap;
+  A.ext = ext_id;
+  A.code = bin_code;
+  A.digest = digest;
+  A.heap_bytes = heap_bytes;
+  A.n = n;
+  A.max_seq_len = max_seq_len;
+  A.n_chrom = ctx->tab.n < 25 ? ctx->tab.n : 25;  // labelled contigs (chromosomes.py:9-38)
+  A.key_off = key_off;
+  A.path_off = path_off;
+  A.key_cap = key_cap;
+  A.path_cap = path_cap;
+  A.key_out = key_out;
+  A.path_out = path_out;
+  A.state = key_state;
+  auto* ko = reinterpret_cast<unsigned long long*>(key_off);
+  auto* po = reinterpret_cast<unsigned long long*>(path_off);
+  if (!key_out) {  // size pass + scans
+    AVDB_HIP_TRY(hipMemsetAsync(ko + n, 0, 8, s));
+    if (bin_code) AVDB_HIP_TRY(hipMemsetAsync(po + n, 0, 8, s));
+    if (n == 0) return AVDB_OK;
+    if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap) {
+      avdb_set_error("avdb_primary_keys: null array");
+      return AVDB_EINVAL;
+    }
+    size_t need = 0;
+    avdb_format_workspace_size(n, &need);
+    if (!workspace || workspace_bytes < need) {
+      avdb_set_error("avdb_primary_keys: workspace of %zu bytes required", need);
+      return AVDB_ERANGE;
+    }
+    const unsigned grid = stream_grid(n, kBlock, 4096);
+    hipLaunchKernelGGL(k_record_keys<false>, dim3(grid), dim3(kBlock), 0, s, A);
+    AVDB_LAUNCH_CHECK("k_record_keys<size>");
+    size_t tb = scan_bytes(n + 1);
+    AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, ko, ko, n + 1, s));
+    if (bin_code) AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, po, po, n + 1, s));
+    return AVDB_OK;
+  }
+  if (n == 0) return AVDB_OK;
+  if (!key_state || (bin_code && !path_out)) {
+    avdb_set_error("avdb_primary_keys: null output");
+    return AVDB_EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(key_out) % 8 || (path_out && reinterpret_cast<uintptr_t>(path_out) % 8)) {
+    avdb_set_error("avdb_primary_keys: outputs must be 8-byte aligned");
+    return AVDB_EINVAL;
+  }
+  const unsigned grid = stream_grid(n, kBlock, 4096);
+  hipLaunchKernelGGL(k_record_keys<true>, dim3(grid), dim3(kBlock), 0, s, A);
+  AVDB_LAUNCH_CHECK("k_record_keys<write>");
   return AVDB_OK;
 }

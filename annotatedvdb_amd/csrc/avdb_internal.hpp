@@ -178,6 +178,7 @@ struct avdb_ctx {
   int k1_blocks_per_cu;  // K1 grid = n_cu * k1_blocks_per_cu workgroups (env AVDB_K1_BLOCKS_PER_CU)
   int k1_variant;        // K1 lane-group shape / memory policy (env AVDB_K1_VARIANT, bins.hip)
   int k1_block;          // K1 workgroup size: 256 or 512 (env AVDB_K1_BLOCK)
+  bool k2_vector;        // K2 4-records-per-lane form (env AVDB_K2_VECTOR, default on)
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
   bool has_digests;

@@ -197,6 +197,32 @@ class FormatResult:
     counters: torch.Tensor
 
 
+@dataclass
+class KeyText:
+    """Output of ``Engine.primary_keys`` (device tensors): key i is
+    ``keys[key_off[i]:key_off[i+1]]`` when ``state[i] == KEY_OK``; path i is
+    ``paths[path_off[i]:path_off[i+1]]`` (empty for an unmappable record)."""
+    ws: torch.Tensor
+    key_off: torch.Tensor
+    path_off: Optional[torch.Tensor]
+    state: torch.Tensor
+    keys: Optional[torch.Tensor]
+    paths: Optional[torch.Tensor]
+
+    def host(self, n: int):
+        """(keys, paths) as Python lists of str (None where not rendered)."""
+        ko = self.key_off[: n + 1].cpu().numpy()
+        kb = self.keys.cpu().numpy().tobytes()
+        st = self.state[:n].cpu().numpy()
+        keys = [kb[ko[i]:ko[i + 1]].decode() if st[i] == N.KEY_OK else None for i in range(n)]
+        paths = None
+        if self.paths is not None:
+            po = self.path_off[: n + 1].cpu().numpy()
+            pb = self.paths.cpu().numpy().tobytes()
+            paths = [pb[po[i]:po[i + 1]].decode() or None for i in range(n)]
+        return keys, paths
+
+
 # ---------------------------------------------------------------------------
 # engine
 # ---------------------------------------------------------------------------
@@ -492,6 +518,42 @@ class Engine:
         if n:
             N.check("avdb_display_attributes", self.lib.avdb_display_attributes(*args, N.ptr(out), N.ptr(state), s))
         return out[:total], off, state[:n]
+
+    # -- K7: primary keys + bin paths as text ------------------------------------
+    def primary_keys(self, b: RecordBatch, code: Optional[torch.Tensor] = None,
+                     digest: Optional[torch.Tensor] = None, max_seq_len: int = 50, *,
+                     out: Optional["KeyText"] = None) -> "KeyText":
+        """``generate_primary_key`` (and, with ``code``, the ltree bin path) for
+        every record of ``b`` as text on the device.  Without ``out`` the size
+        pass is followed by one host read of the totals; passing a ``KeyText``
+        from an earlier call on a same-shaped batch reuses its buffers (no host
+        sync: a text past a buffer's end is not written, its record's state
+        stays as the size pass left it)."""
+        b = b if b.device == self.device else b.to(self.device)
+        self._check_alleles(b)
+        n = b.n
+        s = self._stream()
+        code = self._dev(code)
+        digest = self._dev(digest)
+        if out is None:
+            sz = ctypes.c_size_t()
+            self.lib.avdb_format_workspace_size(n, ctypes.byref(sz))
+            out = KeyText(ws=self.empty(int(sz.value), torch.uint8), key_off=self.empty(n + 1, torch.int64),
+                          path_off=self.empty(n + 1, torch.int64) if code is not None else None,
+                          state=self.empty(max(1, n), torch.uint8), keys=None, paths=None)
+        args = (self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
+                N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), N.ptr(code), N.ptr(digest), n, int(max_seq_len),
+                N.ptr(out.ws), out.ws.numel(), N.ptr(out.key_off), N.ptr(out.path_off))
+        N.check("avdb_primary_keys", self.lib.avdb_primary_keys(*args, None, 0, None, 0, None, s))
+        if out.keys is None:
+            tot = torch.stack([out.key_off[n], out.path_off[n] if code is not None else out.key_off[n]]).cpu().tolist()
+            out.keys = self.empty(max(8, int(tot[0])), torch.uint8)
+            out.paths = self.empty(max(8, int(tot[1])), torch.uint8) if code is not None else None
+        if n:
+            N.check("avdb_primary_keys", self.lib.avdb_primary_keys(
+                *args, N.ptr(out.keys), out.keys.numel(), N.ptr(out.paths),
+                out.paths.numel() if out.paths is not None else 0, N.ptr(out.state), s))
+        return out
 
     # -- K6: existing-variant key set ----------------------------------------
     def keyset_build(self, keys: torch.Tensor, key_off: torch.Tensor) -> torch.Tensor:

@@ -134,6 +134,55 @@ def alleles(n: int, seed: int = 5, device="cuda", pieces: Optional[Sequence[Piec
                        alt_len=al.to(torch.int32), heap=heap, ext_id=ext)
 
 
+C1_N = 1_100_000
+C1_LO, C1_HI = 16_050_000, 50_800_000  # chr22 region a 1000 Genomes VCF covers
+
+
+def np_c1(n: int = C1_N, seed: int = 1, rs_frac: float = 0.6):
+    """C1 (BASELINE configs[0]): ``n`` chr22 records with
+    positions uniform in [16,050,000, 50,800,000], position-sorted; 88 % SNVs,
+    6 % insertions of 1-20 bp and 6 % deletions of 1-30 bp (both VCF-anchored:
+    alt[0] == ref[0]); ``rs_frac`` of the records carry an rsid.  numpy PCG64,
+    host-side, so tests and bench use byte-identical records.
+
+    Returns a dict of numpy arrays in the ``RecordBatch`` layout (``chrom`` u8,
+    ``pos`` i32, ``allele_off`` i64, ``ref_len``/``alt_len`` i32, ``heap`` u8,
+    ``ext_id`` i64: rsid number or 0)."""
+    from .chromosomes import CHROM_NAMES
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pos = np.sort(rng.integers(C1_LO, C1_HI + 1, n)).astype(np.int32)
+    u = rng.random(n)
+    ins = (u >= 0.88) & (u < 0.94)
+    dele = u >= 0.94
+    k_ins = rng.integers(1, 21, n)
+    k_del = rng.integers(1, 31, n)
+    rl = np.where(dele, 1 + k_del, 1).astype(np.int64)
+    al = np.where(ins, 1 + k_ins, 1).astype(np.int64)
+    tot = rl + al
+    off = np.zeros(n, dtype=np.int64)
+    if n:
+        np.cumsum(tot[:-1], out=off[1:])
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    code = rng.integers(0, 4, int(tot.sum()))
+    ref0 = code[off]
+    # SNV alt: one of the three other bases; indel alt/ref anchor = ref[0]
+    snv = ~(ins | dele)
+    code[(off + 1)[snv]] = (ref0[snv] + rng.integers(1, 4, int(snv.sum()))) % 4
+    code[(off + rl)[~snv]] = ref0[~snv]
+    heap = acgt[code]
+    ext = np.where(rng.random(n) < rs_frac, rng.integers(1, 2 * 10 ** 9, n), 0).astype(np.int64)
+    return dict(chrom=np.full(n, CHROM_NAMES.index("22"), dtype=np.uint8), pos=pos, allele_off=off,
+                ref_len=rl.astype(np.int32), alt_len=al.astype(np.int32),
+                heap=heap if heap.size else np.zeros(1, dtype=np.uint8), ext_id=ext)
+
+
+def c1_batch(n: int = C1_N, seed: int = 1, device="cpu"):
+    """C1 as a ``RecordBatch`` (numpy-generated, then moved to ``device``)."""
+    from .engine import RecordBatch
+    d = np_c1(n, seed)
+    return RecordBatch(**{k: torch.from_numpy(v).to(device) for k, v in d.items()})
+
+
 # ---- numpy (CPU) versions, oracle-sized ------------------------------------
 def np_point_snvs(n: int, seed: int = 2, lengths=None):
     rng = np.random.Generator(np.random.PCG64(seed))

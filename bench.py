@@ -35,6 +35,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "variants binned+keyed/sec (node) at 1/2/4/8 MI355X; % of HBM roofline"
 
 WORKLOADS = {
+    "c1": dict(n=1_100_000, desc="C1: chr22 1.1 M records (88% SNV / 6% ins / 6% del, seed 1; BASELINE "
+                                 "configs[0], the config the reference CPU path is quoted on): K2 end + bin, "
+                                 "K3 keep-first dedup, K7 primary-key + ltree-path text",
+               bytes_per=None, kernel="whole C1 step (K2 + K3 + K7)"),
     "c2": dict(n=100_000_000, desc="C2: synthetic GRCh38 SNVs, point-position bin assignment "
                                    "(BASELINE configs[1]); K1 bin_assign + L8 histogram",
                bytes_per=9, kernel="k_bin_assign4"),
@@ -94,6 +98,17 @@ def _cpu_load_worker(k):
     return recs, time.perf_counter() - t0
 
 
+def _cpu_c1_worker(k):
+    """Reference-structured C1 path per record (oracle.c1_port_loop): metaseq id,
+    short primary key, normalized alleles, end inference, cached bin lookup."""
+    from oracle import avdb_oracle as O
+    names, pos, refs, alts, exts = _SAMPLE[k]
+    bi = O.PortBinIndex(_TABLE)
+    t0 = time.perf_counter()
+    n = O.c1_port_loop(names, pos, refs, alts, exts, bi)
+    return n, time.perf_counter() - t0
+
+
 def _cpu_c5_worker(k):
     """Reference-structured C5 path per record: end inference (VariantAnnotator),
     cached bin lookup (BinIndex), primary key (short join, or the VRS Allele digest
@@ -145,6 +160,26 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
     except AttributeError:
         cores = os.cpu_count() or 1
     workers = max(1, min(16, cores))
+    if workload == "c1":
+        # the reference parallelises one process per chromosome file
+        # (load_vcf_file.py:307-313): C1 is one file (chr22), so one process
+        # over the whole C1 record set
+        d = synth.np_c1(synth.C1_N, seed=1)
+        heap = d["heap"].tobytes()
+        o, r, a = d["allele_off"].tolist(), d["ref_len"].tolist(), d["alt_len"].tolist()
+        _SAMPLE = [(["22"] * len(o), d["pos"].tolist(), [heap[x:x + y].decode() for x, y in zip(o, r)],
+                    [heap[x + y:x + y + z].decode() for x, y, z in zip(o, r, a)],
+                    ["rs%d" % e if e else None for e in d["ext_id"].tolist()])]
+        _TABLE = O.BinTable(GRCH38_LENGTHS)
+        n, t = _cpu_c1_worker(0)
+        return {"value": n / t, "unit": "variants/s", "cores": 1, "kind": "port",
+                "per_core": n / t,
+                "sample": f"the whole C1 set ({n:,} chr22 records), one process as the reference runs one "
+                          f"chromosome file (load_vcf_file.py:307-313); oracle.c1_port_loop = metaseq id + "
+                          f"short key + normalized alleles + end inference + PortBinIndex, {t:.2f} s. "
+                          f"Calibration (tools/calibrate_cpu_baseline.py, build container): the port takes "
+                          f"0.72x the verbatim reference's per-record time (5.47 vs 7.57 us), so this "
+                          f"baseline overstates the reference CPU path"}
     if workload == "load":
         # ~80 us per line in the port (calibrated: 0.82x the verbatim reference's time)
         per = int(seconds_per_worker / 80e-6)
@@ -222,7 +257,7 @@ def main():
     # CPU baseline first, before this process touches the GPU (its worker
     # processes are forked and must not inherit an initialised HIP runtime)
     want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and ri.world == 1
-                                          and a.workload in ("c2", "c3", "c5", "load"))
+                                          and a.workload in ("c1", "c2", "c3", "c5", "load"))
     cpu = cpu_baseline(a.workload, a.cpu_seconds) if (ri.rank == 0 and want_cpu) else None
     ri = D.init("nccl")
     dev = torch.device("cuda", ri.local)
@@ -247,6 +282,9 @@ def main():
     elif a.workload in ("c3", "c4"):
         chrom, start, end = synth.spans(n, seed=(3 if a.workload == "c3" else 4) + seed, device=dev,
                                         pieces=pieces, mix=a.workload)
+    elif a.workload == "c1":
+        batch = synth.c1_batch(n, seed=1, device=dev)
+        heap_bytes = int(batch.heap.numel())
     elif a.workload in ("vcf", "load"):
         tile = synth.vcf_text(min(VCF_TILE, n), seed=6 + seed)
         reps = -(-n // min(VCF_TILE, n))
@@ -277,8 +315,22 @@ def main():
         e1.record(stream)
         evs.setdefault(name, []).append((e0, e1))
 
+    def c1_step(record: bool):
+        box = {}
+        timed("record_prep", record, lambda: box.setdefault(
+            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr)))
+        timed("pk_dedup", record, lambda: box.setdefault(
+            "keep", eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3"))))
+        code_ = box["prep"][1]
+        timed("primary_keys", record, lambda: box.setdefault(
+            "kt", eng.primary_keys(batch, code=code_, out=last.get("kt"))))
+        last.setdefault("kt", box["kt"])
+        last["prep"], last["keep"] = box["prep"], box["keep"]
+
     def step(record: bool):
-        if a.workload in ("c2", "c3", "c4"):
+        if a.workload == "c1":
+            c1_step(record)
+        elif a.workload in ("c2", "c3", "c4"):
             timed("bin_assign", record, lambda: eng.bin_assign(
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
         elif a.workload == "vcf":
@@ -299,6 +351,8 @@ def main():
             timed("vrs_digest", record, lambda: eng.vrs_digest(batch, 50))
 
     last = {}
+    if a.workload == "c1":  # dedup workspace, allocated once
+        last["ws3"] = torch.empty(16384 + 4 * ((n + 3) & ~3), dtype=torch.uint8, device=dev)
     for _ in range(a.warmup):
         step(False)
     # the job-level collective once untimed, so any lazy RCCL setup for the
@@ -320,13 +374,23 @@ def main():
     elapsed = D.max_over_ranks(time.perf_counter() - t0, ri, device=dev)
     stage_ms = {k: float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])) for k, v in evs.items()}
     kname = {"c5": "record_prep", "vcf": "vcf_tokenize", "load": "format_write"}.get(a.workload, "bin_assign")
-    kern_ms = stage_ms[kname]
+    kern_ms = stage_ms.get(kname)
+    if a.workload == "c1":
+        kern_ms = elapsed * 1e3 / a.steps  # the whole step (launch-bound at 1.1 M records)
     if a.workload in ("vcf", "load"):
         n_lines, n = n, n_rec  # the unit is emitted variant records (per-ALT rows)
     total_records = n * ri.world * a.steps
     value = total_records / elapsed
 
-    if a.workload == "c5":
+    if a.workload == "c1":
+        # SURVEY.md §8d per-record bytes of the C5-style record path (in chrom 1 + pos 4 +
+        # heap_off 8 + rlen 4 + alen 4 + rs 4, the allele bytes, out bin 4 + end 4 +
+        # keep 1) plus the text K7 writes (keys + ltree paths)
+        kt = last["kt"]
+        rl, al = batch.ref_len.long(), batch.alt_len.long()
+        text = int(kt.key_off[n].item()) + int(kt.path_off[n].item())
+        bytes_per_launch = 34 * n + int((rl + al).sum().item()) + text
+    elif a.workload == "c5":
         # K2 algorithmic bytes per record: in chrom 1 + pos 4 + allele_off 8 + ref_len 4 +
         # alt_len 4, out end 4 + code 4 + status 1 (= 30 B), plus the allele bytes end
         # inference must read: through the first ref/alt mismatch (lcp + 1, capped at each
@@ -375,7 +439,7 @@ def main():
         "data": "synthetic (seeded GRCh38-shaped records generated on device)",
         "config": {"workload": W["desc"], "records_per_gpu": n, "records_total": n * ri.world,
                    "parallelism": f"dp{ri.world} (length-balanced 64 Mb genome pieces per rank)",
-                   "records_checked": int(node_ctr[20].item()) // max(1, a.steps),
+                   "records_processed": int(node_ctr[20].item()) // max(1, a.steps),
                    "stage_ms": stage_ms},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -383,20 +447,30 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "cpu_baseline": cpu,
     }
+    if a.workload == "c1":
+        kt = last["kt"]
+        out["dtype"] = "u8"
+        out["data"] = "synthetic C1 records (numpy PCG64 seed 1, synth.np_c1), resident in HBM"
+        out["config"].update(key_bytes=int(kt.key_off[n].item()), path_bytes=int(kt.path_off[n].item()),
+                             duplicates=int(node_ctr[21].item()) // max(1, a.steps))
+        out["roofline"]["note"] = ("achieved = SURVEY 8d record bytes + key/path text written / whole step "
+                                   "time; at 1.1 M records the step is launch-bound (7 launches), not HBM-bound")
+        if cpu:
+            out["cpu_baseline"]["reference_survey_per_core"] = "285-306 K variants/s (SURVEY.md 6, build container)"
     if a.workload == "load":
         fr = last["fr"]
         out["dtype"] = "u8"
         out["data"] = "synthetic dbSNP-shaped VCF text with INFO FREQ (numpy PCG64 lines tiled on the device)"
         out["config"].update(host_lines=int(fr.counters[27].item()), lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
                              copy_bytes_per_gpu=int(fr.copy.numel()), mapping_bytes_per_gpu=int(fr.mapping.numel()),
-                             records_checked=None)
+                             records_processed=None)
         out["roofline"]["note"] = ("achieved = K5 write-pass algorithmic bytes (text + line table + offsets "
                                    "+ per-record inputs + COPY/.mapping text written) / its HIP-event time")
     if a.workload == "vcf":
         out["dtype"] = "u8"
         out["data"] = "synthetic dbSNP-shaped VCF text (numpy PCG64 lines tiled on the device)"
         out["config"].update(lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
-                             records_checked=None)
+                             records_processed=None)
         out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (5 kernels + "
                                    "2 host syncs for the line and record totals)")
     if ri.rank == 0:

@@ -279,6 +279,32 @@ int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
                             size_t workspace_bytes, uint64_t* out_off, uint8_t* out, uint8_t* rec_state,
                             void* stream);
 
+/* ---- K7: primary keys and bin paths of a record batch as text -----------
+ * Replaces VariantPKGenerator.generate_primary_key (primary_key_generator.py:99-122,
+ * the record_primary_key column) and the ltree text BinIndex.find_bin_index
+ * returns (bin_index.py:75) for a whole record batch:
+ *   key  = <contig label> ':' pos ':' ref ':' alt [':' 'rs'<ext_id>]   (short)
+ *          <contig label> ':' pos ':' <digest>   [':' 'rs'<ext_id>]   (ref_len + alt_len
+ *          > max_seq_len; digest = avdb_vrs_digest output, 32 chars per record)
+ *   path = avdb_format_bin_path(chrom, bin_code) (bin_code NULL: no paths)
+ * ext_id is rendered 'rs' + decimal (canonical refSNP keys, < 2^63).
+ * Call with key_out == NULL first: exclusive offsets key_off[n+1] (and
+ * path_off[n+1]) from the SoA alone; then with key_out (and path_out), 8-byte
+ * aligned, of key_cap (path_cap) bytes >= the totals, which writes the text and
+ * key_state[n] (a text that would end past its cap is not written): */
+#define AVDB_KEY_OK 0
+#define AVDB_KEY_HOST 1          /* ':' in an allele (the reference raises ValueError),
+                                  * non-ASCII bytes, a contig without label or an
+                                  * interned (non-rs) external id: caller renders */
+#define AVDB_KEY_NEED_DIGEST 2   /* long record and digest == NULL */
+int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                      const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap,
+                      size_t heap_bytes, const uint64_t* ext_id, const uint32_t* bin_code,
+                      const char* digest, size_t n, uint32_t max_seq_len, void* workspace,
+                      size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off, uint8_t* key_out,
+                      size_t key_cap, uint8_t* path_out, size_t path_cap, uint8_t* key_state,
+                      void* stream);
+
 /* ---- K6: duplicate check against variants already loaded ---------------
  * Replaces VariantRecord.exists / SQL map_variants(id, firstHitOnly, checkAltVariants)
  * (Util/lib/python/database/variant.py:41,287-309) as used by --skipExisting

@@ -33,5 +33,8 @@ def c_oracle():
         lib.avdb_oracle_dedup_grouped.argtypes = [P, P, P, P, P, P, P, SZ, P]
         lib.avdb_oracle_dedup_grouped.restype = ctypes.c_uint64
         lib.avdb_oracle_sha512.argtypes = [P, SZ, P]
+        lib.avdb_oracle_vrs_digest.argtypes = [P, P, P, P, P, P, SZ, ctypes.c_uint32, ctypes.c_char_p, I, P, P]
+        lib.avdb_oracle_primary_keys.argtypes = [P, P, P, P, P, P, P, P, SZ, ctypes.c_uint32, P, P]
+        lib.avdb_oracle_primary_keys.restype = SZ
         _c = lib
     return _c

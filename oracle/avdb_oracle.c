@@ -167,3 +167,104 @@ void avdb_oracle_sha512(const uint8_t* msg, size_t len, uint8_t out[64]) {
   for (int k = 0; k < 8; ++k)
     for (int b = 0; b < 8; ++b) out[8 * k + b] = (uint8_t)(h[k] >> (56 - 8 * b));
 }
+
+/* ---- sha512t24u + VRS 1.x Allele digest (compute_vrs_identifier,
+ * primary_key_generator.py:147-165; serialisation as oracle/avdb_oracle.py
+ * vrs_allele_digest — PARITY UNPINNED vs vrs-python) ---- */
+static const char B64URL[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+
+static void t24u(const uint8_t* msg, size_t len, char out[32]) {
+  uint8_t h[64];
+  avdb_oracle_sha512(msg, len, h);
+  for (int g = 0; g < 8; ++g) {
+    uint32_t v = ((uint32_t)h[3 * g] << 16) | ((uint32_t)h[3 * g + 1] << 8) | h[3 * g + 2];
+    for (int k = 0; k < 4; ++k) out[4 * g + k] = B64URL[(v >> (18 - 6 * k)) & 63];
+  }
+}
+
+static size_t put_str(uint8_t* o, const char* s) {
+  size_t n = strlen(s);
+  memcpy(o, s, n);
+  return n;
+}
+
+static size_t put_u32(uint8_t* o, uint32_t v) {
+  char t[16];
+  int k = 0;
+  do { t[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+  for (int i = 0; i < k; ++i) o[i] = (uint8_t)t[k - 1 - i];
+  return (size_t)k;
+}
+
+/* digest_out[i*32..] for every record with rl+al > max_len (others untouched);
+ * seq_digest: 32 chars per contig.  buf: scratch of >= 256 + max alt bytes. */
+void avdb_oracle_vrs_digest(const uint8_t* chrom, const uint32_t* pos, const uint64_t* off,
+                            const uint32_t* rl, const uint32_t* al, const uint8_t* heap, size_t n,
+                            uint32_t max_len, const char* seq_digest, int nchrom, uint8_t* buf,
+                            char* digest_out) {
+  for (size_t i = 0; i < n; ++i) {
+    if ((uint64_t)rl[i] + al[i] <= max_len) continue;
+    if ((int)chrom[i] >= nchrom) { memset(digest_out + 32 * i, '?', 32); continue; }
+    const uint32_t s = pos[i] - 1, e = s + rl[i];
+    size_t k = 0;
+    k += put_str(buf + k, "{\"interval\":{\"end\":{\"type\":\"Number\",\"value\":");
+    k += put_u32(buf + k, e);
+    k += put_str(buf + k, "},\"start\":{\"type\":\"Number\",\"value\":");
+    k += put_u32(buf + k, s);
+    k += put_str(buf + k, "},\"type\":\"SequenceInterval\"},\"sequence_id\":\"");
+    memcpy(buf + k, seq_digest + 32 * chrom[i], 32);
+    k += 32;
+    k += put_str(buf + k, "\",\"type\":\"SequenceLocation\"}");
+    char loc[32];
+    t24u(buf, k, loc);
+    k = put_str(buf, "{\"location\":\"");
+    memcpy(buf + k, loc, 32);
+    k += 32;
+    k += put_str(buf + k, "\",\"state\":{\"sequence\":\"");
+    memcpy(buf + k, heap + off[i] + rl[i], al[i]);
+    k += al[i];
+    k += put_str(buf + k, "\",\"type\":\"LiteralSequenceExpression\"},\"type\":\"Allele\"}");
+    t24u(buf, k, digest_out + 32 * i);
+  }
+}
+
+/* primary keys (primary_key_generator.py:99-122): label:pos:ref:alt[:rs<ext>],
+ * or label:pos:<digest>[:rs<ext>] when rl+al > max_len; labels chr1..22,X,Y,M
+ * -> "1".."22","X","Y","M" (enums/chromosomes.py:9-38).  Keys concatenated in
+ * out, out_off[n+1]; returns the bytes written. */
+static const char* LABEL[25] = {"1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13",
+                                "14", "15", "16", "17", "18", "19", "20", "21", "22", "X", "Y", "M"};
+
+size_t avdb_oracle_primary_keys(const uint8_t* chrom, const uint32_t* pos, const uint64_t* off,
+                                const uint32_t* rl, const uint32_t* al, const uint8_t* heap,
+                                const uint64_t* ext, const char* digest, size_t n, uint32_t max_len,
+                                uint8_t* out, uint64_t* out_off) {
+  size_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    out_off[i] = k;
+    k += put_str(out + k, LABEL[chrom[i] < 25 ? chrom[i] : 0]);
+    out[k++] = ':';
+    k += put_u32(out + k, pos[i]);
+    out[k++] = ':';
+    if ((uint64_t)rl[i] + al[i] > max_len) {
+      memcpy(out + k, digest + 32 * i, 32);
+      k += 32;
+    } else {
+      memcpy(out + k, heap + off[i], rl[i]);
+      k += rl[i];
+      out[k++] = ':';
+      memcpy(out + k, heap + off[i] + rl[i], al[i]);
+      k += al[i];
+    }
+    if (ext && ext[i]) {
+      char t[24];
+      int d = 0;
+      uint64_t v = ext[i];
+      do { t[d++] = (char)('0' + v % 10); v /= 10; } while (v);
+      k += put_str(out + k, ":rs");
+      for (int q = 0; q < d; ++q) out[k++] = (uint8_t)t[d - 1 - q];
+    }
+  }
+  out_off[n] = k;
+  return k;
+}

@@ -315,6 +315,22 @@ def primary_key(chrom: str, pos: int, ref: str, alt: str, external_id: Optional[
     return ":".join(pk)
 
 
+def c1_port_loop(names, pos, refs, alts, exts, bin_index) -> int:
+    """Reference-structured per-record path SURVEY.md §6 measured the reference
+    on (the C1 CPU baseline), in the loader's order (vcf_variant_loader.py:
+    243-311): metaseq id (variant_annotator.py:124-126), short primary key
+    (primary_key_generator.py:99-122), normalized alleles (:309), end inference
+    (variant_annotator.py:36-79, which normalizes again) and the one-bin-cached
+    find_bin_index (bin_index.py:59-75), one record at a time."""
+    for c, p, r, a, e in zip(names, pos, refs, alts, exts):
+        metaseq_id(c, p, r, a)
+        primary_key(c, p, r, a, e)
+        normalized_alleles(r, a)
+        end, _ = infer_end(p, r, a)
+        bin_index.find_bin_index(c, p, end)
+    return len(pos)
+
+
 # ---------------------------------------------------------------------------
 # a9: sha512t24u (GA4GH computed-identifier digest) — the pinnable primitive.
 #   primary_key_generator.py:147-165 drops the 'ga4gh:VA.' prefix of the

@@ -27,8 +27,10 @@ Outputs (all small, gzip):
   vcf_lines.tsv.gz            VCF line -> parse_variant mapping + COPY prefix
   long_alleles.tsv.gz         long-allele records -> end + bin (PK unpinned)
   kat.json                    known-answer tests
+  c1_prefix.tsv.gz            BASELINE config C1 (annotatedvdb_amd.synth.np_c1, seed 1):
+                              the first 100,000 records -> end, bin path, primary key
 
-Usage:  python tests/golden/make_golden.py [--quick]
+Usage:  python tests/golden/make_golden.py [--quick] [--only all|load|c1]
 """
 
 from __future__ import annotations
@@ -666,6 +668,34 @@ def gen_long_alleles(VariantAnnotator, bi, n, rng):
     return rows
 
 
+def gen_c1_prefix(VariantAnnotator, bi, n):
+    """The C1 records (chr22; the generator the bench and the GPU
+    tests use) through the reference's per-alt path (vcf_variant_loader.py:
+    243-311): VariantAnnotator -> metaseq id, VariantPKGenerator.generate_primary_key
+    (short path; every C1 allele pair has len(ref)+len(alt) <= 50), then
+    infer_variant_end_location and BinIndex.find_bin_index(chrom, POS, end)."""
+    from AnnotatedVDB.Util.primary_key_generator import VariantPKGenerator
+    from annotatedvdb_amd import synth
+    pkg = VariantPKGenerator("GRCh38", "/nonexistent")
+    d = synth.np_c1(synth.C1_N, seed=1)
+    heap = d["heap"].tobytes()
+    rows = []
+    for i in range(n):
+        o, r, a = int(d["allele_off"][i]), int(d["ref_len"][i]), int(d["alt_len"][i])
+        ref, alt = heap[o:o + r].decode(), heap[o + r:o + r + a].decode()
+        pos = int(d["pos"][i])
+        ext = int(d["ext_id"][i])
+        va = VariantAnnotator(ref, alt, "22", pos)
+        pk = pkg.generate_primary_key(va.get_metaseq_id(), "rs%d" % ext if ext else None)
+        end = VariantAnnotator(ref, alt, "22", pos).infer_variant_end_location()
+        try:
+            b = bi.find_bin_index("22", pos, end)
+        except TypeError:
+            b = "TypeError"
+        rows.append((pk, end, b))
+    return rows
+
+
 def kats(VariantAnnotator, bi):
     cases = [
         ("1", 1510801, "C", "T", None),
@@ -705,8 +735,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
-    ap.add_argument("--only", choices=["all", "load"], default="all",
-                    help="'load': only the load-driver fixtures (vcf_load, display_attrs)")
+    ap.add_argument("--only", choices=["all", "load", "c1"], default="all",
+                    help="'load': only the load-driver fixtures (vcf_load, display_attrs); "
+                         "'c1': only the C1 prefix fixture")
     a = ap.parse_args()
     rng = random.Random(a.seed)
     install_stubs()
@@ -717,6 +748,11 @@ def main():
     bi = BinIndex(None, verbose=False)
 
     k = 0.1 if a.quick else 1.0
+    if a.only == "c1":
+        wtsv("c1_prefix.tsv.gz", ["primary_key", "end", "bin_index"],
+             gen_c1_prefix(VariantAnnotator, BinIndex(None, verbose=False), int(100000 * k)))
+        print("done")
+        return
     # load-driver fixtures: their own seed stream, so the older fixtures stay byte-identical
     lrng = random.Random(a.seed + 1)
     wtsv("vcf_load.tsv.gz", ["line", "error", "mapping", "copy_rows"],

@@ -1,0 +1,169 @@
+"""GPU parity for BASELINE config C1 (chr22, 1.1 M records) and K7 (primary
+keys + bin paths as text): the whole C1 batch through K2 / K3 / K7 vs the C
+oracle, and its 100,000-record prefix vs what the reference itself computed
+(tests/golden/c1_prefix.tsv.gz)."""
+
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from annotatedvdb_amd.chromosomes import CHROM_NAMES, length_table
+from oracle import avdb_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+LENGTHS = np.asarray(length_table(), dtype=np.uint32)
+FIELDS = ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap", "ext_id")
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def host(b):
+    return {k: getattr(b, k).cpu().numpy() for k in FIELDS}
+
+
+def oracle_keys(h, digest=None, max_len=50):
+    import oracle
+    n = len(h["pos"])
+    cap = int(h["ref_len"].astype(np.int64).sum() + h["alt_len"].sum()) + 80 * n + 8
+    out = np.zeros(cap, dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    dg = None if digest is None else digest.ctypes.data
+    oracle.c_oracle().avdb_oracle_primary_keys(
+        h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
+        h["alt_len"].ctypes.data, h["heap"].ctypes.data, h["ext_id"].ctypes.data, dg, n, max_len,
+        out.ctypes.data, off.ctypes.data)
+    return out[: int(off[n])].tobytes(), off
+
+
+def oracle_prep(h):
+    import oracle
+    n = len(h["pos"])
+    end, code, lcp = (np.empty(n, dtype=np.uint32) for _ in range(3))
+    status = np.empty(n, dtype=np.uint8)
+    keep = np.empty(n, dtype=np.uint8)
+    lib = oracle.c_oracle()
+    lib.avdb_oracle_record_prep(h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data,
+                                h["ref_len"].ctypes.data, h["alt_len"].ctypes.data, h["heap"].ctypes.data, n,
+                                LENGTHS.ctypes.data, len(LENGTHS), end.ctypes.data, code.ctypes.data,
+                                status.ctypes.data, lcp.ctypes.data)
+    lib.avdb_oracle_dedup_grouped(h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data,
+                                  h["ref_len"].ctypes.data, h["alt_len"].ctypes.data, h["heap"].ctypes.data,
+                                  h["ext_id"].ctypes.data, n, keep.ctypes.data)
+    return end, code, status, keep
+
+
+def paths_of(chrom, code):
+    """ltree text per record via the Python oracle (one format per distinct code)."""
+    memo = {}
+    out = []
+    for c, k in zip(chrom.tolist(), code.tolist()):
+        if k == O.BIN_NONE:
+            out.append(None)
+            continue
+        p = memo.get((c, k))
+        if p is None:
+            p = memo[(c, k)] = O.format_bin_path(CHROM_NAMES[c], k)
+        out.append(p)
+    return out
+
+
+def test_c1_whole_batch_vs_c_oracle(engine):
+    """All 1.1 M C1 records: end / bin / status (K2), keep (K3), key and path
+    text (K7) bit-exact vs the C oracle."""
+    from annotatedvdb_amd import synth
+    b = synth.c1_batch(device="cuda")
+    n = b.n
+    end, code, status, _ = engine.record_prep(b, want_lcp=False)
+    keep = engine.pk_dedup(b, grouped=True)
+    kt = engine.primary_keys(b, code=code)
+    h = host(b)
+    re_, rc, rs, rk = oracle_prep(h)
+    assert np.array_equal(u32(end), re_)
+    assert np.array_equal(u32(code), rc)
+    assert np.array_equal(status.cpu().numpy(), rs) and not rs.any()
+    assert np.array_equal(keep.cpu().numpy(), rk)
+    assert not kt.state[:n].cpu().numpy().any()
+    kb, ko = oracle_keys(h)
+    assert np.array_equal(kt.key_off.cpu().numpy().astype(np.uint64), ko)
+    assert kt.keys[: len(kb)].cpu().numpy().tobytes() == kb
+    po = kt.path_off.cpu().numpy()
+    pb = kt.paths[: int(po[n])].cpu().numpy().tobytes().decode()
+    exp = paths_of(h["chrom"], rc)
+    assert all(pb[po[i]:po[i + 1]] == exp[i] for i in range(n))
+
+
+def test_c1_prefix_vs_reference_golden(engine):
+    """The first 100,000 C1 records: GPU end, bin path and primary key equal the
+    reference's own VariantAnnotator / BinIndex / VariantPKGenerator output."""
+    from annotatedvdb_amd import synth
+    with gzip.open(os.path.join(GOLDEN, "c1_prefix.tsv.gz"), "rt") as fh:
+        fh.readline()
+        rows = [ln.rstrip("\n").split("\t") for ln in fh]
+    b = synth.c1_batch(device="cuda")
+    end, code, status, _ = engine.record_prep(b, want_lcp=False)
+    kt = engine.primary_keys(b, code=code)
+    keys, paths = kt.host(len(rows))
+    e = u32(end)
+    for i, (pk, ee, path) in enumerate(rows):
+        assert keys[i] == pk, i
+        assert str(e[i]) == ee, i
+        assert paths[i] == path, i
+
+
+def test_k7_keys_long_digests_and_ragged_batches(engine):
+    """K7 on ADSP-style batches (long alleles keyed by the K4 digest, rsids)
+    vs the C oracle, at batch sizes that end off every alignment."""
+    from annotatedvdb_amd import synth
+    digs = ["%032d" % (3 * i) for i in range(25)]
+    eng2 = type(engine)(0, sequence_digests=digs)
+    for n in (1, 7, 4099, 60001):
+        b = synth.alleles(n, seed=70 + n, long_frac=0.1)
+        dig, _ = eng2.vrs_digest(b, 50)
+        end, code, status, _ = eng2.record_prep(b, want_lcp=False)
+        kt = eng2.primary_keys(b, code=code, digest=dig)
+        h = host(b)
+        hd = dig.cpu().numpy().reshape(-1).copy()
+        kb, ko = oracle_keys(h, digest=hd)
+        assert not kt.state[:n].cpu().numpy().any(), n
+        assert np.array_equal(kt.key_off.cpu().numpy().astype(np.uint64), ko), n
+        assert kt.keys[: len(kb)].cpu().numpy().tobytes() == kb, n
+        _, paths = kt.host(n)
+        assert paths == paths_of(h["chrom"], u32(code)), n
+
+
+def test_k7_states_and_edge_records(engine):
+    """':' in an allele (the reference's ValueError), interned external ids,
+    long records without digests, unlabelled contigs and unmappable bins."""
+    from annotatedvdb_amd.engine import pack_records
+    from annotatedvdb_amd import _native as N
+    recs = [(0, 100, b"A", b"G", 0), (1, 5, b"A:C", b"A", 0), (2, 9, b"C", b"T", (1 << 63) | 4),
+            (3, 11, b"A" * 30, b"C" * 30, 7), (30, 12, b"A", b"C", 0), (24, 16569, b"T", b"TAA", 12),
+            (21, 50818468, b"G", b"GT", 0), (22, 1, b"", b"A", 5)]
+    b = pack_records([r[0] for r in recs], [r[1] for r in recs], [r[2] for r in recs], [r[3] for r in recs],
+                     [r[4] for r in recs])
+    b = b.to("cuda")
+    end, code, status, _ = engine.record_prep(b, want_lcp=False)
+    kt = engine.primary_keys(b, code=code)
+    st = kt.state[: b.n].cpu().tolist()
+    keys, paths = kt.host(b.n)
+    assert st == [N.KEY_OK, N.KEY_HOST, N.KEY_HOST, N.KEY_NEED_DIGEST, N.KEY_HOST, N.KEY_OK, N.KEY_OK, N.KEY_OK]
+    assert keys[0] == "1:100:A:G"
+    assert keys[5] == "M:16569:T:TAA:rs12" and paths[5] is None  # end 16570 > chrM
+    assert keys[6] == "22:50818468:G:GT"
+    assert keys[7] == "X:1::A:rs5"
+    c = u32(code)
+    assert paths[4] is None and c[4] == O.BIN_NONE            # contig 30: unknown
+    assert paths[6] is None and c[6] == O.BIN_NONE            # end past chr22's length
+    assert paths[0] == O.format_bin_path("1", int(c[0]))
+    # empty batch
+    e = pack_records([], [], [], []).to("cuda")
+    kt0 = engine.primary_keys(e)
+    assert int(kt0.key_off[0]) == 0

@@ -412,11 +412,21 @@ def test_c5_full_size_vs_c_oracle(engine):
     d, is_long = eng2.vrs_digest(b, 50)
     il = is_long.cpu().numpy()
     assert np.array_equal(il, (h["ref_len"].astype(np.int64) + h["alt_len"] > 50).astype(np.uint8))
+    # every long record's digest vs the C oracle's serialisation + SHA-512
+    exp = np.zeros(n * 32, dtype=np.uint8)
+    buf = np.zeros(8192, dtype=np.uint8)
+    oracle.c_oracle().avdb_oracle_vrs_digest(
+        h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
+        h["alt_len"].ctypes.data, h["heap"].ctypes.data, n, 50, "".join(digs).encode(), 25, buf.ctypes.data,
+        exp.ctypes.data)
+    got = d.cpu().numpy().reshape(n, 32)
     rows = np.nonzero(il)[0]
-    sel = rows[np.random.default_rng(5).choice(len(rows), 300, replace=False)]
-    raw = d[torch.from_numpy(sel).cuda()].cpu().numpy()
-    for k, i in enumerate(sel):
+    assert len(rows) > 1_000_000
+    assert np.array_equal(got[rows], exp.reshape(n, 32)[rows])
+    # and a sample through the Python restatement
+    sel = rows[np.random.default_rng(5).choice(len(rows), 100, replace=False)]
+    for i in sel:
         o, r, a = int(h["allele_off"][i]), int(h["ref_len"][i]), int(h["alt_len"][i])
-        exp = O.vrs_allele_digest(digs[h["chrom"][i]], int(h["pos"][i]), h["heap"][o:o + r].tobytes(),
-                                  h["heap"][o + r:o + r + a].tobytes())
-        assert raw[k].tobytes().decode() == exp
+        e = O.vrs_allele_digest(digs[h["chrom"][i]], int(h["pos"][i]), h["heap"][o:o + r].tobytes(),
+                                h["heap"][o + r:o + r + a].tobytes())
+        assert got[i].tobytes().decode() == e

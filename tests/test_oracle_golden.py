@@ -181,3 +181,72 @@ def test_float_repr_subset():
 def test_dedup_semantics():
     keys = ["1:5:A:G", "1:5:A:T", "1:5:A:G", "1:5:A:G:rs1", "1:5:A:G"]
     assert O.dedup_keep(keys) == [1, 1, 0, 1, 0]
+
+
+def test_c_oracle_vrs_digest_and_keys_match_python_oracle():
+    """The C oracle's long-key digest and primary-key text (used to check whole
+    GPU batches) equal the Python restatement record by record."""
+    import oracle
+    from annotatedvdb_amd import synth
+    d = synth.np_c1(3000, seed=11)
+    rng = np.random.default_rng(3)
+    # splice in long records (ref + alt > 50) so both key forms occur
+    n = len(d["pos"])
+    heap = bytearray(d["heap"].tobytes())
+    off, rl, al = d["allele_off"].copy(), d["ref_len"].copy(), d["alt_len"].copy()
+    for i in rng.choice(n, 300, replace=False):
+        r, a = int(rng.integers(1, 400)), int(rng.integers(51, 700))
+        off[i] = len(heap)
+        heap += bytes(rng.choice(list(b"ACGT"), r + a).astype(np.uint8))
+        rl[i], al[i] = r, a
+    heap_np = np.frombuffer(bytes(heap), dtype=np.uint8)
+    chrom = rng.integers(0, 25, n).astype(np.uint8)
+    digs = "".join("%032d" % (7 * i) for i in range(25))
+    lib = oracle.c_oracle()
+    dig = np.zeros(n * 32, dtype=np.uint8)
+    buf = np.zeros(4096, dtype=np.uint8)
+    lib.avdb_oracle_vrs_digest(chrom.ctypes.data, d["pos"].ctypes.data, off.ctypes.data, rl.ctypes.data,
+                               al.ctypes.data, heap_np.ctypes.data, n, 50, digs.encode(), 25, buf.ctypes.data,
+                               dig.ctypes.data)
+    keys = np.zeros(n * 200, dtype=np.uint8)
+    koff = np.zeros(n + 1, dtype=np.uint64)
+    lib.avdb_oracle_primary_keys(chrom.ctypes.data, d["pos"].ctypes.data, off.ctypes.data, rl.ctypes.data,
+                                 al.ctypes.data, heap_np.ctypes.data, d["ext_id"].ctypes.data, dig.ctypes.data,
+                                 n, 50, keys.ctypes.data, koff.ctypes.data)
+    kb = keys.tobytes()
+    for i in range(n):
+        o, r, a = int(off[i]), int(rl[i]), int(al[i])
+        ref, alt = bytes(heap[o:o + r]), bytes(heap[o + r:o + r + a])
+        label = CHROM_NAMES[chrom[i]]
+        dg = None
+        if r + a > 50:
+            c = int(chrom[i])
+            dg = O.vrs_allele_digest(digs[32 * c:32 * c + 32], int(d["pos"][i]), ref, alt)
+            assert dig[32 * i:32 * i + 32].tobytes().decode() == dg
+        e = int(d["ext_id"][i])
+        exp = O.primary_key(label, int(d["pos"][i]), ref.decode(), alt.decode(), "rs%d" % e if e else None, digest=dg)
+        assert kb[int(koff[i]):int(koff[i + 1])].decode() == exp
+
+
+def test_c1_prefix_golden():
+    """BASELINE config C1 (synth.np_c1, seed 1): the oracle's end, bin path and
+    primary key for the first 100,000 records equal what the reference computed
+    (tests/golden/c1_prefix.tsv.gz, make_golden.py --only c1)."""
+    from annotatedvdb_amd import synth
+    rows = read_tsv("c1_prefix.tsv.gz")
+    d = synth.np_c1(synth.C1_N, seed=1)
+    heap = d["heap"].tobytes()
+    L = GRCH38_LENGTHS["22"]
+    bi = O.PortBinIndex(O.BinTable(GRCH38_LENGTHS))
+    assert len(rows) == 100000
+    for i, row in enumerate(rows):
+        o, r, a = int(d["allele_off"][i]), int(d["ref_len"][i]), int(d["alt_len"][i])
+        ref, alt = heap[o:o + r].decode(), heap[o + r:o + r + a].decode()
+        pos, ext = int(d["pos"][i]), int(d["ext_id"][i])
+        end, _ = O.infer_end(pos, ref, alt)
+        assert str(end) == row["end"], i
+        assert O.primary_key("22", pos, ref, alt, "rs%d" % ext if ext else None) == row["primary_key"], i
+        c, st = O.bin_code(L, pos, end)
+        assert O.format_bin_path("22", c) == row["bin_index"], i
+        if i % 50 == 0:  # the reference-structured cached lookup agrees too
+            assert bi.find_bin_index("22", pos, end) == row["bin_index"]

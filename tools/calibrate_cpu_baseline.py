@@ -58,10 +58,50 @@ def calibrate_load(n_lines):
           f"port {tp / n_lines * 1e6:.2f} us/line ({n_lines / tp:,.0f} lines/s), port/ref time = {tp / tr:.3f}")
 
 
+def c1_records(n):
+    d = synth.np_c1(n, seed=1)
+    heap = d["heap"].tobytes()
+    o, r, a = d["allele_off"].tolist(), d["ref_len"].tolist(), d["alt_len"].tolist()
+    refs = [heap[x:x + y].decode() for x, y in zip(o, r)]
+    alts = [heap[x + y:x + y + z].decode() for x, y, z in zip(o, r, a)]
+    exts = ["rs%d" % e if e else None for e in d["ext_id"].tolist()]
+    return ["22"] * n, d["pos"].tolist(), refs, alts, exts
+
+
+def calibrate_c1(n):
+    """C1 per-record path: the verbatim reference (VariantAnnotator
+    + VariantPKGenerator.generate_primary_key + get_normalized_alleles (loader
+    :309) + infer_variant_end_location on a second annotator, as
+    vcf_parser.py:225-231 does + BinIndex.find_bin_index) vs
+    oracle.c1_port_loop, on the C1 records."""
+    from AnnotatedVDB.BinIndex.bin_index import BinIndex
+    from AnnotatedVDB.Util.primary_key_generator import VariantPKGenerator
+    from AnnotatedVDB.Util.variant_annotator import VariantAnnotator
+    names, pos, refs, alts, exts = c1_records(n)
+    pkg = VariantPKGenerator("GRCh38", "/nonexistent")
+    bi = BinIndex(None, verbose=False)
+    t0 = time.perf_counter()
+    for c, p, r, a, e in zip(names, pos, refs, alts, exts):
+        va = VariantAnnotator(r, a, c, p)
+        pkg.generate_primary_key(va.get_metaseq_id(), e)
+        va.get_normalized_alleles()  # vcf_variant_loader.py:309
+        end = VariantAnnotator(r, a, c, p).infer_variant_end_location()
+        bi.find_bin_index(c, p, end)
+    tr = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    O.c1_port_loop(names, pos, refs, alts, exts, O.PortBinIndex(O.BinTable(GRCH38_LENGTHS)))
+    tp = time.perf_counter() - t0
+    print(f"c1: reference {tr / n * 1e6:.3f} us/record ({n / tr:,.0f}/s), port {tp / n * 1e6:.3f} us/record "
+          f"({n / tp:,.0f}/s), port/ref time = {tp / tr:.3f}")
+
+
 def main():
     n = int(os.environ.get("N", 1_000_000))
     MG.install_stubs()
     MG.build_binindexref()
+    calibrate_c1(int(os.environ.get("N_C1", 1_100_000)))
+    if os.environ.get("C1_ONLY"):
+        return
     calibrate_load(int(os.environ.get("N_LINES", 100_000)))
     if os.environ.get("LOAD_ONLY"):
         return
