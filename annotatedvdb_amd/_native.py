@@ -48,6 +48,8 @@ CTR_SKIPPED_ALTS = 25
 CTR_DUP_ROWS = 26
 CTR_HOST_LINES = 27
 CTR_EXISTING = 28
+CTR_ADSP_UPDATES = 29
+FORMAT_ADSP = 1
 MATCH_NONE, MATCH_EXACT, MATCH_SWITCHED, MATCH_HOST = 0, 1, 2, 255
 LINE_GPU, LINE_HOST, LINE_SKIP = 0, 1, 2
 KEY_OK, KEY_HOST, KEY_NEED_DIGEST = 0, 1, 2
@@ -57,8 +59,8 @@ MAX_ALG_ID = 64
 class FormatOpts(ctypes.Structure):
     """avdb_format_opts (include/avdb.h)."""
     _fields_ = [("alg_id", ctypes.c_char_p), ("max_seq_len", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32), ("match", ctypes.c_void_p), ("match_kind", ctypes.c_void_p),
-                ("frag", ctypes.c_void_p), ("frag_off", ctypes.c_void_p)]
+                ("flags", ctypes.c_uint32), ("match", ctypes.c_void_p), ("match_kind", ctypes.c_void_p),
+                ("frag", ctypes.c_void_p), ("frag_off", ctypes.c_void_p), ("adsp_dup", ctypes.c_void_p)]
 
 # every symbol include/avdb.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED_SYMBOLS = [
@@ -73,7 +75,7 @@ EXPORTED_SYMBOLS = [
     "avdb_format_workspace_size", "avdb_vcf_format_size", "avdb_vcf_format_write",
     "avdb_display_attributes",
     "avdb_keyset_workspace_size", "avdb_keyset_build", "avdb_keyset_probe",
-    "avdb_primary_keys",
+    "avdb_primary_keys", "avdb_keyset_probe_text",
 ]
 
 
@@ -130,6 +132,7 @@ def _sig(lib):
     f.avdb_keyset_build.argtypes = [P, P, P, SZ, P, SZ, P]
     f.avdb_keyset_probe.argtypes = [P, P, SZ, P, P, SZ, P, P, P, P, P, P, SZ, SZ, I32, P, P, P, P]
     f.avdb_primary_keys.argtypes = [P, P, P, P, P, P, P, SZ, P, P, P, SZ, U32, P, SZ, P, P, P, SZ, P, SZ, P, P]
+    f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]
     for name in EXPORTED_SYMBOLS:
         if name not in ("avdb_last_error",):
             getattr(f, name).restype = I32

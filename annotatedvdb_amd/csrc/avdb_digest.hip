@@ -74,6 +74,9 @@ constexpr uint32_t nA0 = sizeof(AL0) - 1;
 constexpr uint32_t nA1 = sizeof(AL1) - 1;
 constexpr uint32_t nA2 = sizeof(AL2) - 1;
 constexpr uint32_t kAlPrefix = nA0 + AVDB_DIGEST_CHARS + nA1;  // ALT starts here
+#ifndef AVDB_SHA_UNROLL
+#define AVDB_SHA_UNROLL 0
+#endif
 static_assert(kAlPrefix == 68, "allele prefix");
 
 constexpr int kLongBuckets = 32;  // allele-message block counts (the last bucket takes the rest)
@@ -164,7 +167,13 @@ __device__ __forceinline__ void sha512_16(uint64_t& a, uint64_t& b, uint64_t& c,
 __device__ __forceinline__ void sha512_block(uint64_t* H, uint64_t* w) {
   uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], hh = H[7];
   sha512_16<false>(a, b, c, d, e, f, g, hh, w, 0);
+  // AVDB_SHA_UNROLL: all 80 rounds unrolled, so the round constants are
+  // immediates instead of scalar loads waited on in every loop trip
+#if AVDB_SHA_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
   for (int r = 16; r < 80; r += 16) sha512_16<true>(a, b, c, d, e, f, g, hh, w, r);
   H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += hh;
 }
@@ -539,15 +548,33 @@ __device__ __forceinline__ uint64_t prefix_word(const uint64_t* locw) {
 //           windows outside the suffix are zero)
 // and the final block's last word is the message length in bits.
 constexpr int kSufTab = 72;  // windows at offsets -8 .. 63 from the suffix start
-__device__ __forceinline__ void allele_block(uint64_t* w, uint32_t ab, const uint64_t* locw, const Heap& hp,
-                                             uint64_t altoff, uint32_t a, uint64_t TA, uint32_t nb,
-                                             const uint64_t* s_suf) {
-  const int64_t Q = int64_t(kAlPrefix) + a;  // first suffix byte
+// ALT word j of a block: 8 heap bytes from `at`.  CLAMP (a block reaching past
+// the heap end): the load starts at most at the last 8 heap bytes and is shifted
+// down (bytes past the heap end lie past the ALT and are masked off anyway).
+template <bool CLAMP>
+__device__ __forceinline__ uint64_t alt_word(const Heap& hp, uint64_t at) {
+  if constexpr (!CLAMP) {
+    return reinterpret_cast<g_u64u>(hp.lo + at)->v;
+  } else {
+    const uint64_t lim = (hp.hi - hp.lo) - 8;
+    const uint64_t c = at < lim ? at : lim;
+    const uint64_t y = reinterpret_cast<g_u64u>(hp.lo + c)->v;
+    return at - c >= 8 ? 0ull : y >> (8 * (at - c));
+  }
+}
+
+template <bool CLAMP>
+__device__ __forceinline__ void allele_words(uint64_t* w, uint32_t ab, const uint64_t* locw, const Heap& hp,
+                                             uint64_t altoff, int64_t Q, const uint64_t* s_suf) {
+  const bool FIRST = ab == 0;  // uniform across the wave
+  // word j's ALT bytes start at heap byte altoff + 128*ab + 8j - 68 (one base per
+  // block, immediate offsets); bytes past the ALT are loaded and masked off
+  const uint64_t b0 = altoff + 128 * uint64_t(ab) - kAlPrefix;  // ab >= 1: >= altoff + 60
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int64_t p = int64_t(ab) * 128 + 8 * j;  // first message byte of the word
     uint64_t le = 0;
-    if (j <= 8 && ab == 0) {
+    if (FIRST && j <= 8) {
       switch (j) {
         case 0: le = prefix_word<0>(locw); break;
         case 1: le = prefix_word<1>(locw); break;
@@ -557,20 +584,31 @@ __device__ __forceinline__ void allele_block(uint64_t* w, uint32_t ab, const uin
         case 5: le = prefix_word<5>(locw); break;
         case 6: le = prefix_word<6>(locw); break;
         case 7: le = prefix_word<7>(locw); break;
-        default: le = prefix_word<8>(locw); break;
+        case 8: le = prefix_word<8>(locw); break;
+        default: break;
       }
     }
-    if (p + 8 > int64_t(kAlPrefix) && p < Q) {
-      // block 0 word 8 holds prefix bytes 64..67 then ALT bytes 0..3
-      const uint64_t x = (j == 8 && ab == 0) ? heap_u64(hp, altoff) << 32
-                                               : heap_u64(hp, altoff + uint64_t(p - int64_t(kAlPrefix)));
-      le |= Q - p < 8 ? x & low_bytes_mask(uint32_t(Q - p)) : x;
+    if (!FIRST || j >= 8) {
+      // block 0 word 8: prefix bytes 64..67, then ALT bytes 0..3
+      const uint64_t x = (FIRST && j == 8) ? alt_word<CLAMP>(hp, altoff) << 32 : alt_word<CLAMP>(hp, b0 + 8 * j);
+      const int64_t nbytes = Q - p;  // ALT bytes from the word start (<= 0: none)
+      le |= nbytes >= 8 ? x : (nbytes > 0 ? x & low_bytes_mask(uint32_t(nbytes)) : 0ull);
     }
     int64_t t = p - Q + 8;
     t = t < 0 ? 0 : (t > kSufTab - 1 ? kSufTab - 1 : t);
     le |= s_suf[t];
     w[j] = __builtin_bswap64(le);
   }
+}
+
+__device__ __forceinline__ void allele_block(uint64_t* w, uint32_t ab, const uint64_t* locw, const Heap& hp,
+                                             uint64_t altoff, uint32_t a, uint64_t TA, uint32_t nb,
+                                             const uint64_t* s_suf) {
+  const int64_t Q = int64_t(kAlPrefix) + a;  // first suffix byte
+  if (hp.lo + altoff + 128 * uint64_t(ab) + 128 <= hp.hi)
+    allele_words<false>(w, ab, locw, hp, altoff, Q, s_suf);
+  else
+    allele_words<true>(w, ab, locw, hp, altoff, Q, s_suf);
   if (ab + 1 == nb) w[15] = TA * 8;  // (w[14], the high length word, is 0 from the table)
 }
 

@@ -96,23 +96,58 @@ __device__ __forceinline__ Dec dec_text(uint32_t v) {
   return Dec{nibbles_to_ascii(d, k < 8 ? k : 8), k > 8 ? nibbles_to_ascii(d >> 32, k - 8) : 0ull, k};
 }
 
-template <bool WRITE>
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+struct LdsImage {};  // constructor tag of the LDS sink
+
+// LDS = true (WRITE only): the sink renders into a workgroup's LDS image of its
+// output span instead of global memory, for a coalesced flush afterwards.  Every
+// LDS access is an aligned 8-byte word: the words a lane shares with its
+// neighbours (the first and the last of its span) are merged with ds_or_b64 into
+// the zeroed image, the words wholly inside its span are plain ds_write_b64.
+template <bool WRITE, bool LDS = false>
 struct Out {
   gbyte* base;
   uint64_t p, lo;
   bool bad;  // set by a formatter that cannot render its input (line goes to the host)
   __device__ __forceinline__ Out(uint8_t* b, uint64_t at)
       : base((gbyte*)b), p(at), lo(at), bad(false) {}
+  // LDS sink: `at` is the byte offset in the image (same alignment mod 8 as the
+  // global destination)
+  __device__ __forceinline__ Out(LdsImage, lds_u64* img, uint64_t at) : base(nullptr), p(at), lo(at), bad(false) {
+    if constexpr (LDS) {
+      pend.img = img;
+      pend.k = uint32_t(at & 7u);
+    }
+  }
   __device__ __forceinline__ uint32_t size() const { return uint32_t(p - lo); }
   struct Pending {  // WRITE: bytes [p-k, p) not yet stored
     uint64_t w = 0;
     uint32_t k = 0;
   };
+  struct LPending {  // LDS: bytes [p-k, p) of the current aligned word (the first
+    uint64_t w = 0;  // word's low bytes belong to the previous lane: zero here)
+    uint32_t k = 0;
+    bool first = true;
+    lds_u64* img = nullptr;
+  };
   struct None {};
-  [[no_unique_address]] std::conditional_t<WRITE, Pending, None> pend;
+  [[no_unique_address]] std::conditional_t<WRITE, std::conditional_t<LDS, LPending, Pending>, None> pend;
   // append t (1..8) bytes, little-endian in x (bytes of x at and above t are 0)
   __device__ __forceinline__ void append(uint64_t x, uint32_t t) {
-    if constexpr (WRITE) {
+    if constexpr (WRITE && LDS) {
+      const uint32_t k = pend.k;  // 0..7
+      pend.w |= x << (8 * k);
+      if (k + t >= 8) {
+        lds_u64* wp = pend.img + ((p - k) >> 3);
+        if (pend.first) __hip_atomic_fetch_or(wp, pend.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else *wp = pend.w;
+        pend.first = false;
+        pend.w = k ? x >> (64 - 8 * k) : 0ull;
+        pend.k = k + t - 8;
+      } else {
+        pend.k = k + t;
+      }
+    } else if constexpr (WRITE) {
       const uint32_t k = pend.k;  // 0..7
       pend.w |= x << (8 * k);
       if (k + t >= 8) {
@@ -128,7 +163,14 @@ struct Out {
   __device__ __forceinline__ void put(uint32_t c) { append(c & 0xFFu, 1); }
   // end of the line: store the buffered tail
   __device__ __forceinline__ void finish() {
-    if constexpr (WRITE) {
+    if constexpr (WRITE && LDS) {
+      // the last (partial) word may be shared with the next lane
+      if (pend.k && (p > lo || !pend.first))
+        __hip_atomic_fetch_or(pend.img + ((p - pend.k) >> 3), pend.w, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      pend.w = 0;
+      pend.k = 0;
+    } else if constexpr (WRITE) {
       for (uint32_t j = 0; j < pend.k; ++j) base[p - pend.k + j] = uint8_t(pend.w >> (8 * j));
       pend.w = 0;
       pend.k = 0;
@@ -539,6 +581,8 @@ struct FormatArgs {
   const uint8_t* match_kind;
   const uint8_t* frag;
   const uint64_t* frag_off;
+  const uint8_t* adsp_dup;  // ADSP: per record, its primary key is already loaded (optional)
+  bool adsp_col;            // ADSP: COPY rows end with is_adsp_variant = True
 };
 
 // allele bytes the GPU writes verbatim into JSON and Python repr text: printable
@@ -637,7 +681,7 @@ __device__ __forceinline__ O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint
 template <bool WRITE, class O, class CP>
 __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, CP s, size_t li,
                                O& oc, O& om, uint32_t* n_rows, uint32_t* n_skip,
-                               uint32_t* n_dup) {
+                               uint32_t* n_dup, uint32_t* n_upd) {
   if (L.flags & AVDB_VCF_COMMENT) return kLineSkip;
   if ((L.flags & kHostFlags) || L.chrom >= 25) return kLineHost;
   // Checks that only decide GPU vs HOST run in the SIZE pass; the WRITE pass
@@ -688,7 +732,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   }
   om.lit("\t[");
   uint64_t r = A.rec_off[li];
-  uint32_t nrec = 0, rows = 0, skip = 0, dups = 0;
+  uint32_t nrec = 0, rows = 0, skip = 0, dups = 0, upd = 0;
   for (uint32_t a0 = alt0, ai = 0; a0 <= alt1; ++ai) {
     const uint32_t a1 = find_byte(s, a0, alt1, ',');
     const CP alt = s + a0;
@@ -713,6 +757,12 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
         a0 = a1 + 1;
         continue;
       }
+    }
+    if (A.adsp_dup && A.adsp_dup[r]) {  // ADSP: key already loaded -> an is_adsp_variant UPDATE,
+      ++upd;                              // no COPY row, no mapping entry (vcf_variant_loader.py:303-307)
+      ++r;
+      a0 = a1 + 1;
+      continue;
     }
     const uint32_t st = A.status[r];
     if (st == AVDB_STATUS_UNKNOWN_CHROM || st == AVDB_STATUS_OUT_OF_RANGE) return kLineHost;
@@ -781,6 +831,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
       } else {
         oc.lit("NULL");
       }
+      if (A.adsp_col) oc.lit("#True");  // is_adsp_variant (vcf_variant_loader.py:336-337)
       oc.put('\n');
       ++rows;
     } else {
@@ -805,6 +856,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   *n_rows += rows;
   *n_skip += skip;
   *n_dup += dups;
+  *n_upd += upd;
   return kLineGpu;
 }
 
@@ -812,7 +864,7 @@ template <bool WRITE>
 __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs A) {
   __shared__ u32x4 s_text[kStage / 16];
   const Heap h = make_heap(A.text, A.text_bytes);
-  uint32_t rows = 0, skip = 0, dups = 0, hosts = 0;
+  uint32_t rows = 0, skip = 0, dups = 0, hosts = 0, upds = 0;
   for (size_t base = size_t(blockIdx.x) * kBlock; base < A.n_lines; base += size_t(gridDim.x) * kBlock) {
     const size_t last = base + kBlock < A.n_lines ? base + kBlock : A.n_lines;
     const avdb_vcf_line& Z = A.lines[last - 1];
@@ -827,7 +879,7 @@ __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs 
           const uint8_t st = A.line_state[li];
           if (st == kLineGpu) {
             Out<true> oc(A.copy_out, A.copy_off[li]), om(A.map_out, A.map_off[li]);
-            format_line<true>(A, L, s, li, oc, om, &rows, &skip, &dups);
+            format_line<true>(A, L, s, li, oc, om, &rows, &skip, &dups, &upds);
             oc.finish();
             om.finish();
           } else if (st == kLineHost) {
@@ -835,7 +887,7 @@ __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs 
           }
         } else {
           Out<false> oc(nullptr, 0), om(nullptr, 0);
-          const uint8_t st = format_line<false>(A, L, s, li, oc, om, &rows, &skip, &dups);
+          const uint8_t st = format_line<false>(A, L, s, li, oc, om, &rows, &skip, &dups, &upds);
           A.line_state[li] = st;
           A.copy_off[li] = st == kLineGpu ? oc.size() : 0;
           A.map_off[li] = st == kLineGpu ? om.size() : 0;
@@ -854,12 +906,14 @@ __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs 
       skip += __shfl_down(skip, d, kWave);
       dups += __shfl_down(dups, d, kWave);
       hosts += __shfl_down(hosts, d, kWave);
+      upds += __shfl_down(upds, d, kWave);
     }
     if (__lane_id() == 0) {
       if (rows) atomicAdd(&A.counters[AVDB_CTR_COPY_ROWS], (unsigned long long)rows);
       if (skip) atomicAdd(&A.counters[AVDB_CTR_SKIPPED_ALTS], (unsigned long long)skip);
       if (dups) atomicAdd(&A.counters[AVDB_CTR_DUP_ROWS], (unsigned long long)dups);
       if (hosts) atomicAdd(&A.counters[AVDB_CTR_HOST_LINES], (unsigned long long)hosts);
+      if (upds) atomicAdd(&A.counters[AVDB_CTR_ADSP_UPDATES], (unsigned long long)upds);
     }
   }
 }
@@ -932,16 +986,53 @@ __device__ __forceinline__ bool key_allele_ok(CP s, uint32_t n) {
   return swar_find(s, n, [](uint64_t x) { return (x & kHiBits) | bytes_eq_mask(x, ':'); }) == n;
 }
 
+// One stream's span of a 256-record tile is staged in LDS when it fits (always
+// for keys <= ~90 B and ltree paths <= 87 B; else the lanes write global memory
+// directly), then flushed with coalesced 16-byte stores: the lanes' texts are
+// adjacent, so a wave of per-lane 8-byte stores would touch 64 partly written
+// lines per instruction.
+constexpr uint32_t kKeyStage = 24 * 1024;  // bytes per workgroup (6 workgroups per CU)
+
+__device__ __forceinline__ void flush_tile(const lds_u64* img, uint8_t* out, uint64_t g0, uint64_t g1) {
+  const uint64_t a0 = g0 & ~uint64_t(15);
+  const uint64_t nchunks = (g1 - a0 + 15) / 16;
+  for (uint64_t q = threadIdx.x; q < nchunks; q += blockDim.x) {
+    const uint64_t a = a0 + 16 * q;
+    const uint64_t lo = img[2 * q], hi = img[2 * q + 1];
+    if (a >= g0 && a + 16 <= g1) {
+      __builtin_nontemporal_store(u32x4{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)},
+                                  reinterpret_cast<u32x4*>(out + a));
+    } else {  // a chunk shared with the neighbouring tiles: only this tile's bytes
+      for (uint32_t k = 0; k < 16; ++k) {
+        if (a + k >= g0 && a + k < g1) out[a + k] = uint8_t((k < 8 ? lo : hi) >> (8 * (k & 7)));
+      }
+    }
+  }
+}
+
 template <bool WRITE>
 __global__ __launch_bounds__(kBlock) void k_record_keys(KeyArgs A) {
-  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < A.n; i += size_t(gridDim.x) * blockDim.x) {
-    const uint32_t c = A.chrom[i], p = A.pos[i], r = A.rl[i], a = A.al[i];
-    const uint64_t e = A.ext ? A.ext[i] : 0ull;
-    const bool lng = uint64_t(r) + a > A.max_seq_len;
-    // SoA-decidable states; the WRITE pass adds the allele-byte checks
-    uint8_t st = AVDB_KEY_OK;
-    if (c >= uint32_t(A.n_chrom) || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
-    else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
+  __shared__ uint64_t s_img[WRITE ? kKeyStage / 8 : 1];
+  lds_u64* img = (lds_u64*)s_img;
+  for (size_t t0 = size_t(blockIdx.x) * blockDim.x; t0 < A.n; t0 += size_t(gridDim.x) * blockDim.x) {
+    const size_t i = t0 + threadIdx.x;
+    const bool live = i < A.n;
+    uint32_t c = 0, p = 0, r = 0, a = 0;
+    uint64_t e = 0;
+    bool lng = false;
+    uint8_t st = AVDB_KEY_HOST;
+    if (live) {
+      c = A.chrom[i];
+      p = A.pos[i];
+      r = A.rl[i];
+      a = A.al[i];
+      e = A.ext ? A.ext[i] : 0ull;
+      lng = uint64_t(r) + a > A.max_seq_len;
+      // SoA-decidable states; the WRITE pass adds the allele-byte checks
+      st = AVDB_KEY_OK;
+      if (c >= uint32_t(A.n_chrom) || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
+      else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
+    }
     auto key = [&](auto o) {  // primary_key_generator.py:106-122
       chrom_name(o, c);
       o.put(':');
@@ -962,23 +1053,53 @@ __global__ __launch_bounds__(kBlock) void k_record_keys(KeyArgs A) {
       return o;
     };
     if constexpr (WRITE) {
-      if (st == AVDB_KEY_OK && !lng) {
+      if (live && st == AVDB_KEY_OK && !lng) {
         const uint64_t off = A.off[i];
         if (off + r + a > A.heap_bytes || !key_allele_ok((glb_cp)(A.heap + off), r + a)) st = AVDB_KEY_HOST;
       }
-      if (st == AVDB_KEY_OK && A.key_off[i + 1] <= A.key_cap) {  // (cap: never write past the buffer)
-        Out<true> o = key(Out<true>(A.key_out, A.key_off[i]));
-        o.finish();
-      }
-      if (A.code) {
-        const uint32_t cd = A.code[i];
-        if (cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom) && A.path_off[i + 1] <= A.path_cap) {
-          Out<true> o = bin_path(Out<true>(A.path_out, A.path_off[i]), c, cd);
+      const size_t last = t0 + blockDim.x < A.n ? t0 + blockDim.x : A.n;
+      // stream 0: keys, stream 1: paths; each staged in LDS when its span fits
+      for (int sidx = 0; sidx < (A.code ? 2 : 1); ++sidx) {
+        const uint64_t* offs = sidx ? A.path_off : A.key_off;
+        uint8_t* out = sidx ? A.path_out : A.key_out;
+        const uint64_t cap = sidx ? A.path_cap : A.key_cap;
+        const uint64_t g0 = offs[t0], g1 = offs[last];
+        const uint64_t a0 = g0 & ~uint64_t(15);
+        const bool staged = g1 - a0 + 16 <= kKeyStage && g1 <= cap;
+        uint32_t cd = AVDB_BIN_NONE;
+        bool emit = false;
+        if (live) {
+          if (sidx == 0) {
+            emit = st == AVDB_KEY_OK && offs[i + 1] <= cap;  // (cap: never write past the buffer)
+          } else {
+            cd = A.code[i];
+            emit = cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom) && offs[i + 1] <= cap;
+          }
+        }
+        if (staged) {
+          for (uint64_t q = threadIdx.x; q < (g1 - a0 + 15) / 16; q += blockDim.x) {
+            img[2 * q] = 0;
+            img[2 * q + 1] = 0;
+          }
+          __syncthreads();
+          if (emit) {
+            Out<true, true> o(LdsImage{}, img, offs[i] - a0);
+            if (sidx == 0) o = key(o);
+            else o = bin_path(o, c, cd);
+            o.finish();
+          }
+          __syncthreads();
+          flush_tile(img, out, g0, g1);
+          __syncthreads();
+        } else if (emit) {
+          Out<true> o(out, offs[i]);
+          if (sidx == 0) o = key(o);
+          else o = bin_path(o, c, cd);
           o.finish();
         }
       }
-      A.state[i] = st;
-    } else {
+      if (live) A.state[i] = st;
+    } else if (live) {
       A.key_off[i] = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;
       if (A.code) {
         const uint32_t cd = A.code[i];
@@ -1043,6 +1164,10 @@ static int fill_args(FormatArgs* A, avdb_ctx* ctx, const uint8_t* text, size_t t
     A->match_kind = opts->match_kind;
     A->frag = opts->frag;
     A->frag_off = opts->frag_off;
+  }
+  if (opts) {
+    A->adsp_dup = opts->adsp_dup;
+    A->adsp_col = (opts->flags & AVDB_FORMAT_ADSP) != 0;
   }
   return AVDB_OK;
 }

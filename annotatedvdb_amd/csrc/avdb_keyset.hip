@@ -171,6 +171,63 @@ __global__ __launch_bounds__(kBlock) void k_keyset_probe(
   }
 }
 
+// K6 over arbitrary strings (e.g. the primary keys K7 rendered): one lane per
+// query string q[q_off[i] .. q_off[i+1]) (skipped where skip[i] != 0);
+// match[i] = index of the first equal key, or -1
+__device__ __forceinline__ bool str_equals(const uint8_t* a, uint64_t alen, const uint8_t* b, uint64_t blen) {
+  if (alen != blen) return false;
+  for (uint64_t i = 0; i < alen; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_keyset_probe_text(
+    const uint8_t* __restrict__ keys, const uint64_t* __restrict__ key_off, size_t n_keys,
+    const unsigned long long* __restrict__ tkey, const uint32_t* __restrict__ tidx, uint64_t mask,
+    const uint8_t* __restrict__ q, const uint64_t* __restrict__ q_off, const uint8_t* __restrict__ skip, size_t n,
+    int32_t* __restrict__ match, unsigned long long* __restrict__ g_ctr) {
+  uint32_t hits = 0, coll = 0;
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+    int32_t m = -1;
+    if (!skip || !skip[i]) {
+      const uint8_t* s = q + q_off[i];
+      const uint64_t len = q_off[i + 1] - q_off[i];
+      Hasher hs;
+      for (uint64_t b = 0; b < len; ++b) hs.put(s[b]);
+      const uint64_t h = hs.done();
+      uint64_t slot = mix(h ^ 0x5bd1e995ull) & mask;
+      for (;;) {
+        const unsigned long long t = tkey[slot];
+        if (t == 0ull) break;
+        if (t == h) {
+          const uint32_t k = tidx[slot];
+          if (str_equals(keys + key_off[k], key_off[k + 1] - key_off[k], s, len)) {
+            m = int32_t(k);
+          } else {  // a different key with the same 64-bit hash: exact scan
+            ++coll;
+            for (size_t j = 0; j < n_keys && m < 0; ++j)
+              if (str_equals(keys + key_off[j], key_off[j + 1] - key_off[j], s, len)) m = int32_t(j);
+          }
+          break;
+        }
+        slot = (slot + 1) & mask;
+      }
+    }
+    match[i] = m;
+    hits += m >= 0;
+  }
+  if (g_ctr) {
+    for (int d = 32; d > 0; d >>= 1) {
+      hits += __shfl_down(hits, d, kWave);
+      coll += __shfl_down(coll, d, kWave);
+    }
+    if (__lane_id() == 0) {
+      if (hits) atomicAdd(&g_ctr[AVDB_CTR_EXISTING], (unsigned long long)hits);
+      if (coll) atomicAdd(&g_ctr[AVDB_CTR_HASH_COLLISIONS], (unsigned long long)coll);
+    }
+  }
+}
+
 }  // namespace avdb
 
 using namespace avdb;
@@ -246,5 +303,31 @@ extern "C" int avdb_keyset_probe(avdb_ctx* ctx, const void* table, size_t table_
                      allele_off, ref_len, alt_len, heap, n, check_alt, match, kind,
                      reinterpret_cast<unsigned long long*>(counters));
   AVDB_LAUNCH_CHECK("k_keyset_probe");
+  return AVDB_OK;
+}
+
+extern "C" int avdb_keyset_probe_text(avdb_ctx* ctx, const void* table, size_t table_bytes, const uint8_t* keys,
+                                      const uint64_t* key_off, size_t n_keys, const uint8_t* q,
+                                      const uint64_t* q_off, const uint8_t* skip, size_t n, int32_t* match,
+                                      uint64_t* counters, void* stream) {
+  if (!ctx || !table || !key_off || !match || (n && !q_off)) {
+    avdb_set_error("avdb_keyset_probe_text: null argument");
+    return AVDB_EINVAL;
+  }
+  size_t need = 0;
+  avdb_keyset_workspace_size(n_keys, &need);
+  if (table_bytes < need) {
+    avdb_set_error("avdb_keyset_probe_text: table of %zu bytes required", need);
+    return AVDB_ERANGE;
+  }
+  if (n == 0) return AVDB_OK;
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  const uint64_t slots = keyset_slots(n_keys);
+  auto* tkey = static_cast<const unsigned long long*>(table);
+  auto* tidx = reinterpret_cast<const uint32_t*>(tkey + slots);
+  hipLaunchKernelGGL(k_keyset_probe_text, dim3(stream_grid(n, kBlock, 4096)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), keys, key_off, n_keys, tkey, tidx, slots - 1, q, q_off, skip,
+                     n, match, reinterpret_cast<unsigned long long*>(counters));
+  AVDB_LAUNCH_CHECK("k_keyset_probe_text");
   return AVDB_OK;
 }

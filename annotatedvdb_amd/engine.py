@@ -456,13 +456,16 @@ class Engine:
                    digest: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None,
                    alg_id="", max_seq_len: int = 50,
                    counters: Optional[torch.Tensor] = None, events: Optional[dict] = None,
-                   existing: Optional[tuple] = None) -> "FormatResult":
+                   existing: Optional[tuple] = None, adsp: bool = False,
+                   adsp_dup: Optional[torch.Tensor] = None) -> "FormatResult":
         """The load driver's COPY buffer and .mapping text for ``vb``'s lines
         (K5b: size pass, scans, one host sync for the totals, write pass)."""
         n = vb.n_lines
         s = self._stream()
         tp = N.ptr(vb.text) if vb.text.numel() else None
-        opts = N.FormatOpts(str(alg_id).encode(), int(max_seq_len), 0)
+        opts = N.FormatOpts(str(alg_id).encode(), int(max_seq_len), N.FORMAT_ADSP if adsp else 0)
+        if adsp_dup is not None:  # ADSP: records whose primary key is already loaded
+            opts.adsp_dup = N.ptr(adsp_dup)
         if existing is not None:  # (match, kind, frag, frag_off) device tensors from keyset_probe
             m, k, fr, fo = existing
             opts.match, opts.match_kind, opts.frag, opts.frag_off = N.ptr(m), N.ptr(k), N.ptr(fr), N.ptr(fo)
@@ -583,6 +586,17 @@ class Engine:
             N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, 1 if check_alt else 0, N.ptr(match), N.ptr(kind),
             N.ptr(counters), self._stream()))
         return match[:n], kind[:n]
+
+    def keyset_probe_text(self, table: torch.Tensor, keys: torch.Tensor, key_off: torch.Tensor,
+                          q: torch.Tensor, q_off: torch.Tensor, n: int, skip: Optional[torch.Tensor] = None,
+                          counters: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``match int32[n]``: first key equal to ``q[q_off[i]:q_off[i+1]]``, or -1."""
+        match = self.empty(max(1, n), torch.int32)
+        N.check("avdb_keyset_probe_text", self.lib.avdb_keyset_probe_text(
+            self.ctx, N.ptr(table), table.numel(), N.ptr(keys) if keys.numel() else None, N.ptr(key_off),
+            key_off.numel() - 1, N.ptr(q) if q.numel() else None, N.ptr(q_off), N.ptr(skip), n, N.ptr(match),
+            N.ptr(counters), self._stream()))
+        return match[:n]
 
     # -- formatting (host) ---------------------------------------------------
     def format_path(self, chrom_code: int, code: int) -> Optional[str]:

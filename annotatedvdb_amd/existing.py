@@ -18,6 +18,14 @@ its ranking and its result shape are **unpinned**.  A match here contributes a
 list of mapping entries (default ``[{'primary_key': pk, 'bin_index': bin}]`` of
 the existing row), which the loader appends exactly as the reference's
 ``primaryKeyMapping += matchedVariant`` does.
+
+ADSP loads additionally ask ``is_duplicate(recordPK)`` for every alt that was
+not skipped (``vcf_variant_loader.py:303-307``): the export's
+``record_primary_key`` column forms a second key set, probed with the primary
+keys K7 rendered (``avdb_keyset_probe_text``).  A primary key without an external
+id equals the metaseq id, which the ``--skipExisting`` check already looked up,
+so a key set over the exported primary keys answers the same as a
+``map_variants`` lookup would on a consistent export (unpinned, as above).
 """
 
 from __future__ import annotations
@@ -31,10 +39,14 @@ import torch
 class ExistingVariants(object):
     """Device key set over the metaseq ids of variants already loaded."""
 
-    def __init__(self, entries: Iterable[Tuple[str, Sequence[dict]]], engine=None, check_alt: bool = True):
+    def __init__(self, entries: Iterable[Tuple[str, Sequence[dict]]], engine=None, check_alt: bool = True,
+                 primary_keys: Optional[Iterable[str]] = None):
         from .engine import default_engine
         self._engine = engine or default_engine()
         self.check_alt = check_alt
+        self._pks: List[str] = list(primary_keys) if primary_keys is not None else []
+        self._pk_set = None
+        self._pk_dev = None
         ids: List[str] = []
         self._payload: List[List[dict]] = []
         for metaseq, match in entries:
@@ -68,14 +80,15 @@ class ExistingVariants(object):
         """``metaseq_id<TAB>record_primary_key<TAB>bin_index`` lines (an export of
         AnnotatedVDB.Variant, e.g. ``COPY (SELECT metaseq_id, record_primary_key,
         bin_index FROM AnnotatedVDB.Variant) TO STDOUT``)."""
-        entries = []
+        entries, pks = [], []
         with open(path) as fh:
             for line in fh:
                 f = line.rstrip("\n").split("\t")
                 if len(f) < 3 or f[0] == "metaseq_id":
                     continue
                 entries.append((f[0], [{"primary_key": f[1], "bin_index": f[2]}]))
-        return cls(entries, **kw)
+                pks.append(f[1])
+        return cls(entries, primary_keys=pks, **kw)
 
     def payload(self, k: int) -> List[dict]:
         return self._payload[k]
@@ -99,3 +112,27 @@ class ExistingVariants(object):
 
     def format_args(self, match, kind):
         return (match, kind, self.frag, self.frag_off)
+
+    # ---- primary keys (ADSP is_duplicate(recordPK)) ---------------------------
+    def has_primary_key(self, pk: str) -> bool:
+        if self._pk_set is None:
+            self._pk_set = set(self._pks)
+        return pk in self._pk_set
+
+    def _pk_table(self):
+        if self._pk_dev is None:
+            kb = [x.encode("utf-8") for x in self._pks]
+            off = np.zeros(len(kb) + 1, dtype=np.int64)
+            np.cumsum(np.fromiter((len(x) for x in kb), dtype=np.int64, count=len(kb)), out=off[1:])
+            dev = self._engine.device
+            keys = torch.from_numpy(np.frombuffer(b"".join(kb) or b"\0", dtype=np.uint8).copy()).to(dev)
+            key_off = torch.from_numpy(off).to(dev)
+            self._pk_dev = (keys, key_off, self._engine.keyset_build(keys, key_off))
+        return self._pk_dev
+
+    def probe_primary_keys(self, text: torch.Tensor, text_off: torch.Tensor, n: int,
+                           skip: Optional[torch.Tensor] = None, counters=None) -> torch.Tensor:
+        """K6 over strings: ``match int32[n]`` (-1: not loaded) for the keys
+        ``text[text_off[i]:text_off[i+1]]`` (rows with ``skip[i]`` not probed)."""
+        keys, key_off, table = self._pk_table()
+        return self._engine.keyset_probe_text(table, keys, key_off, text, text_off, n, skip, counters)

@@ -25,8 +25,13 @@ when a key cannot be built (e.g. ``':'`` inside an allele breaks
 ladder :234-256), ``TypeError`` when the location has no bin
 (bin_index.py:75).  ``--skipExisting`` checks a key set of the rows already
 loaded (``existing.ExistingVariants``, K6) instead of the database; the other
-database-backed features (ADSP duplicate updates, ``update_existing``, COPY
-into Postgres) are outside the bin/key path and raise ``NotImplementedError``.  Display attributes come from
+database-backed features (``update_existing``, COPY into Postgres) are outside
+the bin/key path and raise ``NotImplementedError``.  The ADSP datasource checks
+every alt's primary key against the rows already loaded (``is_duplicate(recordPK)``,
+vcf_variant_loader.py:303-307) through the same exported key set (K7 keys, K6
+text probe): a loaded key becomes an ``is_adsp_variant`` update in
+``update_buffer()`` instead of a COPY row, and COPY rows carry the extra
+``is_adsp_variant`` column (:336-337).  Display attributes come from
 K5a (``avdb_display_attributes``); alleles must be ASCII (VCF 4.x REF/ALT).
 """
 
@@ -81,14 +86,29 @@ class VCFVariantLoader(object):
         self._vcf_header_fields = None
         self.last_load_stats = None
         self._match = None
+        self._adsp_dup = None
+        self._update_buffer = []
         self._initialize_counters()
         self.initialize_copy_buffer()
         self.logger.info(type(self).__name__ + " initialized")
 
     # ---- configuration (variant_loader.py / vcf_variant_loader.py) ---------
-    def initialize_bin_indexer(self, gusConfigFile):
+    def initialize_bin_indexer(self, gusConfigFile, genomeBuild=None, chromosome_lengths=None):
+        """variant_loader.py:357-362.  The reference's bins come from whatever
+        assembly its BinIndexRef table was built for; here the chromosome lengths
+        follow ``genomeBuild`` (default: the PK generator's build, which
+        load_vcf_file.py:62-63 initializes first; else GRCh38) or an explicit
+        ``chromosome_lengths`` table."""
         from .bin_index import BinIndex
-        self._bin_indexer = BinIndex(gusConfigFile, verbose=False, device=self._device)
+        from .chromosomes import ASSEMBLIES
+        build = genomeBuild
+        if build is None and self._pk_generator is not None:
+            build = self._pk_generator.genome_build()
+        build = build or "GRCh38"
+        if chromosome_lengths is None and build not in ASSEMBLIES:
+            raise ValueError("unknown genome build %r: pass chromosome_lengths (one per chr1..22,X,Y,M)" % build)
+        self._bin_indexer = BinIndex(gusConfigFile, verbose=False, assembly=build if build in ASSEMBLIES
+                                     else "GRCh38", chromosome_lengths=chromosome_lengths, device=self._device)
         self._engine = self._bin_indexer._engine
 
     def initialize_pk_generator(self, genomeBuild, seqrepoProxyPath, **kw):
@@ -230,6 +250,18 @@ class VCFVariantLoader(object):
     def load_variants(self):
         raise NotImplementedError("COPY into Postgres is out of scope; read copy_buffer()")
 
+    # ---- ADSP update buffer (variant_loader.py:290-300; vcf_variant_loader.py:222-226)
+    def update_buffer(self, sizeOnly=False):
+        """``(record_primary_key, 'chr' + chromosome)`` per ADSP alt whose key was
+        already loaded (the values of the is_adsp_variant UPDATE)."""
+        return len(self._update_buffer) if sizeOnly else self._update_buffer
+
+    def reset_update_buffer(self):
+        self._update_buffer = []
+
+    def update_variants(self):
+        raise NotImplementedError("UPDATE in Postgres is out of scope; read update_buffer()")
+
     def close(self):
         self.close_copy_buffer()
 
@@ -258,8 +290,6 @@ class VCFVariantLoader(object):
             raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
         if flags is not None:
             raise NotImplementedError("update flags are a database-update feature; out of scope")
-        if self.is_adsp():
-            raise NotImplementedError("ADSP loads check duplicates in the database (is_duplicate); out of scope")
 
         # ---- phase 1: host parse (stops at the first parse error) --------------
         parsed = []  # (entry, variant) | ("skip",) | ("error", exc)
@@ -310,13 +340,9 @@ class VCFVariantLoader(object):
         from types import SimpleNamespace
         if self._bin_indexer is None or self._pk_generator is None:
             raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
-        if self.is_adsp():
-            raise NotImplementedError("ADSP loads check duplicates in the database (is_duplicate); out of scope")
         if not self.resume_load() or self._chromosome_map is not None or self._vcf_header_fields:
             # resume / chromosome maps / custom headers: exact per-line semantics
-            lines = [ln.rstrip() for ln in bytes(text).decode("utf-8").split("\n")
-                     if ln and not ln.startswith("#")]
-            return self.parse_variants(lines, errors=errors, dedup=dedup)
+            return self.parse_variants(_data_lines(bytes(text)), errors=errors, dedup=dedup)
         raw = bytes(text)
         eng = self._engine
         vb = eng.vcf_tokenize(raw)
@@ -399,51 +425,76 @@ class VCFVariantLoader(object):
         return self._emit(parsed, recs, paths, pks, keep, disp, errors)
 
     def load_vcf_text(self, text, dedup: bool = False, errors: str = "raise",
-                      batch_bytes: int = 256 << 20) -> str:
+                      batch_bytes: int = 256 << 20, mapping_out=None) -> str:
         """The load driver (Load/bin/load_vcf_file.py:101-119) on the GPU for a
         block of VCF text: appends every COPY row to ``copy_buffer()`` and
         returns the .mapping text (one ``id<TAB>[{...}]`` line per data line).
         Text larger than ``batch_bytes`` runs as consecutive device batches cut at
         line boundaries (bounded HBM and host memory); ``dedup`` (keep-first per
-        primary key, our addition) applies within each batch."""
+        primary key, our addition) applies within each batch.
+
+        ``mapping_out`` (a file-like ``write``) receives the .mapping text as each
+        batch completes, as the driver prints each line's mapping before reading
+        the next (load_vcf_file.py:116-117).  When a line raises
+        (``errors='raise'``), everything before it — COPY rows, .mapping text,
+        counters — has been emitted exactly as a loop of ``parse_variant`` would
+        have; the .mapping text of the lines before it is also attached to the
+        exception as ``avdb_partial_mapping``."""
         raw = bytes(text)
-        if len(raw) <= batch_bytes:
-            return self._load_vcf_batch(raw, dedup, errors)
-        out = []
+        done = []
+
+        def emit(t):
+            if mapping_out is not None:
+                mapping_out.write(t)
+            done.append(t)
+
         i = 0
-        while i < len(raw):
-            j = min(len(raw), i + batch_bytes)
-            if j < len(raw):
-                k = raw.rfind(b"\n", i, j)
-                if k >= i:
-                    j = k + 1
-                else:  # one line longer than a batch
-                    k = raw.find(b"\n", j)
-                    j = len(raw) if k < 0 else k + 1
-            out.append(self._load_vcf_batch(raw[i:j], dedup, errors))
-            i = j
-        return "".join(out)
+        try:
+            while i < len(raw) or (i == 0 and not raw):
+                j = min(len(raw), i + batch_bytes)
+                if j < len(raw):
+                    k = raw.rfind(b"\n", i, j)
+                    if k >= i:
+                        j = k + 1
+                    else:  # one line longer than a batch
+                        k = raw.find(b"\n", j)
+                        j = len(raw) if k < 0 else k + 1
+                emit(self._load_vcf_batch(raw[i:j], dedup, errors))
+                i = j
+                if not raw:
+                    break
+        except Exception as err:  # noqa: BLE001 — re-raised with the partial mapping text
+            part = getattr(err, "avdb_partial_mapping", "")
+            if mapping_out is not None and part:
+                mapping_out.write(part)
+            try:
+                err.avdb_partial_mapping = "".join(done) + part
+            except AttributeError:
+                pass
+            raise
+        return "".join(done)
 
     def _load_vcf_batch(self, raw: bytes, dedup: bool, errors: str) -> str:
         """One device batch of :meth:`load_vcf_text`.
 
         K0 tokenizes, K2 infers ends and bins, K4 digests long keys, K3 marks
-        in-batch duplicates when ``dedup``, and K5 writes both texts on the
-        device.  Lines K5 leaves to the host (``AVDB_LINE_HOST``) are rendered
-        through ``parse_variants`` and spliced in at their position; with
-        ``errors='raise'`` the first failing line raises after everything before
-        it (and its own earlier alts) was emitted, as a loop of
-        ``parse_variant`` would."""
+        in-batch duplicates when ``dedup``, K6 checks the rows already loaded
+        (``--skipExisting``: metaseq ids; ADSP: the K7 primary keys), and K5
+        writes both texts on the device.  Lines K5 leaves to the host
+        (``AVDB_LINE_HOST``) are rendered through ``parse_variants`` and spliced
+        in at their position; with ``errors='raise'`` the first failing line
+        raises after everything before it (and its own earlier alts) was
+        emitted, as a loop of ``parse_variant`` would."""
         import torch
         from .engine import VCF_HOST_FLAGS
         from . import _native as N
         if self._bin_indexer is None or self._pk_generator is None:
             raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
-        if self.is_adsp():
-            raise NotImplementedError("ADSP loads check duplicates in the database (is_duplicate); out of scope")
-        if not self.resume_load() or self._chromosome_map is not None or self._vcf_header_fields:
-            lines = [ln.rstrip() for ln in raw.decode("utf-8").split("\n") if ln and not ln.startswith("#")]
-            out = self.parse_variants(lines, errors=errors, dedup=dedup)
+        if (not self.resume_load() or self._chromosome_map is not None or self._vcf_header_fields
+                or (self.is_adsp() and self._existing is None)):
+            # resume / chromosome maps / custom headers / ADSP without a validator
+            # (the reference's is_duplicate raises on it): exact per-line semantics
+            out = self.parse_variants(_data_lines(raw), errors=errors, dedup=dedup)
             return "".join("".join("%s\t%s\n" % kv for kv in o.items()) for o in out
                            if isinstance(o, dict))
         eng = self._engine
@@ -464,12 +515,19 @@ class VCFVariantLoader(object):
         if db.n and bool(((db.ref_len + db.alt_len) > mx).any()) and self._pk_generator.has_sequence_digests():
             digest, _ = self._pk_generator._eng().vrs_digest(db, mx)
         keep = eng.pk_dedup(db, grouped=False) if dedup and db.n else None
-        ex = None
+        ex = m_dev = None
         if self._existing is not None and db.n:  # --skipExisting: K6 hash join, consumed by K5
-            m, k = self._existing.probe(db)
-            ex = self._existing.format_args(m, k)
+            m_dev, k = self._existing.probe(db)
+            ex = self._existing.format_args(m_dev, k)
+        adsp_dup = kt = None
+        if self.is_adsp() and db.n:
+            # is_duplicate(recordPK): the primary keys as text (K7), probed against the
+            # exported keys (K6); keys K7 cannot render belong to host lines
+            kt = eng.primary_keys(db, digest=digest, max_seq_len=mx)
+            pm = self._existing.probe_primary_keys(kt.keys, kt.key_off, db.n, skip=kt.state[: db.n])
+            adsp_dup = (pm >= 0).to(torch.uint8)
         fr = eng.vcf_format(vb, end, code, status, digest, keep, alg_id=_xstr(self._alg_invocation_id),
-                            max_seq_len=mx, existing=ex)
+                            max_seq_len=mx, existing=ex, adsp=self.is_adsp(), adsp_dup=adsp_dup)
         state = fr.line_state.cpu().numpy()
         copy_off = fr.copy_off.cpu().numpy()
         map_off = fr.map_off.cpu().numpy()
@@ -478,17 +536,44 @@ class VCFVariantLoader(object):
         ctr = fr.counters.cpu().numpy()
         host = np.nonzero(state == N.LINE_HOST)[0]
         n_data = int(np.count_nonzero(state != N.LINE_SKIP))
-        # GPU-rendered lines' counters (vcf_variant_loader.py:279,344; variant_loader.py:94)
-        self.increment_counter("line", n_data - len(host))
-        self.increment_counter("variant", int(ctr[N.CTR_COPY_ROWS]))
-        self.increment_counter("skipped", int(ctr[N.CTR_SKIPPED_ALTS]))
-        self.increment_counter("duplicates", int(ctr[N.CTR_DUP_ROWS]))
+        rec_off = vb.rec_off.cpu().numpy()
+        # ADSP updates of GPU-rendered lines, in record order: (line, pk, 'chr' + chrom)
+        gpu_updates = []
+        if adsp_dup is not None:
+            dup = adsp_dup.cpu().numpy().astype(bool)
+            if m_dev is not None:
+                dup &= m_dev.cpu().numpy() < 0  # skipped as existing first (vcf_variant_loader.py:285-291)
+            rec_line = vb.rec_line.cpu().numpy()
+            idx = np.nonzero(dup & (state[rec_line] == N.LINE_GPU))[0]
+            if len(idx):
+                ko = kt.key_off.cpu().numpy()
+                kb = kt.keys.cpu().numpy().tobytes()
+                ch = db.chrom.cpu().numpy()
+                from .chromosomes import CHROM_NAMES
+                gpu_updates = [(int(rec_line[i]), kb[ko[i]:ko[i + 1]].decode("ascii"), "chr" + CHROM_NAMES[ch[i]])
+                               for i in idx.tolist()]
         self.last_load_stats = {"lines": n_data, "gpu_lines": n_data - len(host), "host_lines": len(host),
                                 "copy_bytes": len(copy_raw), "mapping_bytes": len(map_raw)}
+
+        def add_gpu_counters(upto=None):
+            """counters of the GPU-rendered lines (vcf_variant_loader.py:279,288,306,344;
+            variant_loader.py:94), or of those before line ``upto``"""
+            if upto is None:
+                self.increment_counter("line", n_data - len(host))
+                self.increment_counter("variant", int(ctr[N.CTR_COPY_ROWS]))
+                self.increment_counter("skipped", int(ctr[N.CTR_SKIPPED_ALTS]))
+                self.increment_counter("duplicates", int(ctr[N.CTR_DUP_ROWS]))
+                self.increment_counter("update", int(ctr[N.CTR_ADSP_UPDATES]))
+                return
+            self._add_partial_counters(vb, state, rec_off, copy_raw[: int(copy_off[upto])], keep, m_dev,
+                                       adsp_dup, upto)
+
+        u = 0  # next GPU update to flush
         if len(host) == 0:
             self._copy_buffer.write(copy_raw)
+            self._update_buffer.extend(x[1:] for x in gpu_updates)
+            add_gpu_counters()
             return map_raw
-        rec_off = vb.rec_off.cpu().numpy()
         keep_h = keep.cpu().numpy() if keep is not None else None
         # the host lines' table rows in one transfer
         Lh = vb.lines[: n * 80].view(n, 80)[torch.from_numpy(host).to(eng.device)].cpu().numpy()
@@ -496,10 +581,13 @@ class VCFVariantLoader(object):
         maps = []
         c0 = m0 = 0
         for hi, li in enumerate(host.tolist()):
-            # GPU text of the lines before this one
+            # GPU text (and ADSP updates) of the lines before this one
             self._copy_buffer.write(copy_raw[c0:copy_off[li]])
             maps.append(map_raw[m0:map_off[li]])
             c0, m0 = int(copy_off[li]), int(map_off[li])
+            while u < len(gpu_updates) and gpu_updates[u][0] < li:
+                self._update_buffer.append(gpu_updates[u][1:])
+                u += 1
             st, ln = int(Lh[hi, 0]), int(Lh[hi, 1] & 0xFFFFFFFF)
             line = raw[st:st + ln].decode("utf-8")
             kov = None if keep_h is None else keep_h[rec_off[li]:rec_off[li + 1]]
@@ -507,13 +595,47 @@ class VCFVariantLoader(object):
                 res = self.parse_variants([line], errors="raise", keep_override=kov)[0]
             except Exception as err:  # noqa: BLE001
                 if errors == "raise":
+                    add_gpu_counters(upto=li)
+                    try:
+                        err.avdb_partial_mapping = "".join(maps)
+                    except AttributeError:
+                        pass
                     raise
                 maps.append("")
                 continue
             maps.append("".join("%s\t%s\n" % kv for kv in res.items()))
         self._copy_buffer.write(copy_raw[c0:])
         maps.append(map_raw[m0:])
+        self._update_buffer.extend(x[1:] for x in gpu_updates[u:])
+        add_gpu_counters()
         return "".join(maps)
+
+    def _add_partial_counters(self, vb, state, rec_off, copy_text, keep, match, adsp_dup, upto):
+        """Counters of the GPU-rendered lines before line ``upto`` (the failing
+        line), from the per-line / per-record arrays."""
+        from . import _native as N
+        n = vb.n_lines
+        L = vb.lines_host()
+        gl = np.nonzero(state[:upto] == N.LINE_GPU)[0]
+        self.increment_counter("line", len(gl))
+        self.increment_counter("variant", copy_text.count("\n"))
+        r_end = int(rec_off[upto])
+        on_gpu = np.zeros(r_end, dtype=bool)
+        for li in gl.tolist():
+            on_gpu[int(rec_off[li]):int(rec_off[li + 1])] = True
+        skipped = int((L["n_alt"][gl].astype(np.int64) - L["n_rec"][gl]).sum())
+        matched = np.zeros(r_end, dtype=bool)
+        if match is not None:
+            matched = match[:r_end].cpu().numpy() >= 0
+        skipped += int((matched & on_gpu).sum())
+        upd = np.zeros(r_end, dtype=bool)
+        if adsp_dup is not None:
+            upd = (adsp_dup[:r_end].cpu().numpy() != 0) & ~matched
+        self.increment_counter("update", int((upd & on_gpu).sum()))
+        self.increment_counter("skipped", skipped)
+        if keep is not None:
+            dup = (keep[:r_end].cpu().numpy() == 0) & ~matched & ~upd
+            self.increment_counter("duplicates", int((dup & on_gpu).sum()))
 
     def _patch_host_records(self, raw, vb, line_ids):
         """Host resolution of K0-flagged lines' chrom / pos / refSNP key in the
@@ -591,7 +713,8 @@ class VCFVariantLoader(object):
             m, k = self._existing.probe(db)
             m, k = m.cpu().numpy(), k.cpu().numpy()
             for i in np.nonzero(k == 255)[0]:
-                m[i] = self._existing.resolve_host(recs[i][2])
+                # (a record whose key cannot be built raises before this check)
+                m[i] = self._existing.resolve_host(recs[i][2]) if recs[i][3] is None else -1
             self._match = m
         # primary keys (short: text; long: K4 digests in one launch)
         items, idx = [], []
@@ -609,6 +732,10 @@ class VCFVariantLoader(object):
                     pks[i] = self._pk_generator.generate_primary_keys([it])[0]
                 except ValueError as err:
                     recs[i][3] = err
+        # ADSP: is_duplicate(recordPK) against the exported keys (vcf_variant_loader.py:303-307)
+        self._adsp_dup = None
+        if self.is_adsp() and self._existing is not None:
+            self._adsp_dup = [pk is not None and self._existing.has_primary_key(pk) for pk in pks]
         return paths, pks, keep, disp
 
     def _emit(self, parsed, recs, paths, pks, keep, disp, errors):
@@ -644,6 +771,14 @@ class VCFVariantLoader(object):
                     mapping += self._existing.payload(int(self._match[i]))
                     self.increment_counter("skipped")
                     continue
+                if self.is_adsp():  # vcf_variant_loader.py:303-307
+                    if self._adsp_dup is None:  # no validator: the reference's None.exists(...)
+                        failed = AttributeError("'NoneType' object has no attribute 'exists'")
+                        break
+                    if self._adsp_dup[i]:
+                        self._update_buffer.append((pks[i], "chr" + _xstr(v.chromosome)))
+                        self.increment_counter("update")
+                        continue
                 path = paths[i]
                 if path is None:
                     failed = TypeError("'NoneType' object is not subscriptable")
@@ -663,7 +798,8 @@ class VCFVariantLoader(object):
                     self.add_copy_str("#".join([
                         "chr" + _xstr(v.chromosome), pk, _xstr(v.position), r[2], path,
                         _xstr(self._alg_invocation_id), _xstr(v.ref_snp_id, nullStr="NULL"),
-                        _xstr(v.is_multi_allelic, falseAsNull=True, nullStr="NULL"), disp[i], freq]))
+                        _xstr(v.is_multi_allelic, falseAsNull=True, nullStr="NULL"), disp[i], freq]
+                        + (["True"] if self.is_adsp() else [])))  # is_adsp_variant (:336-337)
                     self.increment_counter("variant")
                 mapping.append({"primary_key": pk, "bin_index": path})
             if failed is not None:
@@ -699,6 +835,16 @@ def _display_texts(eng, db, d_end) -> List[Optional[str]]:
     o = off.cpu().numpy()
     st = state.cpu().numpy()
     return [raw[o[i]:o[i + 1]] if st[i] == 0 else None for i in range(len(st))]
+
+
+def _data_lines(raw: bytes) -> List[str]:
+    """The load driver's lines (load_vcf_file.py:101-105): split at '\\n', each
+    rstripped, '#' lines skipped.  An interior empty line stays (the reference
+    parses it and raises); only the segment after a final newline is dropped."""
+    parts = raw.decode("utf-8").split("\n")
+    if parts and parts[-1] == "":
+        parts.pop()
+    return [ln.rstrip() for ln in parts if not ln.startswith("#")]
 
 
 def _select(b, idx):

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import json
 import os
+import warnings
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from .chromosomes import CHROM_NAMES, UNKNOWN_CHROM, chrom_code
@@ -60,14 +61,27 @@ class VariantPKGenerator(object):
         self._device = device
         self._engine = None
         digs = dict(sequence_digests or {})
-        if not digs and seqrepoProxyPath and os.path.isfile(str(seqrepoProxyPath)):
-            digs = load_sequence_digests(str(seqrepoProxyPath))
+        if not digs and seqrepoProxyPath:
+            if os.path.isfile(str(seqrepoProxyPath)):
+                digs = load_sequence_digests(str(seqrepoProxyPath))
+            else:
+                # the reference CLI passes a SeqRepo directory (primary_key_generator.py:74-83);
+                # without vrs-python/SeqRepo only a chrom->refget-digest file can be used,
+                # so say now that long alleles (> maxSequenceLength) will fail
+                warnings.warn("seqrepoProxyPath %r is not a chrom<TAB>refget-digest (or JSON) file: long-allele "
+                              "primary keys (len(ref)+len(alt) > %d) will raise ValueError('Sequence mismatch "
+                              "...'); pass sequence_digests or a digest file" % (seqrepoProxyPath,
+                                                                                maxSequenceLength),
+                              RuntimeWarning, stacklevel=2)
         self._ga4gh_sequence_map = digs
         if normalize:
             raise NotImplementedError("VRS normalisation needs vrs-python/SeqRepo (absent)")
 
     def max_sequence_length(self) -> int:
         return self._maxSequenceLength
+
+    def genome_build(self):
+        return self._genomeBuild
 
     def has_sequence_digests(self) -> bool:
         return all(c in self._ga4gh_sequence_map for c in CHROM_NAMES)

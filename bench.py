@@ -55,6 +55,11 @@ WORKLOADS = {
                                   "GPU (K0 tokenizer: line split + field parse + multi-allelic explode)",
                 bytes_per=None, kernel="avdb_vcf (whole tokenizer)"),
 }
+WORKLOADS["dropin"] = dict(
+    n=0, desc="drop-in per-call latency (INTEGRATION.md 1): BinIndex.find_bin_index on sorted C1 records "
+              "(cache hits) and on > 15.6 kb spans (every call a miss), VCFVariantLoader.parse_variant per "
+              "line as load_vcf_file.py:112 calls it, and the batched paths per line",
+    bytes_per=None, kernel=None)
 WORKLOADS["load"] = dict(
     n=8_388_608, desc="SURVEY 8f ranks 1-3: dbSNP-shaped VCF text -> COPY rows + .mapping lines on the GPU "
                       "(K0 tokenize, K2 end+bin, K5 display attributes/FREQ/keys/paths as text)",
@@ -250,8 +255,71 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
 
 
 # ---------------------------------------------------------------------------
+def dropin(a):
+    """Per-call latency of the drop-in API, called exactly as the reference's
+    loader calls the reference API (one record / one line at a time)."""
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.bin_index import BinIndex
+    from annotatedvdb_amd.loaders import VCFVariantLoader
+    from annotatedvdb_amd.chromosomes import CHROM_NAMES, GRCH38_LENGTHS
+
+    def per_call(fn, items, reps=1):
+        fn(items[:20])  # warm (first launch, pinned buffers)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn(items)
+        return (time.perf_counter() - t0) / (reps * len(items)) * 1e6
+
+    res = {}
+    d = synth.np_c1(200_000, seed=1)
+    # hits: sorted chr22 SNV/indel positions (vcf_variant_loader.py:310-311 pattern)
+    bi = BinIndex(None, verbose=False)
+    pos = d["pos"].tolist()
+    res["find_bin_index_sorted_us"] = per_call(lambda xs: [bi.find_bin_index("22", p, p) for p in xs], pos)
+    rng = np.random.default_rng(9)
+    L = GRCH38_LENGTHS["22"]
+    st = rng.integers(1, L - 1_100_000, 3000)
+    sp = (10 ** rng.uniform(np.log10(16_000), 6, 3000)).astype(np.int64)
+    spans = list(zip(st.tolist(), (st + sp).tolist()))
+    bi2 = BinIndex(None, verbose=False)
+    res["find_bin_index_miss_us"] = per_call(lambda xs: [bi2.find_bin_index("22", s, e) for s, e in xs], spans)
+    lines = synth.vcf_text(3000, seed=17).decode().splitlines()
+
+    def fresh():
+        ld = VCFVariantLoader("dbSNP")
+        ld.initialize_pk_generator("GRCh38", None)
+        ld.initialize_bin_indexer(None)
+        ld.set_algorithm_invocation_id(1)
+        ld.initialize_copy_sql()
+        return ld
+    ld = fresh()
+    res["parse_variant_per_line_us"] = per_call(lambda xs: [ld.parse_variant(x) for x in xs], lines)
+    ld = fresh()
+    res["parse_variants_batch_per_line_us"] = per_call(lambda xs: ld.parse_variants(xs), lines, reps=3)
+    ld = fresh()
+    text = ("\n".join(lines) + "\n").encode()
+    res["load_vcf_text_per_line_us"] = per_call(lambda xs: ld.load_vcf_text(text if len(xs) > 20 else
+                                                                            ("\n".join(xs) + "\n").encode()),
+                                                lines, reps=3)
+    res["reference_build_container"] = {"parse_variant_per_line_us": 94.0, "find_bin_index_hit_us": 0.81,
+                                        "find_bin_index_miss_us_fake_db": 8.2,
+                                        "source": "SURVEY.md 6 / tools/calibrate_cpu_baseline.py (verbatim "
+                                                  "reference with an in-process table-search DB: a real "
+                                                  "Postgres round trip per miss costs more)"}
+    out = {"metric": "drop-in per-call latency (find_bin_index, parse_variant)", "value":
+           res["parse_variant_per_line_us"], "unit": "us/line", "n_gpus": 1, "higher_is_better": False,
+           "dtype": "u8", "data": "synthetic C1 records / dbSNP-shaped VCF lines", "config":
+           {"workload": WORKLOADS["dropin"]["desc"]}, "latency": res}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     a = parse()
+    if a.workload == "dropin":
+        torch.cuda.set_device(0)
+        dropin(a)
+        return
     from annotatedvdb_amd import distributed as D
     ri = D.rank_info()
     # CPU baseline first, before this process touches the GPU (its worker
@@ -447,6 +515,32 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "cpu_baseline": cpu,
     }
+    if a.workload == "c5":
+        # SURVEY.md 8d whole-pipeline bytes (34 + rlen + alen + 24 per long record) over
+        # K2 + K3 + K4 time, and K4's VALU roofline (compute-bound SHA-512)
+        rl, al = batch.ref_len.long(), batch.alt_len.long()
+        n_long = int(((rl + al) > 50).sum().item())
+        pipe_bytes = 34 * n + int((rl + al).sum().item()) + 24 * n_long
+        pipe_ms = sum(stage_ms[k] for k in ("record_prep", "pk_dedup", "vrs_digest"))
+        pipe = pipe_bytes / (pipe_ms * 1e-3) / 1e9
+        out["pipeline_roofline"] = {"bound": "hbm", "achieved": pipe, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": pipe / HBM_PEAK_GBS, "algorithmic_bytes_per_step": pipe_bytes,
+                                    "step_kernel_ms": pipe_ms,
+                                    "note": "SURVEY 8d C5 bytes (34 + rlen + alen + 24 if long per record) / "
+                                            "(K2 + K3 + K4 HIP-event time); K4 is VALU-bound, not HBM-bound"}
+        k4 = os.path.join(ROOT, "profiles", "pmc_k4.json")
+        if os.path.exists(k4):
+            pk = json.load(open(k4))
+            vi = float(pk["sq_insts_valu_per_launch"])
+            ach = vi / (stage_ms["vrs_digest"] * 1e-3)
+            peak = 1024 * 2.4e9 / 2  # one wave64 VALU instruction per 2 cycles per SIMD (157 TF fp32 basis)
+            vop3 = 1024 * 2.4e9 / pk["vop3_cycles_per_wave_instr"]
+            out["valu_roofline"] = {"kernel": "avdb_vrs_digest (k_long_hist/scan/scatter + k_vrs_digest)",
+                                    "bound": "valu", "achieved": ach, "peak": peak, "unit": "wave-instr/s",
+                                    "frac": ach / peak, "frac_of_vop3_issue_peak": ach / vop3,
+                                    "vop3_issue_peak": vop3, "sq_insts_valu_per_launch": vi,
+                                    "sha512_compressions_per_launch": pk.get("sha512_compressions_per_launch"),
+                                    "note": pk.get("note")}
     if a.workload == "c1":
         kt = last["kt"]
         out["dtype"] = "u8"

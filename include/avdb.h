@@ -85,6 +85,7 @@ extern "C" {
 #define AVDB_CTR_DUP_ROWS 26            /* records whose COPY row was dropped (keep == 0) */
 #define AVDB_CTR_HOST_LINES 27          /* lines left to the host renderer */
 #define AVDB_CTR_EXISTING 28            /* records found in the existing-variant key set (K6) */
+#define AVDB_CTR_ADSP_UPDATES 29        /* ADSP records whose key was already loaded (is_adsp_variant UPDATEs) */
 #define AVDB_N_COUNTERS 32
 
 typedef struct avdb_ctx avdb_ctx;
@@ -240,10 +241,12 @@ int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t 
 #define AVDB_LINE_SKIP 2
 #define AVDB_MAX_ALG_ID 64
 
+#define AVDB_FORMAT_ADSP 1u           /* opts.flags: COPY rows end with is_adsp_variant = True
+                                        * (vcf_variant_loader.py:336-337) */
 typedef struct avdb_format_opts {
   const char* alg_id;     /* xstr(row_algorithm_id), host NUL-terminated; NULL = "" */
   uint32_t max_seq_len;   /* primary_key_generator.py:53 (default 50) */
-  uint32_t reserved;
+  uint32_t flags;         /* AVDB_FORMAT_* */
   /* --skipExisting (optional, device; NULL = off): K6 match / kind per record and
    * the .mapping text each existing key contributes (its match list, rendered
    * once by the host): frag[frag_off[k] .. frag_off[k+1]).  A matched record gets
@@ -253,6 +256,11 @@ typedef struct avdb_format_opts {
   const uint8_t* match_kind;
   const uint8_t* frag;
   const uint64_t* frag_off;
+  /* ADSP datasource (optional, device; NULL = off): per record, nonzero when its
+   * primary key is already loaded (K6 avdb_keyset_probe_text over K7's keys):
+   * is_duplicate(recordPK) -> an is_adsp_variant UPDATE instead of a COPY row, no
+   * .mapping entry, counters[AVDB_CTR_ADSP_UPDATES] (vcf_variant_loader.py:303-307). */
+  const uint8_t* adsp_dup;
 } avdb_format_opts;
 
 int avdb_format_workspace_size(size_t n, size_t* bytes);
@@ -324,6 +332,14 @@ int avdb_keyset_probe(avdb_ctx* ctx, const void* table, size_t table_bytes, cons
                       const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
                       const uint8_t* heap, size_t heap_bytes, size_t n, int check_alt, int32_t* match,
                       uint8_t* kind, uint64_t* counters, void* stream);
+/* The same key set probed with arbitrary strings q[q_off[i] .. q_off[i+1]) (device),
+ * e.g. the primary keys avdb_primary_keys rendered: ADSP loads check each record's
+ * primary key against the rows already loaded (is_duplicate(recordPK),
+ * vcf_variant_loader.py:303-307).  match[i] = first equal key or -1; rows with
+ * skip[i] != 0 (nullable) are not probed (-1). */
+int avdb_keyset_probe_text(avdb_ctx* ctx, const void* table, size_t table_bytes, const uint8_t* keys,
+                           const uint64_t* key_off, size_t n_keys, const uint8_t* q, const uint64_t* q_off,
+                           const uint8_t* skip, size_t n, int32_t* match, uint64_t* counters, void* stream);
 
 /* ---- host-side formatting of kernel outputs -------------------------------
  * ltree path text (<= AVDB_MAX_PATH bytes).  Returns the length written (no

@@ -29,8 +29,12 @@ Outputs (all small, gzip):
   kat.json                    known-answer tests
   c1_prefix.tsv.gz            BASELINE config C1 (annotatedvdb_amd.synth.np_c1, seed 1):
                               the first 100,000 records -> end, bin path, primary key
+  adsp_load.tsv.gz            the load driver with VCFVariantLoader('ADSP') and
+  adsp_existing.json          --skipExisting over a stub validator answering from
+                              adsp_existing.json: per line COPY rows (is_adsp_variant
+                              column), .mapping, is_adsp_variant updates, counters
 
-Usage:  python tests/golden/make_golden.py [--quick] [--only all|load|c1]
+Usage:  python tests/golden/make_golden.py [--quick] [--only all|load|c1|adsp]
 """
 
 from __future__ import annotations
@@ -696,6 +700,104 @@ def gen_c1_prefix(VariantAnnotator, bi, n):
     return rows
 
 
+class StubVariantRecord:
+    """Stands in for database.variant.VariantRecord (variant.py:287-309) over an
+    in-memory export: ``exists(id)`` answers map_variants(id, firstHitOnly=True,
+    checkAltVariants=True) (external SQL, unpinned) as: the metaseq-id table M
+    (exact, then with the alleles switched), else the primary-key table P."""
+    M = {}
+    P = {}
+
+    def __init__(self, *a, **k):
+        pass
+
+    def use_legacy_pk(self, flag):
+        pass
+
+    def close(self):
+        pass
+
+    def exists(self, variantId, returnMatch=False):
+        m = self.M.get(variantId)
+        if m is None:
+            f = variantId.split(":")
+            if len(f) == 4:
+                m = self.M.get(":".join((f[0], f[1], f[3], f[2])))
+        if m is None and variantId in self.P:
+            m = [{"primary_key": variantId, "bin_index": self.P[variantId]}]
+        if m is None:
+            return None if returnMatch else False
+        return m if returnMatch else True
+
+
+def adsp_existing(lines, rng):
+    """Existing rows for the ADSP fixture, derived from the input's own records:
+    ~10 % of the alts by metaseq id (3 % of them with the alleles switched), and
+    ~12 % of the alts that carry a refSNP id by primary key only (keys with an
+    external id: 5 fields, never a metaseq id)."""
+    from AnnotatedVDB.Util.parsers import VcfEntryParser
+    from AnnotatedVDB.Util.primary_key_generator import VariantPKGenerator
+    pkg = VariantPKGenerator("GRCh38", "/nonexistent")
+    M, P = {}, {}
+    for line in lines:
+        try:
+            v = VcfEntryParser(line).get_variant(namespace=True)
+        except Exception:  # noqa: BLE001
+            continue
+        for alt in v.alt_alleles:
+            if alt == ".":
+                continue
+            ms = ":".join((str(v.chromosome), str(v.position), v.ref_allele, alt))
+            try:
+                pk = pkg.generate_primary_key(ms, v.ref_snp_id)
+            except Exception:  # noqa: BLE001
+                continue
+            u = rng.random()
+            payload = [{"primary_key": pk, "bin_index": "chr%s.L1.B%d" % (v.chromosome, rng.randint(1, 4))}]
+            if u < 0.07:
+                M[ms] = payload
+            elif u < 0.10:
+                M[":".join((str(v.chromosome), str(v.position), alt, v.ref_allele))] = payload
+            elif u < 0.22 and v.ref_snp_id is not None and len(pk.split(":")) == 5:
+                P[pk] = "chr%s" % v.chromosome
+    return M, P
+
+
+def run_adsp_driver(lines, M, P):
+    """Load/bin/load_vcf_file.py:101-119 with --datasource ADSP --skipExisting:
+    per line the COPY rows, .mapping line(s) or exception type, the
+    is_adsp_variant update values and the counter deltas."""
+    import AnnotatedVDB.Util.loaders.variant_loader as VL
+    from AnnotatedVDB.Util.loaders import VCFVariantLoader
+    StubVariantRecord.M, StubVariantRecord.P = M, P
+    VL.VariantRecord = StubVariantRecord
+    loader = VCFVariantLoader("ADSP")
+    loader.initialize_pk_generator("GRCh38", "/nonexistent")
+    loader.initialize_bin_indexer(None)
+    loader._alg_invocation_id = "1"
+    loader.initialize_copy_sql()
+    loader.set_skip_existing(True, None)
+    keys = ("line", "variant", "skipped", "duplicates", "update")
+    rows = []
+    for line in lines:
+        loader.reset_copy_buffer()
+        loader.reset_update_buffer()
+        before = [loader.get_count(k) for k in keys]
+        try:
+            pkm = loader.parse_variant(line.rstrip())
+            mapping = ["%s\t%s" % (k, v) for k, v in pkm.items()]
+            err = ""
+        except Exception as e:  # noqa: BLE001
+            mapping, err = [], type(e).__name__
+        copy = loader.copy_buffer().getvalue().splitlines()
+        upd = [list(x) for x in loader.update_buffer()]
+        delta = [loader.get_count(k) - b for k, b in zip(keys, before)]
+        rows.append((line.replace("\t", "\\t"), err, json.dumps(mapping, separators=(",", ":")),
+                     json.dumps(copy, separators=(",", ":")), json.dumps(upd, separators=(",", ":")),
+                     json.dumps(delta)))
+    return rows
+
+
 def kats(VariantAnnotator, bi):
     cases = [
         ("1", 1510801, "C", "T", None),
@@ -735,7 +837,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
-    ap.add_argument("--only", choices=["all", "load", "c1"], default="all",
+    ap.add_argument("--only", choices=["all", "load", "c1", "adsp"], default="all",
                     help="'load': only the load-driver fixtures (vcf_load, display_attrs); "
                          "'c1': only the C1 prefix fixture")
     a = ap.parse_args()
@@ -748,6 +850,17 @@ def main():
     bi = BinIndex(None, verbose=False)
 
     k = 0.1 if a.quick else 1.0
+    if a.only == "adsp":
+        arng = random.Random(a.seed + 2)
+        lines = gen_load_lines(int(3000 * k), arng)
+        M, P = adsp_existing(lines, arng)
+        with open(os.path.join(HERE, "adsp_existing.json"), "w") as fh:
+            json.dump({"metaseq": M, "primary_key": P}, fh, separators=(",", ":"))
+        wtsv("adsp_load.tsv.gz", ["line", "error", "mapping", "copy_rows", "updates", "counter_deltas"],
+             run_adsp_driver(lines, M, P))
+        print("existing: %d metaseq ids, %d primary keys" % (len(M), len(P)))
+        print("done")
+        return
     if a.only == "c1":
         wtsv("c1_prefix.tsv.gz", ["primary_key", "end", "bin_index"],
              gen_c1_prefix(VariantAnnotator, BinIndex(None, verbose=False), int(100000 * k)))
