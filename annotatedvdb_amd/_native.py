@@ -76,7 +76,25 @@ EXPORTED_SYMBOLS = [
     "avdb_display_attributes",
     "avdb_keyset_workspace_size", "avdb_keyset_build", "avdb_keyset_probe",
     "avdb_primary_keys", "avdb_keyset_probe_text",
+    "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
+    "avdb_small_prep", "avdb_host_alloc", "avdb_host_free",
 ]
+
+
+SMALL_PATH, SMALL_KEY, SMALL_DISPLAY = 1, 2, 4
+SMALL_MAX = 65536
+
+
+class SmallBatch(ctypes.Structure):
+    """avdb_small_batch (include/avdb.h)."""
+    _fields_ = [("chrom", ctypes.c_void_p), ("pos", ctypes.c_void_p), ("end_in", ctypes.c_void_p),
+                ("allele_off", ctypes.c_void_p), ("ref_len", ctypes.c_void_p), ("alt_len", ctypes.c_void_p),
+                ("heap", ctypes.c_void_p), ("ext_id", ctypes.c_void_p), ("heap_bytes", ctypes.c_size_t),
+                ("n", ctypes.c_uint32), ("max_seq_len", ctypes.c_uint32), ("want", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("end_out", ctypes.c_void_p), ("code", ctypes.c_void_p),
+                ("status", ctypes.c_void_p), ("key_state", ctypes.c_void_p), ("disp_state", ctypes.c_void_p),
+                ("off_out", ctypes.c_void_p), ("text_out", ctypes.c_void_p * 3), ("text_cap", ctypes.c_uint32 * 3),
+                ("overflow", ctypes.c_void_p)]
 
 
 class NativeUnavailable(RuntimeError):
@@ -133,6 +151,12 @@ def _sig(lib):
     f.avdb_keyset_probe.argtypes = [P, P, SZ, P, P, SZ, P, P, P, P, P, P, SZ, SZ, I32, P, P, P, P]
     f.avdb_primary_keys.argtypes = [P, P, P, P, P, P, P, SZ, P, P, P, SZ, U32, P, SZ, P, P, P, SZ, P, SZ, P, P]
     f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]
+    f.avdb_small_prep.argtypes = [P, ctypes.POINTER(SmallBatch), P]
+    f.avdb_host_alloc.argtypes = [SZ, ctypes.POINTER(P)]
+    f.avdb_host_free.argtypes = [P]
+    f.avdb_shard_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
+    f.avdb_vcf_select_lines.argtypes = [P, SZ, P, P, P, P, U32, U32, I32, P, SZ, P, P]
+    f.avdb_vcf_select_copy.argtypes = [P, P, SZ, SZ, P, P, P, P]
     for name in EXPORTED_SYMBOLS:
         if name not in ("avdb_last_error",):
             getattr(f, name).restype = I32

@@ -56,27 +56,21 @@ class BinIndex(object):
         self._currentBin = {}
 
     def _lookup_one(self, chrm: str, start: int, end: int) -> Optional[dict]:
-        """One K1 launch for one record (the reference's SQL round trip)."""
-        import torch
+        """One K8 launch for one record (the reference's SQL round trip): the
+        record and its bin path travel through host-mapped memory, so a miss is
+        one launch + one stream sync."""
+        from . import _native as N
         code = bin_index_chrom_code(chrm)
-        if self._one is None:
-            self._one = (torch.empty(1, dtype=torch.uint8).pin_memory(),
-                         torch.empty(2, dtype=torch.int32).pin_memory())
-        hc, hse = self._one
-        hc[0] = min(code, 255)
-        hse[0] = int(start)
-        hse[1] = int(end)
-        dse = hse.to(self._engine.device, non_blocking=True)
-        dc = hc.to(self._engine.device, non_blocking=True)
-        c, st = self._engine.bin_assign(dc, dse[0:1], dse[1:2])
-        out = c.to("cpu").numpy().view(np.uint32)
-        bcode = int(out[0])
+        lo, hi = (start, end) if end >= start else (end, start)
+        if lo < 1 or hi >= 2 ** 32:  # outside any bin (and outside the kernels' u32 positions)
+            return None
+        res = self._engine.small().run([min(code, 255)], [int(start)], ends=[int(end)], want=N.SMALL_PATH)
+        bcode = int(res["code"][0])
         if bcode == 0xFFFFFFFF:
             return None
         lo, hi = bin_location(bcode, self._lengths[code])
         level = bcode >> 28
-        return {"chromosome": "chr" + CHROM_NAMES[code],
-                "global_bin_path": self._engine.format_path(code, bcode),
+        return {"chromosome": "chr" + CHROM_NAMES[code], "global_bin_path": res["path"][0],
                 "location": (lo, hi), "bin_level": 1 + 2 * level}
 
     def _update_current_bin_index(self, chrm, start, end):

@@ -289,57 +289,6 @@ __global__ __launch_bounds__(kBlock) void k_bin_assign1(
 // ---------------------------------------------------------------------------
 // K2: end inference (+ common-prefix length) fused with the bin computation.
 // ---------------------------------------------------------------------------
-// variant_annotator.py:36-79 with lcp from __normalize_alleles (:82-121).
-// Allele bytes are compared 8 at a time (first mismatch via count-trailing-zeros
-// of the XOR); the inversion test reverses 8-byte chunks with a byte swap.
-// wr / wa are the first 8 bytes of ref / alt, loaded by the caller ahead of
-// time; alleles of up to 8 bytes (the bulk) need no further heap reads.
-__device__ __forceinline__ uint32_t infer_end(const Heap& h, uint64_t off, uint32_t r, uint32_t a,
-                                              uint32_t pos, uint64_t wr, uint64_t wa,
-                                              uint32_t* lcp_out) {
-  if (r == 1u && a == 1u) { *lcp_out = 0; return pos; }        // SNV (:54-55)
-  const uint64_t alt = off + r;
-  const uint32_t m = r < a ? r : a;
-  uint32_t n;                                                  // lcp (:100-108)
-  const uint64_t x0 = (wr ^ wa) & low_bytes_mask(m < 8u ? m : 8u);
-  if (x0) {
-    n = uint32_t(__builtin_ctzll(x0)) >> 3;
-  } else if (m <= 8u) {
-    n = m;
-  } else {
-    n = 8;
-    while (n < m) {
-      const uint64_t x = (heap_u64(h, off + n) ^ heap_u64(h, alt + n)) & low_bytes_mask(m - n);
-      if (x) { n += uint32_t(__builtin_ctzll(x)) >> 3; break; }
-      n += 8;
-    }
-    if (n > m) n = m;
-  }
-  *lcp_out = n;
-  const uint32_t nr = r - n, na = a - n;
-  if (r == a) {                                                // MNV (:57-65)
-    bool inv = true;                                           // ref == alt[::-1]
-    if (r <= 8u) {
-      if (r) {
-        const uint64_t mk = low_bytes_mask(r);
-        inv = (wr & mk) == (__builtin_bswap64(wa & mk) >> (8 * (8 - r)));
-      }
-    } else {
-      for (uint32_t i = 0; i < r && inv; i += 8) {
-        const uint32_t c = r - i < 8 ? r - i : 8;
-        const uint64_t mk = low_bytes_mask(c);
-        const uint64_t fw = heap_u64(h, off + i) & mk;
-        const uint64_t bw = __builtin_bswap64(heap_u64(h, alt + (r - i - c)) & mk) >> (8 * (8 - c));
-        inv = fw == bw;
-      }
-    }
-    return inv ? pos + r - 1u : pos + nr - 1u;
-  }
-  if (na >= 1u)                                                // insertion (:67-74)
-    return nr >= 1u ? pos + nr : (r > 1u ? pos + r - 1u : pos + 1u);
-  return nr == 0u ? pos + r - 1u : pos + nr;                   // deletion (:77-79)
-}
-
 // Records per lane per pass: all their SoA loads, then all their first heap
 // words, are issued before any is consumed (the heap reads depend on
 // allele_off, so one record per lane leaves K2 latency-bound).

@@ -198,3 +198,18 @@ extern "C" int avdb_format_bin_paths(const avdb_ctx* ctx, const uint8_t* chrom, 
   out_off[n] = pos;
   return AVDB_OK;
 }
+
+extern "C" int avdb_host_alloc(size_t bytes, void** ptr) {
+  if (!ptr || bytes == 0) {
+    avdb_set_error("avdb_host_alloc: null pointer or zero size");
+    return AVDB_EINVAL;
+  }
+  *ptr = nullptr;
+  AVDB_HIP_TRY(hipHostMalloc(ptr, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  return AVDB_OK;
+}
+
+extern "C" int avdb_host_free(void* ptr) {
+  if (ptr) AVDB_HIP_TRY(hipHostFree(ptr));
+  return AVDB_OK;
+}

@@ -223,6 +223,115 @@ class KeyText:
         return keys, paths
 
 
+class SmallPrep:
+    """K8 (``avdb_small_prep``) over one host-mapped pinned arena: the
+    per-record / per-line drop-in path as one launch + one stream sync, no
+    copies (the kernel reads the records and writes the results over PCIe).
+    Batches that do not fit the arena return ``None`` (callers then use the
+    multi-kernel path)."""
+
+    _IN = (("chrom", np.uint8), ("pos", np.uint32), ("end_in", np.uint32), ("allele_off", np.uint64),
+           ("ref_len", np.uint32), ("alt_len", np.uint32), ("ext_id", np.uint64), ("end_out", np.uint32),
+           ("code", np.uint32), ("status", np.uint8), ("key_state", np.uint8), ("disp_state", np.uint8))
+
+    def __init__(self, engine: "Engine", max_records: int = 4096, heap_bytes: int = 1 << 20,
+                 text_bytes: Tuple[int, int, int] = (1 << 19, 1 << 19, 1 << 21)):
+        self.eng = engine
+        self.R = int(max_records)
+        self.H = int(heap_bytes)
+        self.T = tuple(int(t) for t in text_bytes)
+        sizes = [(name, dt, self.R) for name, dt in self._IN] + [("heap", np.uint8, self.H),
+                                                               ("off_out", np.uint32, 3 * (self.R + 1)),
+                                                               ("overflow", np.uint32, 2)]
+        sizes += [("text%d" % k, np.uint8, self.T[k]) for k in range(3)]
+        total = 0
+        layout = []
+        for name, dt, cnt in sizes:
+            total = (total + 15) & ~15
+            layout.append((name, dt, cnt, total))
+            total += np.dtype(dt).itemsize * cnt
+        p = ctypes.c_void_p()
+        N.check("avdb_host_alloc", engine.lib.avdb_host_alloc(total, ctypes.byref(p)))
+        self._ptr = p.value
+        self._buf = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(self._ptr))
+        self.a = {}
+        self.addr = {}
+        for name, dt, cnt, off in layout:
+            self.a[name] = self._buf[off:off + np.dtype(dt).itemsize * cnt].view(dt)
+            self.addr[name] = self._ptr + off
+
+    def close(self):
+        if getattr(self, "_ptr", None):
+            self.eng.lib.avdb_host_free(self._ptr)
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, chrom, pos, ends=None, refs: Optional[Sequence[bytes]] = None,
+            alts: Optional[Sequence[bytes]] = None, ext=None, want: int = 1, max_seq_len: int = 50):
+        """Returns a dict of numpy results (copies) or ``None`` when the batch does
+        not fit.  Text streams: ``path`` / ``key`` / ``display`` lists of str
+        (None where not rendered)."""
+        n = len(pos)
+        if n > self.R:
+            return None
+        a = self.a
+        a["chrom"][:n] = chrom
+        a["pos"][:n] = pos
+        b = N.SmallBatch()
+        b.chrom, b.pos = self.addr["chrom"], self.addr["pos"]
+        if refs is not None:
+            rl = np.fromiter((len(x) for x in refs), dtype=np.int64, count=n)
+            al = np.fromiter((len(x) for x in alts), dtype=np.int64, count=n)
+            tot = rl + al
+            hb = int(tot.sum())
+            if hb > self.H:
+                return None
+            off = np.zeros(n, dtype=np.int64)
+            if n:
+                np.cumsum(tot[:-1], out=off[1:])
+            heap = b"".join(r + x for r, x in zip(refs, alts))
+            a["heap"][:hb] = np.frombuffer(heap, dtype=np.uint8)
+            a["allele_off"][:n] = off
+            a["ref_len"][:n] = rl
+            a["alt_len"][:n] = al
+            b.allele_off, b.ref_len, b.alt_len, b.heap = (self.addr["allele_off"], self.addr["ref_len"],
+                                                          self.addr["alt_len"], self.addr["heap"])
+            b.heap_bytes = max(hb, 1)
+            b.key_state, b.disp_state = self.addr["key_state"], self.addr["disp_state"]
+            if ext is not None:
+                a["ext_id"][:n] = np.asarray(ext, dtype=np.uint64)
+                b.ext_id = self.addr["ext_id"]
+        else:
+            a["end_in"][:n] = ends
+            b.end_in = self.addr["end_in"]
+        b.n, b.max_seq_len, b.want = n, int(max_seq_len), int(want)
+        b.end_out, b.code, b.status = self.addr["end_out"], self.addr["code"], self.addr["status"]
+        b.off_out, b.overflow = self.addr["off_out"], self.addr["overflow"]
+        for k in range(3):
+            b.text_out[k] = self.addr["text%d" % k]
+            b.text_cap[k] = self.T[k]
+        N.check("avdb_small_prep", self.eng.lib.avdb_small_prep(self.eng.ctx, ctypes.byref(b), self.eng._stream()))
+        torch.cuda.current_stream(self.eng.device).synchronize()
+        if int(a["overflow"][0]) & want:
+            return None
+        out = {"end": a["end_out"][:n].copy(), "code": a["code"][:n].copy(), "status": a["status"][:n].copy()}
+        if refs is not None:
+            out["key_state"] = a["key_state"][:n].copy()
+            out["disp_state"] = a["disp_state"][:n].copy()
+        for k, name in enumerate(("path", "key", "display")):
+            if not (want >> k) & 1:
+                continue
+            o = a["off_out"][k * (n + 1): k * (n + 1) + n + 1]
+            raw = a["text%d" % k][: int(o[n])].tobytes().decode("ascii")
+            out[name] = [raw[o[i]:o[i + 1]] if o[i + 1] > o[i] else None for i in range(n)]
+        return out
+
+
 # ---------------------------------------------------------------------------
 # engine
 # ---------------------------------------------------------------------------
@@ -251,6 +360,9 @@ class Engine:
 
     # -- lifecycle ---------------------------------------------------------
     def close(self):
+        if getattr(self, "_small", None) is not None:
+            self._small.close()
+            self._small = None
         if getattr(self, "_ctx", None):
             self.lib.avdb_ctx_destroy(self._ctx)
             self._ctx = None
@@ -269,6 +381,13 @@ class Engine:
 
     def _stream(self):
         return N.stream_handle(self.device)
+
+    def small(self) -> SmallPrep:
+        """The engine's K8 arena (created on first use)."""
+        sp = getattr(self, "_small", None)
+        if sp is None:
+            sp = self._small = SmallPrep(self)
+        return sp
 
     def set_sequence_digests(self, digests: Sequence[str]):
         if len(digests) != len(self.lengths) or any(len(d) != N.DIGEST_CHARS for d in digests):
@@ -450,6 +569,28 @@ class Engine:
                 N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s))
         return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
                         records=b, rec_line=rec_line, rec_alt=rec_alt)
+
+    # -- K9: this rank's lines of a VCF text -----------------------------------
+    def vcf_select(self, vb: "VcfBatch", assignment, rank: int, cut: int = 64_000_000) -> torch.Tensor:
+        """The lines of ``vb`` that piece plan ``assignment`` gives to ``rank``
+        (each + '\\n', file order) as a device text tensor."""
+        from .shard import piece_table
+        base, count, prank = piece_table(assignment, self.lengths, cut)
+        n = vb.n_lines
+        sz = ctypes.c_size_t()
+        self.lib.avdb_shard_workspace_size(n, ctypes.byref(sz))
+        ws = self.empty(max(1, int(sz.value)), torch.uint8)
+        sel = self.empty(n + 1, torch.int64)
+        s = self._stream()
+        N.check("avdb_vcf_select_lines", self.lib.avdb_vcf_select_lines(
+            self.ctx, n, N.ptr(vb.lines), base.ctypes.data, count.ctypes.data, prank.ctypes.data, len(prank),
+            int(cut), int(rank), N.ptr(ws), ws.numel(), N.ptr(sel), s))
+        total = int(sel[n].item())
+        out = self.empty(max(1, total), torch.uint8)
+        if total:
+            N.check("avdb_vcf_select_copy", self.lib.avdb_vcf_select_copy(
+                self.ctx, N.ptr(vb.text), vb.text.numel(), n, N.ptr(vb.lines), N.ptr(sel), N.ptr(out), s))
+        return out[:total]
 
     # -- K5: COPY rows / .mapping lines / display attributes --------------------
     def vcf_format(self, vb: "VcfBatch", end: torch.Tensor, code: torch.Tensor, status: torch.Tensor,

@@ -314,16 +314,29 @@ class VCFVariantLoader(object):
         # ---- phase 2: per-alt records -> GPU --------------------------------
         recs = self._records_of(parsed)
         db = codes = None
+        small = None
         if recs:
             from .engine import ExtIdInterner, pack_records
+            from . import _native as N
             interner = ExtIdInterner()
             codes = np.asarray([min(bin_index_chrom_code(r[5].chromosome), 255) for r in recs],
                                dtype=np.uint8)
-            b = pack_records(codes, [r[5].position for r in recs],
-                             [r[5].ref_allele.encode() for r in recs], [r[1].encode() for r in recs],
-                             [interner.key(r[5].ref_snp_id) for r in recs])
-            db = b.to(self._engine.device)
-        paths, pks, keep, disp = self._gpu_prep(recs, db, codes, dedup, keep_override)
+            pos = [r[5].position for r in recs]
+            refs = [r[5].ref_allele.encode() for r in recs]
+            alts = [r[1].encode() for r in recs]
+            ext = [interner.key(r[5].ref_snp_id) for r in recs]
+            if not dedup and keep_override is None and self._existing is None and all(0 < p < 2 ** 32 for p in pos):
+                # the per-line drop-in path: K2 + K7 + K5a in one launch (K8), no copies
+                small = self._engine.small().run(
+                    codes, pos, refs=refs, alts=alts, ext=ext,
+                    want=N.SMALL_PATH | N.SMALL_KEY | N.SMALL_DISPLAY,
+                    max_seq_len=self._pk_generator.max_sequence_length())
+            if small is None:
+                db = pack_records(codes, pos, refs, alts, ext).to(self._engine.device)
+        if small is not None:
+            paths, pks, keep, disp = self._small_prep(recs, small)
+        else:
+            paths, pks, keep, disp = self._gpu_prep(recs, db, codes, dedup, keep_override)
         # ---- phase 3: emit in order --------------------------------------------
         return self._emit(parsed, recs, paths, pks, keep, disp, errors)
 
@@ -690,6 +703,41 @@ class VCFVariantLoader(object):
                     pk_err = ValueError("too many values to unpack (expected 4)")
                 recs.append([li, alt, metaseq, pk_err, len(ref) + len(alt) > max_len, v])
         return recs
+
+    def _small_prep(self, recs, res):
+        """K8's outputs as ``_gpu_prep`` returns them.  Keys K8 rendered are used
+        as is; the others (long alleles: the VRS digest; ':' in an allele; ids
+        without a canonical form) go through the PK generator, which raises where
+        the reference raises."""
+        from . import _native as N
+        n = len(recs)
+        pks: List[Optional[str]] = [None] * n
+        ks = res["key_state"]
+        items, idx = [], []
+        for i, r in enumerate(recs):
+            if r[3] is not None:
+                continue
+            if ks[i] == N.KEY_OK:
+                pks[i] = res["key"][i]
+            else:
+                items.append((r[2], r[5].ref_snp_id))
+                idx.append(i)
+        if items:
+            try:
+                for i, k in zip(idx, self._pk_generator.generate_primary_keys(items)):
+                    pks[i] = k
+            except ValueError:
+                for i, it in zip(idx, items):  # isolate the failing records
+                    try:
+                        pks[i] = self._pk_generator.generate_primary_keys([it])[0]
+                    except ValueError as err:
+                        recs[i][3] = err
+        self._match = None
+        self._adsp_dup = None
+        if self.is_adsp() and self._existing is not None:
+            self._adsp_dup = [pk is not None and self._existing.has_primary_key(pk) for pk in pks]
+        disp = [d if st == 0 else None for d, st in zip(res["display"], res["disp_state"])]
+        return res["path"], pks, None, disp
 
     def _gpu_prep(self, recs, db, codes, dedup, keep_override=None):
         """K2 (+K3) and K5a on the device batch, then ltree text, primary keys

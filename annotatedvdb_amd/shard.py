@@ -66,6 +66,47 @@ def imbalance(assignment: List[List[Piece]]) -> float:
     return max(loads) / mean if mean else 1.0
 
 
+def piece_table(assignment: List[List[Piece]], lengths: Sequence[int] | None = None, cut: int = PIECE):
+    """The plan as the flat tables K9 (``avdb_vcf_select_lines``) stages in LDS:
+    ``(piece_base[n_chrom], piece_count[n_chrom], piece_rank[n_pieces])`` over
+    ``pieces(lengths, cut)`` order (numpy arrays)."""
+    import numpy as np
+    ps = pieces(lengths, cut)
+    owner = {}
+    for r, a in enumerate(assignment):
+        for p in a:
+            owner[(p.chrom, p.lo)] = r
+    n_chrom = len(list(lengths) if lengths is not None else length_table())
+    base = np.zeros(n_chrom, dtype=np.uint32)
+    count = np.zeros(n_chrom, dtype=np.uint32)
+    rank = np.zeros(len(ps), dtype=np.uint8)
+    for i, p in enumerate(ps):
+        if count[p.chrom] == 0:
+            base[p.chrom] = i
+        count[p.chrom] += 1
+        rank[i] = owner[(p.chrom, p.lo)]
+    return base, count, rank
+
+
+def owner_of_lines(assignment: List[List[Piece]], chrom, pos, flags, n_chrom: int = 25,
+                   lengths: Sequence[int] | None = None, cut: int = PIECE):
+    """Host restatement of K9's line placement (the test checker): -1 for
+    comment lines, 0 for lines K0 could not place, else the piece owner."""
+    import numpy as np
+    base, count, rank = piece_table(assignment, lengths, cut)
+    chrom = np.asarray(chrom, dtype=np.int64)
+    pos = np.asarray(pos, dtype=np.int64)
+    flags = np.asarray(flags, dtype=np.int64)
+    out = np.zeros(len(chrom), dtype=np.int64)
+    ok = (chrom < n_chrom) & ((flags & (0x004 | 0x080 | 0x100 | 0x002)) == 0)
+    c = np.where(ok, chrom, 0)
+    k = np.where(pos > 0, (pos - 1) // cut, 0)
+    k = np.minimum(k, count[c].astype(np.int64) - 1)
+    out[ok] = rank[(base[c].astype(np.int64) + k)[ok]]
+    out[(flags & 0x001) != 0] = -1
+    return out
+
+
 def shard_of(assignment: List[List[Piece]], chrom: int, start: int) -> int:
     for r, ps in enumerate(assignment):
         for p in ps:

@@ -313,6 +313,54 @@ int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, 
                       size_t key_cap, uint8_t* path_out, size_t path_cap, uint8_t* key_state,
                       void* stream);
 
+/* ---- K8: the per-record drop-in path in one launch -------------------------
+ * The reference calls its per-record API once per alt allele
+ * (vcf_variant_loader.py:282-311: __generate_primary_key, infer_variant_end_location,
+ * find_bin_index, get_display_attributes).  For a small batch (one VCF line, one
+ * find_bin_index miss) this entry does K2 + K7 + K5a in ONE launch of one
+ * workgroup; every array may live in host-mapped pinned memory (avdb_host_alloc),
+ * so a call is one launch + one stream sync, no copies.
+ * Inputs: chrom, pos, and either end_in (bin of [pos, end_in]) or the alleles
+ * (allele_off/ref_len/alt_len/heap, ext_id nullable: end inferred).  Outputs:
+ * end_out, code, status per record; with alleles key_state (AVDB_KEY_*) and
+ * disp_state (0 ok, 1 non-ASCII, 2 heap overrun); text streams selected by `want`
+ * (AVDB_SMALL_PATH / _KEY / _DISPLAY) into text_out[k] (8-byte aligned, text_cap[k]
+ * bytes) with offsets off_out[k*(n+1) + i] (u32).  A stream whose total exceeds
+ * its cap is not written and sets bit k of *overflow. */
+#define AVDB_SMALL_PATH 1u
+#define AVDB_SMALL_KEY 2u
+#define AVDB_SMALL_DISPLAY 4u
+#define AVDB_SMALL_MAX 65536
+typedef struct avdb_small_batch {
+  const uint8_t* chrom;
+  const uint32_t* pos;
+  const uint32_t* end_in;
+  const uint64_t* allele_off;
+  const uint32_t* ref_len;
+  const uint32_t* alt_len;
+  const uint8_t* heap;
+  const uint64_t* ext_id;
+  size_t heap_bytes;
+  uint32_t n;
+  uint32_t max_seq_len;
+  uint32_t want;
+  uint32_t reserved;
+  uint32_t* end_out;
+  uint32_t* code;
+  uint8_t* status;
+  uint8_t* key_state;
+  uint8_t* disp_state;
+  uint32_t* off_out;
+  uint8_t* text_out[3];
+  uint32_t text_cap[3];
+  uint32_t* overflow;
+} avdb_small_batch;
+int avdb_small_prep(avdb_ctx* ctx, const avdb_small_batch* batch, void* stream);
+/* Pinned host memory mapped into the device address space (hipHostMalloc,
+ * mapped + coherent): the same pointer is valid on the host and in kernels. */
+int avdb_host_alloc(size_t bytes, void** ptr);
+int avdb_host_free(void* ptr);
+
 /* ---- K6: duplicate check against variants already loaded ---------------
  * Replaces VariantRecord.exists / SQL map_variants(id, firstHitOnly, checkAltVariants)
  * (Util/lib/python/database/variant.py:41,287-309) as used by --skipExisting
@@ -340,6 +388,29 @@ int avdb_keyset_probe(avdb_ctx* ctx, const void* table, size_t table_bytes, cons
 int avdb_keyset_probe_text(avdb_ctx* ctx, const void* table, size_t table_bytes, const uint8_t* keys,
                            const uint64_t* key_off, size_t n_keys, const uint8_t* q, const uint64_t* q_off,
                            const uint8_t* skip, size_t n, int32_t* match, uint64_t* counters, void* stream);
+
+/* ---- K9: genome-piece sharding of VCF text --------------------------------
+ * The reference runs one process per chromosome file (Load/bin/load_vcf_file.py:
+ * 307-313).  One file is split over the ranks of a node by a piece plan
+ * (annotatedvdb_amd/shard.py: contigs cut at `cut` bp, pieces assigned to ranks):
+ * piece_base[c] / piece_count[c] (host, one per contig) index piece_rank[]
+ * (host, n_pieces <= 1024).  A K0 data line belongs to the rank owning the piece
+ * that holds its POS (a POS past the contig end: its last piece); lines K0 could
+ * not place (host-resolved CHROM/POS, empty or short lines) belong to rank 0;
+ * comment lines to none.
+ *   avdb_vcf_select_lines: sel_off[n_lines+1] = exclusive scan of this rank's
+ *     bytes per line (line length + 1), total in sel_off[n_lines]; workspace of
+ *     avdb_shard_workspace_size(n_lines) bytes.
+ *   avdb_vcf_select_copy:  the rank's lines, each + '
+', into out (sel_off[n_lines]
+ *     bytes), in file order. */
+int avdb_shard_workspace_size(size_t n_lines, size_t* bytes);
+int avdb_vcf_select_lines(avdb_ctx* ctx, size_t n_lines, const avdb_vcf_line* lines,
+                          const uint32_t* piece_base_host, const uint32_t* piece_count_host,
+                          const uint8_t* piece_rank_host, uint32_t n_pieces, uint32_t cut, int rank,
+                          void* workspace, size_t workspace_bytes, uint64_t* sel_off, void* stream);
+int avdb_vcf_select_copy(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                         const avdb_vcf_line* lines, const uint64_t* sel_off, uint8_t* out, void* stream);
 
 /* ---- host-side formatting of kernel outputs -------------------------------
  * ltree path text (<= AVDB_MAX_PATH bytes).  Returns the length written (no

@@ -167,3 +167,51 @@ def test_k7_states_and_edge_records(engine):
     e = pack_records([], [], [], []).to("cuda")
     kt0 = engine.primary_keys(e)
     assert int(kt0.key_off[0]) == 0
+
+
+def test_k8_small_batch_equals_multi_kernel_path(engine):
+    """K8 (one launch, host-mapped memory: the per-line drop-in path) gives the
+    same end / bin / status, key text, ltree path and display-attribute JSON as
+    K2 + K7 + K5a on the same records, across allele classes and edge records."""
+    from annotatedvdb_amd import _native as N
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.engine import pack_records
+    b = synth.alleles(3000, seed=81, long_frac=0.05)
+    h = host(b)
+    n = b.n
+    refs = [h["heap"][o:o + r].tobytes() for o, r in zip(h["allele_off"], h["ref_len"])]
+    alts = [h["heap"][o + r:o + r + a].tobytes() for o, r, a in zip(h["allele_off"], h["ref_len"], h["alt_len"])]
+    extra = [(0, 100, b"A:C", b"A", 0), (24, 16569, b"T", b"TAA", 12), (30, 5, b"A", b"G", 0),
+             (21, 50818468, b"G", b"GT", 0), (0, 7, b"AT", b"AT", 5), (2, 9, b"C", b"T", (1 << 63) | 4)]
+    chrom = list(h["chrom"]) + [e[0] for e in extra]
+    pos = list(h["pos"]) + [e[1] for e in extra]
+    refs += [e[2] for e in extra]
+    alts += [e[3] for e in extra]
+    ext = [int(x) for x in h["ext_id"]] + [e[4] for e in extra]
+    res = engine.small().run(chrom, pos, refs=refs, alts=alts, ext=ext,
+                             want=N.SMALL_PATH | N.SMALL_KEY | N.SMALL_DISPLAY)
+    assert res is not None
+    db = pack_records(chrom, pos, refs, alts, ext).to("cuda")
+    end, code, status, _ = engine.record_prep(db, want_lcp=False)
+    assert np.array_equal(res["end"], u32(end))
+    assert np.array_equal(res["code"], u32(code))
+    assert np.array_equal(res["status"], status.cpu().numpy())
+    kt = engine.primary_keys(db, code=code)
+    keys, paths = kt.host(db.n)
+    ks = kt.state[: db.n].cpu().numpy()
+    # K7 without digests: long records are NEED_DIGEST in both
+    assert np.array_equal(res["key_state"], ks)
+    assert [k if s == N.KEY_OK else None for k, s in zip(res["key"], res["key_state"])] == keys
+    assert res["path"] == paths
+    text, off, st = engine.display_attributes(db, end)
+    raw = text.cpu().numpy().tobytes().decode()
+    o = off.cpu().numpy()
+    assert np.array_equal(res["disp_state"], st.cpu().numpy())
+    exp_disp = [raw[o[i]:o[i + 1]] if st[i] == 0 else None for i in range(db.n)]
+    assert res["display"] == exp_disp
+    # bins of explicit intervals (the find_bin_index miss path)
+    r2 = engine.small().run([0, 0, 21, 99], [15625, 1, 50818468, 5], ends=[15626, 248956422, 50818469, 5],
+                            want=N.SMALL_PATH)
+    assert r2["path"][0] == O.format_bin_path("1", int(r2["code"][0])) and r2["path"][1] == "chr1"
+    assert r2["path"][2] is None and r2["path"][3] is None
+    assert list(r2["status"]) == [0, 0, 2, 1]

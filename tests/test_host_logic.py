@@ -126,3 +126,37 @@ def test_bench_step_does_not_shadow_main_buffers():
     step = next(n for n in ast.walk(main) if isinstance(n, ast.FunctionDef) and n.name == "step")
     stored = {n.id for n in ast.walk(step) if isinstance(n, ast.Name) and isinstance(n.ctx, ast.Store)}
     assert not stored & {"chrom", "start", "end", "code", "hist", "ctr", "batch", "text", "eng"}, stored
+
+
+def test_piece_table_and_line_owner_oracle():
+    """The flat piece tables K9 stages and the host restatement of its line
+    placement agree with shard_of on every piece boundary."""
+    from annotatedvdb_amd import shard
+    from annotatedvdb_amd.chromosomes import length_table
+    lens = length_table()
+    for world in (1, 2, 3, 8):
+        plan = shard.plan(world, lens)
+        base, count, rank = shard.piece_table(plan, lens)
+        assert count.sum() == len(rank) == len(shard.pieces(lens))
+        chrom, pos = [], []
+        for p in shard.pieces(lens):
+            for x in (p.lo + 1, p.hi, (p.lo + p.hi) // 2):
+                chrom.append(p.chrom)
+                pos.append(x)
+        own = shard.owner_of_lines(plan, chrom, pos, [0] * len(pos))
+        assert [shard.shard_of(plan, c, x) for c, x in zip(chrom, pos)] == own.tolist()
+        # comments: nobody; unplaced (unknown contig / host-resolved POS): rank 0; past the end: last piece
+        o = shard.owner_of_lines(plan, [0, 255, 3, 24], [5, 5, 5, 10 ** 9], [0x001, 0, 0x004, 0])
+        assert o[0] == -1 and o[1] == 0 and o[2] == 0 and o[3] == shard.shard_of(plan, 24, lens[24])
+
+
+def test_driver_file_assignment_lpt(tmp_path):
+    from annotatedvdb_amd import load_vcf_file
+    fs = []
+    for i, sz in enumerate([50, 10, 40, 30, 20]):
+        f = tmp_path / ("f%d" % i)
+        f.write_bytes(b"x" * sz)
+        fs.append(str(f))
+    a = load_vcf_file.assign_files(fs, 2)
+    assert sorted(sum(a, [])) == sorted(fs)
+    assert a[0] == [fs[0], fs[1], fs[4]] and a[1] == [fs[2], fs[3]]
