@@ -42,6 +42,20 @@ def _xstr(v, nullStr="", falseAsNull=False):
 DEFAULT_FIELDS = ["chrom", "pos", "id", "ref", "alt", "qual", "filter", "info"]
 
 
+class _LazyInfo(object):
+    """An INFO string not yet split into its dict (vcf_parser.py:101-110)."""
+
+    __slots__ = ("s",)
+
+    def __init__(self, s: str):
+        self.s = s
+
+    def resolve(self) -> dict:
+        infoStr = self.s.replace("\\x59", "/").replace("#", ":")
+        info = dict(item.split("=", 1) if "=" in item else [item, True] for item in infoStr.split(";"))
+        return convert_str2numeric_values(info)
+
+
 class VcfEntryParser(object):
     """Drop-in for the reference ``VcfEntryParser`` (hot-path subset)."""
 
@@ -55,7 +69,10 @@ class VcfEntryParser(object):
         self.__entry = None if entry is None else self.parse_entry(entry)
 
     def parse_entry(self, inputStr):
-        """vcf_parser.py:76-114"""
+        """vcf_parser.py:76-114.  The INFO dict is built and coerced on first
+        use (get_info / get_refsnp / get_entry): the per-line loader reads at
+        most RS, RSPOS and FREQ of it, and an INFO value the reference could not
+        parse still raises here, at parse time."""
         fields = self._header_fields
         values = inputStr.split("\t")
         try:
@@ -63,11 +80,9 @@ class VcfEntryParser(object):
                 else {field: values[index] for index, field in enumerate(fields)}
             result = convert_str2numeric_values(entry)
             if "info" in result:
+                # (a numeric INFO has no .replace: the reference's ImportError, raised now)
                 infoStr = result["info"].replace("\\x2c", ",")
-                infoStr = infoStr.replace("\\x59", "/")
-                infoStr = infoStr.replace("#", ":")
-                info = dict(item.split("=", 1) if "=" in item else [item, True] for item in infoStr.split(";"))
-                result["info"] = convert_str2numeric_values(info)
+                result["info"] = _LazyInfo(infoStr)
         except IndexError:
             raise IndexError("The number of fields in the VCF entry do not match number expected "
                              "from provided VCF Header")
@@ -106,16 +121,26 @@ class VcfEntryParser(object):
         self.__verify_entry()
         if "rs" in self.__entry["id"]:
             return self.__entry["id"]
-        if "info" in self.__entry and "RS" in self.__entry["info"]:
-            return "rs" + str(self.__entry["info"]["RS"])
+        if "info" in self.__entry and "RS" in self._info():
+            return "rs" + str(self._info()["RS"])
         return None
 
+    def _info(self) -> dict:
+        info = self.__entry["info"]
+        if isinstance(info, _LazyInfo):
+            info = self.__entry["info"] = info.resolve()
+        return info
+
     def get_entry(self):
+        if self.__entry is not None and "info" in self.__entry:
+            self._info()
         return self.__entry
 
     def get(self, key, raiseError=True):
         self.__verify_entry()
         try:
+            if key == "info" and "info" in self.__entry:
+                return self._info()
             return self.__entry[key]
         except KeyError as err:
             if raiseError:
@@ -126,8 +151,9 @@ class VcfEntryParser(object):
         self.__verify_entry()
         if "info" not in self.__entry:
             return None
-        if key in self.__entry["info"]:
-            return self.__entry["info"][key]
+        info = self._info()
+        if key in info:
+            return info[key]
         return default
 
     def get_frequencies(self, allele):
