@@ -39,18 +39,56 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build libavdb_hip.so)")
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not _stale():
+def _obj(src: str, flags) -> str:
+    tag = "".join(f for f in flags if f.startswith("-D")).replace("-D", "_").replace("=", "")
+    return os.path.join(OUT_DIR, "obj", os.path.basename(src)[:-4] + tag + ".o")
+
+
+def _obj_stale(src: str, obj: str) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    deps = [src] + glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _reap(job) -> None:
+    pr, obj = job
+    if pr.wait() != 0:
+        raise subprocess.CalledProcessError(pr.returncode, "hipcc -c -> " + obj)
+    os.replace(obj + ".tmp", obj)
+
+
+def build(force: bool = False, verbose: bool = True, out: str = None, flags=()) -> str:
+    """One object per source, compiled concurrently (each .hip is its own
+    translation unit: no device code crosses files), then one link."""
+    out = out or LIB
+    if not force and out == LIB and not flags and not _stale():
         return LIB
-    os.makedirs(OUT_DIR, exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-I", INCLUDE, "-o", tmp] + sources()
+    os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
+    base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", INCLUDE] + list(flags)
+    procs = []
+    objs = []
+    jobs = max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    for src in sources():
+        obj = _obj(src, flags)
+        objs.append(obj)
+        if force or _obj_stale(src, obj):
+            cmd = base + ["-c", src, "-o", obj + ".tmp"]
+            if verbose:
+                print("[avdb] " + " ".join(cmd), file=sys.stderr)
+            if len(procs) >= jobs:
+                _reap(procs.pop(0))
+            procs.append((subprocess.Popen(cmd), obj))
+    for job in procs:
+        _reap(job)
+    tmp = out + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print("[avdb] " + " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

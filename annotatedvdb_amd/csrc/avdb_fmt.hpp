@@ -1,0 +1,549 @@
+// Text sink and JSON / key / ltree-path renderers shared by the K5 (avdb_format.hip),
+// K5a + K7 (avdb_keys.hip) and K8 (avdb_small.hip) kernels.
+#pragma once
+
+#include "avdb_internal.hpp"
+#include "avdb_text.hpp"
+
+#include <type_traits>
+
+namespace avdb {
+
+
+// ---------------------------------------------------------------------------
+// output sink: SIZE pass counts, WRITE pass stores
+// ---------------------------------------------------------------------------
+// WRITE pass sink: each lane's bytes are packed into a 64-bit register word and
+// stored 8 at a time (an unaligned global_store_dwordx2; gfx950 runs in
+// unaligned mode), the tail (< 8 bytes) byte by byte at the end of the line.
+// The lanes of a wave write 64 different lines, so every store instruction
+// touches up to 64 cache lines: what costs is the number of lane-stores, not
+// bytes.  A/B on MI355X, 8.39 M dbSNP-shaped lines, 5.25 GB written (write
+// pass; size pass 5.1 ms; tools/k5_ab.sh):
+//   byte stores, noinline helpers, 3 waves/SIMD            15.0 ms
+//   same, stores made coalesced (wrong output; the floor)     4.6 ms
+//   8-byte word, noinline helpers, 3 waves/SIMD             9.7 ms
+//   8-byte word, inlined helpers, 3 waves/SIMD              9.3 ms
+//   8-byte word, inlined helpers, 4 waves/SIMD (this)       8.1 ms
+//   16-byte word (two u64), 2 waves/SIMD (VGPR-bound)      17.4 ms
+//   per-lane LDS ring (32/64 B per stream) flushing 16-byte
+//     chunks at convergent points, 2 waves/SIMD             13.4 / 17.7 ms
+// Occupancy decides: the pass is latency-bound on LDS text reads and store
+// back-pressure, so 4 waves/SIMD (launch bound; ~120 B of spills) beats every
+// wider sink that costs registers or LDS.
+// Round 2 (tools/k5_probe.py, same workload, A/B on one box each; the write pass
+// was 5.73 ms before): sink variants, all byte-identical output —
+//   32-byte sectors through 3 LDS slots/lane, 16-byte stores, 4 waves  11.5 ms
+//     (3 waves, 36 KB text window: 8.1 ms; WRITE_SIZE 10.7 -> 8.0 GB)
+//   aligned 8-byte words, byte-masked first/last word                  +32 %
+//   16-byte pending word (two registers), 4 / 3 waves                  +17 / +31 %
+//   32-bit span-relative positions                                     +4 %
+//   pieces concatenated in registers before the sink (Dec-style)       +24 %
+// and what helped: the variant-class strings as constant literals (a string
+// chosen at run time was measured and copied a byte at a time from memory:
+// write 5.43 -> 4.34 ms, size 2.80 -> 2.26 ms) and ranking each tile's lines
+// by shape (-3 %).  SQ/TA counters put the remaining time in VALU issue
+// (1.8e9 wave-instructions per launch) and the texture path (TD busy 90 %):
+// the lanes' 8-byte stores touch 64 lines per instruction, but every
+// alternative above that makes them wider or aligned costs more instructions
+// than it saves.
+typedef __attribute__((address_space(1))) uint8_t gbyte;
+typedef __attribute__((address_space(1))) U64u* gw_u64u;
+// per SIMD: the text window's LDS allows 4 workgroups per CU (re-checked after
+// the append sink: 4 waves with ~100 B of spills 5.5 ms, 3 waves without 6.2 ms)
+constexpr int kFormatWaves = 4;
+
+// decimal digits of v as nibbles, most significant digit in the lowest nibble
+// (registers only: a local char array would live in scratch memory)
+__device__ __forceinline__ uint64_t dec_nibbles(uint32_t v, uint32_t* ndig) {
+  uint64_t d = 0;
+  uint32_t k = 0;
+  do { d = (d << 4) | (v % 10u); v /= 10u; ++k; } while (v);
+  *ndig = k;
+  return d;
+}
+
+__device__ __forceinline__ uint32_t ndigits(uint32_t v) {  // decimal digits
+  uint32_t k = 1;
+  while (v >= 10u) { v /= 10u; ++k; }
+  return k;
+}
+
+// a decimal number as ASCII text in registers (up to 16 digits), so a value
+// printed several times per line is converted once
+struct Dec {
+  uint64_t lo, hi;  // digits 0..7 and 8..15, little-endian bytes
+  uint32_t n;
+};
+
+__device__ __forceinline__ uint64_t nibbles_to_ascii(uint64_t d, uint32_t k) {  // k <= 8
+  uint64_t y = d & 0xFFFFFFFFull;
+  y = (y | (y << 16)) & 0x0000FFFF0000FFFFull;
+  y = (y | (y << 8)) & 0x00FF00FF00FF00FFull;
+  y = (y | (y << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  return (y + 0x3030303030303030ull) & low_bytes_mask(k);
+}
+
+__device__ __forceinline__ Dec dec_text(uint32_t v) {
+  uint32_t k;
+  const uint64_t d = dec_nibbles(v, &k);
+  return Dec{nibbles_to_ascii(d, k < 8 ? k : 8), k > 8 ? nibbles_to_ascii(d >> 32, k - 8) : 0ull, k};
+}
+
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+struct LdsImage {};  // constructor tag of the LDS sink
+
+// LDS = true (WRITE only): the sink renders into a workgroup's LDS image of its
+// output span instead of global memory, for a coalesced flush afterwards.  Every
+// LDS access is an aligned 8-byte word: the words a lane shares with its
+// neighbours (the first and the last of its span) are merged with ds_or_b64 into
+// the zeroed image, the words wholly inside its span are plain ds_write_b64.
+template <bool WRITE, bool LDS = false>
+struct Out {
+  gbyte* base;
+  uint64_t p, lo;
+  bool bad;  // set by a formatter that cannot render its input (line goes to the host)
+  __device__ __forceinline__ Out(uint8_t* b, uint64_t at)
+      : base((gbyte*)b), p(at), lo(at), bad(false) {}
+  // LDS sink: `at` is the byte offset in the image (same alignment mod 8 as the
+  // global destination)
+  __device__ __forceinline__ Out(LdsImage, lds_u64* img, uint64_t at) : base(nullptr), p(at), lo(at), bad(false) {
+    if constexpr (LDS) {
+      pend.img = img;
+      pend.k = uint32_t(at & 7u);
+    }
+  }
+  __device__ __forceinline__ uint32_t size() const { return uint32_t(p - lo); }
+  struct Pending {  // WRITE: bytes [p-k, p) not yet stored
+    uint64_t w = 0;
+    uint32_t k = 0;
+  };
+  struct LPending {  // LDS: bytes [p-k, p) of the current aligned word (the first
+    uint64_t w = 0;  // word's low bytes belong to the previous lane: zero here)
+    uint32_t k = 0;
+    bool first = true;
+    lds_u64* img = nullptr;
+  };
+  struct None {};
+  [[no_unique_address]] std::conditional_t<WRITE, std::conditional_t<LDS, LPending, Pending>, None> pend;
+  // append t (1..8) bytes, little-endian in x (bytes of x at and above t are 0)
+  __device__ __forceinline__ void append(uint64_t x, uint32_t t) {
+    if constexpr (WRITE && LDS) {
+      const uint32_t k = pend.k;  // 0..7
+      pend.w |= x << (8 * k);
+      if (k + t >= 8) {
+        lds_u64* wp = pend.img + ((p - k) >> 3);
+        if (pend.first) __hip_atomic_fetch_or(wp, pend.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else *wp = pend.w;
+        pend.first = false;
+        pend.w = k ? x >> (64 - 8 * k) : 0ull;
+        pend.k = k + t - 8;
+      } else {
+        pend.k = k + t;
+      }
+    } else if constexpr (WRITE) {
+      const uint32_t k = pend.k;  // 0..7
+      pend.w |= x << (8 * k);
+      if (k + t >= 8) {
+        reinterpret_cast<gw_u64u>(base + p - k)->v = pend.w;
+        pend.w = k ? x >> (64 - 8 * k) : 0ull;
+        pend.k = k + t - 8;
+      } else {
+        pend.k = k + t;
+      }
+    }
+    p += t;
+  }
+  __device__ __forceinline__ void put(uint32_t c) { append(c & 0xFFu, 1); }
+  // end of the line: store the buffered tail
+  __device__ __forceinline__ void finish() {
+    if constexpr (WRITE && LDS) {
+      // the last (partial) word may be shared with the next lane
+      if (pend.k && (p > lo || !pend.first))
+        __hip_atomic_fetch_or(pend.img + ((p - pend.k) >> 3), pend.w, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      pend.w = 0;
+      pend.k = 0;
+    } else if constexpr (WRITE) {
+      const uint32_t k = pend.k;
+      for (uint32_t j = 0; j < k; ++j) base[p - k + j] = uint8_t(pend.w >> (8 * j));
+      pend.w = 0;
+      pend.k = 0;
+    }
+  }
+  // (literal strings: the length and the 8-byte chunks fold at compile time)
+  __device__ __forceinline__ void lit(const char* s) {
+    uint32_t n = 0;
+    while (s[n]) ++n;
+    for (uint32_t i = 0; i < n; i += 8) {
+      const uint32_t t = n - i < 8u ? n - i : 8u;
+      uint64_t x = 0;
+      for (uint32_t j = 0; j < t; ++j) x |= uint64_t(uint8_t(s[i + j])) << (8 * j);
+      append(x, t);
+    }
+  }
+  template <class CP>
+  __device__ __forceinline__ void bytes(CP s, uint32_t n) {
+    if constexpr (!WRITE) {
+      p += n;
+    } else if constexpr (std::is_same_v<CP, lds_cp> || std::is_same_v<CP, glb_cp>) {
+      // aligned 8-byte text words, up to 8 bytes per append
+      const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(s)) & 7u;
+      const typename Word64<CP>::T w = reinterpret_cast<typename Word64<CP>::T>(s - mis);
+      for (uint32_t i = 0; i < n;) {
+        const uint32_t q = mis + i, o = q & 7u;
+        const uint32_t t = (8u - o) < (n - i) ? 8u - o : n - i;
+        append((w[q >> 3] >> (8 * o)) & low_bytes_mask(t), t);
+        i += t;
+      }
+    } else {
+      for (uint32_t k = 0; k < n; ++k) put(s[k]);
+    }
+  }
+  // up to 8 decimal digits given as nibbles (most significant lowest) -> ASCII
+  __device__ __forceinline__ void digits8(uint64_t d, uint32_t k) { append(nibbles_to_ascii(d, k), k); }
+  __device__ __forceinline__ void dec(const Dec& t) {
+    if constexpr (!WRITE) {
+      p += t.n;
+    } else {
+      append(t.lo, t.n < 8 ? t.n : 8);
+      if (t.n > 8) append(t.hi, t.n - 8);
+    }
+  }
+  __device__ __forceinline__ void u32v(uint32_t v) {
+    if constexpr (!WRITE) {
+      p += ndigits(v);
+      return;
+    }
+    uint32_t k;
+    const uint64_t d = dec_nibbles(v, &k);
+    if (k > 8) {
+      digits8(d, 8);
+      digits8(d >> 32, k - 8);
+    } else {
+      digits8(d, k);
+    }
+  }
+  __device__ __forceinline__ void u64v(uint64_t v) {
+    if (v <= 0xFFFFFFFFull) { u32v(uint32_t(v)); return; }
+    const uint64_t q = v / 1000000000ull;
+    if (q <= 0xFFFFFFFFull) {
+      u32v(uint32_t(q));
+    } else {
+      u32v(uint32_t(q / 1000000000ull));
+      dec9(uint32_t(q % 1000000000ull));
+    }
+    dec9(uint32_t(v % 1000000000ull));
+  }
+  __device__ __forceinline__ void dec9(uint32_t v) {  // exactly 9 digits, zero-padded
+    if constexpr (!WRITE) {
+      p += 9;
+      return;
+    }
+    uint64_t d = 0;
+    for (int i = 0; i < 9; ++i) { d = (d << 4) | (v % 10u); v /= 10u; }
+    digits8(d, 8);
+    digits8(d >> 32, 1);
+  }
+};
+
+// contig label (Util/lib/python/enums/chromosomes.py:9-38 order)
+template <class O>
+__device__ __forceinline__ void chrom_name(O& o, uint32_t c) {
+  if (c < 9) o.put('1' + c);
+  else if (c < 22) o.append(uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8), 2);
+  else if (c == 22) o.put('X');
+  else if (c == 23) o.put('Y');
+  else if (c == 24) o.put('M');
+  else o.u32v(c);  // contigs beyond the human 25: numeric label (matches avdb_format_bin_path)
+}
+
+// ltree path of a bin code (generate_bin_index_references.py:54,60-61,74): one
+// 6- or 7-byte append per level (".L<l>.B<b>").
+// Helpers take and return the sink by value (never by reference: a sink whose
+// address escapes lives in scratch memory); all are inlined (see the A/B above).
+template <class O>
+__device__ __forceinline__ O bin_path(O o, uint32_t c, uint32_t code) {
+  o.lit("chr");
+  chrom_name(o, c);
+  const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
+  for (uint32_t l = 1; l <= level; ++l) {
+    const uint32_t gl = g >> (level - l);
+    const uint32_t b = l == 1 ? gl + 1 : (gl & 1u) + 1;
+    if (b >= 10) {  // L1 of a contig longer than 576 Mb (custom chromosome tables)
+      o.lit(".L");
+      o.u32v(l);
+      o.lit(".B");
+      o.u32v(b);
+    } else if (l < 10) {
+      o.append(0x000000422E004C2Eull | (uint64_t('0' + l) << 16) | (uint64_t('0' + b) << 40), 6);
+    } else {
+      o.append(0x00422E00314C2Eull | (uint64_t('0' + l - 10) << 24) | (uint64_t('0' + b) << 48), 7);
+    }
+  }
+  return o;
+}
+
+// ---------------------------------------------------------------------------
+// JSON strings (json.dumps, ensure_ascii): '"' '\\' and the short escapes,
+// other bytes outside ' '..'~' as \u00XX (lowercase hex)
+// ---------------------------------------------------------------------------
+template <bool ESC, class O, class CP>
+__device__ __forceinline__ void jstr(O& o, CP s, uint32_t n) {
+  if constexpr (!ESC) {
+    o.bytes(s, n);
+  } else {
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint8_t c = s[i];
+      if (c >= 0x20 && c < 0x7F && c != '"' && c != '\\') { o.put(c); continue; }
+      o.put('\\');
+      switch (c) {
+        case '"': o.put('"'); break;
+        case '\\': o.put('\\'); break;
+        case '\n': o.put('n'); break;
+        case '\r': o.put('r'); break;
+        case '\t': o.put('t'); break;
+        case '\b': o.put('b'); break;
+        case '\f': o.put('f'); break;
+        default: {
+          const char* hx = "0123456789abcdef";
+          o.lit("u00");
+          o.put(uint8_t(hx[c >> 4]));
+          o.put(uint8_t(hx[c & 15]));
+        }
+      }
+    }
+  }
+}
+
+// an allele in its display form: bytes, or '-' for an empty normalized allele
+// (variant_annotator.py:111-116, snvDivMinus=True)
+template <class CP>
+struct Al {
+  CP p;
+  uint32_t n;
+  bool dash;
+};
+
+template <bool ESC, class O, class CP>
+__device__ __forceinline__ void al_str(O& o, const Al<CP>& a) {
+  if (a.dash) o.put('-');
+  else jstr<ESC>(o, a.p, a.n);
+}
+
+// truncate(s, cap) = s if len(s) <= cap else s[:cap] + '...' (variant_annotator.py:8-10)
+template <bool ESC, class O, class CP>
+__device__ __forceinline__ void al_trunc(O& o, const Al<CP>& a, uint32_t cap) {
+  if (a.dash) { o.put('-'); return; }
+  jstr<ESC>(o, a.p, a.n < cap ? a.n : cap);
+  if (a.n > cap) o.lit("...");
+}
+
+// ', "variant_class": .., "variant_class_abbrev": ..' of a display class
+// (variant_annotator.py:150-239).  Constant literals per case: a string chosen
+// at run time would be measured and copied a byte at a time from memory.
+template <class O>
+__device__ __forceinline__ void variant_class_text(O& o, int cls, bool dup) {
+  switch (cls) {
+    case 0: o.lit(", \"variant_class\": \"single nucleotide variant\", \"variant_class_abbrev\": \"SNV\""); break;
+    case 1: o.lit(", \"variant_class\": \"inversion\", \"variant_class_abbrev\": \"MNV\""); break;
+    case 2: o.lit(", \"variant_class\": \"substitution\", \"variant_class_abbrev\": \"MNV\""); break;
+    case 3:
+    case 4: o.lit(", \"variant_class\": \"indel\", \"variant_class_abbrev\": \"INDEL\""); break;
+    case 5:
+      if (dup) o.lit(", \"variant_class\": \"duplication\", \"variant_class_abbrev\": \"DUP\"");
+      else o.lit(", \"variant_class\": \"insertion\", \"variant_class_abbrev\": \"INS\"");
+      break;
+    default: o.lit(", \"variant_class\": \"deletion\", \"variant_class_abbrev\": \"DEL\""); break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// get_display_attributes (variant_annotator.py:134-241) as json.dumps text.
+// Keys in the reference's dict insertion order: location_start, location_end,
+// [normalized_metaseq_id], then variant_class, variant_class_abbrev,
+// display_allele, sequence_allele — except the insertion branch (:192-229),
+// whose update() lists display_allele and sequence_allele first.
+// chrom >= 25 writes no label in normalized_metaseq_id (the caller prepends it).
+// ---------------------------------------------------------------------------
+template <bool ESC, class O, class CP>
+__device__ __forceinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, CP ref, uint32_t r,
+                                       CP alt, uint32_t a, Dec posd = Dec{0, 0, 0}) {
+  const bool snv = r == 1u && a == 1u;
+  uint32_t l = 0;  // common prefix (__normalize_alleles :100-107); SNVs untouched (:97-98)
+  if (!snv) {
+    const uint32_t m = r < a ? r : a;
+    while (l < m && ref[l] == alt[l]) ++l;
+  }
+  const uint32_t nr = r - l, na = a - l;
+  const Al<CP> nref{ref + l, nr, l > 0 && nr == 0}, nalt{alt + l, na, l > 0 && na == 0};
+  uint32_t ls = pos, le = pos;
+  int cls;  // 0 SNV, 1 inversion, 2 substitution, 3 indel, 4 indel (ins downstream), 5 ins/dup, 6 deletion
+  bool dup = false;
+  const Al<CP> orig{r ? ref + 1 : ref, r ? r - 1 : 0, false};
+  if (snv) {
+    cls = 0;
+  } else if (r == a) {  // MNV (:171-189)
+    bool inv = true;
+    for (uint32_t i = 0; i < r && inv; ++i) inv = ref[i] == alt[r - 1 - i];
+    cls = inv ? 1 : 2;
+    le = end;
+  } else if (na >= 1) {  // insertion (:192-229)
+    ls = pos + 1;
+    // originalRef.count(normAlt) non-overlapping and len/count == len(normAlt)
+    // <=> originalRef == normAlt * k, k >= 1
+    if (orig.n > 0 && orig.n % na == 0) {
+      dup = true;
+      for (uint32_t i = 0, j = 0; i < orig.n && dup; ++i) {
+        dup = orig.p[i] == nalt.p[j];
+        if (++j == na) j = 0;
+      }
+    }
+    if (nr >= 1) { cls = 3; le = end; }
+    else if (end != pos + 1) { cls = 4; le = end; }
+    else { cls = 5; le = pos + 1; }
+  } else {  // deletion (:231-239)
+    cls = 6;
+    ls = pos + 1;
+    le = end;
+  }
+  o.lit("{\"location_start\": ");
+  if (posd.n && ls == pos) o.dec(posd);  // posd: POS as text, when the caller has it
+  else o.u32v(ls);
+  o.lit(", \"location_end\": ");
+  if (posd.n && le == pos) o.dec(posd);
+  else o.u32v(le);
+  if (!snv && l > 0) {  // normalized id differs from the metaseq id iff a prefix was trimmed
+    o.lit(", \"normalized_metaseq_id\": \"");
+    if (chrom < 25) chrom_name(o, chrom);
+    o.put(':');
+    if (posd.n) o.dec(posd);
+    else o.u32v(pos);
+    o.put(':');
+    al_str<ESC>(o, nref);
+    o.put(':');
+    al_str<ESC>(o, nalt);
+    o.put('"');
+  }
+  const bool order_b = cls >= 3 && cls <= 5;
+  if (!order_b) variant_class_text(o, cls, dup);
+  const uint64_t pre = dup ? 0x707564ull : 0x736E69ull;  // "dup" / "ins"
+  const Al<CP> raw_ref{ref, r, false}, raw_alt{alt, a, false};
+  o.lit(", \"display_allele\": \"");
+  switch (cls) {
+    case 0: al_str<ESC>(o, raw_ref); o.put('>'); al_str<ESC>(o, raw_alt); break;
+    case 1: o.lit("inv"); al_str<ESC>(o, raw_ref); break;
+    case 2: al_str<ESC>(o, nref); o.put('>'); al_str<ESC>(o, nalt); break;
+    case 3: o.lit("del"); al_trunc<ESC>(o, nref, 100); o.append(pre, 3); al_trunc<ESC>(o, nalt, 100); break;
+    case 4: o.lit("del"); al_trunc<ESC>(o, orig, 100); o.append(pre, 3); al_trunc<ESC>(o, nalt, 100); break;
+    case 5: o.append(pre, 3); al_trunc<ESC>(o, nalt, 100); break;
+    default: o.lit("del"); al_trunc<ESC>(o, nref, 100); break;
+  }
+  o.lit("\", \"sequence_allele\": \"");
+  switch (cls) {
+    case 0: al_str<ESC>(o, raw_ref); o.put('/'); al_str<ESC>(o, raw_alt); break;
+    case 1: al_trunc<ESC>(o, raw_ref, 8); o.put('/'); al_trunc<ESC>(o, raw_alt, 8); break;
+    case 5: o.append(pre, 3); al_trunc<ESC>(o, nalt, 8); break;
+    case 6: al_trunc<ESC>(o, nref, 8); o.lit("/-"); break;
+    default: al_trunc<ESC>(o, nref, 8); o.put('/'); al_trunc<ESC>(o, nalt, 8); break;
+  }
+  o.put('"');
+  if (order_b) variant_class_text(o, cls, dup);
+  o.put('}');
+  return o;
+}
+
+// ---------------------------------------------------------------------------
+// to_numeric(str) as json.dumps prints it, for the canonical subset:
+//   [0-9]+            int()   -> digits without leading zeros
+//   [0-9]*.[0-9]*     float() -> repr(): <= 15 significant digits round-trip to
+//                     exactly those digits, fixed notation for decimal exponent
+//                     -4..15, else d.ddde[+-]XX
+// Anything else (signs, exponents, '_', spaces, nan/inf, > 15 significant
+// digits) returns false: the line is rendered by the host.
+// ---------------------------------------------------------------------------
+template <class CP>
+__device__ __forceinline__ bool number_plain(CP f, uint32_t n) {
+  if (n == 0 || n > 40) return false;
+  uint32_t dot = n, f0 = n, l0 = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (f[i] == '.') {
+      if (dot != n) return false;
+      dot = i;
+    } else if (!is_digit(f[i])) {
+      return false;
+    } else if (f[i] != '0') {
+      if (f0 == n) f0 = i;
+      l0 = i;
+    }
+  }
+  if (dot == n) return true;                  // int
+  if (n == 1) return false;                   // "." alone
+  if (f0 == n) return true;                   // 0.0
+  const uint32_t nd = l0 - f0 + 1 - (f0 < dot && dot < l0 ? 1u : 0u);
+  return nd <= 15;                            // repr == these digits
+}
+
+template <class O, class CP>
+__device__ __forceinline__ O json_number(O o, CP f, uint32_t n) {
+  o.bad = !number_plain(f, n);
+  if (o.bad) return o;
+  uint32_t dot = n;
+  for (uint32_t i = 0; i < n; ++i)
+    if (f[i] == '.') dot = i;
+  if (dot == n) {  // int
+    uint32_t i = 0;
+    while (i + 1 < n && f[i] == '0') ++i;
+    o.bytes(f + i, n - i);
+    return o;
+  }
+  // digits without the dot: S[k] = f[k < dot ? k : k + 1], ns = n - 1
+  const uint32_t ns = n - 1;
+  auto S = [&](uint32_t k) -> uint8_t { return f[k < dot ? k : k + 1]; };
+  int32_t f0 = -1, l0 = -1;
+  for (uint32_t k = 0; k < ns; ++k) {
+    if (S(k) != '0') {
+      if (f0 < 0) f0 = int32_t(k);
+      l0 = int32_t(k);
+    }
+  }
+  if (f0 < 0) { o.lit("0.0"); return o; }
+  const int32_t nd = l0 - f0 + 1;
+  const int32_t e = int32_t(dot) - 1 - f0;  // decimal exponent of the first significant digit
+  if (e >= -4 && e < 16) {
+    if (e >= 0) {
+      for (int32_t k = 0; k <= e; ++k) o.put(k < nd ? S(uint32_t(f0 + k)) : '0');
+      o.put('.');
+      if (nd > e + 1) {
+        for (int32_t k = e + 1; k < nd; ++k) o.put(S(uint32_t(f0 + k)));
+      } else {
+        o.put('0');
+      }
+    } else {
+      o.lit("0.");
+      for (int32_t k = 0; k < -e - 1; ++k) o.put('0');
+      for (int32_t k = 0; k < nd; ++k) o.put(S(uint32_t(f0 + k)));
+    }
+  } else {
+    o.put(S(uint32_t(f0)));
+    if (nd > 1) {
+      o.put('.');
+      for (int32_t k = 1; k < nd; ++k) o.put(S(uint32_t(f0 + k)));
+    }
+    o.put('e');
+    o.put(e < 0 ? '-' : '+');
+    const uint32_t ae = uint32_t(e < 0 ? -e : e);
+    if (ae < 10) o.put('0');
+    o.u32v(ae);
+  }
+  return o;
+}
+
+// ':' in an allele (the reference's metaseq split raises ValueError,
+// primary_key_generator.py:106) or a non-ASCII byte (outside the contract)
+template <class CP>
+__device__ __forceinline__ bool key_allele_ok(CP s, uint32_t n) {
+  return swar_find(s, n, [](uint64_t x) { return (x & kHiBits) | bytes_eq_mask(x, ':'); }) == n;
+}
+
+}  // namespace avdb

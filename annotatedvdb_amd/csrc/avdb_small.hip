@@ -1,0 +1,221 @@
+// K8 avdb_small_prep: the per-record drop-in path in one launch (gfx950).
+#include "avdb_fmt.hpp"
+
+#include <string.h>
+
+namespace avdb {
+
+// ---------------------------------------------------------------------------
+// K8: the per-record / per-line drop-in path in ONE launch.  The reference
+// calls its per-record API once per alt allele (vcf_variant_loader.py:
+// 282-311): the drop-in's parse_variant / find_bin_index must not pay a chain of
+// launches, scans and host syncs per call.  One workgroup takes a small batch
+// (records in host-mapped pinned memory, read over PCIe): end inference + bin
+// (K2), ltree path, primary key (K7) and display-attribute JSON (K5a) per lane,
+// sizes -> LDS scan -> text written straight into host-mapped output buffers.
+// A stream over its capacity sets *overflow and is not written (the caller
+// then takes the multi-kernel path).
+// ---------------------------------------------------------------------------
+struct SmallArgs {
+  const uint8_t* chrom;
+  const uint32_t* pos;
+  const uint32_t* end_in;  // nullable: infer from the alleles
+  const uint64_t* off;
+  const uint32_t* rl;
+  const uint32_t* al;
+  const uint8_t* heap;
+  const uint64_t* ext;     // nullable
+  size_t heap_bytes;
+  uint32_t n, max_seq_len, want, n_chrom;  // want: AVDB_SMALL_* bits
+  ChromTable tab;
+  uint32_t* end_out;
+  uint32_t* code;
+  uint8_t* status;
+  uint8_t* key_state;
+  uint8_t* disp_state;
+  uint32_t* off_out;       // [3][n+1]: path, key, display offsets
+  uint8_t* text_out[3];
+  uint32_t cap[3];
+  uint32_t* overflow;
+};
+
+constexpr int kSmallBlock = 256;
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t* total) {
+  const int lane = __lane_id(), wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t u = __shfl_up(x, d, kWave);
+    if (lane >= d) x += u;
+  }
+  if (lane == kWave - 1) s_tmp[wv] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (int w = 0; w < kSmallBlock / kWave; ++w) {
+    if (w < wv) base += s_tmp[w];
+    tot += s_tmp[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(kSmallBlock) void k_small_prep(SmallArgs A) {
+  __shared__ uint32_t s_tmp[kSmallBlock / kWave];
+  __shared__ uint32_t s_len[AVDB_MAX_CHROM];
+  if (threadIdx.x < AVDB_MAX_CHROM) s_len[threadIdx.x] = A.tab.len[threadIdx.x];
+  __syncthreads();
+  const Heap hp = make_heap(A.heap, A.heap_bytes);
+  uint32_t run[3] = {0, 0, 0};
+  bool over[3] = {false, false, false};
+  for (uint32_t t0 = 0; t0 < A.n; t0 += kSmallBlock) {
+    const uint32_t i = t0 + threadIdx.x;
+    const bool live = i < A.n;
+    uint32_t c = 0, p = 0, e = 0, cd = AVDB_BIN_NONE, r = 0, a = 0;
+    uint64_t o = 0, x = 0;
+    uint8_t kst = AVDB_KEY_HOST, dst = 1;
+    bool lng = false;
+    if (live) {
+      c = A.chrom[i];
+      p = A.pos[i];
+      uint8_t st;
+      if (A.rl) {
+        o = A.off[i];
+        r = A.rl[i];
+        a = A.al[i];
+        x = A.ext ? A.ext[i] : 0ull;
+        lng = uint64_t(r) + a > A.max_seq_len;
+      }
+      if (A.end_in) {
+        e = A.end_in[i];
+      } else {
+        const bool snv = r == 1u && a == 1u;
+        uint32_t l;
+        e = infer_end(hp, o, r, a, p, snv ? 0 : heap_u64(hp, o), snv ? 0 : heap_u64(hp, o + r), &l);
+      }
+      st = uint8_t(classify(c, p, e, int(A.n_chrom), s_len, &cd));
+      A.end_out[i] = e;
+      A.code[i] = cd;
+      A.status[i] = st;
+      if (A.rl) {
+        const bool fits = o + r + a <= A.heap_bytes;
+        const bool ascii = fits && swar_find((glb_cp)(A.heap + o), r + a,
+                                             [](uint64_t w) { return w & kHiBits; }) == r + a;
+        dst = fits ? (ascii ? 0 : 1) : 2;
+        if (c >= 25 || (x >> 63) || !ascii) kst = AVDB_KEY_HOST;  // no label / interned id / non-ASCII
+        else if (lng) kst = AVDB_KEY_NEED_DIGEST;                  // the VRS digest path (K4)
+        else if (!key_allele_ok((glb_cp)(A.heap + o), r + a)) kst = AVDB_KEY_HOST;  // ':' -> ValueError
+        else kst = AVDB_KEY_OK;
+        A.key_state[i] = kst;
+        A.disp_state[i] = dst;
+      }
+    }
+    // three text streams: 0 ltree path, 1 primary key, 2 display-attribute JSON
+    auto render = [&](int sidx, auto o_) {
+      if (sidx == 0) return bin_path(o_, c, cd);
+      if (sidx == 1) {
+        chrom_name(o_, c);
+        o_.put(':');
+        o_.u32v(p);
+        o_.put(':');
+        o_.bytes((glb_cp)(A.heap + o), r);
+        o_.put(':');
+        o_.bytes((glb_cp)(A.heap + o + r), a);
+        if (x) {
+          o_.lit(":rs");
+          o_.u64v(x);
+        }
+        return o_;
+      }
+      return display_json<true>(o_, c, p, e, (glb_cp)(A.heap + o), r, (glb_cp)(A.heap + o + r), a);
+    };
+    for (int sidx = 0; sidx < 3; ++sidx) {
+      if (!(A.want & (1u << sidx))) continue;
+      bool emit = live;
+      if (sidx == 0) emit = emit && cd != AVDB_BIN_NONE && c < 25;
+      if (sidx == 1) emit = emit && kst == AVDB_KEY_OK;
+      if (sidx == 2) emit = emit && dst == 0;
+      const uint32_t len = emit ? render(sidx, Out<false>(nullptr, 0)).size() : 0u;
+      uint32_t tot;
+      const uint32_t at = run[sidx] + block_excl_scan(len, s_tmp, &tot);
+      uint32_t* offs = A.off_out + size_t(sidx) * (A.n + 1);
+      if (live) offs[i] = at;
+      if (run[sidx] + tot > A.cap[sidx]) over[sidx] = true;
+      if (emit && !over[sidx]) {
+        auto w = render(sidx, Out<true>(A.text_out[sidx], at));
+        w.finish();
+      }
+      run[sidx] += tot;
+    }
+  }
+  if (threadIdx.x == 0) {
+    uint32_t ov = 0;
+    for (int sidx = 0; sidx < 3; ++sidx) {
+      if (!(A.want & (1u << sidx))) continue;
+      A.off_out[size_t(sidx) * (A.n + 1) + A.n] = run[sidx];
+      ov |= uint32_t(over[sidx]) << sidx;
+    }
+    *A.overflow = ov;
+  }
+}
+
+}  // namespace avdb
+
+using namespace avdb;
+
+extern "C" int avdb_small_prep(avdb_ctx* ctx, const avdb_small_batch* b, void* stream) {
+  if (!ctx || !b || !b->chrom || !b->pos || !b->end_out || !b->code || !b->status || !b->off_out ||
+      !b->overflow || (!b->end_in && !b->ref_len)) {
+    avdb_set_error("avdb_small_prep: null argument");
+    return AVDB_EINVAL;
+  }
+  if (b->ref_len && (!b->allele_off || !b->alt_len || !b->heap || !b->key_state || !b->disp_state)) {
+    avdb_set_error("avdb_small_prep: alleles need allele_off, alt_len, heap, key_state and disp_state");
+    return AVDB_EINVAL;
+  }
+  if ((b->want & (AVDB_SMALL_KEY | AVDB_SMALL_DISPLAY)) && !b->ref_len) {
+    avdb_set_error("avdb_small_prep: keys and display attributes need alleles");
+    return AVDB_EINVAL;
+  }
+  for (int k = 0; k < 3; ++k)
+    if ((b->want & (1u << k)) && !b->text_out[k]) {
+      avdb_set_error("avdb_small_prep: text stream %d requested without a buffer", k);
+      return AVDB_EINVAL;
+    }
+  if (b->n > AVDB_SMALL_MAX) {
+    avdb_set_error("avdb_small_prep: at most %d records", AVDB_SMALL_MAX);
+    return AVDB_EINVAL;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  SmallArgs A;
+  memset(&A, 0, sizeof(A));
+  A.chrom = b->chrom;
+  A.pos = b->pos;
+  A.end_in = b->end_in;
+  A.off = b->allele_off;
+  A.rl = b->ref_len;
+  A.al = b->alt_len;
+  A.heap = b->heap;
+  A.ext = b->ext_id;
+  A.heap_bytes = b->heap_bytes;
+  A.n = b->n;
+  A.max_seq_len = b->max_seq_len;
+  A.want = b->want;
+  A.n_chrom = uint32_t(ctx->tab.n);
+  A.tab = ctx->tab;
+  A.end_out = b->end_out;
+  A.code = b->code;
+  A.status = b->status;
+  A.key_state = b->key_state;
+  A.disp_state = b->disp_state;
+  A.off_out = b->off_out;
+  A.overflow = b->overflow;
+  for (int k = 0; k < 3; ++k) {
+    A.text_out[k] = b->text_out[k];
+    A.cap[k] = b->text_cap[k];
+  }
+  hipLaunchKernelGGL(k_small_prep, dim3(1), dim3(kSmallBlock), 0, static_cast<hipStream_t>(stream), A);
+  AVDB_LAUNCH_CHECK("k_small_prep");
+  return AVDB_OK;
+}

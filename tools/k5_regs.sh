@@ -7,11 +7,11 @@ cd "$T" || exit 1
 for opts in "$@"; do
   echo "== $opts"
   # shellcheck disable=SC2086
-  hipcc --offload-arch=gfx950 -O3 -std=c++17 -I "$ROOT/include" $opts -c "$ROOT/annotatedvdb_amd/csrc/avdb_format.hip" \
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -I "$ROOT/include" $opts -c "$ROOT/annotatedvdb_amd/csrc/avdb_format_write.hip" \
     --save-temps -o f.o 2>&1 | grep -A3 error
   python3 - <<'EOF'
 import re
-s = open("avdb_format-hip-amdgcn-amd-amdhsa-gfx950.s").read()
+s = open("avdb_format_write-hip-amdgcn-amd-amdhsa-gfx950.s").read()
 for b in re.split(r"\n  - ", s):
     n = re.search(r"\.name:\s+(\S+)", b)
     if n and ("format" in n.group(1) or "display" in n.group(1)):
