@@ -469,7 +469,22 @@ def main():
         need = (torch.minimum(lcp.long() + 1, rl) + torch.minimum(lcp.long() + 1, al))
         need = torch.where((rl == 1) & (al == 1), torch.zeros_like(need), need)
         bytes_per_launch = n * 30 + int(need.sum().item())
-        del lcp, need, rl, al
+        # the same bytes at the memory's granularity: every read is a 128-B request
+        # (profiles/traffic_c5.json), and a long record's ref and alt starts lie in
+        # different lines, so the floor for these reads is the distinct 128-B heap
+        # lines holding the needed bytes, plus the SoA and the outputs
+        off = batch.allele_off.long()
+        lines = []
+        for beg, ln in ((off, torch.minimum(lcp.long() + 1, rl)), (off + rl, torch.minimum(lcp.long() + 1, al))):
+            keep = need > 0
+            b0, b1 = beg[keep] // 128, (beg[keep] + ln[keep] - 1) // 128
+            span = (b1 - b0 + 1)
+            idx = torch.repeat_interleave(b0, span) + (
+                torch.arange(int(span.sum().item()), device=b0.device) -
+                torch.repeat_interleave(torch.cumsum(span, 0) - span, span))
+            lines.append(idx)
+        line_bytes = n * 30 + 128 * int(torch.unique(torch.cat(lines)).numel())
+        del lcp, need, rl, al, off, lines
     elif a.workload == "load":
         # K5 write pass: text read once + line table (80 B) + rec_off (8) + both offset
         # arrays (16) + line state (1) per line + end/code/status (9) per record, and
@@ -516,6 +531,11 @@ def main():
         "cpu_baseline": cpu,
     }
     if a.workload == "c5":
+        out["roofline"]["line_granular"] = {
+            "bytes_per_launch": line_bytes, "achieved": line_bytes / (kern_ms * 1e-3) / 1e9,
+            "frac": line_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "note": "SoA + outputs + the distinct 128-B heap lines holding the bytes end inference needs "
+                    "(the smallest read the memory serves); traffic / this = HBM bytes over the line floor"}
         # SURVEY.md 8d whole-pipeline bytes (34 + rlen + alen + 24 per long record) over
         # K2 + K3 + K4 time, and K4's VALU roofline (compute-bound SHA-512)
         rl, al = batch.ref_len.long(), batch.alt_len.long()
