@@ -620,12 +620,12 @@ extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint3
                    aligned(ref_len, 16) && aligned(alt_len, 16) && aligned(end_out, 16) && aligned(bin_code, 16) &&
                    (!status || aligned(status, 4)) && (!lcp || aligned(lcp, 16));
   if (vec) {
-    constexpr int U = 2;
     const size_t ngroups = n / 4;
     const unsigned bdim = unsigned(kK1Block);
-    const unsigned grid = stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k1_blocks_per_cu));
-#define K2V(HI)                                                                                           \
-  hipLaunchKernelGGL((k_record_prep4<HI, U>), dim3(grid), dim3(bdim), shm, s,                            \
+    const int U = ctx->k2_unroll;
+    const unsigned grid = stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
+#define K2V(HI, UU)                                                                                       \
+  hipLaunchKernelGGL((k_record_prep4<HI, UU>), dim3(grid), dim3(bdim), shm, s,                           \
                      reinterpret_cast<const uint32_t*>(chrom), reinterpret_cast<const u32x4*>(pos),      \
                      reinterpret_cast<const u64x2*>(allele_off), reinterpret_cast<const u32x4*>(ref_len), \
                      reinterpret_cast<const u32x4*>(alt_len), heap, heap_bytes, ngroups,                  \
@@ -633,8 +633,16 @@ extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint3
                      reinterpret_cast<uint32_t*>(status), reinterpret_cast<u32x4*>(lcp), ctx->tab, hist_l8, \
                      ctr, lds_hist, chrom, pos, allele_off, ref_len, alt_len, ngroups * 4, n, end_out,   \
                      bin_code, status, lcp)
-    if (hist) K2V(true);
-    else K2V(false);
+    if (U == 1) {
+      if (hist) K2V(true, 1);
+      else K2V(false, 1);
+    } else if (U == 4) {
+      if (hist) K2V(true, 4);
+      else K2V(false, 4);
+    } else {
+      if (hist) K2V(true, 2);
+      else K2V(false, 2);
+    }
 #undef K2V
     AVDB_LAUNCH_CHECK("k_record_prep4");
     return AVDB_OK;

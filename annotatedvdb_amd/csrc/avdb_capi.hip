@@ -97,6 +97,16 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
   // aligned; AVDB_K2_VECTOR=0 keeps the one-record-per-lane form (A/B)
   c->k2_vector = true;
   if (const char* s = getenv("AVDB_K2_VECTOR")) c->k2_vector = atoi(s) != 0;
+  c->k2_unroll = 2;
+  if (const char* s = getenv("AVDB_K2_UNROLL")) {
+    const int v = atoi(s);
+    if (v == 1 || v == 2 || v == 4) c->k2_unroll = v;
+  }
+  c->k2_blocks_per_cu = 4;
+  if (const char* s = getenv("AVDB_K2_BLOCKS_PER_CU")) {
+    const int v = atoi(s);
+    if (v >= 1 && v <= 64) c->k2_blocks_per_cu = v;
+  }
   *out = c;
   return AVDB_OK;
 }

@@ -232,6 +232,8 @@ struct avdb_ctx {
   int k1_variant;        // K1 lane-group shape / memory policy (env AVDB_K1_VARIANT, bins.hip)
   int k1_block;          // K1 workgroup size: 256 or 512 (env AVDB_K1_BLOCK)
   bool k2_vector;        // K2 4-records-per-lane form (env AVDB_K2_VECTOR, default on)
+  int k2_unroll;         // K2 groups of 4 records per lane per trip (env AVDB_K2_UNROLL: 1, 2, 4)
+  int k2_blocks_per_cu;  // K2 grid = n_cu * this (env AVDB_K2_BLOCKS_PER_CU)
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
   bool has_digests;
