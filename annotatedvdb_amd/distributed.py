@@ -37,9 +37,19 @@ def rank_info() -> RankInfo:
                     int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def device_index(ri: RankInfo) -> int:
+    """GPU of this rank: LOCAL_RANK (one process per GPU).  Only a rehearsal
+    with more ranks than GPUs (``AVDB_DIST_BACKEND=gloo`` on a 1-GPU box) wraps."""
+    n = torch.cuda.device_count()
+    return ri.local % n if n else ri.local
+
+
 def init(backend: Optional[str] = None) -> RankInfo:
-    """Initialise the process group from torchrun's environment (no-op at N=1)."""
+    """Initialise the process group from torchrun's environment (no-op at N=1).
+    ``AVDB_DIST_BACKEND`` overrides the backend (``gloo`` rehearses the N>1 path
+    with several ranks sharing one GPU; RCCL refuses two ranks on one device)."""
     ri = rank_info()
+    backend = os.environ.get("AVDB_DIST_BACKEND", backend)
     if ri.distributed and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -61,16 +71,23 @@ def allgather_stats(hist: torch.Tensor, counters: torch.Tensor, ri: RankInfo
     totals (sum over ranks).  One collective per tensor, issued back to back."""
     if not ri.distributed:
         return hist.clone(), counters.clone()
+    dev = hist.device
+    if dist.get_backend() == "gloo" and dev.type != "cpu":
+        # gloo rehearsal of the N>1 path with several ranks on one GPU: the
+        # exchange goes through host memory (RCCL never takes this branch)
+        hist, counters = hist.cpu(), counters.cpu()
     hs = [torch.empty_like(hist) for _ in range(ri.world)]
     cs = [torch.empty_like(counters) for _ in range(ri.world)]
     dist.all_gather(hs, hist)
     dist.all_gather(cs, counters)
-    return torch.stack(hs).sum(0), torch.stack(cs).sum(0)
+    return torch.stack(hs).sum(0).to(dev), torch.stack(cs).sum(0).to(dev)
 
 
 def max_over_ranks(value: float, ri: RankInfo, device=None) -> float:
     if not ri.distributed:
         return value
+    if dist.get_backend() == "gloo":
+        device = None
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -77,24 +77,28 @@ def spans(n: int, seed: int = 3, device="cuda", pieces: Optional[Sequence[Piece]
 
 
 def alleles(n: int, seed: int = 5, device="cuda", pieces: Optional[Sequence[Piece]] = None,
-            long_frac: float = 0.05, dup_frac: float = 0.02, rs_frac: float = 0.6):
+            long_frac: float = 0.05, dup_frac: float = 0.02, rs_frac: float = 0.6,
+            classes=(0.80, 0.85, 0.90), indel_max: int = 20):
     """C5: a RecordBatch (device) of ADSP-style records, position-sorted, with
-    exact duplicates injected adjacent (so the grouped dedup path applies)."""
+    exact duplicates injected adjacent (so the grouped dedup path applies).
+    ``classes`` are the cumulative SNV / insertion / deletion thresholds (MNV up
+    to ``1 - long_frac``, long above); indels add 1..``indel_max`` bases."""
     from .engine import RecordBatch
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     chrom, pos = _positions(pieces or all_pieces(), n, g, device)
     u = torch.rand(n, generator=g, device=device)
-    r1 = torch.randint(1, 21, (n,), generator=g, device=device)
+    r1 = torch.randint(1, indel_max + 1, (n,), generator=g, device=device)
     r2 = torch.randint(1, 21, (n,), generator=g, device=device)
     L = torch.randint(51, 2001, (n,), generator=g, device=device)
     split = (torch.rand(n, generator=g, device=device) * (L - 1).float()).long() + 1
     one = torch.ones(n, dtype=torch.long, device=device)
     # classes: SNV 80 %, insertion 5 %, deletion 5 %, MNV 5 %, long 5 % (by long_frac)
-    snv = u < 0.80
-    ins = (u >= 0.80) & (u < 0.85)
-    dele = (u >= 0.85) & (u < 0.90)
-    mnv = (u >= 0.90) & (u < 1.0 - long_frac)
+    c_snv, c_ins, c_del = classes
+    snv = u < c_snv
+    ins = (u >= c_snv) & (u < c_ins)
+    dele = (u >= c_ins) & (u < c_del)
+    mnv = (u >= c_del) & (u < 1.0 - long_frac)
     lng = u >= 1.0 - long_frac
     rl = torch.where(snv, one, torch.where(ins, one, torch.where(dele, r1 + 1, torch.where(mnv, r2 + 1, split))))
     al = torch.where(snv, one, torch.where(ins, r1 + 1, torch.where(dele, one, torch.where(mnv, r2 + 1, L - split))))
@@ -132,6 +136,18 @@ def alleles(n: int, seed: int = 5, device="cuda", pieces: Optional[Sequence[Piec
     ext = ext[src]
     return RecordBatch(chrom=chrom, pos=pos, allele_off=off, ref_len=rl.to(torch.int32),
                        alt_len=al.to(torch.int32), heap=heap, ext_id=ext)
+
+
+def dbsnp_alleles(n: int, seed: int = 4, device="cuda", pieces: Optional[Sequence[Piece]] = None):
+    """C4 with alleles (the keyed form of BASELINE configs[3]): SURVEY §8d's
+    dbSNP mix as VCF records — 90 % SNV, 8 % anchored indels (4 % insertions,
+    4 % deletions of 1-48 bases, so ref+alt <= 50 and the key stays short), 2 %
+    long alleles (ref+alt in (50, 2000], keyed by the VRS digest); every record
+    carries an rsid; 0.5 % exact duplicates injected adjacent.  The 2 % of
+    SURVEY's spans up to 1 Mb are binned by K1 in C3/C4; as literal alleles
+    they are capped at 2 kb here to bound the heap."""
+    return alleles(n, seed=seed, device=device, pieces=pieces, long_frac=0.02, dup_frac=0.005,
+                   rs_frac=1.0, classes=(0.90, 0.94, 0.98), indel_max=48)
 
 
 C1_N = 1_100_000

@@ -48,6 +48,11 @@ WORKLOADS = {
     "c4": dict(n=125_000_000, desc="C4: dbSNP-scale mix (90% SNV / 8% indel <= 50 bp / 2% <= 1 Mb), "
                                    "1e9 over 8 GPUs = 1.25e8 per GPU (BASELINE configs[3]); K1 + L8 histogram",
                bytes_per=13, kernel="k_bin_assign4"),
+    "c4k": dict(n=125_000_000, desc="C4 keyed: dbSNP-scale 1e9 records over 8 GPUs = 1.25e8 per GPU as VCF "
+                                     "alleles (90% SNV / 8% indel <= 48 bp / 2% long, rsids; synth.dbsnp_alleles, "
+                                     "BASELINE configs[3] + north_star's 'bin paths and primary keys for 1B'): K2 end "
+                                     "+ bin, K3 dedup, K4 long-key digests, K7 primary-key + ltree-path text",
+                bytes_per=None, kernel="whole C4k step (K2 + K3 + K4 + K7)"),
     "c5": dict(n=25_000_000, desc="C5: ADSP-style alleles, end inference + bin + grouped PK dedup + "
                                   "long-allele key digests (BASELINE configs[4])",
                bytes_per=None, kernel="k_record_prep"),
@@ -203,10 +208,11 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
                           f"(oracle/avdb_oracle.py load_line + PortBinIndex; 0.82x the verbatim "
                           f"reference's per-line time, tools/calibrate_cpu_baseline.py), per-process "
                           f"{np.mean([r[1] for r in res]):.2f} s"}
-    if workload == "c5":
-        # ADSP-style records generated on the CPU (same generator, CPU stream)
+    if workload in ("c5", "c4k"):
+        # ADSP-style (or dbSNP-mix) records generated on the CPU (same generator, CPU stream)
         per = int(seconds_per_worker / 6e-6)  # ~5.6 us per record in the port
-        b = synth.alleles(per * workers, seed=5, device="cpu")
+        b = synth.alleles(per * workers, seed=5, device="cpu") if workload == "c5" else \
+            synth.dbsnp_alleles(per * workers, seed=4, device="cpu")
         heap = b.heap.numpy().tobytes()
         off, rl, al = b.allele_off.numpy(), b.ref_len.numpy(), b.alt_len.numpy()
         names = [CHROM_NAMES[c] for c in b.chrom.numpy().tolist()]
@@ -225,7 +231,8 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
         wall = time.perf_counter() - t0
         n = sum(r[0] for r in res)
         return {"value": n / wall, "unit": "variants/s", "cores": workers, "kind": "port",
-                "sample": f"{n:,} ADSP-style records (C5 generator on the CPU), {workers} processes x "
+                "sample": f"{n:,} {'ADSP-style' if workload == 'c5' else 'dbSNP-mix'} records "
+                          f"({workload.upper()} generator on the CPU), {workers} processes x "
                           f"{per:,} records; reference-structured end inference + PortBinIndex + primary "
                           f"key (hashlib SHA-512 VRS digests for long alleles) + keep-first dedup "
                           f"(oracle/avdb_oracle.py), per-process {np.mean([r[1] for r in res]):.2f} s"}
@@ -325,10 +332,10 @@ def main():
     # CPU baseline first, before this process touches the GPU (its worker
     # processes are forked and must not inherit an initialised HIP runtime)
     want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and ri.world == 1
-                                          and a.workload in ("c1", "c2", "c3", "c5", "load"))
+                                          and a.workload in ("c1", "c2", "c3", "c5", "c4k", "load"))
     cpu = cpu_baseline(a.workload, a.cpu_seconds) if (ri.rank == 0 and want_cpu) else None
     ri = D.init("nccl")
-    dev = torch.device("cuda", ri.local)
+    dev = torch.device("cuda", D.device_index(ri))
     torch.cuda.set_device(dev)
 
     from annotatedvdb_amd import synth
@@ -337,8 +344,8 @@ def main():
     W = WORKLOADS[a.workload]
     n = a.n or W["n"]
     pieces = D.my_pieces(ri)
-    eng = Engine(ri.local)
-    if a.workload == "c5":
+    eng = Engine(dev.index)
+    if a.workload in ("c5", "c4k"):
         digs = ["%032d" % i for i in range(25)]  # synthetic refget ids (no SeqRepo offline)
         eng.set_sequence_digests(digs)
 
@@ -352,6 +359,9 @@ def main():
                                         pieces=pieces, mix=a.workload)
     elif a.workload == "c1":
         batch = synth.c1_batch(n, seed=1, device=dev)
+        heap_bytes = int(batch.heap.numel())
+    elif a.workload == "c4k":
+        batch = synth.dbsnp_alleles(n, seed=4 + seed, device=dev, pieces=pieces)
         heap_bytes = int(batch.heap.numel())
     elif a.workload in ("vcf", "load"):
         tile = synth.vcf_text(min(VCF_TILE, n), seed=6 + seed)
@@ -395,9 +405,25 @@ def main():
         last.setdefault("kt", box["kt"])
         last["prep"], last["keep"] = box["prep"], box["keep"]
 
+    def c4k_step(record: bool):
+        box = {}
+        timed("record_prep", record, lambda: box.setdefault(
+            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr)))
+        timed("pk_dedup", record, lambda: box.setdefault(
+            "keep", eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3"))))
+        timed("vrs_digest", record, lambda: box.setdefault(
+            "dig", eng.vrs_digest(batch, 50, workspace=last.get("ws4"))))
+        code_, dig_ = box["prep"][1], box["dig"][0]
+        timed("primary_keys", record, lambda: box.setdefault(
+            "kt", eng.primary_keys(batch, code=code_, digest=dig_, out=last.get("kt"))))
+        last.setdefault("kt", box["kt"])
+        last["prep"], last["keep"], last["dig"] = box["prep"], box["keep"], box["dig"]
+
     def step(record: bool):
         if a.workload == "c1":
             c1_step(record)
+        elif a.workload == "c4k":
+            c4k_step(record)
         elif a.workload in ("c2", "c3", "c4"):
             timed("bin_assign", record, lambda: eng.bin_assign(
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
@@ -419,8 +445,13 @@ def main():
             timed("vrs_digest", record, lambda: eng.vrs_digest(batch, 50))
 
     last = {}
-    if a.workload == "c1":  # dedup workspace, allocated once
+    if a.workload in ("c1", "c4k"):  # dedup workspace, allocated once
         last["ws3"] = torch.empty(16384 + 4 * ((n + 3) & ~3), dtype=torch.uint8, device=dev)
+    if a.workload == "c4k":  # K4 compaction workspace, allocated once
+        import ctypes
+        sz = ctypes.c_size_t()
+        eng.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
+        last["ws4"] = torch.empty(int(sz.value), dtype=torch.uint8, device=dev)
     for _ in range(a.warmup):
         step(False)
     # the job-level collective once untimed, so any lazy RCCL setup for the
@@ -445,12 +476,28 @@ def main():
     kern_ms = stage_ms.get(kname)
     if a.workload == "c1":
         kern_ms = elapsed * 1e3 / a.steps  # the whole step (launch-bound at 1.1 M records)
+    if a.workload == "c4k":
+        kern_ms = sum(stage_ms[k] for k in ("record_prep", "pk_dedup", "vrs_digest", "primary_keys"))
     if a.workload in ("vcf", "load"):
         n_lines, n = n, n_rec  # the unit is emitted variant records (per-ALT rows)
     total_records = n * ri.world * a.steps
     value = total_records / elapsed
 
-    if a.workload == "c1":
+    if a.workload == "c4k":
+        # SURVEY.md §8d per-record bytes of the keyed record path (34 + rlen + alen + 24 per
+        # long record) plus the key and ltree-path text K7 writes, over the four kernels' time
+        kt = last["kt"]
+        rl, al = batch.ref_len.long(), batch.alt_len.long()
+        n_long = int(((rl + al) > 50).sum().item())
+        text = int(kt.key_off[n].item()) + int(kt.path_off[n].item())
+        bytes_per_launch = 34 * n + int((rl + al).sum().item()) + 24 * n_long + text
+        # K7 alone: SoA in (chrom 1 + pos 4 + allele_off 8 + ref_len 4 + alt_len 4 + ext_id 8 +
+        # code 4 = 33 B), the allele bytes of short records, 32 digest chars per long record;
+        # out key_off 8 + path_off 8 + state 1 and the text
+        short = (rl + al) <= 50
+        k7_bytes = 50 * n + int((rl + al)[short].sum().item()) + 32 * n_long + text
+        del rl, al, short
+    elif a.workload == "c1":
         # SURVEY.md §8d per-record bytes of the C5-style record path (in chrom 1 + pos 4 +
         # heap_off 8 + rlen 4 + alen 4 + rs 4, the allele bytes, out bin 4 + end 4 +
         # keep 1) plus the text K7 writes (keys + ltree paths)
@@ -561,6 +608,21 @@ def main():
                                     "vop3_issue_peak": vop3, "sq_insts_valu_per_launch": vi,
                                     "sha512_compressions_per_launch": pk.get("sha512_compressions_per_launch"),
                                     "note": pk.get("note")}
+    if a.workload == "c4k":
+        kt = last["kt"]
+        out["dtype"] = "u8"
+        out["data"] = "synthetic dbSNP-mix records (synth.dbsnp_alleles, torch PCG on device), resident in HBM"
+        out["config"].update(key_bytes=int(kt.key_off[n].item()), path_bytes=int(kt.path_off[n].item()),
+                             long_records=n_long, heap_bytes=heap_bytes,
+                             duplicates=int(node_ctr[21].item()) // max(1, a.steps))
+        k7_ms = stage_ms["primary_keys"]
+        out["k7_roofline"] = {"kernel": "avdb_primary_keys (size pass + 2 scans + LDS-staged write pass)",
+                              "bound": "hbm", "achieved": k7_bytes / (k7_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": k7_bytes / (k7_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                              "algorithmic_bytes_per_launch": k7_bytes, "stage_ms": k7_ms}
+        out["roofline"]["note"] = ("achieved = SURVEY 8d keyed-record bytes (34 + rlen + alen + 24 if long) + "
+                                   "key/path text written, over K2 + K3 + K4 + K7 HIP-event time; K4 (SHA-512) "
+                                   "is VALU-bound, the others HBM-bound")
     if a.workload == "c1":
         kt = last["kt"]
         out["dtype"] = "u8"

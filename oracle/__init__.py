@@ -36,5 +36,7 @@ def c_oracle():
         lib.avdb_oracle_vrs_digest.argtypes = [P, P, P, P, P, P, SZ, ctypes.c_uint32, ctypes.c_char_p, I, P, P]
         lib.avdb_oracle_primary_keys.argtypes = [P, P, P, P, P, P, P, P, SZ, ctypes.c_uint32, P, P]
         lib.avdb_oracle_primary_keys.restype = SZ
+        lib.avdb_oracle_bin_paths.argtypes = [P, P, SZ, P, P]
+        lib.avdb_oracle_bin_paths.restype = SZ
         _c = lib
     return _c

@@ -268,3 +268,29 @@ size_t avdb_oracle_primary_keys(const uint8_t* chrom, const uint32_t* pos, const
   out_off[n] = k;
   return k;
 }
+
+/* ltree bin paths (generate_bin_index_references.py:54,60-61,74): "chr<label>"
+ * then ".L<l>.B<k>" for l = 1..level, k = global index at level 1 + 1, else the
+ * index's lowest bit + 1 (B restarts under every parent).  BIN_NONE -> empty
+ * text (K7's convention for an unmappable record).  Concatenated in out,
+ * out_off[n+1]; returns the bytes written. */
+size_t avdb_oracle_bin_paths(const uint8_t* chrom, const uint32_t* code, size_t n, uint8_t* out,
+                             uint64_t* out_off) {
+  size_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    out_off[i] = k;
+    if (code[i] == BIN_NONE || chrom[i] >= 25) continue;
+    const uint32_t level = code[i] >> 28, g = code[i] & 0x0FFFFFFFu;
+    k += put_str(out + k, "chr");
+    k += put_str(out + k, LABEL[chrom[i]]);
+    for (uint32_t l = 1; l <= level; ++l) {
+      const uint32_t gl = g >> (level - l);
+      k += put_str(out + k, ".L");
+      k += put_u32(out + k, l);
+      k += put_str(out + k, ".B");
+      k += put_u32(out + k, l == 1 ? gl + 1 : (gl & 1) + 1);
+    }
+  }
+  out_off[n] = k;
+  return k;
+}

@@ -116,6 +116,28 @@ def test_synthetic_numpy_generators_shape():
     assert np.mean(e == s) > 0.4
 
 
+def test_dbsnp_allele_mix():
+    """The keyed C4 generator (bench --workload c4k): SURVEY 8d's 90 / 8 / 2 %
+    mix, short indels keep ref+alt <= 50, anchored indels, rsids everywhere,
+    sorted positions inside the requested pieces."""
+    from annotatedvdb_amd import shard, synth
+    plan = shard.plan(8)
+    b = synth.dbsnp_alleles(100000, seed=4, device="cpu", pieces=plan[3])
+    rl, al = b.ref_len.long(), b.alt_len.long()
+    tot = rl + al
+    assert abs((tot == 2).float().mean().item() - 0.90) < 0.01
+    assert abs(((tot > 2) & (tot <= 50)).float().mean().item() - 0.08) < 0.01
+    assert abs((tot > 50).float().mean().item() - 0.02) < 0.005
+    assert bool((b.ext_id > 0).all())
+    c, p = b.chrom.numpy().astype(np.int64), b.pos.numpy().astype(np.int64)
+    assert np.all(np.diff(c * 2**32 + p) >= 0)
+    assert all(shard.shard_of(plan, int(x), int(y)) == 3 for x, y in zip(c[::997], p[::997]))
+    heap, off = b.heap.numpy(), b.allele_off.numpy()
+    indel = ((tot > 2) & (tot <= 50) & ((rl == 1) | (al == 1))).numpy()
+    i = np.nonzero(indel)[0][:500]
+    assert np.array_equal(heap[off[i]], heap[off[i] + rl.numpy()[i]])  # alt[0] == ref[0]
+
+
 def test_bench_step_does_not_shadow_main_buffers():
     """bench.py's step() closes over main()'s resident buffers; a local of the
     same name anywhere in step() breaks every workload (UnboundLocalError)."""
