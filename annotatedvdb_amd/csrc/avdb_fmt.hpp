@@ -53,8 +53,31 @@ typedef __attribute__((address_space(1))) U64u* gw_u64u;
 // the append sink: 4 waves with ~100 B of spills 5.5 ms, 3 waves without 6.2 ms)
 constexpr int kFormatWaves = 4;
 
-// decimal digits of v as nibbles, most significant digit in the lowest nibble
-// (registers only: a local char array would live in scratch memory)
+// decimal digit count of v (compare chain: no division)
+__device__ __forceinline__ uint32_t ndigits(uint32_t v) {
+  return 1u + (v >= 10u) + (v >= 100u) + (v >= 1000u) + (v >= 10000u) + (v >= 100000u) +
+         (v >= 1000000u) + (v >= 10000000u) + (v >= 100000000u) + (v >= 1000000000u);
+}
+
+// v < 10^8 as exactly 8 ASCII digits (leading zeros), most significant digit in
+// the lowest byte: SWAR in one 64-bit register — two 4-digit halves in 32-bit
+// lanes, each split into 2-digit pairs (x/100 = x*5243 >> 19 for x < 10^4) in
+// 16-bit lanes, each into tens / ones (x/10 = x*103 >> 10 for x < 100) in bytes.
+// About 20 VALU instructions instead of a divide-by-10 loop per digit.
+__device__ __forceinline__ uint64_t ascii8(uint32_t v) {
+  const uint32_t a = v / 10000u, b = v - a * 10000u;
+  uint64_t x = uint64_t(a) | (uint64_t(b) << 32);
+  const uint64_t q = ((x * 5243ull) >> 19) & 0x0000007F0000007Full;
+  x = q | ((x - q * 100ull) << 16);
+  const uint64_t t = ((x * 103ull) >> 10) & 0x000F000F000F000Full;
+  x = t | ((x - t * 10ull) << 8);
+  return x + 0x3030303030303030ull;
+}
+
+// decimal digits of v as nibbles, most significant digit in the lowest nibble: a
+// divide-by-10 loop with few live registers (the K5 write pass, which runs at its
+// register limit, keeps this form: the SWAR form above spilled 124 -> 232 B/lane
+// there and cost +7 %)
 __device__ __forceinline__ uint64_t dec_nibbles(uint32_t v, uint32_t* ndig) {
   uint64_t d = 0;
   uint32_t k = 0;
@@ -62,19 +85,6 @@ __device__ __forceinline__ uint64_t dec_nibbles(uint32_t v, uint32_t* ndig) {
   *ndig = k;
   return d;
 }
-
-__device__ __forceinline__ uint32_t ndigits(uint32_t v) {  // decimal digits
-  uint32_t k = 1;
-  while (v >= 10u) { v /= 10u; ++k; }
-  return k;
-}
-
-// a decimal number as ASCII text in registers (up to 16 digits), so a value
-// printed several times per line is converted once
-struct Dec {
-  uint64_t lo, hi;  // digits 0..7 and 8..15, little-endian bytes
-  uint32_t n;
-};
 
 __device__ __forceinline__ uint64_t nibbles_to_ascii(uint64_t d, uint32_t k) {  // k <= 8
   uint64_t y = d & 0xFFFFFFFFull;
@@ -84,10 +94,22 @@ __device__ __forceinline__ uint64_t nibbles_to_ascii(uint64_t d, uint32_t k) {  
   return (y + 0x3030303030303030ull) & low_bytes_mask(k);
 }
 
+// a decimal number as ASCII text in registers (up to 16 digits), so a value
+// printed several times per line is converted once
+struct Dec {
+  uint64_t lo, hi;  // digits 0..7 and 8..15, little-endian bytes
+  uint32_t n;
+};
+
 __device__ __forceinline__ Dec dec_text(uint32_t v) {
-  uint32_t k;
-  const uint64_t d = dec_nibbles(v, &k);
-  return Dec{nibbles_to_ascii(d, k < 8 ? k : 8), k > 8 ? nibbles_to_ascii(d >> 32, k - 8) : 0ull, k};
+  const uint32_t n = ndigits(v);
+  if (n <= 8) return Dec{ascii8(v) >> (8 * (8 - n)), 0ull, n};
+  const uint32_t hi = v / 100000000u;  // 1..42
+  const uint64_t b = ascii8(v - hi * 100000000u);
+  const uint32_t nh = n - 8;           // 1 or 2 leading digits
+  const uint64_t a = hi < 10u ? uint64_t('0' + hi)
+                              : (uint64_t('0' + hi / 10u) | (uint64_t('0' + hi % 10u) << 8));
+  return Dec{a | (b << (8 * nh)), b >> (64 - 8 * nh), n};
 }
 
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
@@ -200,8 +222,6 @@ struct Out {
       for (uint32_t k = 0; k < n; ++k) put(s[k]);
     }
   }
-  // up to 8 decimal digits given as nibbles (most significant lowest) -> ASCII
-  __device__ __forceinline__ void digits8(uint64_t d, uint32_t k) { append(nibbles_to_ascii(d, k), k); }
   __device__ __forceinline__ void dec(const Dec& t) {
     if constexpr (!WRITE) {
       p += t.n;
@@ -215,13 +235,17 @@ struct Out {
       p += ndigits(v);
       return;
     }
-    uint32_t k;
-    const uint64_t d = dec_nibbles(v, &k);
-    if (k > 8) {
-      digits8(d, 8);
-      digits8(d >> 32, k - 8);
+    if constexpr (LDS) {  // K7's LDS sink: SWAR conversion
+      dec(dec_text(v));
     } else {
-      digits8(d, k);
+      uint32_t k;
+      const uint64_t d = dec_nibbles(v, &k);
+      if (k > 8) {
+        append(nibbles_to_ascii(d, 8), 8);
+        append(nibbles_to_ascii(d >> 32, k - 8), k - 8);
+      } else {
+        append(nibbles_to_ascii(d, k), k);
+      }
     }
   }
   __device__ __forceinline__ void u64v(uint64_t v) {
@@ -240,10 +264,9 @@ struct Out {
       p += 9;
       return;
     }
-    uint64_t d = 0;
-    for (int i = 0; i < 9; ++i) { d = (d << 4) | (v % 10u); v /= 10u; }
-    digits8(d, 8);
-    digits8(d >> 32, 1);
+    const uint32_t hi = v / 100000000u;  // 0..9
+    append(uint64_t('0' + hi), 1);
+    append(ascii8(v - hi * 100000000u), 8);
   }
 };
 
@@ -262,11 +285,83 @@ __device__ __forceinline__ void chrom_name(O& o, uint32_t c) {
 // 6- or 7-byte append per level (".L<l>.B<b>").
 // Helpers take and return the sink by value (never by reference: a sink whose
 // address escapes lives in scratch memory); all are inlined (see the A/B above).
+// A leaf (level-13) path of a labelled contig has a fixed shape: "chr" + a
+// 1- or 2-byte label + 9 six-byte and 4 seven-byte level pieces (86 / 87
+// bytes), each piece's bin digit '1' or '2' (L1: '1'..'4').  It is rendered as
+// eleven compile-time template words with the label and the 13 digit bits added
+// at constant byte positions (~40 instructions instead of a per-level loop).
+// Leaves are what SNVs and short indels get: nearly every record.
+#ifndef AVDB_LEAF_PATH
+#define AVDB_LEAF_PATH 1  // 0: the per-level loop for every level (A/B knob)
+#endif
+template <uint32_t L>
+struct LeafPath {
+  static constexpr uint32_t kLen = 3 + L + 9 * 6 + 4 * 7;
+  static constexpr uint32_t digit_pos(uint32_t l) {  // byte index of level l's bin digit
+    return l < 10 ? 3 + L + 6 * (l - 1) + 5 : 3 + L + 54 + 7 * (l - 10) + 6;
+  }
+  static constexpr uint8_t byte(uint32_t i) {
+    if (i < 3) return "chr"[i];
+    if (i < 3 + L) return 0;  // label, added at run time
+    uint32_t k = i - (3 + L);
+    if (k < 54) {
+      const uint32_t l = k / 6 + 1, off = k % 6;
+      const char piece[6] = {'.', 'L', char('0' + l), '.', 'B', '1'};
+      return uint8_t(piece[off]);
+    }
+    k -= 54;
+    if (k >= 28) return 0;
+    const uint32_t l = 10 + k / 7, off = k % 7;
+    const char piece[7] = {'.', 'L', '1', char('0' + l - 10), '.', 'B', '1'};
+    return uint8_t(piece[off]);
+  }
+  static constexpr uint64_t word(uint32_t j) {
+    uint64_t w = 0;
+    for (uint32_t b = 0; b < 8; ++b) w |= uint64_t(byte(8 * j + b)) << (8 * b);
+    return w;
+  }
+};
+
+template <uint32_t L, uint32_t J>
+__device__ __forceinline__ uint64_t leaf_word(uint64_t label, uint32_t g) {  // word J of the path
+  using P = LeafPath<L>;
+  uint64_t w = P::word(J);
+  if constexpr (J == 0) w |= label << 24;
+  if constexpr (P::digit_pos(1) / 8 == J) w += uint64_t(g >> 12) << (8 * (P::digit_pos(1) % 8));
+#pragma unroll
+  for (uint32_t l = 2; l <= 13; ++l)
+    if (P::digit_pos(l) / 8 == J) w += uint64_t((g >> (13 - l)) & 1u) << (8 * (P::digit_pos(l) % 8));
+  return w;
+}
+
+// each word is built just before it is appended (one live word: the K5 write
+// pass runs at its register limit)
+template <uint32_t L, class O>
+__device__ __forceinline__ O leaf_path(O o, uint64_t label, uint32_t g) {
+  o.append(leaf_word<L, 0>(label, g), 8);
+  o.append(leaf_word<L, 1>(label, g), 8);
+  o.append(leaf_word<L, 2>(label, g), 8);
+  o.append(leaf_word<L, 3>(label, g), 8);
+  o.append(leaf_word<L, 4>(label, g), 8);
+  o.append(leaf_word<L, 5>(label, g), 8);
+  o.append(leaf_word<L, 6>(label, g), 8);
+  o.append(leaf_word<L, 7>(label, g), 8);
+  o.append(leaf_word<L, 8>(label, g), 8);
+  o.append(leaf_word<L, 9>(label, g), 8);
+  o.append(leaf_word<L, 10>(label, g), LeafPath<L>::kLen - 80);
+  return o;
+}
+
 template <class O>
 __device__ __forceinline__ O bin_path(O o, uint32_t c, uint32_t code) {
+  const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
+  if (AVDB_LEAF_PATH && level == 13 && c < 25 && (g >> 12) < 9) {
+    if (c < 9) return leaf_path<1>(o, uint64_t('1' + c), g);
+    if (c < 22) return leaf_path<2>(o, uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8), g);
+    return leaf_path<1>(o, c == 22 ? uint64_t('X') : (c == 23 ? uint64_t('Y') : uint64_t('M')), g);
+  }
   o.lit("chr");
   chrom_name(o, c);
-  const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
   for (uint32_t l = 1; l <= level; ++l) {
     const uint32_t gl = g >> (level - l);
     const uint32_t b = l == 1 ? gl + 1 : (gl & 1u) + 1;

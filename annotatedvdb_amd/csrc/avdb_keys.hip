@@ -68,19 +68,64 @@ struct KeyArgs {
   uint8_t* state;
 };
 
-// One stream's span of a 256-record tile is staged in LDS when it fits (always
-// for keys <= ~90 B and ltree paths <= 87 B; else the lanes write global memory
-// directly), then flushed with coalesced 16-byte stores: the lanes' texts are
-// adjacent, so a wave of per-lane 8-byte stores would touch 64 partly written
-// lines per instruction.
-constexpr uint32_t kKeyStage = 24 * 1024;  // bytes per workgroup (6 workgroups per CU)
+// WRITE renders each wave's 64 records as a tile: each stream's span (the
+// records' texts are adjacent) is staged in the wave's own LDS image when it fits
+// (keys <= 40 B and ltree paths <= 87 B on average; else the lanes write global
+// memory directly), then flushed by the same wave with coalesced 16-byte stores
+// (a wave of per-lane 8-byte stores would touch 64 partly written lines per
+// instruction).  Tiles are per wave, with no s_barrier (the workgroup-tile form
+// with two barriers per tile measured the same: 13.46 vs 13.40 ms on C4k).  The
+// flush zeroes what it read, which keeps the images zero between tiles (the sink
+// ORs the words lanes share).  2.5 + 5.5 KB per wave, 32 KB per workgroup: 5
+// workgroups per CU, and the kernel is bounded to 96 VGPRs for 5 waves per SIMD.
+// What the key stream waited on was its loads inside per-lane branches (the
+// digest, short-allele and long-indel pieces each a dependent global load in
+// turn): the register window below took keys + paths from 13.40 to 10.19 ms.
+// AVDB_K7_EXP: on-device A/B knobs for the write pass (tools/k7_ab.sh; some
+// produce wrong text and exist only to time a part): 1 no heap bytes, 2 no rsid
+// digits, 4 no allele check, 8 no POS digits, 16 keys to global (no LDS image),
+// 32 paths to global, 64 key bytes read per piece (no register window).
+// (A periodic-span flush for tiles whose 64 records share one bin — the path
+// rendered once, each chunk read from it at its phase — measured no faster:
+// 10.21 vs 10.19 ms on C4k keys + paths; not kept.)
+#ifndef AVDB_K7_EXP
+#define AVDB_K7_EXP 0
+#endif
+constexpr uint32_t kKeyWave = 2560;
+constexpr uint32_t kPathWave = 5632;
+constexpr uint32_t kWavesPerBlock = kBlock / kWave;
 
-__device__ __forceinline__ void flush_tile(const lds_u64* img, uint8_t* out, uint64_t g0, uint64_t g1) {
+// bytes [s, s+n) of the 7-word register window w (s + n <= 56)
+constexpr uint32_t kKeyWords = 7;
+template <class O>
+__device__ __forceinline__ void append_range(O& o, const uint64_t (&w)[kKeyWords], uint32_t s, uint32_t n) {
+  const uint32_t e = s + n;
+#pragma unroll
+  for (uint32_t k = 0; k < kKeyWords; ++k) {
+    const uint32_t lo = s > 8 * k ? s : 8 * k;
+    const uint32_t hi = e < 8 * k + 8 ? e : 8 * k + 8;
+    if (hi > lo) o.append((w[k] >> (8 * (lo - 8 * k))) & low_bytes_mask(hi - lo), hi - lo);
+  }
+}
+
+// the wave's LDS writes (lanes OR into words their neighbours share) are complete
+// and visible to all its lanes before it reads them back: DS instructions of one
+// wave execute in order; the fences keep the compiler from moving LDS accesses
+// across this point
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void flush_wave(lds_u64* img, uint8_t* out, uint64_t g0, uint64_t g1, uint32_t lane) {
   const uint64_t a0 = g0 & ~uint64_t(15);
   const uint64_t nchunks = (g1 - a0 + 15) / 16;
-  for (uint64_t q = threadIdx.x; q < nchunks; q += blockDim.x) {
+  for (uint64_t q = lane; q < nchunks; q += kWave) {
     const uint64_t a = a0 + 16 * q;
     const uint64_t lo = img[2 * q], hi = img[2 * q + 1];
+    img[2 * q] = 0;
+    img[2 * q + 1] = 0;
     if (a >= g0 && a + 16 <= g1) {
       __builtin_nontemporal_store(u32x4{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)},
                                   reinterpret_cast<u32x4*>(out + a));
@@ -93,11 +138,21 @@ __device__ __forceinline__ void flush_tile(const lds_u64* img, uint8_t* out, uin
 }
 
 template <bool WRITE>
-__global__ __launch_bounds__(kBlock) void k_record_keys(KeyArgs A) {
-  __shared__ uint64_t s_img[WRITE ? kKeyStage / 8 : 1];
-  lds_u64* img = (lds_u64*)s_img;
-  for (size_t t0 = size_t(blockIdx.x) * blockDim.x; t0 < A.n; t0 += size_t(gridDim.x) * blockDim.x) {
-    const size_t i = t0 + threadIdx.x;
+__global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
+  __shared__ uint64_t s_kimg[WRITE ? kWavesPerBlock * kKeyWave / 8 : 1];
+  __shared__ uint64_t s_pimg[WRITE ? kWavesPerBlock * kPathWave / 8 : 1];
+  const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
+  lds_u64* kimg = (lds_u64*)s_kimg + (WRITE ? wv * (kKeyWave / 8) : 0);
+  lds_u64* pimg = (lds_u64*)s_pimg + (WRITE ? wv * (kPathWave / 8) : 0);
+  if constexpr (WRITE) {
+    for (uint32_t q = lane; q < kKeyWave / 8; q += kWave) kimg[q] = 0;
+    for (uint32_t q = lane; q < kPathWave / 8; q += kWave) pimg[q] = 0;
+    wave_lds_sync();
+  }
+  // WRITE: one 64-record tile per wave; SIZE: one record per lane (same indexing)
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  for (size_t t0 = size_t(blockIdx.x) * blockDim.x + size_t(wv) * kWave; t0 < A.n; t0 += stride) {
+    const size_t i = t0 + lane;
     const bool live = i < A.n;
     uint32_t c = 0, p = 0, r = 0, a = 0;
     uint64_t e = 0;
@@ -115,12 +170,34 @@ __global__ __launch_bounds__(kBlock) void k_record_keys(KeyArgs A) {
       if (c >= uint32_t(A.n_chrom) || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
       else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
     }
+    // WRITE: the bytes a key copies — a short record's ref+alt, or a long record's
+    // 32 digest characters — are loaded into a 7-word register window up front,
+    // all loads independent and outside any branch.  Loads inside the per-lane
+    // branches (digest / short / long-indel paths) each cost the wave a full
+    // memory latency in turn, since nearly every wave has lanes on several paths.
+    uint64_t w[kKeyWords];
+#pragma unroll
+    for (uint32_t k = 0; k < kKeyWords; ++k) w[k] = 0;
+    uint32_t wmis = 0;     // byte offset of the first key byte in w
+    bool in_regs = false;  // the window holds them (else: the per-piece global path)
     auto key = [&](auto o) {  // primary_key_generator.py:106-122
       chrom_name(o, c);
+      if constexpr (!(WRITE && (AVDB_K7_EXP & 8))) {
+        o.put(':');
+        o.u32v(p);
+      } else {
+        o.put(':');
+      }
       o.put(':');
-      o.u32v(p);
-      o.put(':');
-      if (lng) {  // only reached with a digest array (st == OK)
+      if (WRITE && (AVDB_K7_EXP & 1)) {
+        o.append(0x473A41ull, 3);
+      } else if (WRITE && in_regs && lng) {
+        append_range(o, w, 0, AVDB_DIGEST_CHARS);
+      } else if (WRITE && in_regs) {
+        append_range(o, w, wmis, r);
+        o.put(':');
+        append_range(o, w, wmis + r, a);
+      } else if (lng) {  // only reached with a digest array (st == OK)
         o.bytes((glb_cp)(A.digest + 32 * i), AVDB_DIGEST_CHARS);
       } else {
         const uint64_t off = A.off[i];
@@ -130,57 +207,88 @@ __global__ __launch_bounds__(kBlock) void k_record_keys(KeyArgs A) {
       }
       if (e && !(e >> 63)) {
         o.lit(":rs");
-        o.u64v(e);
+        if constexpr (!(WRITE && (AVDB_K7_EXP & 2))) o.u64v(e);
       }
       return o;
     };
     if constexpr (WRITE) {
-      if (live && st == AVDB_KEY_OK && !lng) {
-        const uint64_t off = A.off[i];
-        if (off + r + a > A.heap_bytes || !key_allele_ok((glb_cp)(A.heap + off), r + a)) st = AVDB_KEY_HOST;
-      }
-      const size_t last = t0 + blockDim.x < A.n ? t0 + blockDim.x : A.n;
-      // stream 0: keys, stream 1: paths; each staged in LDS when its span fits
-      for (int sidx = 0; sidx < (A.code ? 2 : 1); ++sidx) {
-        const uint64_t* offs = sidx ? A.path_off : A.key_off;
-        uint8_t* out = sidx ? A.path_out : A.key_out;
-        const uint64_t cap = sidx ? A.path_cap : A.key_cap;
-        const uint64_t g0 = offs[t0], g1 = offs[last];
-        const uint64_t a0 = g0 & ~uint64_t(15);
-        const bool staged = g1 - a0 + 16 <= kKeyStage && g1 <= cap;
-        uint32_t cd = AVDB_BIN_NONE;
-        bool emit = false;
-        if (live) {
-          if (sidx == 0) {
-            emit = st == AVDB_KEY_OK && offs[i + 1] <= cap;  // (cap: never write past the buffer)
-          } else {
-            cd = A.code[i];
-            emit = cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom) && offs[i + 1] <= cap;
+      if (live && st == AVDB_KEY_OK) {
+        const uint64_t off = lng ? 0 : A.off[i];
+        const uint32_t ra = r + a;
+        if (!lng && off + ra > A.heap_bytes) {
+          st = AVDB_KEY_HOST;
+        } else if (!(AVDB_K7_EXP & 64)) {
+          const uintptr_t src = lng ? reinterpret_cast<uintptr_t>(A.digest) + 32 * i
+                                    : reinterpret_cast<uintptr_t>(A.heap) + off;
+          const uintptr_t aw = src & ~uintptr_t(7);
+          wmis = uint32_t(src & 7);
+          const uint32_t nb = lng ? AVDB_DIGEST_CHARS : ra;
+          in_regs = wmis + nb <= 8 * kKeyWords;
+          if (in_regs) {
+            const uint32_t nw = (wmis + nb + 7) >> 3;
+            // (bytes outside the digest row / the heap allocation read as 0)
+            const Heap h = lng ? Heap{src, src + AVDB_DIGEST_CHARS} : make_heap(A.heap, A.heap_bytes);
+#pragma unroll
+            for (uint32_t k = 0; k < kKeyWords; ++k)
+              if (k < nw) w[k] = heap_word(aw + 8 * k, h);
           }
         }
-        if (staged) {
-          for (uint64_t q = threadIdx.x; q < (g1 - a0 + 15) / 16; q += blockDim.x) {
-            img[2 * q] = 0;
-            img[2 * q + 1] = 0;
+        if (!lng && st == AVDB_KEY_OK && !(AVDB_K7_EXP & 4)) {
+          if (in_regs) {  // no ':' (metaseqId.split) and ASCII only, on the window
+            uint64_t bad = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kKeyWords; ++k) {
+              const uint32_t lo = wmis > 8 * k ? wmis : 8 * k, e2 = wmis + ra;
+              const uint32_t hi = e2 < 8 * k + 8 ? e2 : 8 * k + 8;
+              if (hi > lo) {
+                const uint64_t m = low_bytes_mask(hi - 8 * k) & ~low_bytes_mask(lo - 8 * k);
+                bad |= ((w[k] & kHiBits) | bytes_eq_mask(w[k], ':')) & m & kHiBits;
+              }
+            }
+            if (bad) st = AVDB_KEY_HOST;
+          } else if (!key_allele_ok((glb_cp)(A.heap + off), ra)) {
+            st = AVDB_KEY_HOST;
           }
-          __syncthreads();
-          if (emit) {
-            Out<true, true> o(LdsImage{}, img, offs[i] - a0);
-            if (sidx == 0) o = key(o);
-            else o = bin_path(o, c, cd);
-            o.finish();
+        }
+      }
+      const size_t last = t0 + kWave < A.n ? t0 + kWave : A.n;
+      // stream 0: keys
+      const uint64_t gk0 = A.key_off[t0], gk1 = A.key_off[last];
+      const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap && !(AVDB_K7_EXP & 16);
+      if (live && st == AVDB_KEY_OK && A.key_off[i + 1] <= A.key_cap) {  // (cap: never write past the buffer)
+        const uint64_t at = A.key_off[i];
+        if (kst) {
+          Out<true, true> o(LdsImage{}, kimg, at - (gk0 & ~uint64_t(15)));
+          key(o).finish();
+        } else {
+          Out<true> o(A.key_out, at);
+          key(o).finish();
+        }
+      }
+      // stream 1: ltree paths
+      bool pst = false;
+      uint64_t gp0 = 0, gp1 = 0;
+      if (A.code) {
+        gp0 = A.path_off[t0];
+        gp1 = A.path_off[last];
+        pst = gp1 - (gp0 & ~uint64_t(15)) + 16 <= kPathWave && gp1 <= A.path_cap && !(AVDB_K7_EXP & 32);
+        const uint32_t cd = live ? A.code[i] : AVDB_BIN_NONE;
+        if (live && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom) && A.path_off[i + 1] <= A.path_cap) {
+          const uint64_t at = A.path_off[i];
+          if (pst) {
+            Out<true, true> o(LdsImage{}, pimg, at - (gp0 & ~uint64_t(15)));
+            bin_path(o, c, cd).finish();
+          } else {
+            Out<true> o(A.path_out, at);
+            bin_path(o, c, cd).finish();
           }
-          __syncthreads();
-          flush_tile(img, out, g0, g1);
-          __syncthreads();
-        } else if (emit) {
-          Out<true> o(out, offs[i]);
-          if (sidx == 0) o = key(o);
-          else o = bin_path(o, c, cd);
-          o.finish();
         }
       }
       if (live) A.state[i] = st;
+      wave_lds_sync();
+      if (kst) flush_wave(kimg, A.key_out, gk0, gk1, lane);
+      if (pst) flush_wave(pimg, A.path_out, gp0, gp1, lane);
+      wave_lds_sync();
     } else if (live) {
       A.key_off[i] = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;
       if (A.code) {
