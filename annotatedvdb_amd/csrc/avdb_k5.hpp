@@ -18,6 +18,9 @@ enum : uint8_t { kLineGpu = 0, kLineHost = 1, kLineSkip = 2 };
 constexpr uint32_t kHostFlags = AVDB_VCF_FEW_FIELDS | AVDB_VCF_BAD_POS | AVDB_VCF_EXT_HOST |
                                 AVDB_VCF_CHROM_HOST | AVDB_VCF_EMPTY | AVDB_VCF_ID_HOST;
 constexpr int kMaxPops = 64;
+#ifndef AVDB_K5_PRELOAD
+#define AVDB_K5_PRELOAD 1  // A/B knob: 0 loads every record's inputs inside the ALT loop
+#endif
 
 struct FormatArgs {
   const uint8_t* text;
@@ -194,6 +197,17 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
   }
   om.lit("\t[");
   uint64_t r = A.rec_off[li];
+  // WRITE: the first record's status / bin / keep / end are loaded before the
+  // ALT loop (nearly every line has one ALT), not inside it behind the LDS scans
+  const uint64_t r0 = r;
+  uint32_t st0 = 0, code0 = 0, end0 = 0;
+  bool keep0 = true;
+  if constexpr (WRITE && AVDB_K5_PRELOAD) {
+    st0 = A.status[r0];
+    code0 = A.code[r0];
+    end0 = A.end[r0];
+    keep0 = !A.keep || A.keep[r0];
+  }
   uint32_t nrec = 0, rows = 0, skip = 0, dups = 0, upd = 0;
   for (uint32_t a0 = alt0, ai = 0; a0 <= alt1; ++ai) {
     const uint32_t a1 = find_byte(s, a0, alt1, ',');
@@ -226,10 +240,11 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
       a0 = a1 + 1;
       continue;
     }
-    const uint32_t st = A.status[r];
+    const bool first = WRITE && AVDB_K5_PRELOAD && r == r0;
+    const uint32_t st = first ? st0 : A.status[r];
     if (st == AVDB_STATUS_UNKNOWN_CHROM || st == AVDB_STATUS_OUT_OF_RANGE) return kLineHost;
-    const uint32_t code = A.code[r];
-    const bool keep = !A.keep || A.keep[r];
+    const uint32_t code = first ? code0 : A.code[r];
+    const bool keep = first ? keep0 : (!A.keep || A.keep[r]);
     // altIndex = altAlleles.index(allele) + 1: the first equal ALT
     uint32_t k = ai + 1;
     for (uint32_t b0 = alt0, bi = 0; bi < ai; ++bi) {
@@ -285,7 +300,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
       oc.put('#');
       oc.append(L.n_alt > 1 ? 0x65757254ull : 0x4C4C554Eull, 4);  // "True" / "NULL"
       oc.put('#');
-      oc = display_json<false>(oc, c, L.pos, A.end[r], ref, rl, alt, al, posd);
+      oc = display_json<false>(oc, c, L.pos, first ? end0 : A.end[r], ref, rl, alt, al, posd);
       oc.put('#');
       if (fq0 >= 0) {
         oc = freq_json(oc, s, uint32_t(fq0), uint32_t(fq1), k);
