@@ -113,6 +113,9 @@ __device__ __forceinline__ Dec dec_text(uint32_t v) {
 }
 
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
+#ifndef AVDB_SINK_ALLOR
+#define AVDB_SINK_ALLOR 1  // every LDS-sink word store as ds_or_b64 (no first-word branch; 0 = plain stores inside a span)
+#endif
 struct LdsImage {};  // constructor tag of the LDS sink
 
 // LDS = true (WRITE only): the sink renders into a workgroup's LDS image of its
@@ -133,6 +136,7 @@ struct Out {
     if constexpr (LDS) {
       pend.img = img;
       pend.k = uint32_t(at & 7u);
+      pend.wq = uint32_t(at >> 3);
     }
   }
   __device__ __forceinline__ uint32_t size() const { return uint32_t(p - lo); }
@@ -144,6 +148,7 @@ struct Out {
     uint64_t w = 0;  // word's low bytes belong to the previous lane: zero here)
     uint32_t k = 0;
     bool first = true;
+    uint32_t wq = 0;  // image word of byte p - k (32-bit: no 64-bit address math per append)
     lds_u64* img = nullptr;
   };
   struct None {};
@@ -154,10 +159,12 @@ struct Out {
       const uint32_t k = pend.k;  // 0..7
       pend.w |= x << (8 * k);
       if (k + t >= 8) {
-        lds_u64* wp = pend.img + ((p - k) >> 3);
-        if (pend.first) __hip_atomic_fetch_or(wp, pend.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_u64* wp = pend.img + pend.wq;
+        if (AVDB_SINK_ALLOR || pend.first)
+          __hip_atomic_fetch_or(wp, pend.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         else *wp = pend.w;
         pend.first = false;
+        ++pend.wq;
         pend.w = k ? x >> (64 - 8 * k) : 0ull;
         pend.k = k + t - 8;
       } else {
@@ -180,10 +187,10 @@ struct Out {
   // end of the line: store the buffered tail
   __device__ __forceinline__ void finish() {
     if constexpr (WRITE && LDS) {
-      // the last (partial) word may be shared with the next lane
-      if (pend.k && (p > lo || !pend.first))
-        __hip_atomic_fetch_or(pend.img + ((p - pend.k) >> 3), pend.w, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      // the last (partial) word may be shared with the next lane (an empty text
+      // ORs a zero word: harmless)
+      if (pend.k)
+        __hip_atomic_fetch_or(pend.img + pend.wq, pend.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       pend.w = 0;
       pend.k = 0;
     } else if constexpr (WRITE) {

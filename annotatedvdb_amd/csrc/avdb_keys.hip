@@ -111,6 +111,39 @@ __device__ __forceinline__ void append_range(O& o, const uint64_t (&w)[kKeyWords
   }
 }
 
+// "ref:alt" from the window: the bytes [s, s+r+a) shifted to byte 0, a ':'
+// inserted at byte r (the words past it move up one byte), then appended as up
+// to seven words — one append per 8 output bytes instead of one per piece of
+// each allele
+#ifndef AVDB_K7_KEYJOIN
+#define AVDB_K7_KEYJOIN 1  // A/B knob: 0 appends ref, ':' and alt as separate ranges
+#endif
+template <class O>
+__device__ __forceinline__ void append_joined(O& o, const uint64_t (&w)[kKeyWords], uint32_t s, uint32_t r,
+                                              uint32_t a) {
+  uint64_t y[kKeyWords];
+#pragma unroll
+  for (uint32_t k = 0; k < kKeyWords; ++k) {
+    const uint64_t nx = k + 1 < kKeyWords ? w[k + 1] : 0ull;
+    y[k] = s ? (w[k] >> (8 * s)) | (nx << (64 - 8 * s)) : w[k];
+  }
+  const uint32_t len = r + 1 + a;
+  uint64_t prev = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kKeyWords; ++j) {
+    const int32_t rel = int32_t(r) - int32_t(8 * j);  // ':' position in word j
+    const uint64_t mlo = rel <= 0 ? 0ull : (rel >= 8 ? ~0ull : low_bytes_mask(uint32_t(rel)));
+    const uint64_t mhi = rel >= 7 ? 0ull : (rel < 0 ? ~0ull : ~low_bytes_mask(uint32_t(rel + 1)));
+    const uint64_t colon = (rel >= 0 && rel < 8) ? (0x3Aull << (8 * rel)) : 0ull;
+    const uint64_t z = (y[j] & mlo) | (((y[j] << 8) | (prev >> 56)) & mhi) | colon;
+    prev = y[j];
+    if (8 * j < len) {
+      const uint32_t t = len - 8 * j < 8u ? len - 8 * j : 8u;
+      o.append(z & low_bytes_mask(t), t);
+    }
+  }
+}
+
 // the wave's LDS writes (lanes OR into words their neighbours share) are complete
 // and visible to all its lanes before it reads them back: DS instructions of one
 // wave execute in order; the fences keep the compiler from moving LDS accesses
@@ -229,6 +262,8 @@ __global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
         o.append(0x473A41ull, 3);
       } else if (WRITE && in_regs && lng) {
         append_range(o, w, 0, AVDB_DIGEST_CHARS);
+      } else if (WRITE && in_regs && AVDB_K7_KEYJOIN) {
+        append_joined(o, w, wmis, r, a);
       } else if (WRITE && in_regs) {
         append_range(o, w, wmis, r);
         o.put(':');
