@@ -154,57 +154,6 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// bytes [lo, hi) (0 <= lo < hi <= 16) of the 16-byte value (v0, v1) to the
-// 16-aligned global chunk at a, as naturally aligned 1/2/4/8-byte stores:
-// straight-line and predicated (at most 8 stores), not a 16-step byte loop
-__device__ __forceinline__ void store_part16(uint8_t* out, uint64_t a, uint32_t lo, uint32_t hi, uint64_t v0,
-                                             uint64_t v1) {
-  auto bytes_at = [&](uint32_t s) -> uint64_t {  // value bytes from s on (s < 16)
-    return s == 0 ? v0 : (s < 8 ? (v0 >> (8 * s)) | (v1 << (64 - 8 * s)) : v1 >> (8 * (s - 8)));
-  };
-  uint32_t s = lo;
-  if ((s & 1) && s < hi) { out[a + s] = uint8_t(bytes_at(s)); s += 1; }
-  if ((s & 2) && s + 2 <= hi) { *reinterpret_cast<uint16_t*>(out + a + s) = uint16_t(bytes_at(s)); s += 2; }
-  if ((s & 4) && s + 4 <= hi) { *reinterpret_cast<uint32_t*>(out + a + s) = uint32_t(bytes_at(s)); s += 4; }
-  if ((s & 8) && s + 8 <= hi) { *reinterpret_cast<uint64_t*>(out + a + s) = bytes_at(s); s += 8; }
-  if (s + 8 <= hi) { *reinterpret_cast<uint64_t*>(out + a + s) = bytes_at(s); s += 8; }
-  if (s + 4 <= hi) { *reinterpret_cast<uint32_t*>(out + a + s) = uint32_t(bytes_at(s)); s += 4; }
-  if (s + 2 <= hi) { *reinterpret_cast<uint16_t*>(out + a + s) = uint16_t(bytes_at(s)); s += 2; }
-  if (s < hi) out[a + s] = uint8_t(bytes_at(s));
-}
-
-// The wave's span [g0, g1) leaves its image (image byte 0 = address g0 & ~15):
-// full 16-byte chunks as coalesced nontemporal stores, then the partial head and
-// tail chunks (shared with the neighbouring tiles) by lanes 0 and 1 together.
-// Every image word read is zeroed again.
-__device__ __forceinline__ void flush_wave(lds_u64* img, uint8_t* out, uint64_t g0, uint64_t g1, uint32_t lane) {
-  const uint64_t a0 = g0 & ~uint64_t(15);
-  const uint64_t f0 = (g0 + 15) & ~uint64_t(15), f1 = g1 & ~uint64_t(15);  // full chunks [f0, f1)
-  if (f1 > f0) {
-    for (uint64_t q = (f0 - a0) / 16 + lane; q < (f1 - a0) / 16; q += kWave) {
-      const uint64_t lo = img[2 * q], hi = img[2 * q + 1];
-      img[2 * q] = 0;
-      img[2 * q + 1] = 0;
-      __builtin_nontemporal_store(u32x4{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)},
-                                  reinterpret_cast<u32x4*>(out + a0 + 16 * q));
-    }
-  }
-  // head: the chunk at a0 when g0 is not 16-aligned (it may also hold g1);
-  // tail: the chunk at f1 when g1 is not 16-aligned and it is not the head's
-  const bool head = g0 != f0 || f1 < f0;
-  const bool tail = (g1 & 15) && f1 >= f0 && (f1 != a0 || !head);
-  if ((lane == 0 && head) || (lane == 1 && tail)) {
-    const uint64_t a = lane == 0 ? a0 : f1;
-    const uint64_t q = (a - a0) / 16;
-    const uint64_t v0 = img[2 * q], v1 = img[2 * q + 1];
-    img[2 * q] = 0;
-    img[2 * q + 1] = 0;
-    const uint32_t lo = a < g0 ? uint32_t(g0 - a) : 0u;
-    const uint32_t hi = a + 16 > g1 ? uint32_t(g1 - a) : 16u;
-    store_part16(out, a, lo, hi, v0, v1);
-  }
-}
-
 template <bool WRITE>
 __global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
   __shared__ uint64_t s_kimg[WRITE ? kWavesPerBlock * kKeyWave / 8 : 1];
@@ -357,8 +306,8 @@ __global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
       }
       if (live) A.state[i] = st;
       wave_lds_sync();
-      if (kst) flush_wave(kimg, A.key_out, gk0, gk1, lane);
-      if (pst) flush_wave(pimg, A.path_out, gp0, gp1, lane);
+      if (kst) flush_span(kimg, A.key_out, gk0, gk1, lane, kWave);
+      if (pst) flush_span(pimg, A.path_out, gp0, gp1, lane, kWave);
       wave_lds_sync();
     } else if (live) {
       A.key_off[i] = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;

@@ -18,8 +18,7 @@
 //                  REF+ALT copied to the allele heap
 // Only canonical text is resolved here; the rest is flagged (AVDB_VCF_*_HOST) for
 // the host to resolve with Python's own coercion rules.
-#include "avdb_internal.hpp"
-#include "avdb_text.hpp"
+#include "avdb_fmt.hpp"
 
 #include <hipcub/hipcub.hpp>
 
@@ -437,13 +436,19 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
   }
 }
 
-template <class CP>
+// The allele heap bytes of a tile's lines are contiguous ([heap_off[base],
+// heap_off[last])): they are rendered into an LDS image of that span and leave as
+// coalesced 16-byte stores (per-lane byte stores touched a cache line per byte
+// and lane).  Spans over kHeapImg bytes fall back to per-lane stores.
+constexpr uint32_t kHeapImg = 4096;
+
+template <class CP, class O>
 __device__ __forceinline__ void emit_line(CP s, const avdb_vcf_line& L, size_t li,
                                           uint64_t r, uint64_t h, uint8_t* __restrict__ chrom,
                                           uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
                                           uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
-                                          uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap,
-                                          uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
+                                          uint64_t* __restrict__ ext_id, uint32_t* __restrict__ rec_line,
+                                          uint32_t* __restrict__ rec_alt, O& hs) {
     const uint32_t nfields = L.n_fields < 8 ? L.n_fields : 8;
     const uint32_t rend = L.field[4] - 1;
     const uint32_t aend = 5 < nfields ? L.field[5] - 1 : L.len;
@@ -464,8 +469,8 @@ __device__ __forceinline__ void emit_line(CP s, const avdb_vcf_line& L, size_t l
           ext_id[r] = L.ext_id;
           rec_line[r] = uint32_t(li);
           rec_alt[r] = ai;
-          for (uint32_t k = 0; k < rlen; ++k) heap[h + k] = ref[k];
-          for (uint32_t k = 0; k < al; ++k) heap[h + rlen + k] = alt[a0 + k];
+          hs.bytes(ref, rlen);
+          hs.bytes(alt + a0, al);
           h += rlen + al;
           ++r;
         }
@@ -483,6 +488,9 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
     uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap, uint32_t* __restrict__ rec_line,
     uint32_t* __restrict__ rec_alt) {
   __shared__ u32x4 s_text[kStage / 16];
+  __shared__ uint64_t s_heap[kHeapImg / 8];
+  lds_u64* himg = (lds_u64*)s_heap;
+  for (uint32_t q = threadIdx.x; q < kHeapImg / 8; q += blockDim.x) himg[q] = 0;
   const Heap h = make_heap(text, text_bytes);
   for (size_t base = size_t(blockIdx.x) * kBlock; base < n_lines; base += size_t(gridDim.x) * kBlock) {
     const size_t last = base + kBlock < n_lines ? base + kBlock : n_lines;
@@ -490,21 +498,33 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
     const size_t s0 = lines[base].start;
     const avdb_vcf_line& Z = lines[last - 1];
     const size_t s1 = Z.start + Z.len;
-    const Window w = stage_window(h, s0, s1, s_text);
+    const Window w = stage_window(h, s0, s1, s_text);  // (its barrier also orders the heap image)
+    const uint64_t g0 = heap_off[base], g1 = heap_off[last];
+    const uint64_t ha0 = g0 & ~uint64_t(15);
+    const bool hst = g1 - ha0 + 16 <= kHeapImg;
     const size_t li = base + threadIdx.x;
     if (li < n_lines) {
       const avdb_vcf_line L = lines[li];
       if (L.n_rec) {
-        if (w.staged)
-          emit_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)), L, li,
-                    rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id, heap,
-                    rec_line, rec_alt);
-        else
-          emit_line((glb_cp)(text + L.start), L, li, rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len,
-                    alt_len, ext_id, heap, rec_line, rec_alt);
+        auto run = [&](auto s, auto& hs) {
+          emit_line(s, L, li, rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id,
+                    rec_line, rec_alt, hs);
+          hs.finish();
+        };
+        if (hst) {
+          Out<true, true> hs(LdsImage{}, himg, heap_off[li] - ha0);
+          if (w.staged) run((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)), hs);
+          else run((glb_cp)(text + L.start), hs);
+        } else {
+          Out<true> hs(heap, heap_off[li]);
+          if (w.staged) run((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)), hs);
+          else run((glb_cp)(text + L.start), hs);
+        }
       }
     }
     __syncthreads();
+    if (hst) flush_span(himg, heap, g0, g1, threadIdx.x, blockDim.x);
+    __syncthreads();  // the window and the heap image are reused by the next trip
   }
 }
 
