@@ -237,6 +237,58 @@ __device__ uint64_t rs_number(CP p, uint32_t n) {
   return v;
 }
 
+// ---- SWAR field helpers: a field's bytes as two registers, read with
+// independent aligned word loads (the byte loops these replace waited on one
+// dependent LDS byte read per iteration) ----
+// 16 bytes of the line from line offset f (bytes at and past `len` read as 0)
+template <class WordAt>
+__device__ __forceinline__ void line16(const WordAt& word_at, uint32_t mis, uint32_t len, uint32_t f,
+                                       uint64_t* x0, uint64_t* x1) {
+  const uint32_t a = f + mis, k = a >> 3, sh = 8 * (a & 7);
+  const uint32_t kend = (len + mis + 7) >> 3;  // words holding line bytes
+  const uint64_t w0 = k < kend ? word_at(k) : 0ull;
+  const uint64_t w1 = k + 1 < kend ? word_at(k + 1) : 0ull;
+  const uint64_t w2 = k + 2 < kend ? word_at(k + 2) : 0ull;
+  uint64_t y0 = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  uint64_t y1 = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  // clip at the line end
+  const uint32_t n = len > f ? len - f : 0u;
+  if (n < 16) {
+    y1 &= n > 8 ? low_bytes_mask(n - 8) : 0ull;
+    y0 &= low_bytes_mask(n < 8 ? n : 8);
+  }
+  *x0 = y0;
+  *x1 = y1;
+}
+
+// bit 7 set in every byte of x that is not an ASCII digit
+__device__ __forceinline__ uint64_t nondigit_mask(uint64_t x) {
+  const uint64_t d = x ^ 0x3030303030303030ull;
+  return (((d & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | d) & kHiBits;
+}
+
+// up to 8 ASCII digits (most significant in the lowest byte, n of them) -> value
+__device__ __forceinline__ uint32_t digits8_value(uint64_t x, uint32_t n) {
+  if (n == 0) return 0;
+  uint64_t v = (x ^ 0x3030303030303030ull) << (8 * (8 - n));  // leading zero digits below
+  v = (v * 10 + (v >> 8)) & 0x00FF00FF00FF00FFull;
+  v = (v * 100 + (v >> 16)) & 0x0000FFFF0000FFFFull;
+  v = (v * 10000 + (v >> 32)) & 0xFFFFFFFFull;
+  return uint32_t(v);
+}
+
+// a decimal field of n <= 16 bytes in (x0, x1): *ok = all digits; value (64-bit)
+__device__ __forceinline__ uint64_t decimal16(uint64_t x0, uint64_t x1, uint32_t n, bool* ok) {
+  const uint64_t m0 = low_bytes_mask(n < 8 ? n : 8), m1 = n > 8 ? low_bytes_mask(n - 8) : 0ull;
+  *ok = n > 0 && !((nondigit_mask(x0) & m0) | (nondigit_mask(x1) & m1));
+  if (n <= 8) return digits8_value(x0 & m0, n);
+  // the first n - 8 digits, then 8 more
+  const uint32_t h = n - 8, sh = 8 * h;
+  const uint64_t hi = x0 & low_bytes_mask(h);
+  const uint64_t lo = sh < 64 ? (x0 >> sh) | (x1 << (64 - sh)) : x1;
+  return uint64_t(digits8_value(hi, h)) * 100000000ull + digits8_value(lo, 8);
+}
+
 constexpr uint64_t kTab = 0x0909090909090909ull;
 constexpr uint64_t kSemi = 0x3B3B3B3B3B3B3B3Bull;
 
@@ -300,36 +352,55 @@ __device__ __forceinline__ void parse_line(CP s, const WordAt& word_at, uint32_t
         if (host) L.flags |= AVDB_VCF_CHROM_HOST;
         // POS: plain decimal < 2^32
         {
-          const CP p = s + L.field[1];
           const uint32_t n = fend(1) - L.field[1];
-          uint64_t v = 0;
-          bool ok = n > 0 && n <= 10;
-          for (uint32_t i = 0; ok && i < n; ++i) {
-            ok = is_digit(p[i]);
-            v = v * 10 + (p[i] - '0');
-          }
+          uint64_t x0, x1;
+          line16(word_at, mis, len, L.field[1], &x0, &x1);
+          bool ok = false;
+          const uint64_t v = n <= 10 ? decimal16(x0, x1, n, &ok) : 0ull;
           if (ok && v <= 0xFFFFFFFFull) L.pos = uint32_t(v); else L.flags |= AVDB_VCF_BAD_POS;
         }
         // ID
         const CP id = s + L.field[2];
         const uint32_t idn = fend(2) - L.field[2];
+        // ID, 16 bytes at a time: digits / number-like bytes / an "rs" pair
+        bool has_rs = false;
         {
           bool numlike = idn > 0, has_digit = false;
-          for (uint32_t i = 0; i < idn; ++i) {
-            const uint8_t c = id[i];
-            has_digit = has_digit || is_digit(c);
-            numlike = numlike && (is_digit(c) || c == '+' || c == '-' || c == '.' || c == 'e' ||
-                                  c == 'E' || c == '_');
+          uint64_t carry_r = 0;  // bit 7: the byte before this block is 'r'
+          for (uint32_t b = 0; b < idn; b += 16) {
+            uint64_t y[2];
+            line16(word_at, mis, len, L.field[2] + b, &y[0], &y[1]);
+            const uint32_t nb = idn - b < 16u ? idn - b : 16u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t nh = h ? (nb > 8 ? nb - 8 : 0u) : (nb < 8 ? nb : 8u);
+              const uint64_t m = low_bytes_mask(nh) & kHiBits;
+              const uint64_t x = y[h];
+              const uint64_t dig = ~nondigit_mask(x) & m;
+              has_digit = has_digit || dig;
+              const uint64_t numb = dig | bytes_eq_mask(x, '+') | bytes_eq_mask(x, '-') | bytes_eq_mask(x, '.') |
+                                    bytes_eq_mask(x, 'e') | bytes_eq_mask(x, 'E') | bytes_eq_mask(x, '_');
+              numlike = numlike && !((~numb) & m);
+              const uint64_t rm = bytes_eq_mask(x, 'r') & m, sm = bytes_eq_mask(x, 's') & m;
+              has_rs = has_rs || (((rm << 8) | carry_r) & sm);
+              carry_r = nh == 8 ? (rm >> 56) : 0ull;
+            }
           }
           if (numlike && has_digit) L.flags |= AVDB_VCF_ID_HOST;  // Python coerces it to a number
         }
-        bool has_rs = false;
-        for (uint32_t i = 0; i + 1 < idn; ++i) has_rs = has_rs || (id[i] == 'r' && id[i + 1] == 's');
         if ((idn == 1 && id[0] == '.') || (idn >= 2 && id[0] == 'r' && id[1] == 's'))
           L.flags |= AVDB_VCF_ID_METASEQ;
         if (has_rs) {
           L.flags |= AVDB_VCF_ID_RS;
-          L.ext_id = rs_number(id, idn);
+          if (idn >= 3 && idn <= 18 && id[0] == 'r' && id[1] == 's' && id[2] != '0') {
+            uint64_t y0, y1;  // "rs" + up to 16 digits, SWAR
+            line16(word_at, mis, len, L.field[2] + 2, &y0, &y1);
+            bool ok;
+            const uint64_t v = decimal16(y0, y1, idn - 2, &ok);
+            L.ext_id = ok ? v : 0ull;
+          } else {
+            L.ext_id = rs_number(id, idn);
+          }
           if (!L.ext_id) L.flags |= AVDB_VCF_EXT_HOST;
         } else {
           // INFO: last entry whose key is exactly "RS" (dict(...) keeps the last)
@@ -381,8 +452,26 @@ __device__ __forceinline__ void parse_line(CP s, const WordAt& word_at, uint32_t
         const uint32_t rlen = fend(3) - L.field[3];
         const CP alt = s + L.field[4];
         const uint32_t an = fend(4) - L.field[4];
+        // SWAR: commas and '.' bytes of the ALT field; without a '.', every ALT is a
+        // record and the counts follow from the comma count
+        uint32_t commas = 0;
+        bool dot = false;
+        for (uint32_t b = 0; b < an; b += 16) {
+          uint64_t y0, y1;
+          line16(word_at, mis, len, L.field[4] + b, &y0, &y1);
+          const uint32_t nb = an - b < 16u ? an - b : 16u;
+          const uint64_t m0 = low_bytes_mask(nb < 8 ? nb : 8) & kHiBits;
+          const uint64_t m1 = (nb > 8 ? low_bytes_mask(nb - 8) : 0ull) & kHiBits;
+          commas += uint32_t(__popcll(bytes_eq_mask(y0, ',') & m0) + __popcll(bytes_eq_mask(y1, ',') & m1));
+          dot = dot || ((bytes_eq_mask(y0, '.') & m0) | (bytes_eq_mask(y1, '.') & m1));
+        }
+        if (!dot) {
+          L.n_alt = commas + 1;
+          L.n_rec = L.n_alt;
+          hbytes = uint64_t(L.n_rec) * rlen + (an - commas);
+        }
         uint32_t a0 = 0;
-        for (uint32_t i = 0; i <= an; ++i) {
+        for (uint32_t i = 0; dot && i <= an; ++i) {
           if (i == an || alt[i] == ',') {
             const uint32_t al = i - a0;
             ++L.n_alt;
@@ -436,19 +525,16 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
   }
 }
 
-// The allele heap bytes of a tile's lines are contiguous ([heap_off[base],
-// heap_off[last])): they are rendered into an LDS image of that span and leave as
-// coalesced 16-byte stores (per-lane byte stores touched a cache line per byte
-// and lane).  Spans over kHeapImg bytes fall back to per-lane stores.
-constexpr uint32_t kHeapImg = 4096;
-
-template <class CP, class O>
+// (Rendering the allele heap through an LDS image of the tile's heap span with a
+// coalesced flush, as K7 does for its text, measured slower: 0.66 vs 0.60 ms for
+// 8.4 M lines — the pass is bound by re-staging the text, not by these stores.)
+template <class CP>
 __device__ __forceinline__ void emit_line(CP s, const avdb_vcf_line& L, size_t li,
                                           uint64_t r, uint64_t h, uint8_t* __restrict__ chrom,
                                           uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
                                           uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
-                                          uint64_t* __restrict__ ext_id, uint32_t* __restrict__ rec_line,
-                                          uint32_t* __restrict__ rec_alt, O& hs) {
+                                          uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap,
+                                          uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
     const uint32_t nfields = L.n_fields < 8 ? L.n_fields : 8;
     const uint32_t rend = L.field[4] - 1;
     const uint32_t aend = 5 < nfields ? L.field[5] - 1 : L.len;
@@ -456,28 +542,30 @@ __device__ __forceinline__ void emit_line(CP s, const avdb_vcf_line& L, size_t l
     const uint32_t rlen = rend - L.field[3];
     const CP alt = s + L.field[4];
     const uint32_t an = aend - L.field[4];
-    uint32_t a0 = 0, ai = 0;
-    for (uint32_t i = 0; i <= an; ++i) {
-      if (i == an || alt[i] == ',') {
-        const uint32_t al = i - a0;
-        if (!(al == 1 && alt[a0] == '.')) {
-          chrom[r] = L.chrom;
-          pos[r] = L.pos;
-          allele_off[r] = h;
-          ref_len[r] = rlen;
-          alt_len[r] = al;
-          ext_id[r] = L.ext_id;
-          rec_line[r] = uint32_t(li);
-          rec_alt[r] = ai;
-          hs.bytes(ref, rlen);
-          hs.bytes(alt + a0, al);
-          h += rlen + al;
-          ++r;
-        }
-        ++ai;
-        a0 = i + 1;
+    // ALTs found with SWAR comma scans; the heap bytes leave through the 8-byte
+    // register sink (this lane's records are contiguous in the heap)
+    Out<true> hs(heap, h);
+    uint32_t ai = 0;
+    for (uint32_t a0 = 0; a0 <= an; ++ai) {
+      const uint32_t a1 = a0 + swar_find(alt + a0, an - a0, [](uint64_t x) { return bytes_eq_mask(x, ','); });
+      const uint32_t al = a1 - a0;
+      if (!(al == 1 && alt[a0] == '.')) {
+        chrom[r] = L.chrom;
+        pos[r] = L.pos;
+        allele_off[r] = h;
+        ref_len[r] = rlen;
+        alt_len[r] = al;
+        ext_id[r] = L.ext_id;
+        rec_line[r] = uint32_t(li);
+        rec_alt[r] = ai;
+        hs.bytes(ref, rlen);
+        hs.bytes(alt + a0, al);
+        h += rlen + al;
+        ++r;
       }
+      a0 = a1 + 1;
     }
+    hs.finish();
 }
 
 __global__ __launch_bounds__(kBlock) void k_vcf_emit(
@@ -488,9 +576,6 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
     uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap, uint32_t* __restrict__ rec_line,
     uint32_t* __restrict__ rec_alt) {
   __shared__ u32x4 s_text[kStage / 16];
-  __shared__ uint64_t s_heap[kHeapImg / 8];
-  lds_u64* himg = (lds_u64*)s_heap;
-  for (uint32_t q = threadIdx.x; q < kHeapImg / 8; q += blockDim.x) himg[q] = 0;
   const Heap h = make_heap(text, text_bytes);
   for (size_t base = size_t(blockIdx.x) * kBlock; base < n_lines; base += size_t(gridDim.x) * kBlock) {
     const size_t last = base + kBlock < n_lines ? base + kBlock : n_lines;
@@ -498,33 +583,21 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
     const size_t s0 = lines[base].start;
     const avdb_vcf_line& Z = lines[last - 1];
     const size_t s1 = Z.start + Z.len;
-    const Window w = stage_window(h, s0, s1, s_text);  // (its barrier also orders the heap image)
-    const uint64_t g0 = heap_off[base], g1 = heap_off[last];
-    const uint64_t ha0 = g0 & ~uint64_t(15);
-    const bool hst = g1 - ha0 + 16 <= kHeapImg;
+    const Window w = stage_window(h, s0, s1, s_text);
     const size_t li = base + threadIdx.x;
     if (li < n_lines) {
       const avdb_vcf_line L = lines[li];
       if (L.n_rec) {
-        auto run = [&](auto s, auto& hs) {
-          emit_line(s, L, li, rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id,
-                    rec_line, rec_alt, hs);
-          hs.finish();
-        };
-        if (hst) {
-          Out<true, true> hs(LdsImage{}, himg, heap_off[li] - ha0);
-          if (w.staged) run((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)), hs);
-          else run((glb_cp)(text + L.start), hs);
-        } else {
-          Out<true> hs(heap, heap_off[li]);
-          if (w.staged) run((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)), hs);
-          else run((glb_cp)(text + L.start), hs);
-        }
+        if (w.staged)
+          emit_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)), L, li,
+                    rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id, heap,
+                    rec_line, rec_alt);
+        else
+          emit_line((glb_cp)(text + L.start), L, li, rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len,
+                    alt_len, ext_id, heap, rec_line, rec_alt);
       }
     }
     __syncthreads();
-    if (hst) flush_span(himg, heap, g0, g1, threadIdx.x, blockDim.x);
-    __syncthreads();  // the window and the heap image are reused by the next trip
   }
 }
 

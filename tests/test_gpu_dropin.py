@@ -229,3 +229,60 @@ def test_variant_annotator_display_attributes_matches_reference():
         assert json.dumps(va.get_display_attributes()) == r["attributes"], r
     va = VariantAnnotator("CAG", "C", "chrUn_KI270302v1", 100)  # label the kernel leaves to the host
     assert va.get_display_attributes()["normalized_metaseq_id"] == "chrUn_KI270302v1:100:AG:-"
+
+
+def test_vcf_tokenizer_swar_fields(engine):
+    """K0's SWAR POS / ID / rsid / ALT scans: every synthetic dbSNP line is
+    resolved on the GPU (no host flag) with the host parser's POS, refSNP id and
+    alleles; edge fields (leading zeros, 10-digit and 2^32 positions, long and
+    zero-led rsids, numeric-looking IDs, '.' and empty ALTs) get the flags and
+    values the byte loops gave."""
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.engine import VCF_HOST_FLAGS
+    from annotatedvdb_amd.parsers import VcfEntryParser
+    lines = synth.vcf_text(20000, seed=23).decode().splitlines()
+    vb = engine.vcf_tokenize(("\n".join(lines) + "\n").encode())
+    L = vb.lines_host()
+    assert not (L["flags"] & VCF_HOST_FLAGS).any()
+    b = vb.records
+    pos, ext = b.pos.cpu().numpy(), b.ext_id.cpu().numpy().view(np.uint64)
+    rl, al, off = b.ref_len.cpu().numpy(), b.alt_len.cpu().numpy(), b.allele_off.cpu().numpy()
+    heap = b.heap.cpu().numpy().tobytes()
+    r = 0
+    for li, line in enumerate(lines):
+        v = VcfEntryParser(line).get_variant(namespace=True)
+        for alt in v.alt_alleles:
+            assert pos[r] == v.position and ext[r] == int(v.ref_snp_id[2:]), line
+            assert heap[off[r]:off[r] + rl[r] + al[r]].decode() == v.ref_allele + alt
+            r += 1
+    assert r == b.n
+    info = "RS=5;VC=SNV"
+    cases = [  # (line, expect pos, expect flags set, expect flags clear, n_alt, n_rec)
+        ("1\t00123\trs7\tA\tG\t.\t.\t" + info, 123, 0x10, 0x4, 1, 1),
+        ("1\t4294967295\trs7\tA\tG\t.\t.\t" + info, 4294967295, 0x10, 0x4, 1, 1),
+        ("1\t4294967296\trs7\tA\tG\t.\t.\t" + info, None, 0x4, 0, 1, 1),
+        ("1\t12345678901\trs7\tA\tG\t.\t.\t" + info, None, 0x4, 0, 1, 1),
+        ("1\t12a4\trs7\tA\tG\t.\t.\t" + info, None, 0x4, 0, 1, 1),
+        ("1\t55\trs0123\tA\tG\t.\t.\t" + info, 55, 0x18, 0, 1, 1),
+        ("1\t55\trs1234567890123456\tA\tG\t.\t.\t" + info, 55, 0x10, 0x8, 1, 1),
+        ("1\t55\t1e5\tA\tG\t.\t.\t" + info, 55, 0x200, 0, 1, 1),
+        ("1\t55\tfoo;rsbar\tA\tG\t.\t.\t" + info, 55, 0x18, 0, 1, 1),
+        ("1\t55\tr\tA\tG\t.\t.\t" + info, 55, 0x20, 0x10, 1, 1),
+        ("1\t55\tabcdefgrs1\tA\tG\t.\t.\t" + info, 55, 0x18, 0, 1, 1),
+        ("1\t55\tabcdefghijklmnors1\tA\tG\t.\t.\t" + info, 55, 0x18, 0, 1, 1),
+        ("1\t55\trs9\tA\t.\t.\t.\t" + info, 55, 0x10, 0, 1, 0),
+        ("1\t55\trs9\tA\tC,.,G\t.\t.\t" + info, 55, 0x10, 0, 3, 2),
+        ("1\t55\trs9\tA\tC,G,T,AC,AAAAAAAAAAAAAAAAAAAAAA\t.\t.\t" + info, 55, 0x10, 0, 5, 5),
+        ("1\t55\trs9\tA\t\t.\t.\t" + info, 55, 0x10, 0, 1, 1),
+    ]
+    text = ("\n".join(c[0] for c in cases) + "\n").encode()
+    vb = engine.vcf_tokenize(text)
+    L = vb.lines_host()
+    for k, (line, p, fset, fclr, na, nr) in enumerate(cases):
+        f = int(L[k]["flags"])
+        assert f & fset == fset and not (f & fclr), (line, hex(f))
+        if p is not None:
+            assert int(L[k]["pos"]) == p, line
+        assert int(L[k]["n_alt"]) == na and int(L[k]["n_rec"]) == nr, line
+    assert int(L[6]["ext_id"]) == 1234567890123456 and int(L[0]["ext_id"]) == 7
+    assert int(L[1]["pos"]) == 4294967295
