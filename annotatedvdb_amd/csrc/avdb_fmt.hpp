@@ -125,6 +125,7 @@ struct LdsImage {};  // constructor tag of the LDS sink
 // the zeroed image, the words wholly inside its span are plain ds_write_b64.
 template <bool WRITE, bool LDS = false>
 struct Out {
+  static constexpr bool kWrite = WRITE;
   gbyte* base;
   uint64_t p, lo;
   bool bad;  // set by a formatter that cannot render its input (line goes to the host)
@@ -642,8 +643,95 @@ __device__ __forceinline__ bool number_plain(CP f, uint32_t n) {
   return nd <= 15;                            // repr == these digits
 }
 
+#ifndef AVDB_JSON_SWAR
+#define AVDB_JSON_SWAR 1  // FREQ numbers via the SWAR form: 0 never, 1 size pass only (default: in the
+                          // write pass its registers spill, 4.37 -> 4.86 ms), 2 both passes
+#endif
+
+// n <= 16 text bytes at s as two registers (independent aligned word reads; the
+// words hold only bytes of the text's own window, bytes past n are 0)
+template <class CP>
+__device__ __forceinline__ void load16(CP s, uint32_t n, uint64_t* x0, uint64_t* x1) {
+  const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(s)) & 7u;
+  const typename Word64<CP>::T w = reinterpret_cast<typename Word64<CP>::T>(s - mis);
+  const uint32_t nw = (mis + n + 7) >> 3;
+  const uint64_t w0 = nw > 0 ? w[0] : 0ull, w1 = nw > 1 ? w[1] : 0ull, w2 = nw > 2 ? w[2] : 0ull;
+  const uint32_t sh = 8 * mis;
+  uint64_t y0 = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  uint64_t y1 = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  y0 &= low_bytes_mask(n < 8 ? n : 8);
+  y1 &= n > 8 ? low_bytes_mask(n - 8) : 0ull;
+  *x0 = y0;
+  *x1 = y1;
+}
+
+// bytes [a, b) (b <= 16) of the register pair (x0, x1) to the sink
+template <class O>
+__device__ __forceinline__ void append_pair(O& o, uint64_t x0, uint64_t x1, uint32_t a, uint32_t b) {
+  if (b <= a) return;
+  const uint32_t n = b - a;
+  uint64_t y0, y1;
+  if (a == 0) { y0 = x0; y1 = x1; }
+  else if (a < 8) { y0 = (x0 >> (8 * a)) | (x1 << (64 - 8 * a)); y1 = x1 >> (8 * a); }
+  else { y0 = x1 >> (8 * (a - 8)); y1 = 0; }
+  o.append(y0 & low_bytes_mask(n < 8 ? n : 8), n < 8 ? n : 8);
+  if (n > 8) o.append(y1 & low_bytes_mask(n - 8), n - 8);
+}
+
+// lowest / highest flagged byte index of a 16-byte mask pair (bit 7 per byte), 16 if none
+__device__ __forceinline__ uint32_t first_byte16(uint64_t m0, uint64_t m1) {
+  return m0 ? uint32_t(__builtin_ctzll(m0)) >> 3 : (m1 ? 8 + (uint32_t(__builtin_ctzll(m1)) >> 3) : 16u);
+}
+__device__ __forceinline__ uint32_t last_byte16(uint64_t m0, uint64_t m1) {
+  return m1 ? 15 - (uint32_t(__builtin_clzll(m1)) >> 3) : (m0 ? 7 - (uint32_t(__builtin_clzll(m0)) >> 3) : 16u);
+}
+
 template <class O, class CP>
 __device__ __forceinline__ O json_number(O o, CP f, uint32_t n) {
+  // SWAR form for fields of <= 16 bytes in fixed notation (repr's decimal
+  // exponent -4..15): the canonical text is the integer digits without leading
+  // zeros (or "0"), '.', the fraction without trailing zeros (or "0") — two byte
+  // ranges of the field, read once into registers.  Exponent forms and longer
+  // fields take the digit-by-digit path below.
+  constexpr bool swar = AVDB_JSON_SWAR == 2 || (AVDB_JSON_SWAR == 1 && !O::kWrite);
+  if (swar && n >= 1 && n <= 16) {
+    uint64_t x0, x1;
+    load16(f, n, &x0, &x1);
+    const uint64_t m0 = low_bytes_mask(n < 8 ? n : 8) & kHiBits, m1 = (n > 8 ? low_bytes_mask(n - 8) : 0ull) & kHiBits;
+    const uint64_t d0 = bytes_eq_mask(x0, '.') & m0, d1 = bytes_eq_mask(x1, '.') & m1;
+    const uint64_t nd0 = nondigit_mask(x0) & m0 & ~d0, nd1 = nondigit_mask(x1) & m1 & ~d1;
+    const uint32_t ndots = uint32_t(__popcll(d0) + __popcll(d1));
+    if (nd0 | nd1 || ndots > 1 || (ndots == 1 && n == 1)) {
+      o.bad = true;
+      return o;
+    }
+    const uint64_t z0 = ~bytes_eq_mask(x0, '0') & m0 & ~d0, z1 = ~bytes_eq_mask(x1, '0') & m1 & ~d1;  // nonzero digits
+    const uint32_t f0 = first_byte16(z0, z1), l0 = last_byte16(z0, z1);
+    if (ndots == 0) {  // int: leading zeros stripped, at least one digit
+      append_pair(o, x0, x1, f0 < n ? f0 : n - 1, n);
+      return o;
+    }
+    const uint32_t dot = first_byte16(d0, d1);
+    if (f0 == 16) {  // all zeros
+      o.lit("0.0");
+      return o;
+    }
+    const uint32_t nsig = l0 - f0 + 1 - (f0 < dot && dot < l0 ? 1u : 0u);
+    if (nsig > 15) {  // repr would not be these digits
+      o.bad = true;
+      return o;
+    }
+    const int32_t k = f0 < dot ? int32_t(f0) : int32_t(f0) - 1;  // index in the digits without the dot
+    const int32_t e = int32_t(dot) - 1 - k;
+    if (e >= -4 && e < 16) {
+      if (f0 < dot) append_pair(o, x0, x1, f0, dot);
+      else o.put('0');
+      o.put('.');
+      if (l0 > dot) append_pair(o, x0, x1, dot + 1, l0 + 1);
+      else o.put('0');
+      return o;
+    }
+  }
   o.bad = !number_plain(f, n);
   if (o.bad) return o;
   uint32_t dot = n;

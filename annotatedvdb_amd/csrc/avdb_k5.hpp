@@ -88,10 +88,12 @@ __device__ bool freq_plain(CP s, uint32_t v0, uint32_t v1) {
     const uint32_t p1 = find_byte(s, p0, v1, '|');
     const uint32_t c1 = find_byte(s, p0, p1, ':');
     if (c1 == p1 || np >= kMaxPops) return false;
-    for (uint32_t i = p0; i < c1; ++i) {
-      const uint8_t c = s[i];
-      if (c < 0x20 || c > 0x7E || c == '"' || c == '\\') return false;
-    }
+    // population name: printable ASCII without '"' or '\\' (SWAR)
+    if (swar_find(s + p0, c1 - p0, [](uint64_t x) {
+          const uint64_t lt20 = ~((x & 0x7F7F7F7F7F7F7F7Full) + 0x6060606060606060ull) & kHiBits;
+          return (x & kHiBits) | lt20 | bytes_eq_mask(x, 0x7F) | bytes_eq_mask(x, '"') | bytes_eq_mask(x, '\\');
+        }) != c1 - p0)
+      return false;
     // duplicate name among the earlier populations
     for (uint32_t q0 = v0; q0 < p0;) {
       const uint32_t q1 = find_byte(s, q0, v1, '|');

@@ -54,6 +54,12 @@ __device__ __forceinline__ uint64_t bytes_eq_mask(uint64_t x, uint8_t c) {
 // 8 bytes at aligned address a (bytes outside [lo,hi) read as 0x00)
 __device__ __forceinline__ uint64_t text_word(uintptr_t a, const Heap& h) { return heap_word(a, h); }
 
+// bit 7 set in every byte of x that is not an ASCII digit
+__device__ __forceinline__ uint64_t nondigit_mask(uint64_t x) {
+  const uint64_t d = x ^ 0x3030303030303030ull;
+  return (((d & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | d) & kHiBits;
+}
+
 __device__ __forceinline__ bool is_ws(uint8_t c) {
   return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
 }

@@ -261,11 +261,6 @@ __device__ __forceinline__ void line16(const WordAt& word_at, uint32_t mis, uint
   *x1 = y1;
 }
 
-// bit 7 set in every byte of x that is not an ASCII digit
-__device__ __forceinline__ uint64_t nondigit_mask(uint64_t x) {
-  const uint64_t d = x ^ 0x3030303030303030ull;
-  return (((d & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | d) & kHiBits;
-}
 
 // up to 8 ASCII digits (most significant in the lowest byte, n of them) -> value
 __device__ __forceinline__ uint32_t digits8_value(uint64_t x, uint32_t n) {
