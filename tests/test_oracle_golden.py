@@ -228,6 +228,47 @@ def test_c_oracle_vrs_digest_and_keys_match_python_oracle():
         assert kb[int(koff[i]):int(koff[i + 1])].decode() == exp
 
 
+def test_c_oracle_bin_paths_match_python_oracle_and_golden():
+    """The C oracle's ltree path formatter (the checker of K7's path text over
+    whole keyed-C4 shards) equals the Python restatement on spans of every
+    level and contig, gives empty text for unmappable codes, and reproduces the
+    reference-generated C1 prefix paths."""
+    import oracle
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.chromosomes import length_table
+    c, s, e = synth.np_spans(30000, seed=19)
+    code, _ = O.bin_codes_np(c, s, e, length_table())
+    code = code.astype(np.uint32)
+    code[::97] = O.BIN_NONE
+    c = c.astype(np.uint8)
+    out = np.zeros(96 * len(c), dtype=np.uint8)
+    off = np.zeros(len(c) + 1, dtype=np.uint64)
+    lib = oracle.c_oracle()
+    lib.avdb_oracle_bin_paths(c.ctypes.data, code.ctypes.data, len(c), out.ctypes.data, off.ctypes.data)
+    b = out.tobytes()
+    levels = set()
+    for i in range(len(c)):
+        exp = "" if code[i] == O.BIN_NONE else O.format_bin_path(CHROM_NAMES[c[i]], int(code[i]))
+        assert b[off[i]:off[i + 1]].decode() == exp, i
+        levels.add(int(code[i]) >> 28)
+    assert len(levels) >= 12
+    # against the reference's own paths (tests/golden/c1_prefix.tsv.gz, make_golden.py)
+    with gzip.open(os.path.join(GOLDEN, "c1_prefix.tsv.gz"), "rt") as fh:
+        fh.readline()
+        rows = [ln.rstrip("\n").split("\t") for ln in fh][:20000]
+    d = synth.np_c1(seed=1)  # the golden rows are the prefix of the whole C1 set
+    d = {k: v[:len(rows)] for k, v in d.items() if k in ("chrom", "pos")}
+    end = np.array([int(r[1]) for r in rows], dtype=np.uint32)
+    code, _ = O.bin_codes_np(d["chrom"], d["pos"], end, length_table())
+    code = code.astype(np.uint32)
+    ch = d["chrom"].astype(np.uint8)
+    out = np.zeros(96 * len(rows), dtype=np.uint8)
+    off = np.zeros(len(rows) + 1, dtype=np.uint64)
+    lib.avdb_oracle_bin_paths(ch.ctypes.data, code.ctypes.data, len(rows), out.ctypes.data, off.ctypes.data)
+    b = out.tobytes()
+    assert all(b[off[i]:off[i + 1]].decode() == rows[i][2] for i in range(len(rows)))
+
+
 def test_c1_prefix_golden():
     """BASELINE config C1 (synth.np_c1, seed 1): the oracle's end, bin path and
     primary key for the first 100,000 records equal what the reference computed
