@@ -51,7 +51,10 @@ typedef __attribute__((address_space(1))) uint8_t gbyte;
 typedef __attribute__((address_space(1))) U64u* gw_u64u;
 // per SIMD: the text window's LDS allows 4 workgroups per CU (re-checked after
 // the append sink: 4 waves with ~100 B of spills 5.5 ms, 3 waves without 6.2 ms)
-constexpr int kFormatWaves = 4;
+#ifndef AVDB_K5_WAVES
+#define AVDB_K5_WAVES 4  // A/B knob
+#endif
+constexpr int kFormatWaves = AVDB_K5_WAVES;
 
 // decimal digit count of v (compare chain: no division)
 __device__ __forceinline__ uint32_t ndigits(uint32_t v) {
