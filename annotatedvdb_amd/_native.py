@@ -26,6 +26,8 @@ AVDB_EINVAL = -1
 AVDB_EHIP = -2
 AVDB_ENOMEM = -3
 AVDB_ERANGE = -4
+AVDB_ERCCL = -5
+RCCL_ID_BYTES = 128
 
 STATUS_OK = 0
 STATUS_UNKNOWN_CHROM = 1
@@ -78,6 +80,8 @@ EXPORTED_SYMBOLS = [
     "avdb_primary_keys", "avdb_keyset_probe_text",
     "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
     "avdb_small_prep", "avdb_host_alloc", "avdb_host_free",
+    "avdb_rccl_unique_id", "avdb_rccl_comm_init", "avdb_rccl_comm_destroy",
+    "avdb_hist_allgather_workspace_size", "avdb_hist_allgather",
 ]
 
 
@@ -155,6 +159,11 @@ def _sig(lib):
     f.avdb_host_alloc.argtypes = [SZ, ctypes.POINTER(P)]
     f.avdb_host_free.argtypes = [P]
     f.avdb_shard_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
+    f.avdb_rccl_unique_id.argtypes = [P]
+    f.avdb_rccl_comm_init.argtypes = [P, I32, I32, P, ctypes.POINTER(P)]
+    f.avdb_rccl_comm_destroy.argtypes = [P]
+    f.avdb_hist_allgather_workspace_size.argtypes = [I32, SZ, SZ, ctypes.POINTER(SZ)]
+    f.avdb_hist_allgather.argtypes = [P, P, P, SZ, P, SZ, P, P, P, SZ, P]
     f.avdb_vcf_select_lines.argtypes = [P, SZ, P, P, P, P, U32, U32, I32, P, SZ, P, P]
     f.avdb_vcf_select_copy.argtypes = [P, P, SZ, SZ, P, P, P, P]
     for name in EXPORTED_SYMBOLS:

@@ -83,6 +83,54 @@ def allgather_stats(hist: torch.Tensor, counters: torch.Tensor, ri: RankInfo
     return torch.stack(hs).sum(0).to(dev), torch.stack(cs).sum(0).to(dev)
 
 
+class RcclExchange:
+    """The node exchange through the C ABI (``avdb_hist_allgather``, SURVEY.md
+    §8b) instead of ``torch.distributed``: for a caller that binds only
+    ``libavdb_hip.so``.  Rank 0 makes the id (``new_id``) and hands its bytes to
+    the other ranks out of band; every rank builds its communicator with its
+    rank.  ``allgather`` returns the node totals (sum over ranks), as
+    ``allgather_stats`` does."""
+
+    def __init__(self, engine, world: int, rank: int, unique_id: bytes):
+        import ctypes
+        from . import _native as N
+        self._N = N
+        self.engine = engine
+        self.world = world
+        comm = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(unique_id), N.RCCL_ID_BYTES)
+        N.check("avdb_rccl_comm_init", engine.lib.avdb_rccl_comm_init(engine.ctx, world, rank, buf,
+                                                                     ctypes.byref(comm)))
+        self.comm = comm
+
+    @staticmethod
+    def new_id() -> bytes:
+        import ctypes
+        from . import _native as N
+        buf = ctypes.create_string_buffer(N.RCCL_ID_BYTES)
+        N.check("avdb_rccl_unique_id", N.load_library().avdb_rccl_unique_id(buf))
+        return buf.raw
+
+    def allgather(self, hist: torch.Tensor, counters: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        import ctypes
+        N, e = self._N, self.engine
+        nb, nc = hist.numel(), counters.numel()
+        sz = ctypes.c_size_t()
+        N.check("avdb_hist_allgather_workspace_size",
+                e.lib.avdb_hist_allgather_workspace_size(self.world, nb, nc, ctypes.byref(sz)))
+        ws = torch.empty(int(sz.value), dtype=torch.uint8, device=hist.device)
+        node_h, node_c = torch.empty_like(hist), torch.empty_like(counters)
+        N.check("avdb_hist_allgather", e.lib.avdb_hist_allgather(
+            e.ctx, self.comm, N.ptr(hist), nb, N.ptr(counters), nc, N.ptr(node_h), N.ptr(node_c), N.ptr(ws),
+            ws.numel(), e._stream()))
+        return node_h, node_c
+
+    def close(self):
+        if self.comm:
+            self._N.check("avdb_rccl_comm_destroy", self.engine.lib.avdb_rccl_comm_destroy(self.comm))
+            self.comm = None
+
+
 def max_over_ranks(value: float, ri: RankInfo, device=None) -> float:
     if not ri.distributed:
         return value

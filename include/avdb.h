@@ -59,6 +59,7 @@ extern "C" {
 #define AVDB_EHIP (-2)     /* HIP runtime error (launch / allocation) */
 #define AVDB_ENOMEM (-3)
 #define AVDB_ERANGE (-4)   /* output buffer too small */
+#define AVDB_ERCCL (-5)    /* RCCL could not be loaded, or a collective failed */
 
 /* per-record status (u8) */
 #define AVDB_STATUS_OK 0
@@ -411,6 +412,25 @@ int avdb_vcf_select_lines(avdb_ctx* ctx, size_t n_lines, const avdb_vcf_line* li
                           void* workspace, size_t workspace_bytes, uint64_t* sel_off, void* stream);
 int avdb_vcf_select_copy(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
                          const avdb_vcf_line* lines, const uint64_t* sel_off, uint8_t* out, void* stream);
+
+/* ---- node exchange over RCCL (SURVEY.md §8b avdb_hist_allgather, §8e) ------
+ * The one collective of the path: every rank's L8 histogram (u32[n_bins], the
+ * hist_l8 K1/K2 accumulate) and counters (u64[n_counters]) all-gathered in one
+ * RCCL call (xGMI inside a node) and summed over the ranks on the device into
+ * node_hist / node_counters.  The reference has no collective (one process per
+ * chromosome file, Load/bin/load_vcf_file.py:307-313).  Rank 0 makes the id
+ * with avdb_rccl_unique_id, hands its AVDB_RCCL_ID_BYTES bytes to the other
+ * ranks out of band, and every rank calls avdb_rccl_comm_init with its rank.
+ * RCCL is loaded at first use (dlopen); these calls return AVDB_ERCCL when it
+ * is absent.  Workspace: avdb_hist_allgather_workspace_size, 8-byte aligned. */
+#define AVDB_RCCL_ID_BYTES 128
+int avdb_rccl_unique_id(void* id);
+int avdb_rccl_comm_init(avdb_ctx* ctx, int world, int rank, const void* id, void** comm);
+int avdb_rccl_comm_destroy(void* comm);
+int avdb_hist_allgather_workspace_size(int world, size_t n_bins, size_t n_counters, size_t* bytes);
+int avdb_hist_allgather(avdb_ctx* ctx, void* comm, const uint32_t* hist, size_t n_bins,
+                        const uint64_t* counters, size_t n_counters, uint32_t* node_hist,
+                        uint64_t* node_counters, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- host-side formatting of kernel outputs -------------------------------
  * ltree path text (<= AVDB_MAX_PATH bytes).  Returns the length written (no

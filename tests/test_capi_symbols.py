@@ -108,3 +108,17 @@ def test_product_path_fails_loudly_without_gpu():
     from annotatedvdb_amd.bin_index import BinIndex
     with pytest.raises(N.NativeUnavailable):
         BinIndex(None, verbose=False)
+
+
+def test_hist_allgather_argument_checks(host_ctx):
+    """The RCCL entry points refuse bad arguments before touching RCCL or a GPU;
+    the workspace is (world + 1) per-rank slots of padded histogram + counters."""
+    lib, ctx = host_ctx
+    sz = ctypes.c_size_t()
+    assert lib.avdb_hist_allgather_workspace_size(8, 6189, 32, ctypes.byref(sz)) == 0
+    assert sz.value == 9 * ((4 * 6189 + 7) // 8 * 8 + 8 * 32)
+    assert lib.avdb_hist_allgather_workspace_size(0, 1, 1, ctypes.byref(sz)) == N.AVDB_EINVAL
+    assert lib.avdb_hist_allgather(ctx, None, None, 0, None, 0, None, None, None, 0, None) == N.AVDB_EINVAL
+    comm = ctypes.c_void_p()
+    assert lib.avdb_rccl_comm_init(ctx, 2, 2, b"x" * 128, ctypes.byref(comm)) == N.AVDB_EINVAL
+    assert lib.avdb_rccl_comm_destroy(None) == 0
