@@ -416,6 +416,42 @@ __global__ __launch_bounds__(1024) void k_long_scan(uint32_t* __restrict__ count
   if (threadIdx.x == 1023) *total = base;
 }
 
+// the same scatter from the is_long flags k_long_hist wrote (1 byte per record,
+// 4 per load) instead of both length arrays (8 bytes per record): only a long
+// record's ALT length is read again, for its bucket
+__global__ __launch_bounds__(kBlock) void k_long_scatter_flags(const uint8_t* __restrict__ is_long,
+                                                               const uint32_t* __restrict__ al, size_t n,
+                                                               const uint32_t* __restrict__ offs,
+                                                               uint32_t* __restrict__ list) {
+  __shared__ uint32_t s_cur[kLongBuckets];
+  if (threadIdx.x < kLongBuckets) s_cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const size_t per = (((n + gridDim.x - 1) / gridDim.x) + 3) & ~size_t(3);  // k_long_hist's chunks
+  const size_t i0 = size_t(blockIdx.x) * per;
+  const size_t i1 = i0 + per < n ? i0 + per : n;
+  const size_t step = 4 * size_t(blockDim.x);
+  for (size_t j = i0 + 4 * size_t(threadIdx.x); j < i1; j += 2 * step) {
+    const size_t j2 = j + step;
+    const uint32_t f0 = j + 4 <= i1 ? *reinterpret_cast<const uint32_t*>(is_long + j) : 0u;
+    const uint32_t f1 = j2 + 4 <= i1 ? *reinterpret_cast<const uint32_t*>(is_long + j2) : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if ((f0 >> (8 * k)) & 1u) list[atomicAdd(&s_cur[bucket_of(al[j + k])], 1u)] = uint32_t(j + k);
+      if ((f1 >> (8 * k)) & 1u) list[atomicAdd(&s_cur[bucket_of(al[j2 + k])], 1u)] = uint32_t(j2 + k);
+    }
+    // a chunk ending inside a group
+    if (j + 4 > i1)
+      for (size_t k = j; k < i1; ++k)
+        if (is_long[k]) list[atomicAdd(&s_cur[bucket_of(al[k])], 1u)] = uint32_t(k);
+    if (j2 < i1 && j2 + 4 > i1)
+      for (size_t k = j2; k < i1; ++k)
+        if (is_long[k]) list[atomicAdd(&s_cur[bucket_of(al[k])], 1u)] = uint32_t(k);
+  }
+}
+
+#ifndef AVDB_K4_SCATTER_FLAGS
+#define AVDB_K4_SCATTER_FLAGS 1  // A/B knob: 0 scatters from the length arrays
+#endif
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_long_scatter(const uint32_t* __restrict__ rl,
                                                          const uint32_t* __restrict__ al, size_t n,
@@ -752,7 +788,10 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   AVDB_LAUNCH_CHECK("k_long_hist");
   hipLaunchKernelGGL(k_long_scan, dim3(1), dim3(1024), 0, s, counts, total);
   AVDB_LAUNCH_CHECK("k_long_scan");
-  if (vec)
+  if (vec && is_long && AVDB_K4_SCATTER_FLAGS)
+    hipLaunchKernelGGL(k_long_scatter_flags, dim3(kCompactGrid), dim3(kBlock), 0, s, is_long, alt_len, n, counts,
+                       list);
+  else if (vec)
     hipLaunchKernelGGL(k_long_scatter<true>, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
                        max_seq_len, counts, list);
   else
