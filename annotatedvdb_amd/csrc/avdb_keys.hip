@@ -154,8 +154,20 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifndef AVDB_K7_PREFETCH
+#define AVDB_K7_PREFETCH 0  // A/B knob: 1 loads the next tile's SoA and offsets before rendering this one
+#endif
+// a tile's per-record inputs (WRITE with AVDB_K7_PREFETCH)
+struct KeyTileIn {
+  uint32_t c, p, r, a, cd;
+  uint64_t e, off, ko, po;
+};
+
 template <bool WRITE>
-__global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
+#ifndef AVDB_K7_WAVES
+#define AVDB_K7_WAVES (AVDB_K7_PREFETCH ? 4 : 5)
+#endif
+__global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A) {
   __shared__ uint64_t s_kimg[WRITE ? kWavesPerBlock * kKeyWave / 8 : 1];
   __shared__ uint64_t s_pimg[WRITE ? kWavesPerBlock * kPathWave / 8 : 1];
   const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
@@ -169,19 +181,42 @@ __global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
   // WRITE: one 64-record tile per wave; SIZE: one record per lane (same indexing).
   const uint32_t bid = blockIdx.x;
   const size_t stride = size_t(gridDim.x) * blockDim.x;
+  constexpr bool PF = WRITE && AVDB_K7_PREFETCH;
+  auto load_in = [&](size_t t) {
+    KeyTileIn v{};
+    const size_t j = t + lane;
+    if (j < A.n) {
+      v.c = A.chrom[j];
+      v.p = A.pos[j];
+      v.r = A.rl[j];
+      v.a = A.al[j];
+      v.e = A.ext ? A.ext[j] : 0ull;
+      v.off = A.off[j];
+      v.ko = A.key_off[j];
+      if (A.code) {
+        v.cd = A.code[j];
+        v.po = A.path_off[j];
+      }
+    }
+    return v;
+  };
+  KeyTileIn nx{};
+  if (PF && size_t(bid) * blockDim.x + size_t(wv) * kWave < A.n) nx = load_in(size_t(bid) * blockDim.x + size_t(wv) * kWave);
   for (size_t t0 = size_t(bid) * blockDim.x + size_t(wv) * kWave; t0 < A.n; t0 += stride) {
     const size_t i = t0 + lane;
     const bool live = i < A.n;
+    const KeyTileIn cur = nx;
+    if (PF && t0 + stride < A.n) nx = load_in(t0 + stride);
     uint32_t c = 0, p = 0, r = 0, a = 0;
     uint64_t e = 0;
     bool lng = false;
     uint8_t st = AVDB_KEY_HOST;
     if (live) {
-      c = A.chrom[i];
-      p = A.pos[i];
-      r = A.rl[i];
-      a = A.al[i];
-      e = A.ext ? A.ext[i] : 0ull;
+      c = PF ? cur.c : A.chrom[i];
+      p = PF ? cur.p : A.pos[i];
+      r = PF ? cur.r : A.rl[i];
+      a = PF ? cur.a : A.al[i];
+      e = PF ? cur.e : (A.ext ? A.ext[i] : 0ull);
       lng = uint64_t(r) + a > A.max_seq_len;
       // SoA-decidable states; the WRITE pass adds the allele-byte checks
       st = AVDB_KEY_OK;
@@ -233,7 +268,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
     };
     if constexpr (WRITE) {
       if (live && st == AVDB_KEY_OK) {
-        const uint64_t off = lng ? 0 : A.off[i];
+        const uint64_t off = lng ? 0 : (PF ? cur.off : A.off[i]);
         const uint32_t ra = r + a;
         if (!lng && off + ra > A.heap_bytes) {
           st = AVDB_KEY_HOST;
@@ -274,9 +309,17 @@ __global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
       const size_t last = t0 + kWave < A.n ? t0 + kWave : A.n;
       // stream 0: keys
       const uint64_t gk0 = A.key_off[t0], gk1 = A.key_off[last];
+      // (PF: a record's end offset is the next lane's start; the tile's last live
+      // record ends at gk1 / gp1)
+      auto next_of = [&](uint64_t v, uint64_t g1) -> uint64_t {
+        const uint64_t nv = (uint64_t(uint32_t(__shfl_down(uint32_t(v >> 32), 1, kWave))) << 32) |
+                            uint32_t(__shfl_down(uint32_t(v), 1, kWave));
+        return i + 1 == last ? g1 : nv;
+      };
+      const uint64_t ko = PF ? cur.ko : 0ull, ko1 = PF ? next_of(cur.ko, gk1) : 0ull;
       const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap && !(AVDB_K7_EXP & 16);
-      if (live && st == AVDB_KEY_OK && A.key_off[i + 1] <= A.key_cap) {  // (cap: never write past the buffer)
-        const uint64_t at = A.key_off[i];
+      if (live && st == AVDB_KEY_OK && (PF ? ko1 : A.key_off[i + 1]) <= A.key_cap) {  // (cap: never write past the buffer)
+        const uint64_t at = PF ? ko : A.key_off[i];
         if (kst) {
           Out<true, true> o(LdsImage{}, kimg, at - (gk0 & ~uint64_t(15)));
           key(o).finish();
@@ -292,9 +335,10 @@ __global__ __launch_bounds__(kBlock, 5) void k_record_keys(KeyArgs A) {
         gp0 = A.path_off[t0];
         gp1 = A.path_off[last];
         pst = gp1 - (gp0 & ~uint64_t(15)) + 16 <= kPathWave && gp1 <= A.path_cap && !(AVDB_K7_EXP & 32);
-        const uint32_t cd = live ? A.code[i] : AVDB_BIN_NONE;
-        if (live && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom) && A.path_off[i + 1] <= A.path_cap) {
-          const uint64_t at = A.path_off[i];
+        const uint32_t cd = live ? (PF ? cur.cd : A.code[i]) : AVDB_BIN_NONE;
+        const uint64_t po1 = PF ? next_of(cur.po, gp1) : 0ull;
+        if (live && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom) && (PF ? po1 : A.path_off[i + 1]) <= A.path_cap) {
+          const uint64_t at = PF ? cur.po : A.path_off[i];
           if (pst) {
             Out<true, true> o(LdsImage{}, pimg, at - (gp0 & ~uint64_t(15)));
             bin_path(o, c, cd).finish();
