@@ -76,11 +76,13 @@ struct KeyArgs {
 // instruction).  Tiles are per wave, with no s_barrier (the workgroup-tile form
 // with two barriers per tile measured the same: 13.46 vs 13.40 ms on C4k).  The
 // flush zeroes what it read, which keeps the images zero between tiles (the sink
-// ORs the words lanes share).  2.5 + 5.5 KB per wave, 32 KB per workgroup: 5
-// workgroups per CU, and the kernel is bounded to 96 VGPRs for 5 waves per SIMD.
+// ORs the words lanes share).  2.5 + 5.5 KB per wave, 32 KB per workgroup.
 // What the key stream waited on was its loads inside per-lane branches (the
 // digest, short-allele and long-indel pieces each a dependent global load in
 // turn): the register window below took keys + paths from 13.40 to 10.19 ms.
+// Then each tile's SoA and offsets are loaded one tile ahead (a record's end
+// offset is the next lane's start, by shuffle): 9.89 -> 8.20 ms at 4 waves/SIMD
+// (104 VGPRs; forcing 5 waves measured the same).
 // AVDB_K7_EXP: on-device A/B knobs for the write pass (tools/k7_ab.sh; some
 // produce wrong text and exist only to time a part): 1 no heap bytes, 2 no rsid
 // digits, 4 no allele check, 8 no POS digits, 16 keys to global (no LDS image),
@@ -155,7 +157,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 #ifndef AVDB_K7_PREFETCH
-#define AVDB_K7_PREFETCH 0  // A/B knob: 1 loads the next tile's SoA and offsets before rendering this one
+#define AVDB_K7_PREFETCH 1  // the next tile's SoA and offsets are loaded before this one renders (0: A/B)
 #endif
 // a tile's per-record inputs (WRITE with AVDB_K7_PREFETCH)
 struct KeyTileIn {

@@ -1,0 +1,12 @@
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+for lib in annotatedvdb_amd/_lib/var/libavdb_b_pf1.so annotatedvdb_amd/_lib/var/libavdb_c_pf1w5.so; do
+AVDB_LIB=$lib timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_c1.py tests/test_gpu_c4k.py -m gpu -k "not c4k_shard or c4k_shard and 0" -p no:cacheprovider > gpurun_out/pytest_ai.log 2>&1 || { tail -40 gpurun_out/pytest_ai.log; exit 1; }
+tail -1 gpurun_out/pytest_ai.log
+done
+for rep in 1 2; do
+for lib in annotatedvdb_amd/_lib/var/libavdb_*.so; do
+  echo "== $lib"
+  AVDB_LIB=$lib timeout -k 10 200 python tools/k7_probe.py 125000000 3 || exit 1
+done
+done
