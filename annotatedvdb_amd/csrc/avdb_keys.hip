@@ -163,6 +163,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 struct KeyTileIn {
   uint32_t c, p, r, a, cd;
   uint64_t e, off, ko, po;
+  // AVDB_K7_PREFETCH >= 2: the key window too, loaded once `off` has arrived
+  uint64_t w[kKeyWords];
+  uint32_t wmis;
+  bool in_regs;
 };
 
 template <bool WRITE>
@@ -202,8 +206,38 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
     }
     return v;
   };
+  constexpr bool PFW = WRITE && AVDB_K7_PREFETCH >= 2;
+  // the key bytes of record j (a short record's ref+alt, a long one's digest row)
+  // as the register window, for a tile loaded ahead
+  auto load_window = [&](KeyTileIn& v, size_t j) {
+    v.in_regs = false;
+    v.wmis = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kKeyWords; ++k) v.w[k] = 0;
+    if (j >= A.n || (AVDB_K7_EXP & 64)) return;
+    const bool lngj = uint64_t(v.r) + v.a > A.max_seq_len;
+    const uint32_t ra = v.r + v.a;
+    if (v.c >= uint32_t(A.n_chrom) || (v.e >> 63) || (lngj && !A.digest) || (!lngj && v.off + ra > A.heap_bytes))
+      return;
+    const uintptr_t src = lngj ? reinterpret_cast<uintptr_t>(A.digest) + 32 * j
+                               : reinterpret_cast<uintptr_t>(A.heap) + v.off;
+    const uintptr_t aw = src & ~uintptr_t(7);
+    v.wmis = uint32_t(src & 7);
+    const uint32_t nb = lngj ? AVDB_DIGEST_CHARS : ra;
+    v.in_regs = v.wmis + nb <= 8 * kKeyWords;
+    if (v.in_regs) {
+      const uint32_t nw = (v.wmis + nb + 7) >> 3;
+      const Heap h = lngj ? Heap{src, src + AVDB_DIGEST_CHARS} : make_heap(A.heap, A.heap_bytes);
+#pragma unroll
+      for (uint32_t k = 0; k < kKeyWords; ++k)
+        if (k < nw) v.w[k] = heap_word(aw + 8 * k, h);
+    }
+  };
   KeyTileIn nx{};
-  if (PF && size_t(bid) * blockDim.x + size_t(wv) * kWave < A.n) nx = load_in(size_t(bid) * blockDim.x + size_t(wv) * kWave);
+  if (PF && size_t(bid) * blockDim.x + size_t(wv) * kWave < A.n) {
+    nx = load_in(size_t(bid) * blockDim.x + size_t(wv) * kWave);
+    if (PFW) load_window(nx, size_t(bid) * blockDim.x + size_t(wv) * kWave + lane);
+  }
   for (size_t t0 = size_t(bid) * blockDim.x + size_t(wv) * kWave; t0 < A.n; t0 += stride) {
     const size_t i = t0 + lane;
     const bool live = i < A.n;
@@ -274,6 +308,11 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
         const uint32_t ra = r + a;
         if (!lng && off + ra > A.heap_bytes) {
           st = AVDB_KEY_HOST;
+        } else if (PFW) {
+#pragma unroll
+          for (uint32_t k = 0; k < kKeyWords; ++k) w[k] = cur.w[k];
+          wmis = cur.wmis;
+          in_regs = cur.in_regs;
         } else if (!(AVDB_K7_EXP & 64)) {
           const uintptr_t src = lng ? reinterpret_cast<uintptr_t>(A.digest) + 32 * i
                                     : reinterpret_cast<uintptr_t>(A.heap) + off;
@@ -354,6 +393,8 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       wave_lds_sync();
       if (kst) flush_span(kimg, A.key_out, gk0, gk1, lane, kWave);
       if (pst) flush_span(pimg, A.path_out, gp0, gp1, lane, kWave);
+      // the next tile's key window: its offsets have arrived by now
+      if (PFW && t0 + stride < A.n) load_window(nx, t0 + stride + lane);
       wave_lds_sync();
     } else if (live) {
       A.key_off[i] = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;
