@@ -82,7 +82,8 @@ struct KeyArgs {
 // turn): the register window below took keys + paths from 13.40 to 10.19 ms.
 // Then each tile's SoA and offsets are loaded one tile ahead (a record's end
 // offset is the next lane's start, by shuffle): 9.89 -> 8.20 ms at 4 waves/SIMD
-// (104 VGPRs; forcing 5 waves measured the same).
+// (104 VGPRs; forcing 5 waves measured the same).  Loading the next tile's key
+// window ahead as well (AVDB_K7_PREFETCH=2, 121 VGPRs) was slower: 8.30 vs 8.16.
 // AVDB_K7_EXP: on-device A/B knobs for the write pass (tools/k7_ab.sh; some
 // produce wrong text and exist only to time a part): 1 no heap bytes, 2 no rsid
 // digits, 4 no allele check, 8 no POS digits, 16 keys to global (no LDS image),
