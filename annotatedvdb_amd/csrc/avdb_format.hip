@@ -37,7 +37,8 @@ static size_t scan_bytes(size_t n) {
 
 extern "C" int avdb_format_workspace_size(size_t n, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
-  *bytes = scan_bytes(n + 1) + 256;
+  const size_t a = scan_bytes(n + 1), b = avdb::key_size_workspace(n);  // (K7's u16 sizes + scan)
+  *bytes = (a > b ? a : b) + 256;
   return AVDB_OK;
 }
 

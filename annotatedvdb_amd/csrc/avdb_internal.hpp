@@ -241,6 +241,11 @@ struct avdb_ctx {
 
 void avdb_set_error(const char* fmt, ...);
 
+namespace avdb {
+// workspace bytes K7's size pass needs for n records (u16 sizes + their scan)
+size_t key_size_workspace(size_t n);
+}  // namespace avdb
+
 #define AVDB_HIP_TRY(expr)                                                         \
   do {                                                                             \
     hipError_t _e = (expr);                                                        \

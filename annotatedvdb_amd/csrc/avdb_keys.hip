@@ -66,6 +66,8 @@ struct KeyArgs {
   uint8_t* key_out;
   uint8_t* path_out;
   uint8_t* state;
+  uint16_t* key_sz;   // SIZE: sizes as u16 in the workspace (scanned into key_off), or NULL
+  uint16_t* path_sz;
 };
 
 // WRITE renders each wave's 64 records as a tile: each stream's span (the
@@ -88,6 +90,9 @@ struct KeyArgs {
 // produce wrong text and exist only to time a part): 1 no heap bytes, 2 no rsid
 // digits, 4 no allele check, 8 no POS digits, 16 keys to global (no LDS image),
 // 32 paths to global, 64 key bytes read per piece (no register window).
+#ifndef AVDB_K7_SIZE16
+#define AVDB_K7_SIZE16 1  // A/B knob: 0 writes u64 sizes and scans them in place
+#endif
 #ifndef AVDB_K7_GRID
 #define AVDB_K7_GRID 4096u  // write-pass workgroups (A/B knob)
 #endif
@@ -398,11 +403,15 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       if (PFW && t0 + stride < A.n) load_window(nx, t0 + stride + lane);
       wave_lds_sync();
     } else if (live) {
-      A.key_off[i] = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;
+      const uint32_t ks = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;
+      if (A.key_sz) A.key_sz[i] = uint16_t(ks);
+      else A.key_off[i] = ks;
       if (A.code) {
         const uint32_t cd = A.code[i];
-        A.path_off[i] = (cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom))
-                            ? bin_path(Out<false>(nullptr, 0), c, cd).size() : 0;
+        const uint32_t ps = (cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom))
+                                ? bin_path(Out<false>(nullptr, 0), c, cd).size() : 0;
+        if (A.path_sz) A.path_sz[i] = uint16_t(ps);
+        else A.path_off[i] = ps;
       }
     }
   }
@@ -418,6 +427,28 @@ static size_t scan_bytes(size_t n) {
                                          static_cast<unsigned long long*>(nullptr), n);
   return (t + 255) & ~size_t(255);
 }
+
+// K7's size pass writes each record's key and path size as u16 into the
+// workspace and the scans widen them to the u64 offsets: the pass writes 4
+// bytes per record instead of 16 and the scans read 2 instead of 8 per array
+// (C4k: 1.25e8 records, two 1 GB u64 scans at 0.76 ms each).
+struct Widen16 {
+  __host__ __device__ unsigned long long operator()(const uint16_t& x) const { return x; }
+};
+typedef hipcub::TransformInputIterator<unsigned long long, Widen16, const uint16_t*> Wide16It;
+
+static size_t scan16_bytes(size_t n) {
+  size_t t = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, Wide16It(nullptr, Widen16()),
+                                         static_cast<unsigned long long*>(nullptr), n);
+  return (t + 255) & ~size_t(255);
+}
+
+static size_t size16_slot(size_t n) { return ((2 * (n + 1)) + 255) & ~size_t(255); }
+
+namespace avdb {
+size_t key_size_workspace(size_t n) { return scan16_bytes(n + 1) + 2 * size16_slot(n); }
+}  // namespace avdb
 
 extern "C" int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                        const uint32_t* end, const uint64_t* allele_off,
@@ -517,6 +548,21 @@ extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint
       return AVDB_ERANGE;
     }
     const unsigned grid = stream_grid(n, kBlock, 4096);
+    if (max_seq_len <= 60000 && AVDB_K7_SIZE16) {  // every key and path fits in u16
+      size_t tb = scan16_bytes(n + 1);
+      auto* ksz = reinterpret_cast<uint16_t*>(static_cast<char*>(workspace) + tb);
+      auto* psz = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(ksz) + size16_slot(n));
+      AVDB_HIP_TRY(hipMemsetAsync(ksz + n, 0, 2, s));
+      AVDB_HIP_TRY(hipMemsetAsync(psz + n, 0, 2, s));
+      A.key_sz = ksz;
+      A.path_sz = bin_code ? psz : nullptr;
+      hipLaunchKernelGGL(k_record_keys<false>, dim3(grid), dim3(kBlock), 0, s, A);
+      AVDB_LAUNCH_CHECK("k_record_keys<size>");
+      AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, Wide16It(ksz, Widen16()), ko, n + 1, s));
+      if (bin_code)
+        AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, Wide16It(psz, Widen16()), po, n + 1, s));
+      return AVDB_OK;
+    }
     hipLaunchKernelGGL(k_record_keys<false>, dim3(grid), dim3(kBlock), 0, s, A);
     AVDB_LAUNCH_CHECK("k_record_keys<size>");
     size_t tb = scan_bytes(n + 1);
