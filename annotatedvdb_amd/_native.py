@@ -64,6 +64,11 @@ class FormatOpts(ctypes.Structure):
                 ("flags", ctypes.c_uint32), ("match", ctypes.c_void_p), ("match_kind", ctypes.c_void_p),
                 ("frag", ctypes.c_void_p), ("frag_off", ctypes.c_void_p), ("adsp_dup", ctypes.c_void_p)]
 
+class LineResult(ctypes.Structure):
+    """avdb_line_result (include/avdb.h)."""
+    _fields_ = [(name, ctypes.c_uint32) for name in ("state", "flags", "copy_bytes", "map_bytes", "n_rec", "n_rows",
+                                                     "n_skip", "n_dup", "n_upd", "reserved")]
+
 # every symbol include/avdb.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED_SYMBOLS = [
     "avdb_abi_version", "avdb_last_error", "avdb_device_count",
@@ -74,12 +79,12 @@ EXPORTED_SYMBOLS = [
     "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest",
     "avdb_format_bin_path", "avdb_format_bin_paths",
     "avdb_vcf_workspace_size", "avdb_vcf_count_lines", "avdb_vcf_parse_lines", "avdb_vcf_emit",
-    "avdb_format_workspace_size", "avdb_vcf_format_size", "avdb_vcf_format_write",
+    "avdb_format_workspace_size", "avdb_vcf_format_size", "avdb_vcf_format_write", "avdb_vcf_line_host",
     "avdb_display_attributes",
     "avdb_keyset_workspace_size", "avdb_keyset_build", "avdb_keyset_probe",
     "avdb_primary_keys", "avdb_keyset_probe_text",
     "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
-    "avdb_small_prep", "avdb_host_alloc", "avdb_host_free",
+    "avdb_small_prep", "avdb_small_prep_host", "avdb_bin_path_host", "avdb_host_alloc", "avdb_host_free",
     "avdb_rccl_unique_id", "avdb_rccl_comm_init", "avdb_rccl_comm_destroy",
     "avdb_hist_allgather_workspace_size", "avdb_hist_allgather",
 ]
@@ -149,6 +154,8 @@ def _sig(lib):
                                        P, SZ, P, P, P, P]
     f.avdb_vcf_format_write.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, ctypes.POINTER(FormatOpts),
                                         P, P, P, P, P, P, P]
+    f.avdb_vcf_line_host.argtypes = [P, ctypes.c_char_p, SZ, ctypes.POINTER(FormatOpts), P, SZ, P, SZ,
+                                     ctypes.POINTER(LineResult)]
     f.avdb_display_attributes.argtypes = [P, P, P, P, P, P, P, P, SZ, SZ, P, SZ, P, P, P, P]
     f.avdb_keyset_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_build.argtypes = [P, P, P, SZ, P, SZ, P]
@@ -156,6 +163,8 @@ def _sig(lib):
     f.avdb_primary_keys.argtypes = [P, P, P, P, P, P, P, SZ, P, P, P, SZ, U32, P, SZ, P, P, P, SZ, P, SZ, P, P]
     f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]
     f.avdb_small_prep.argtypes = [P, ctypes.POINTER(SmallBatch), P]
+    f.avdb_small_prep_host.argtypes = [P, ctypes.POINTER(SmallBatch)]
+    f.avdb_bin_path_host.argtypes = [P, U8, U32, U32, ctypes.POINTER(U32), ctypes.POINTER(U8), P, SZ]
     f.avdb_host_alloc.argtypes = [SZ, ctypes.POINTER(P)]
     f.avdb_host_free.argtypes = [P]
     f.avdb_shard_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]

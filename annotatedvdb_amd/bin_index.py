@@ -14,6 +14,7 @@ L13 bins, :66-71) and ``TypeError`` for unmappable locations (``None[...]`` at
 from __future__ import annotations
 
 import sys
+from ctypes import string_at as ctypes_string_at
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -21,6 +22,8 @@ import numpy as np
 from .chromosomes import CHROM_NAMES, N_CHROM, UNKNOWN_CHROM, bin_index_chrom_code, length_table
 
 INC = [0] + [64000000 >> (lvl - 1) for lvl in range(1, 14)]
+_CODES = {}  # chromosome argument -> contig code (bin_index_chrom_code), memoised
+_LABELS = ["chr" + c for c in CHROM_NAMES]
 
 
 def bin_location(code: int, chrom_len: int) -> Tuple[int, int]:
@@ -31,6 +34,27 @@ def bin_location(code: int, chrom_len: int) -> Tuple[int, int]:
         return 0, chrom_len
     lo = g * INC[level]
     return lo, min(lo + INC[level], chrom_len)
+
+
+class _K1h:
+    """``avdb_bin_path_host`` with its ctypes arguments allocated once."""
+
+    def __init__(self, engine):
+        import ctypes
+        from . import _native as N
+        self.eng, self.N = engine, N
+        self.code, self.status = ctypes.c_uint32(), ctypes.c_uint8()
+        self._buf = ctypes.create_string_buffer(N.MAX_PATH)
+        self._args = (ctypes.byref(self.code), ctypes.byref(self.status), self._buf, N.MAX_PATH)
+        self._addr = ctypes.addressof(self._buf)
+        self._fn = engine.lib.avdb_bin_path_host
+
+    def path(self, chrom: int, start: int, end: int) -> Optional[str]:
+        k = self._fn(self.eng.ctx, chrom, start, end, *self._args)
+        if k <= 0:
+            self.N.check("avdb_bin_path_host", k)
+            return None
+        return ctypes_string_at(self._addr, k).decode("ascii")
 
 
 class BinIndex(object):
@@ -48,7 +72,7 @@ class BinIndex(object):
         else:
             self._engine = Engine(device, lengths=chromosome_lengths, assembly=assembly)
         self._lengths = self._engine.lengths
-        self._one = None
+        self._k1h = None
 
     # ---- reference API ----------------------------------------------------
     def close(self):
@@ -56,22 +80,30 @@ class BinIndex(object):
         self._currentBin = {}
 
     def _lookup_one(self, chrm: str, start: int, end: int) -> Optional[dict]:
-        """One K8 launch for one record (the reference's SQL round trip): the
-        record and its bin path travel through host-mapped memory, so a miss is
-        one launch + one stream sync."""
-        from . import _native as N
-        code = bin_index_chrom_code(chrm)
+        """The reference's SQL round trip for one record: K1h
+        (``avdb_bin_path_host``, K1's closed form in the library's host code) —
+        a miss costs one library call, not a GPU launch + stream sync."""
+        code = _CODES.get(chrm)
+        if code is None:
+            code = _CODES[chrm] = min(bin_index_chrom_code(chrm), 255)
         lo, hi = (start, end) if end >= start else (end, start)
-        if lo < 1 or hi >= 2 ** 32:  # outside any bin (and outside the kernels' u32 positions)
+        if lo < 1 or hi >= 4294967296:  # outside any bin (and outside the kernels' u32 positions)
             return None
-        res = self._engine.small().run([min(code, 255)], [int(start)], ends=[int(end)], want=N.SMALL_PATH)
-        bcode = int(res["code"][0])
-        if bcode == 0xFFFFFFFF:
+        k1h = self._k1h
+        if k1h is None:
+            k1h = self._k1h = _K1h(self._engine)
+        path = k1h.path(code, int(start), int(end))
+        if path is None:
             return None
-        lo, hi = bin_location(bcode, self._lengths[code])
+        bcode = k1h.code.value
         level = bcode >> 28
-        return {"chromosome": "chr" + CHROM_NAMES[code], "global_bin_path": res["path"][0],
-                "location": (lo, hi), "bin_level": 1 + 2 * level}
+        if level:
+            lo = (bcode & 0x0FFFFFFF) * INC[level]
+            hi = min(lo + INC[level], self._lengths[code])
+        else:
+            lo, hi = 0, self._lengths[code]
+        return {"chromosome": _LABELS[code], "global_bin_path": path, "location": (lo, hi),
+                "bin_level": 1 + 2 * level}
 
     def _update_current_bin_index(self, chrm, start, end):
         if self._verbose:

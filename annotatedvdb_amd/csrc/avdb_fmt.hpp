@@ -57,7 +57,7 @@ typedef __attribute__((address_space(1))) U64u* gw_u64u;
 constexpr int kFormatWaves = AVDB_K5_WAVES;
 
 // decimal digit count of v (compare chain: no division)
-__device__ __forceinline__ uint32_t ndigits(uint32_t v) {
+AVDB_HD uint32_t ndigits(uint32_t v) {
   return 1u + (v >= 10u) + (v >= 100u) + (v >= 1000u) + (v >= 10000u) + (v >= 100000u) +
          (v >= 1000000u) + (v >= 10000000u) + (v >= 100000000u) + (v >= 1000000000u);
 }
@@ -67,7 +67,7 @@ __device__ __forceinline__ uint32_t ndigits(uint32_t v) {
 // lanes, each split into 2-digit pairs (x/100 = x*5243 >> 19 for x < 10^4) in
 // 16-bit lanes, each into tens / ones (x/10 = x*103 >> 10 for x < 100) in bytes.
 // About 20 VALU instructions instead of a divide-by-10 loop per digit.
-__device__ __forceinline__ uint64_t ascii8(uint32_t v) {
+AVDB_HD uint64_t ascii8(uint32_t v) {
   const uint32_t a = v / 10000u, b = v - a * 10000u;
   uint64_t x = uint64_t(a) | (uint64_t(b) << 32);
   const uint64_t q = ((x * 5243ull) >> 19) & 0x0000007F0000007Full;
@@ -104,7 +104,7 @@ struct Dec {
   uint32_t n;
 };
 
-__device__ __forceinline__ Dec dec_text(uint32_t v) {
+AVDB_HD Dec dec_text(uint32_t v) {
   const uint32_t n = ndigits(v);
   if (n <= 8) return Dec{ascii8(v) >> (8 * (8 - n)), 0ull, n};
   const uint32_t hi = v / 100000000u;  // 1..42
@@ -129,6 +129,7 @@ struct LdsImage {};  // constructor tag of the LDS sink
 template <bool WRITE, bool LDS = false>
 struct Out {
   static constexpr bool kWrite = WRITE;
+  using Counter = Out<false>;  // a sink of the same family that only counts bytes
   gbyte* base;
   uint64_t p, lo;
   bool bad;  // set by a formatter that cannot render its input (line goes to the host)
@@ -281,6 +282,45 @@ struct Out {
   }
 };
 
+// The sink interface of Out<> over a host byte buffer, for the library's per-call
+// host entries (K8h avdb_small_prep_host, K5h avdb_vcf_line_host): the AVDB_HD
+// renderers below run unchanged into it.  base == nullptr counts bytes only.
+struct HostOut {
+  static constexpr bool kWrite = true;
+  using Counter = HostOut;
+  uint8_t* base;
+  uint64_t p, lo;
+  bool bad;
+  HostOut(uint8_t* b, uint64_t at) : base(b), p(at), lo(at), bad(false) {}
+  uint32_t size() const { return uint32_t(p - lo); }
+  void append(uint64_t x, uint32_t t) {
+    if (base)
+      for (uint32_t j = 0; j < t; ++j) base[p + j] = uint8_t(x >> (8 * j));
+    p += t;
+  }
+  void put(uint32_t c) { append(c & 0xFFu, 1); }
+  void finish() {}
+  void lit(const char* s) {
+    for (; *s; ++s) put(uint8_t(*s));
+  }
+  void bytes(const uint8_t* s, uint32_t n) {
+    if (base)
+      for (uint32_t j = 0; j < n; ++j) base[p + j] = s[j];
+    p += n;
+  }
+  void dec(const Dec& t) {
+    append(t.lo, t.n < 8 ? t.n : 8);
+    if (t.n > 8) append(t.hi, t.n - 8);
+  }
+  void u32v(uint32_t v) { dec(dec_text(v)); }
+  void u64v(uint64_t v) {
+    char t[20];
+    int k = 0;
+    do { t[k++] = char('0' + v % 10u); v /= 10u; } while (v);
+    while (k) put(uint8_t(t[--k]));
+  }
+};
+
 // ---------------------------------------------------------------------------
 // LDS-image spans (K7 keys / paths, K0 allele heap)
 // ---------------------------------------------------------------------------
@@ -339,7 +379,7 @@ __device__ __forceinline__ void flush_span(lds_u64* img, uint8_t* out, uint64_t 
 
 // contig label (Util/lib/python/enums/chromosomes.py:9-38 order)
 template <class O>
-__device__ __forceinline__ void chrom_name(O& o, uint32_t c) {
+AVDB_HD void chrom_name(O& o, uint32_t c) {
   if (c < 9) o.put('1' + c);
   else if (c < 22) o.append(uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8), 2);
   else if (c == 22) o.put('X');
@@ -390,7 +430,7 @@ struct LeafPath {
 };
 
 template <uint32_t L, uint32_t J>
-__device__ __forceinline__ uint64_t leaf_word(uint64_t label, uint32_t g) {  // word J of the path
+AVDB_HD uint64_t leaf_word(uint64_t label, uint32_t g) {  // word J of the path
   using P = LeafPath<L>;
   uint64_t w = P::word(J);
   if constexpr (J == 0) w |= label << 24;
@@ -404,7 +444,7 @@ __device__ __forceinline__ uint64_t leaf_word(uint64_t label, uint32_t g) {  // 
 // each word is built just before it is appended (one live word: the K5 write
 // pass runs at its register limit)
 template <uint32_t L, class O>
-__device__ __forceinline__ O leaf_path(O o, uint64_t label, uint32_t g) {
+AVDB_HD O leaf_path(O o, uint64_t label, uint32_t g) {
   o.append(leaf_word<L, 0>(label, g), 8);
   o.append(leaf_word<L, 1>(label, g), 8);
   o.append(leaf_word<L, 2>(label, g), 8);
@@ -420,7 +460,7 @@ __device__ __forceinline__ O leaf_path(O o, uint64_t label, uint32_t g) {
 }
 
 template <class O>
-__device__ __forceinline__ O bin_path(O o, uint32_t c, uint32_t code) {
+AVDB_HD O bin_path(O o, uint32_t c, uint32_t code) {
   const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
   if (AVDB_LEAF_PATH && level == 13 && c < 25 && (g >> 12) < 9) {
     if (c < 9) return leaf_path<1>(o, uint64_t('1' + c), g);
@@ -451,7 +491,7 @@ __device__ __forceinline__ O bin_path(O o, uint32_t c, uint32_t code) {
 // other bytes outside ' '..'~' as \u00XX (lowercase hex)
 // ---------------------------------------------------------------------------
 template <bool ESC, class O, class CP>
-__device__ __forceinline__ void jstr(O& o, CP s, uint32_t n) {
+AVDB_HD void jstr(O& o, CP s, uint32_t n) {
   if constexpr (!ESC) {
     o.bytes(s, n);
   } else {
@@ -488,14 +528,14 @@ struct Al {
 };
 
 template <bool ESC, class O, class CP>
-__device__ __forceinline__ void al_str(O& o, const Al<CP>& a) {
+AVDB_HD void al_str(O& o, const Al<CP>& a) {
   if (a.dash) o.put('-');
   else jstr<ESC>(o, a.p, a.n);
 }
 
 // truncate(s, cap) = s if len(s) <= cap else s[:cap] + '...' (variant_annotator.py:8-10)
 template <bool ESC, class O, class CP>
-__device__ __forceinline__ void al_trunc(O& o, const Al<CP>& a, uint32_t cap) {
+AVDB_HD void al_trunc(O& o, const Al<CP>& a, uint32_t cap) {
   if (a.dash) { o.put('-'); return; }
   jstr<ESC>(o, a.p, a.n < cap ? a.n : cap);
   if (a.n > cap) o.lit("...");
@@ -505,7 +545,7 @@ __device__ __forceinline__ void al_trunc(O& o, const Al<CP>& a, uint32_t cap) {
 // (variant_annotator.py:150-239).  Constant literals per case: a string chosen
 // at run time would be measured and copied a byte at a time from memory.
 template <class O>
-__device__ __forceinline__ void variant_class_text(O& o, int cls, bool dup) {
+AVDB_HD void variant_class_text(O& o, int cls, bool dup) {
   switch (cls) {
     case 0: o.lit(", \"variant_class\": \"single nucleotide variant\", \"variant_class_abbrev\": \"SNV\""); break;
     case 1: o.lit(", \"variant_class\": \"inversion\", \"variant_class_abbrev\": \"MNV\""); break;
@@ -529,7 +569,7 @@ __device__ __forceinline__ void variant_class_text(O& o, int cls, bool dup) {
 // chrom >= 25 writes no label in normalized_metaseq_id (the caller prepends it).
 // ---------------------------------------------------------------------------
 template <bool ESC, class O, class CP>
-__device__ __forceinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, CP ref, uint32_t r,
+AVDB_HD O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, CP ref, uint32_t r,
                                        CP alt, uint32_t a, Dec posd = Dec{0, 0, 0}) {
   const bool snv = r == 1u && a == 1u;
   uint32_t l = 0;  // common prefix (__normalize_alleles :100-107); SNVs untouched (:97-98)
@@ -625,7 +665,7 @@ __device__ __forceinline__ O display_json(O o, uint32_t chrom, uint32_t pos, uin
 // digits) returns false: the line is rendered by the host.
 // ---------------------------------------------------------------------------
 template <class CP>
-__device__ __forceinline__ bool number_plain(CP f, uint32_t n) {
+AVDB_HD bool number_plain(CP f, uint32_t n) {
   if (n == 0 || n > 40) return false;
   uint32_t dot = n, f0 = n, l0 = 0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -654,7 +694,7 @@ __device__ __forceinline__ bool number_plain(CP f, uint32_t n) {
 // n <= 16 text bytes at s as two registers (independent aligned word reads; the
 // words hold only bytes of the text's own window, bytes past n are 0)
 template <class CP>
-__device__ __forceinline__ void load16(CP s, uint32_t n, uint64_t* x0, uint64_t* x1) {
+AVDB_HD void load16(CP s, uint32_t n, uint64_t* x0, uint64_t* x1) {
   const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(s)) & 7u;
   const typename Word64<CP>::T w = reinterpret_cast<typename Word64<CP>::T>(s - mis);
   const uint32_t nw = (mis + n + 7) >> 3;
@@ -670,7 +710,7 @@ __device__ __forceinline__ void load16(CP s, uint32_t n, uint64_t* x0, uint64_t*
 
 // bytes [a, b) (b <= 16) of the register pair (x0, x1) to the sink
 template <class O>
-__device__ __forceinline__ void append_pair(O& o, uint64_t x0, uint64_t x1, uint32_t a, uint32_t b) {
+AVDB_HD void append_pair(O& o, uint64_t x0, uint64_t x1, uint32_t a, uint32_t b) {
   if (b <= a) return;
   const uint32_t n = b - a;
   uint64_t y0, y1;
@@ -682,15 +722,15 @@ __device__ __forceinline__ void append_pair(O& o, uint64_t x0, uint64_t x1, uint
 }
 
 // lowest / highest flagged byte index of a 16-byte mask pair (bit 7 per byte), 16 if none
-__device__ __forceinline__ uint32_t first_byte16(uint64_t m0, uint64_t m1) {
+AVDB_HD uint32_t first_byte16(uint64_t m0, uint64_t m1) {
   return m0 ? uint32_t(__builtin_ctzll(m0)) >> 3 : (m1 ? 8 + (uint32_t(__builtin_ctzll(m1)) >> 3) : 16u);
 }
-__device__ __forceinline__ uint32_t last_byte16(uint64_t m0, uint64_t m1) {
+AVDB_HD uint32_t last_byte16(uint64_t m0, uint64_t m1) {
   return m1 ? 15 - (uint32_t(__builtin_clzll(m1)) >> 3) : (m0 ? 7 - (uint32_t(__builtin_clzll(m0)) >> 3) : 16u);
 }
 
 template <class O, class CP>
-__device__ __forceinline__ O json_number(O o, CP f, uint32_t n) {
+AVDB_HD O json_number(O o, CP f, uint32_t n) {
   // SWAR form for fields of <= 16 bytes in fixed notation (repr's decimal
   // exponent -4..15): the canonical text is the integer digits without leading
   // zeros (or "0"), '.', the fraction without trailing zeros (or "0") — two byte
@@ -703,7 +743,7 @@ __device__ __forceinline__ O json_number(O o, CP f, uint32_t n) {
     const uint64_t m0 = low_bytes_mask(n < 8 ? n : 8) & kHiBits, m1 = (n > 8 ? low_bytes_mask(n - 8) : 0ull) & kHiBits;
     const uint64_t d0 = bytes_eq_mask(x0, '.') & m0, d1 = bytes_eq_mask(x1, '.') & m1;
     const uint64_t nd0 = nondigit_mask(x0) & m0 & ~d0, nd1 = nondigit_mask(x1) & m1 & ~d1;
-    const uint32_t ndots = uint32_t(__popcll(d0) + __popcll(d1));
+    const uint32_t ndots = uint32_t(__builtin_popcountll(d0) + __builtin_popcountll(d1));
     if (nd0 | nd1 || ndots > 1 || (ndots == 1 && n == 1)) {
       o.bad = true;
       return o;
@@ -791,7 +831,7 @@ __device__ __forceinline__ O json_number(O o, CP f, uint32_t n) {
 // ':' in an allele (the reference's metaseq split raises ValueError,
 // primary_key_generator.py:106) or a non-ASCII byte (outside the contract)
 template <class CP>
-__device__ __forceinline__ bool key_allele_ok(CP s, uint32_t n) {
+AVDB_HD bool key_allele_ok(CP s, uint32_t n) {
   return swar_find(s, n, [](uint64_t x) { return (x & kHiBits) | bytes_eq_mask(x, ':'); }) == n;
 }
 

@@ -10,6 +10,10 @@
 
 namespace avdb {
 
+// Record arithmetic shared by the kernels and the library's per-call host path
+// (avdb_small_prep_host): one definition, compiled for both sides.
+#define AVDB_HD __host__ __device__ __forceinline__
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
@@ -33,11 +37,11 @@ struct ChromTable {
 // smallest enclosing bin of the closed interval [lo, hi], 1 <= lo <= hi.
 // Level = largest l in 1..13 with (lo-1)/w_l == (hi-1)/w_l, w_l = 15625<<(13-l),
 // else 0 (whole chromosome) — BinIndexRef's nested (lo,hi] rows.
-__device__ __forceinline__ uint32_t bin_code_closed(uint32_t lo, uint32_t hi) {
+AVDB_HD uint32_t bin_code_closed(uint32_t lo, uint32_t hi) {
   const uint32_t qs = (lo - 1u) / kLeafWidth;   // magic-multiply, no divide
   const uint32_t qe = (hi - 1u) / kLeafWidth;
   const uint32_t x = qs ^ qe;
-  const int blen = x ? 32 - __clz(x) : 0;
+  const int blen = x ? 32 - __builtin_clz(x) : 0;
   const int level = blen <= 12 ? 13 - blen : 0;
   const uint32_t idx = level ? (qs >> (13 - level)) : 0u;
   return (uint32_t(level) << 28) | idx;
@@ -45,7 +49,7 @@ __device__ __forceinline__ uint32_t bin_code_closed(uint32_t lo, uint32_t hi) {
 
 // Full classification of one record against the staged length table.
 // Returns the status; writes code (AVDB_BIN_NONE when unmappable).
-__device__ __forceinline__ uint32_t classify(uint32_t c, uint32_t s, uint32_t e, int n_chrom,
+AVDB_HD uint32_t classify(uint32_t c, uint32_t s, uint32_t e, int n_chrom,
                                              const uint32_t* __restrict__ s_len, uint32_t* code) {
   if (c >= uint32_t(n_chrom)) { *code = AVDB_BIN_NONE; return AVDB_STATUS_UNKNOWN_CHROM; }
   uint32_t st = AVDB_STATUS_OK;
@@ -66,11 +70,11 @@ struct Heap {
   uintptr_t lo, hi;
 };
 
-__device__ __forceinline__ Heap make_heap(const uint8_t* p, size_t bytes) {
+AVDB_HD Heap make_heap(const uint8_t* p, size_t bytes) {
   return Heap{reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + bytes};
 }
 
-__device__ __forceinline__ uint64_t heap_word(uintptr_t a, const Heap& h) {  // a 8-aligned
+AVDB_HD uint64_t heap_word(uintptr_t a, const Heap& h) {  // a 8-aligned
   if (a >= h.lo && a + 8 <= h.hi) return *reinterpret_cast<const uint64_t*>(a);
   uint64_t v = 0;
   for (int k = 0; k < 8; ++k) {
@@ -88,9 +92,13 @@ struct __attribute__((packed)) U64u {
 typedef const __attribute__((address_space(1))) U64u* g_u64u;
 
 // little-endian 8 bytes starting at heap offset p (bytes past the heap read 0)
-__device__ __forceinline__ uint64_t heap_u64(const Heap& h, uint64_t p) {
+AVDB_HD uint64_t heap_u64(const Heap& h, uint64_t p) {
   const uintptr_t addr = h.lo + p;
+#if defined(__HIP_DEVICE_COMPILE__)
   if (addr + 8 <= h.hi) return reinterpret_cast<g_u64u>(addr)->v;
+#else
+  if (addr + 8 <= h.hi) return reinterpret_cast<const U64u*>(addr)->v;
+#endif
   // within 8 bytes of the heap end: aligned words, zero fill
   const uintptr_t a = addr & ~uintptr_t(7);
   const uint32_t sh = uint32_t(addr & 7) * 8;
@@ -100,12 +108,12 @@ __device__ __forceinline__ uint64_t heap_u64(const Heap& h, uint64_t p) {
   return (lo >> sh) | (hi << (64 - sh));
 }
 
-__device__ __forceinline__ uint64_t low_bytes_mask(uint32_t k) {  // k in 0..8
+AVDB_HD uint64_t low_bytes_mask(uint32_t k) {  // k in 0..8
   return k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1);
 }
 
 // byte-exact equality of L bytes at heap offsets p and q
-__device__ __forceinline__ bool heap_equal(const Heap& h, uint64_t p, uint64_t q, uint32_t L) {
+AVDB_HD bool heap_equal(const Heap& h, uint64_t p, uint64_t q, uint32_t L) {
   if (p == q) return true;
   for (uint32_t k = 0; k < L; k += 8) {
     const uint64_t m = low_bytes_mask(L - k);
@@ -120,7 +128,7 @@ __device__ __forceinline__ bool heap_equal(const Heap& h, uint64_t p, uint64_t q
 // of the XOR); the inversion test reverses 8-byte chunks with a byte swap.
 // wr / wa are the first 8 bytes of ref / alt, loaded by the caller ahead of
 // time; alleles of up to 8 bytes (the bulk) need no further heap reads.
-__device__ __forceinline__ uint32_t infer_end(const Heap& h, uint64_t off, uint32_t r, uint32_t a,
+AVDB_HD uint32_t infer_end(const Heap& h, uint64_t off, uint32_t r, uint32_t a,
                                               uint32_t pos, uint64_t wr, uint64_t wa,
                                               uint32_t* lcp_out) {
   if (r == 1u && a == 1u) { *lcp_out = 0; return pos; }        // SNV (:54-55)

@@ -55,7 +55,7 @@ struct FormatArgs {
 // metaseqId.split(':'), primary_key_generator.py:106)
 // (SWAR, 8 bytes per step: bytes >= 0x80, < 0x20, 0x7F and the four specials)
 template <class CP>
-__device__ __forceinline__ bool plain_allele(CP s, uint32_t n) {
+AVDB_HD bool plain_allele(CP s, uint32_t n) {
   return swar_find(s, n, [](uint64_t x) {
            const uint64_t lt20 = ~((x & 0x7F7F7F7F7F7F7F7Full) + 0x6060606060606060ull) & kHiBits;
            return (x & kHiBits) | lt20 | bytes_eq_mask(x, 0x7F) | bytes_eq_mask(x, '"') |
@@ -64,7 +64,7 @@ __device__ __forceinline__ bool plain_allele(CP s, uint32_t n) {
 }
 
 template <class CP>
-__device__ __forceinline__ bool bytes_eq(CP a, CP b, uint32_t n) {
+AVDB_HD bool bytes_eq(CP a, CP b, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)
     if (a[i] != b[i]) return false;
   return true;
@@ -72,7 +72,7 @@ __device__ __forceinline__ bool bytes_eq(CP a, CP b, uint32_t n) {
 
 // next separator at or after i in [i, e), or e
 template <class CP>
-__device__ __forceinline__ uint32_t find_byte(CP s, uint32_t i, uint32_t e, uint8_t c) {
+AVDB_HD uint32_t find_byte(CP s, uint32_t i, uint32_t e, uint8_t c) {
   if (i >= e) return i;
   return i + swar_find(s + i, e - i, [c](uint64_t x) { return bytes_eq_mask(x, c); });
 }
@@ -82,7 +82,7 @@ __device__ __forceinline__ uint32_t find_byte(CP s, uint32_t i, uint32_t e, uint
 // (the reference's dict comprehension keeps the last value at the first
 // position).
 template <class CP>
-__device__ bool freq_plain(CP s, uint32_t v0, uint32_t v1) {
+AVDB_HD bool freq_plain(CP s, uint32_t v0, uint32_t v1) {
   uint32_t np = 0;
   for (uint32_t p0 = v0; p0 <= v1; ++np) {
     const uint32_t p1 = find_byte(s, p0, v1, '|');
@@ -110,7 +110,7 @@ __device__ bool freq_plain(CP s, uint32_t v0, uint32_t v1) {
 // json.dumps text or NULL; false when the reference would raise or print a
 // number the GPU does not format
 template <class O, class CP>
-__device__ __forceinline__ O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint32_t k) {
+AVDB_HD O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint32_t k) {
   bool any = false;
   for (uint32_t p0 = v0; p0 <= v1;) {
     const uint32_t p1 = find_byte(s, p0, v1, '|');
@@ -146,7 +146,7 @@ __device__ __forceinline__ O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint
 }
 
 template <bool WRITE, class O, class CP>
-__device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, CP s, size_t li,
+AVDB_HD uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, CP s, size_t li,
                                O& oc, O& om, uint32_t* n_rows, uint32_t* n_skip,
                                uint32_t* n_dup, uint32_t* n_upd) {
   if (L.flags & AVDB_VCF_COMMENT) return kLineSkip;
@@ -316,7 +316,7 @@ __device__ __forceinline__ uint8_t format_line(const FormatArgs& A, const avdb_v
     } else {
       // no COPY row, but the reference would still have evaluated FREQ
       if (fq0 >= 0) {
-        if (freq_json(Out<false>(nullptr, 0), s, uint32_t(fq0), uint32_t(fq1), k).bad) return kLineHost;
+        if (freq_json(typename O::Counter(nullptr, 0), s, uint32_t(fq0), uint32_t(fq1), k).bad) return kLineHost;
       }
       ++dups;
     }

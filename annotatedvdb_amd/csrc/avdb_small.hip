@@ -164,29 +164,34 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_prep(SmallArgs A) {
 
 using namespace avdb;
 
-extern "C" int avdb_small_prep(avdb_ctx* ctx, const avdb_small_batch* b, void* stream) {
+static int check_small_batch(const char* fn, const void* ctx, const avdb_small_batch* b) {
   if (!ctx || !b || !b->chrom || !b->pos || !b->end_out || !b->code || !b->status || !b->off_out ||
       !b->overflow || (!b->end_in && !b->ref_len)) {
-    avdb_set_error("avdb_small_prep: null argument");
+    avdb_set_error("%s: null argument", fn);
     return AVDB_EINVAL;
   }
   if (b->ref_len && (!b->allele_off || !b->alt_len || !b->heap || !b->key_state || !b->disp_state)) {
-    avdb_set_error("avdb_small_prep: alleles need allele_off, alt_len, heap, key_state and disp_state");
+    avdb_set_error("%s: alleles need allele_off, alt_len, heap, key_state and disp_state", fn);
     return AVDB_EINVAL;
   }
   if ((b->want & (AVDB_SMALL_KEY | AVDB_SMALL_DISPLAY)) && !b->ref_len) {
-    avdb_set_error("avdb_small_prep: keys and display attributes need alleles");
+    avdb_set_error("%s: keys and display attributes need alleles", fn);
     return AVDB_EINVAL;
   }
   for (int k = 0; k < 3; ++k)
     if ((b->want & (1u << k)) && !b->text_out[k]) {
-      avdb_set_error("avdb_small_prep: text stream %d requested without a buffer", k);
+      avdb_set_error("%s: text stream %d requested without a buffer", fn, k);
       return AVDB_EINVAL;
     }
   if (b->n > AVDB_SMALL_MAX) {
-    avdb_set_error("avdb_small_prep: at most %d records", AVDB_SMALL_MAX);
+    avdb_set_error("%s: at most %d records", fn, AVDB_SMALL_MAX);
     return AVDB_EINVAL;
   }
+  return AVDB_OK;
+}
+
+extern "C" int avdb_small_prep(avdb_ctx* ctx, const avdb_small_batch* b, void* stream) {
+  if (int rc = check_small_batch("avdb_small_prep", ctx, b)) return rc;
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   SmallArgs A;
   memset(&A, 0, sizeof(A));
@@ -218,4 +223,133 @@ extern "C" int avdb_small_prep(avdb_ctx* ctx, const avdb_small_batch* b, void* s
   hipLaunchKernelGGL(k_small_prep, dim3(1), dim3(kSmallBlock), 0, static_cast<hipStream_t>(stream), A);
   AVDB_LAUNCH_CHECK("k_small_prep");
   return AVDB_OK;
+}
+
+// ---------------------------------------------------------------------------
+// K8h: the same per-record work for a call that arrives one record / one VCF
+// line at a time (BinIndex.find_bin_index, VCFVariantLoader.parse_variant —
+// the reference's own calling pattern, bin_index.py:59-75,
+// vcf_variant_loader.py:351-391).  A GPU launch plus a stream sync costs more
+// than the whole reference call (~1 us per record of arithmetic), so the
+// per-call entry runs the kernels' record arithmetic (infer_end, classify,
+// bin_path, display_json: the AVDB_HD definitions K2/K7/K8 compile) in the
+// library's host code.  Batches go to the kernels.
+// ---------------------------------------------------------------------------
+namespace {
+
+// ':' (the reference's metaseq split raises ValueError) or a non-ASCII byte
+inline bool host_key_allele_ok(const uint8_t* s, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if ((s[i] & 0x80u) || s[i] == ':') return false;
+  return true;
+}
+
+inline bool host_ascii(const uint8_t* s, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (s[i] & 0x80u) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int avdb_small_prep_host(const avdb_ctx* ctx, const avdb_small_batch* b) {
+  if (int rc = check_small_batch("avdb_small_prep_host", ctx, b)) return rc;
+  const uint32_t n = b->n;
+  const Heap hp = make_heap(b->heap, b->heap ? b->heap_bytes : 0);
+  uint32_t run[3] = {0, 0, 0};
+  uint32_t ov = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t c = b->chrom[i], p = b->pos[i];
+    uint32_t e, cd = AVDB_BIN_NONE, r = 0, a = 0;
+    uint64_t o = 0, x = 0;
+    uint8_t kst = AVDB_KEY_HOST, dst = 1;
+    bool fits = true;
+    if (b->ref_len) {
+      o = b->allele_off[i];
+      r = b->ref_len[i];
+      a = b->alt_len[i];
+      x = b->ext_id ? b->ext_id[i] : 0ull;
+      fits = o <= b->heap_bytes && uint64_t(r) + a <= b->heap_bytes - o;
+    }
+    if (b->end_in) {
+      e = b->end_in[i];
+    } else {
+      const bool snv = r == 1u && a == 1u;
+      uint32_t l;
+      e = infer_end(hp, o, r, a, p, snv ? 0 : heap_u64(hp, o), snv ? 0 : heap_u64(hp, o + r), &l);
+    }
+    const uint8_t st = uint8_t(classify(c, p, e, ctx->tab.n, ctx->tab.len, &cd));
+    b->end_out[i] = e;
+    b->code[i] = cd;
+    b->status[i] = st;
+    const uint8_t* ref = fits && b->heap ? b->heap + o : nullptr;
+    if (b->ref_len) {
+      const bool ascii = fits && host_ascii(ref, r + a);
+      dst = fits ? (ascii ? 0 : 1) : 2;
+      if (c >= 25 || (x >> 63) || !ascii) kst = AVDB_KEY_HOST;
+      else if (uint64_t(r) + a > b->max_seq_len) kst = AVDB_KEY_NEED_DIGEST;
+      else if (!host_key_allele_ok(ref, r + a)) kst = AVDB_KEY_HOST;
+      else kst = AVDB_KEY_OK;
+      b->key_state[i] = kst;
+      b->disp_state[i] = dst;
+    }
+    for (int sidx = 0; sidx < 3; ++sidx) {
+      if (!(b->want & (1u << sidx))) continue;
+      uint32_t* offs = b->off_out + size_t(sidx) * (n + 1);
+      offs[i] = run[sidx];
+      bool emit = true;
+      if (sidx == 0) emit = cd != AVDB_BIN_NONE && c < 25;
+      if (sidx == 1) emit = kst == AVDB_KEY_OK;
+      if (sidx == 2) emit = dst == 0;
+      if (!emit) continue;
+      auto render = [&](HostOut o_) -> HostOut {
+        if (sidx == 0) return bin_path(o_, c, cd);
+        if (sidx == 1) {
+          chrom_name(o_, c);
+          o_.put(':');
+          o_.u32v(p);
+          o_.put(':');
+          o_.bytes(ref, r);
+          o_.put(':');
+          o_.bytes(ref + r, a);
+          if (x) {
+            o_.lit(":rs");
+            o_.u64v(x);
+          }
+          return o_;
+        }
+        return display_json<true>(o_, c, p, e, ref, r, ref + r, a);
+      };
+      const uint32_t len = render(HostOut(nullptr, 0)).size();
+      if (uint64_t(run[sidx]) + len > b->text_cap[sidx]) ov |= 1u << sidx;
+      if (!(ov & (1u << sidx))) render(HostOut(b->text_out[sidx], run[sidx]));
+      run[sidx] += len;
+    }
+  }
+  for (int sidx = 0; sidx < 3; ++sidx)
+    if (b->want & (1u << sidx)) b->off_out[size_t(sidx) * (n + 1) + n] = run[sidx];
+  *b->overflow = ov;
+  return AVDB_OK;
+}
+
+// K1h: one interval's smallest enclosing bin and its ltree path on the host — a
+// BinIndex.find_bin_index cache miss (bin_index.py:43-56,75), the reference's
+// per-call SQL round trip.  classify + bin_path are K1/K7's AVDB_HD definitions.
+extern "C" int avdb_bin_path_host(const avdb_ctx* ctx, uint8_t chrom, uint32_t start, uint32_t end,
+                                  uint32_t* code, uint8_t* status, char* out, size_t cap) {
+  if (!ctx || !code || !status || (!out && cap)) {
+    avdb_set_error("avdb_bin_path_host: null argument");
+    return AVDB_EINVAL;
+  }
+  uint32_t cd;
+  *status = uint8_t(classify(chrom, start, end, ctx->tab.n, ctx->tab.len, &cd));
+  *code = cd;
+  if (cd == AVDB_BIN_NONE || chrom >= 25) return 0;
+  const uint32_t len = bin_path(HostOut(nullptr, 0), chrom, cd).size();
+  if (len > cap) {
+    avdb_set_error("avdb_bin_path_host: %u bytes needed", len);
+    return AVDB_ERANGE;
+  }
+  bin_path(HostOut(reinterpret_cast<uint8_t*>(out), 0), chrom, cd);
+  return int(len);
 }

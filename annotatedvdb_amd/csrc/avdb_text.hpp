@@ -6,7 +6,7 @@
 
 namespace avdb {
 
-__device__ __forceinline__ uint64_t zero_bytes_mask(uint64_t y) {  // bit 7 of each zero byte
+AVDB_HD uint64_t zero_bytes_mask(uint64_t y) {  // bit 7 of each zero byte
   const uint64_t lo7 = 0x7F7F7F7F7F7F7F7Full;
   return ~(((y & lo7) + lo7) | y | lo7);
 }
@@ -25,13 +25,14 @@ typedef const __attribute__((address_space(1))) uint64_t* glb_cp64;
 template <class CP> struct Word64;
 template <> struct Word64<lds_cp> { typedef lds_cp64 T; };
 template <> struct Word64<glb_cp> { typedef glb_cp64 T; };
+template <> struct Word64<const uint8_t*> { typedef const uint64_t* T; };  // host text (per-line entries)
 
 // SWAR scan of s[0, n) eight bytes at a time (aligned words: an aligned word
 // holding a byte of the text never leaves its LDS window / global page).  F maps a
 // word to a mask with bit 7 set in every flagged byte; returns the index of the
 // first flagged byte, or n.
 template <class CP, class F>
-__device__ __forceinline__ uint32_t swar_find(CP s, uint32_t n, F f) {
+AVDB_HD uint32_t swar_find(CP s, uint32_t n, F f) {
   if (n == 0) return 0;
   const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(s)) & 7u;
   const typename Word64<CP>::T w = reinterpret_cast<typename Word64<CP>::T>(s - mis);
@@ -47,7 +48,7 @@ __device__ __forceinline__ uint32_t swar_find(CP s, uint32_t n, F f) {
   return at >= total ? n : at - mis;
 }
 
-__device__ __forceinline__ uint64_t bytes_eq_mask(uint64_t x, uint8_t c) {
+AVDB_HD uint64_t bytes_eq_mask(uint64_t x, uint8_t c) {
   return zero_bytes_mask(x ^ (0x0101010101010101ull * c));
 }
 
@@ -55,16 +56,16 @@ __device__ __forceinline__ uint64_t bytes_eq_mask(uint64_t x, uint8_t c) {
 __device__ __forceinline__ uint64_t text_word(uintptr_t a, const Heap& h) { return heap_word(a, h); }
 
 // bit 7 set in every byte of x that is not an ASCII digit
-__device__ __forceinline__ uint64_t nondigit_mask(uint64_t x) {
+AVDB_HD uint64_t nondigit_mask(uint64_t x) {
   const uint64_t d = x ^ 0x3030303030303030ull;
   return (((d & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | d) & kHiBits;
 }
 
-__device__ __forceinline__ bool is_ws(uint8_t c) {
+AVDB_HD bool is_ws(uint8_t c) {
   return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
 }
-__device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
-__device__ __forceinline__ bool is_alnum(uint8_t c) {
+AVDB_HD bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+AVDB_HD bool is_alnum(uint8_t c) {
   return is_digit(c) || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z');
 }
 

@@ -1,0 +1,311 @@
+// K0's per-line VCF parse (VcfEntryParser, Util/lib/python/parsers/vcf_parser.py:
+// 76-169): one line's fields, contig code, POS, refSNP key, ALT and record counts.
+// Shared by the tokenizer kernel (avdb_vcf.hip, lines staged in LDS) and the
+// library's per-line host entry (avdb_line_host.hip): one definition, compiled
+// for both sides.
+#pragma once
+
+#include "avdb_text.hpp"
+
+namespace avdb {
+
+// contig code of a CHROM field (vcf_parser.py:133-150 + bin_index.py:64): plain
+// digits go through int(); 'MT' -> 'M'; every 'chr' removed in one left-to-right
+// pass (str.replace); then chr1..22, X, Y, M.  *host set for non-alphanumeric bytes.
+template <class CP>
+AVDB_HD uint8_t chrom_code_of(CP p, uint32_t n, bool* host) {
+  *host = false;
+  if (n == 0) return 255;
+  bool digits = true;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!is_alnum(p[i])) { *host = true; return 255; }
+    digits = digits && is_digit(p[i]);
+  }
+  if (digits) {
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      v = v * 10 + (p[i] - '0');
+      if (v > 1000) return 255;
+    }
+    return (v >= 1 && v <= 22) ? uint8_t(v - 1) : 255;
+  }
+  if (n == 2 && p[0] == 'M' && p[1] == 'T') return 24;
+  uint8_t lab[3];
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n;) {
+    if (i + 3 <= n && p[i] == 'c' && p[i + 1] == 'h' && p[i + 2] == 'r') { i += 3; continue; }
+    if (m == 3) return 255;
+    lab[m++] = p[i++];
+  }
+  if (m == 1) {
+    if (lab[0] >= '1' && lab[0] <= '9') return uint8_t(lab[0] - '1');
+    if (lab[0] == 'X') return 22;
+    if (lab[0] == 'Y') return 23;
+    if (lab[0] == 'M') return 24;
+    return 255;
+  }
+  if (m == 2 && is_digit(lab[0]) && is_digit(lab[1]) && lab[0] != '0') {
+    const uint32_t v = (lab[0] - '0') * 10 + (lab[1] - '0');
+    return (v >= 10 && v <= 22) ? uint8_t(v - 1) : 255;
+  }
+  return 255;
+}
+
+// canonical refSNP number of "rs<N>" bytes (N without leading zeros, < 10^18), else 0
+template <class CP>
+AVDB_HD uint64_t rs_number(CP p, uint32_t n) {
+  if (n < 3 || n > 20 || p[0] != 'r' || p[1] != 's' || p[2] == '0') return 0;
+  uint64_t v = 0;
+  for (uint32_t i = 2; i < n; ++i) {
+    if (!is_digit(p[i])) return 0;
+    v = v * 10 + (p[i] - '0');
+  }
+  return v;
+}
+
+// ---- SWAR field helpers: a field's bytes as two registers, read with
+// independent aligned word loads (the byte loops these replace waited on one
+// dependent LDS byte read per iteration) ----
+// 16 bytes of the line from line offset f (bytes at and past `len` read as 0)
+template <class WordAt>
+AVDB_HD void line16(const WordAt& word_at, uint32_t mis, uint32_t len, uint32_t f,
+                                       uint64_t* x0, uint64_t* x1) {
+  const uint32_t a = f + mis, k = a >> 3, sh = 8 * (a & 7);
+  const uint32_t kend = (len + mis + 7) >> 3;  // words holding line bytes
+  const uint64_t w0 = k < kend ? word_at(k) : 0ull;
+  const uint64_t w1 = k + 1 < kend ? word_at(k + 1) : 0ull;
+  const uint64_t w2 = k + 2 < kend ? word_at(k + 2) : 0ull;
+  uint64_t y0 = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  uint64_t y1 = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  // clip at the line end
+  const uint32_t n = len > f ? len - f : 0u;
+  if (n < 16) {
+    y1 &= n > 8 ? low_bytes_mask(n - 8) : 0ull;
+    y0 &= low_bytes_mask(n < 8 ? n : 8);
+  }
+  *x0 = y0;
+  *x1 = y1;
+}
+
+
+// up to 8 ASCII digits (most significant in the lowest byte, n of them) -> value
+AVDB_HD uint32_t digits8_value(uint64_t x, uint32_t n) {
+  if (n == 0) return 0;
+  uint64_t v = (x ^ 0x3030303030303030ull) << (8 * (8 - n));  // leading zero digits below
+  v = (v * 10 + (v >> 8)) & 0x00FF00FF00FF00FFull;
+  v = (v * 100 + (v >> 16)) & 0x0000FFFF0000FFFFull;
+  v = (v * 10000 + (v >> 32)) & 0xFFFFFFFFull;
+  return uint32_t(v);
+}
+
+// a decimal field of n <= 16 bytes in (x0, x1): *ok = all digits; value (64-bit)
+AVDB_HD uint64_t decimal16(uint64_t x0, uint64_t x1, uint32_t n, bool* ok) {
+  const uint64_t m0 = low_bytes_mask(n < 8 ? n : 8), m1 = n > 8 ? low_bytes_mask(n - 8) : 0ull;
+  *ok = n > 0 && !((nondigit_mask(x0) & m0) | (nondigit_mask(x1) & m1));
+  if (n <= 8) return digits8_value(x0 & m0, n);
+  // the first n - 8 digits, then 8 more
+  const uint32_t h = n - 8, sh = 8 * h;
+  const uint64_t hi = x0 & low_bytes_mask(h);
+  const uint64_t lo = sh < 64 ? (x0 >> sh) | (x1 << (64 - sh)) : x1;
+  return uint64_t(digits8_value(hi, h)) * 100000000ull + digits8_value(lo, 8);
+}
+
+constexpr uint64_t kTab = 0x0909090909090909ull;
+constexpr uint64_t kSemi = 0x3B3B3B3B3B3B3B3Bull;
+
+// one line: s points at its first byte (LDS or global), len = bytes up to its
+// newline; word_at/mis give the same bytes as aligned 8-byte words (SWAR scans)
+template <class CP, class WordAt>
+AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
+                                           uint32_t len, avdb_vcf_line& L, uint64_t& recs,
+                                           uint64_t& hbytes) {
+    while (len && is_ws(s[len - 1])) --len;  // str.rstrip()
+    L.len = len;
+    L.flags = 0;
+    L.pos = 0;
+    L.ext_id = 0;
+    L.n_alt = 0;
+    L.n_rec = 0;
+    L.chrom = 255;
+    L.pad[0] = L.pad[1] = L.pad[2] = 0;
+    uint32_t nf = 1;
+    L.field[0] = 0;
+    for (int k = 1; k < 8; ++k) L.field[k] = len + 1;
+    L.field_end8 = len;
+    if (len && s[0] == '#') L.flags |= AVDB_VCF_COMMENT;
+    if (!len) L.flags |= AVDB_VCF_EMPTY;
+    // tab-separated fields (first 8 starts; INFO ends at the 8th tab or the end)
+    {
+      const uint32_t k1 = (len + mis + 7) >> 3;
+      for (uint32_t k = 0; k < k1; ++k) {
+        uint64_t m = zero_bytes_mask(word_at(k) ^ kTab) & kHiBits;
+        if (k == 0) m &= ~low_bytes_mask(mis);
+        const uint32_t hi = len + mis - 8 * k;
+        if (hi < 8) m &= low_bytes_mask(hi);
+        if (nf > 8) {  // past INFO: only the count matters
+          nf += uint32_t(__builtin_popcountll(m));
+          continue;
+        }
+        while (m) {
+          const uint32_t i = 8 * k + (uint32_t(__builtin_ctzll(m)) >> 3) - mis;
+          m &= m - 1;
+#pragma unroll
+          for (int f = 1; f < 8; ++f)  // register-resident field table (no dynamic index)
+            if (nf == uint32_t(f)) L.field[f] = i + 1;
+          if (nf == 8) L.field_end8 = i;
+          ++nf;
+        }
+      }
+    }
+    L.n_fields = nf;
+    recs = 0;
+    hbytes = 0;
+    if (!(L.flags & (AVDB_VCF_COMMENT | AVDB_VCF_EMPTY))) {
+      if (nf < 8) L.flags |= AVDB_VCF_FEW_FIELDS;
+      const uint32_t nfields = nf < 8 ? nf : 8;
+      auto fend = [&](int k) -> uint32_t {  // end of field k (exclusive)
+        return (k + 1 < int(nfields)) ? L.field[k + 1] - 1 : (k == 7 ? L.field_end8 : len);
+      };
+      if (!(L.flags & AVDB_VCF_FEW_FIELDS)) {
+        // CHROM
+        bool host = false;
+        L.chrom = chrom_code_of(s, fend(0), &host);
+        if (host) L.flags |= AVDB_VCF_CHROM_HOST;
+        // POS: plain decimal < 2^32
+        {
+          const uint32_t n = fend(1) - L.field[1];
+          uint64_t x0, x1;
+          line16(word_at, mis, len, L.field[1], &x0, &x1);
+          bool ok = false;
+          const uint64_t v = n <= 10 ? decimal16(x0, x1, n, &ok) : 0ull;
+          if (ok && v <= 0xFFFFFFFFull) L.pos = uint32_t(v); else L.flags |= AVDB_VCF_BAD_POS;
+        }
+        // ID
+        const CP id = s + L.field[2];
+        const uint32_t idn = fend(2) - L.field[2];
+        // ID, 16 bytes at a time: digits / number-like bytes / an "rs" pair
+        bool has_rs = false;
+        {
+          bool numlike = idn > 0, has_digit = false;
+          uint64_t carry_r = 0;  // bit 7: the byte before this block is 'r'
+          for (uint32_t b = 0; b < idn; b += 16) {
+            uint64_t y[2];
+            line16(word_at, mis, len, L.field[2] + b, &y[0], &y[1]);
+            const uint32_t nb = idn - b < 16u ? idn - b : 16u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t nh = h ? (nb > 8 ? nb - 8 : 0u) : (nb < 8 ? nb : 8u);
+              const uint64_t m = low_bytes_mask(nh) & kHiBits;
+              const uint64_t x = y[h];
+              const uint64_t dig = ~nondigit_mask(x) & m;
+              has_digit = has_digit || dig;
+              const uint64_t numb = dig | bytes_eq_mask(x, '+') | bytes_eq_mask(x, '-') | bytes_eq_mask(x, '.') |
+                                    bytes_eq_mask(x, 'e') | bytes_eq_mask(x, 'E') | bytes_eq_mask(x, '_');
+              numlike = numlike && !((~numb) & m);
+              const uint64_t rm = bytes_eq_mask(x, 'r') & m, sm = bytes_eq_mask(x, 's') & m;
+              has_rs = has_rs || (((rm << 8) | carry_r) & sm);
+              carry_r = nh == 8 ? (rm >> 56) : 0ull;
+            }
+          }
+          if (numlike && has_digit) L.flags |= AVDB_VCF_ID_HOST;  // Python coerces it to a number
+        }
+        if ((idn == 1 && id[0] == '.') || (idn >= 2 && id[0] == 'r' && id[1] == 's'))
+          L.flags |= AVDB_VCF_ID_METASEQ;
+        if (has_rs) {
+          L.flags |= AVDB_VCF_ID_RS;
+          if (idn >= 3 && idn <= 18 && id[0] == 'r' && id[1] == 's' && id[2] != '0') {
+            uint64_t y0, y1;  // "rs" + up to 16 digits, SWAR
+            line16(word_at, mis, len, L.field[2] + 2, &y0, &y1);
+            bool ok;
+            const uint64_t v = decimal16(y0, y1, idn - 2, &ok);
+            L.ext_id = ok ? v : 0ull;
+          } else {
+            L.ext_id = rs_number(id, idn);
+          }
+          if (!L.ext_id) L.flags |= AVDB_VCF_EXT_HOST;
+        } else {
+          // INFO: last entry whose key is exactly "RS" (dict(...) keeps the last)
+          const CP inf = s + L.field[7];
+          const uint32_t f7 = L.field[7], e7 = fend(7);
+          int64_t vs = -1, ve = -1;
+          bool bare = false;
+          // entries are [i, j) between ';' (INFO-relative), scanned 8 bytes at a time
+          uint32_t i = 0;
+          const uint32_t in = e7 >= f7 ? e7 - f7 : 0;
+          for (uint32_t at = 0; at <= in;) {
+            // next ';' at or after `at` (SWAR), or the INFO end
+            uint32_t j = in;
+            {
+              const uint32_t from = f7 + at, to = e7;
+              const uint32_t k1 = (to + mis + 7) >> 3;
+              for (uint32_t k = (from + mis) >> 3; k < k1; ++k) {
+                uint64_t m = zero_bytes_mask(word_at(k) ^ kSemi) & kHiBits;
+                const int32_t lo = int32_t(from + mis) - int32_t(8 * k);
+                if (lo > 0) m &= ~low_bytes_mask(uint32_t(lo));
+                const uint32_t hi = to + mis - 8 * k;
+                if (hi < 8) m &= low_bytes_mask(hi);
+                if (m) {
+                  j = 8 * k + (uint32_t(__builtin_ctzll(m)) >> 3) - mis - f7;
+                  break;
+                }
+              }
+            }
+            if (j - i >= 2 && inf[i] == 'R' && inf[i + 1] == 'S') {
+              if (j - i == 2) { bare = true; vs = ve = -1; }
+              else if (inf[i + 2] == '=') { bare = false; vs = i + 3; ve = j; }
+            }
+            i = j + 1;
+            at = j + 1;
+          }
+          if (vs >= 0 || bare) {
+            L.flags |= AVDB_VCF_INFO_RS;
+            uint64_t v = 0;
+            bool ok = !bare && ve > vs && ve - vs <= 18;
+            for (int64_t i = vs; ok && i < ve; ++i) {
+              ok = is_digit(inf[i]);
+              v = v * 10 + (inf[i] - '0');
+            }
+            if (ok && v >= 1) L.ext_id = v;  // 'rs' + str(int(value))
+            else L.flags |= AVDB_VCF_EXT_HOST;
+          }
+        }
+        // REF / ALT
+        const uint32_t rlen = fend(3) - L.field[3];
+        const CP alt = s + L.field[4];
+        const uint32_t an = fend(4) - L.field[4];
+        // SWAR: commas and '.' bytes of the ALT field; without a '.', every ALT is a
+        // record and the counts follow from the comma count
+        uint32_t commas = 0;
+        bool dot = false;
+        for (uint32_t b = 0; b < an; b += 16) {
+          uint64_t y0, y1;
+          line16(word_at, mis, len, L.field[4] + b, &y0, &y1);
+          const uint32_t nb = an - b < 16u ? an - b : 16u;
+          const uint64_t m0 = low_bytes_mask(nb < 8 ? nb : 8) & kHiBits;
+          const uint64_t m1 = (nb > 8 ? low_bytes_mask(nb - 8) : 0ull) & kHiBits;
+          commas += uint32_t(__builtin_popcountll(bytes_eq_mask(y0, ',') & m0) + __builtin_popcountll(bytes_eq_mask(y1, ',') & m1));
+          dot = dot || ((bytes_eq_mask(y0, '.') & m0) | (bytes_eq_mask(y1, '.') & m1));
+        }
+        if (!dot) {
+          L.n_alt = commas + 1;
+          L.n_rec = L.n_alt;
+          hbytes = uint64_t(L.n_rec) * rlen + (an - commas);
+        }
+        uint32_t a0 = 0;
+        for (uint32_t i = 0; dot && i <= an; ++i) {
+          if (i == an || alt[i] == ',') {
+            const uint32_t al = i - a0;
+            ++L.n_alt;
+            if (!(al == 1 && alt[a0] == '.')) {
+              ++L.n_rec;
+              hbytes += rlen + al;
+            }
+            a0 = i + 1;
+          }
+        }
+        recs = L.n_rec;
+      }
+    }
+}
+
+}  // namespace avdb

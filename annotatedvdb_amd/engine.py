@@ -21,7 +21,9 @@ heap           uint8    concatenated raw REF+ALT bytes
 from __future__ import annotations
 
 import ctypes
+import os
 import re
+import struct
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -228,37 +230,53 @@ class SmallPrep:
     per-record / per-line drop-in path as one launch + one stream sync, no
     copies (the kernel reads the records and writes the results over PCIe).
     Batches that do not fit the arena return ``None`` (callers then use the
-    multi-kernel path)."""
+    multi-kernel path).
 
-    _IN = (("chrom", np.uint8), ("pos", np.uint32), ("end_in", np.uint32), ("allele_off", np.uint64),
-           ("ref_len", np.uint32), ("alt_len", np.uint32), ("ext_id", np.uint64), ("end_out", np.uint32),
-           ("code", np.uint32), ("status", np.uint8), ("key_state", np.uint8), ("disp_state", np.uint8))
+    A call of at most ``host_max`` records (one ``find_bin_index`` miss, one
+    ``parse_variant`` line) runs K8h instead, ``avdb_small_prep_host``: the
+    same record arithmetic compiled into the library's host code, over the same
+    arena.  A launch plus a stream sync costs ~25 us on MI355X, more than the
+    reference's whole per-line call; the kernels take every batch.
+    ``AVDB_PERCALL=gpu`` (or ``mode='gpu'``) sends every call to K8,
+    ``AVDB_PERCALL=host`` every call that fits to K8h."""
+
+    HOST_MAX = 32
 
     def __init__(self, engine: "Engine", max_records: int = 4096, heap_bytes: int = 1 << 20,
                  text_bytes: Tuple[int, int, int] = (1 << 19, 1 << 19, 1 << 21)):
         self.eng = engine
+        self.mode = os.environ.get("AVDB_PERCALL", "auto")  # auto | host | gpu
+        self.host_max = self.HOST_MAX
+        self.last_path = None  # "host" | "gpu": which entry served the last call
         self.R = int(max_records)
         self.H = int(heap_bytes)
         self.T = tuple(int(t) for t in text_bytes)
-        sizes = [(name, dt, self.R) for name, dt in self._IN] + [("heap", np.uint8, self.H),
-                                                               ("off_out", np.uint32, 3 * (self.R + 1)),
-                                                               ("overflow", np.uint32, 2)]
-        sizes += [("text%d" % k, np.uint8, self.T[k]) for k in range(3)]
+        # arena: the per-call SoA region (inputs then outputs of one call, packed
+        # per call size by _layout: <= 62 bytes per record), the allele heap and
+        # the three text streams
+        self.scratch = 64 * (self.R + 1)
+        regions = [("soa", self.scratch), ("heap", self.H)] + [("text%d" % k, self.T[k]) for k in range(3)]
         total = 0
-        layout = []
-        for name, dt, cnt in sizes:
-            total = (total + 15) & ~15
-            layout.append((name, dt, cnt, total))
-            total += np.dtype(dt).itemsize * cnt
-        p = ctypes.c_void_p()
-        N.check("avdb_host_alloc", engine.lib.avdb_host_alloc(total, ctypes.byref(p)))
-        self._ptr = p.value
-        self._buf = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(self._ptr))
-        self.a = {}
         self.addr = {}
-        for name, dt, cnt, off in layout:
-            self.a[name] = self._buf[off:off + np.dtype(dt).itemsize * cnt].view(dt)
+        offs = {}
+        for name, nbytes in regions:
+            total = (total + 63) & ~63
+            offs[name] = total
+            total += nbytes
+        self._ptr = self._alloc(total)
+        self._buf = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(self._ptr))
+        self._mv = memoryview(self._buf).cast("B")
+        self._layouts = {}
+        for name, off in offs.items():
             self.addr[name] = self._ptr + off
+        self._heap0 = offs["heap"]
+        self._text0 = [offs["text%d" % k] for k in range(3)]
+
+    def _alloc(self, total: int) -> int:
+        """The arena: pinned host memory mapped into the device (avdb_host_alloc)."""
+        p = ctypes.c_void_p()
+        N.check("avdb_host_alloc", self.eng.lib.avdb_host_alloc(total, ctypes.byref(p)))
+        return p.value
 
     def close(self):
         if getattr(self, "_ptr", None):
@@ -271,65 +289,165 @@ class SmallPrep:
         except Exception:
             pass
 
-    def run(self, chrom, pos, ends=None, refs: Optional[Sequence[bytes]] = None,
-            alts: Optional[Sequence[bytes]] = None, ext=None, want: int = 1, max_seq_len: int = 50):
-        """Returns a dict of numpy results (copies) or ``None`` when the batch does
-        not fit.  Text streams: ``path`` / ``key`` / ``display`` lists of str
-        (None where not rendered)."""
-        n = len(pos)
-        if n > self.R:
-            return None
-        a = self.a
-        a["chrom"][:n] = chrom
-        a["pos"][:n] = pos
-        b = N.SmallBatch()
-        b.chrom, b.pos = self.addr["chrom"], self.addr["pos"]
-        if refs is not None:
-            rl = np.fromiter((len(x) for x in refs), dtype=np.int64, count=n)
-            al = np.fromiter((len(x) for x in alts), dtype=np.int64, count=n)
-            tot = rl + al
-            hb = int(tot.sum())
-            if hb > self.H:
-                return None
-            off = np.zeros(n, dtype=np.int64)
-            if n:
-                np.cumsum(tot[:-1], out=off[1:])
-            heap = b"".join(r + x for r, x in zip(refs, alts))
-            a["heap"][:hb] = np.frombuffer(heap, dtype=np.uint8)
-            a["allele_off"][:n] = off
-            a["ref_len"][:n] = rl
-            a["alt_len"][:n] = al
-            b.allele_off, b.ref_len, b.alt_len, b.heap = (self.addr["allele_off"], self.addr["ref_len"],
-                                                          self.addr["alt_len"], self.addr["heap"])
-            b.heap_bytes = max(hb, 1)
-            b.key_state, b.disp_state = self.addr["key_state"], self.addr["disp_state"]
-            if ext is not None:
-                a["ext_id"][:n] = np.asarray(ext, dtype=np.uint64)
-                b.ext_id = self.addr["ext_id"]
+    def _layout(self, n: int, kind: int):
+        """Per-call layout for ``n`` records (cached): the arrays of one call
+        packed back to back at the start of the arena, a ``SmallBatch`` holding
+        their pointers, and one ``struct`` each for all inputs and all outputs.
+        kind: 0 intervals (end_in), 1 alleles, 2 alleles + ext_id."""
+        key = (n, kind)
+        lay = self._layouts.get(key)
+        if lay is not None:
+            return lay
+        fmt_in, fmt_out = ["<"], ["<"]
+        at = [0]
+        ptr = {}
+
+        def put(fmt, name, code, cnt, size):
+            pad = (-at[0]) % 8
+            if pad:
+                fmt.append("%dx" % pad)
+                at[0] += pad
+            ptr[name] = self._ptr + at[0]
+            fmt.append("%d%s" % (cnt, code))
+            at[0] += cnt * size
+        put(fmt_in, "chrom", "B", n, 1)
+        put(fmt_in, "pos", "I", n, 4)
+        if kind == 0:
+            put(fmt_in, "end_in", "I", n, 4)
         else:
-            a["end_in"][:n] = ends
-            b.end_in = self.addr["end_in"]
-        b.n, b.max_seq_len, b.want = n, int(max_seq_len), int(want)
-        b.end_out, b.code, b.status = self.addr["end_out"], self.addr["code"], self.addr["status"]
-        b.off_out, b.overflow = self.addr["off_out"], self.addr["overflow"]
+            put(fmt_in, "allele_off", "Q", n, 8)
+            put(fmt_in, "ref_len", "I", n, 4)
+            put(fmt_in, "alt_len", "I", n, 4)
+            if kind == 2:
+                put(fmt_in, "ext_id", "Q", n, 8)
+        in_bytes = at[0] = (at[0] + 15) & ~15
+        put(fmt_out, "end_out", "I", n, 4)
+        put(fmt_out, "code", "I", n, 4)
+        put(fmt_out, "status", "B", n, 1)
+        if kind:
+            put(fmt_out, "key_state", "B", n, 1)
+            put(fmt_out, "disp_state", "B", n, 1)
+        put(fmt_out, "off_out", "I", 3 * (n + 1), 4)
+        put(fmt_out, "overflow", "I", 2, 4)
+        if at[0] > self.scratch:
+            return None
+        b = N.SmallBatch()
+        for name in ("chrom", "pos", "end_in", "allele_off", "ref_len", "alt_len", "ext_id", "end_out", "code",
+                     "status", "key_state", "disp_state", "off_out", "overflow"):
+            if name in ptr:
+                setattr(b, name, ptr[name])
+        b.heap = self.addr["heap"]
         for k in range(3):
             b.text_out[k] = self.addr["text%d" % k]
             b.text_cap[k] = self.T[k]
-        N.check("avdb_small_prep", self.eng.lib.avdb_small_prep(self.eng.ctx, ctypes.byref(b), self.eng._stream()))
-        torch.cuda.current_stream(self.eng.device).synchronize()
-        if int(a["overflow"][0]) & want:
+        b.n = n
+        lay = (b, struct.Struct("".join(fmt_in)), struct.Struct("".join(fmt_out)), in_bytes)
+        self._layouts[key] = lay
+        return lay
+
+    def run(self, chrom, pos, ends=None, refs: Optional[Sequence[bytes]] = None,
+            alts: Optional[Sequence[bytes]] = None, ext=None, want: int = 1, max_seq_len: int = 50):
+        """Returns a dict of results (lists) or ``None`` when the batch does not
+        fit.  Text streams: ``path`` / ``key`` / ``display`` lists of str (None
+        where not rendered).  All inputs of a call go into the arena with one
+        ``struct.pack_into`` and all outputs come back with one ``unpack_from``
+        (plus the allele bytes and the texts): a call of a few records costs a
+        few microseconds of Python around the library call."""
+        n = len(pos)
+        if n > self.R:
             return None
-        out = {"end": a["end_out"][:n].copy(), "code": a["code"][:n].copy(), "status": a["status"][:n].copy()}
-        if refs is not None:
-            out["key_state"] = a["key_state"][:n].copy()
-            out["disp_state"] = a["disp_state"][:n].copy()
+        kind = 0 if refs is None else (2 if ext is not None else 1)
+        lay = self._layout(n, kind)
+        if lay is None:
+            return None
+        b, s_in, s_out, in_bytes = lay
+        mv = self._mv
+        if kind:
+            rl = [len(x) for x in refs]
+            al = [len(x) for x in alts]
+            heap = b"".join([r + x for r, x in zip(refs, alts)])
+            hb = len(heap)
+            if hb > self.H:
+                return None
+            offs = [0] * n
+            t = 0
+            for i in range(n):
+                offs[i] = t
+                t += rl[i] + al[i]
+            h0 = self._heap0
+            mv[h0:h0 + hb] = heap
+            b.heap_bytes = max(hb, 1)
+            if kind == 2:
+                s_in.pack_into(mv, 0, *chrom, *pos, *offs, *rl, *al, *ext)
+            else:
+                s_in.pack_into(mv, 0, *chrom, *pos, *offs, *rl, *al)
+        else:
+            s_in.pack_into(mv, 0, *chrom, *pos, *ends)
+        b.max_seq_len, b.want = int(max_seq_len), int(want)
+        on_host = self.mode == "host" or (self.mode == "auto" and n <= self.host_max)
+        if on_host:
+            N.check("avdb_small_prep_host", self.eng.lib.avdb_small_prep_host(self.eng.ctx, ctypes.byref(b)))
+        else:
+            N.check("avdb_small_prep", self.eng.lib.avdb_small_prep(self.eng.ctx, ctypes.byref(b),
+                                                                    self.eng._stream()))
+            torch.cuda.current_stream(self.eng.device).synchronize()
+        self.last_path = "host" if on_host else "gpu"
+        r = s_out.unpack_from(mv, in_bytes)
+        if r[-2] & want:  # overflow
+            return None
+        out = {"end": list(r[:n]), "code": list(r[n:2 * n]), "status": list(r[2 * n:3 * n])}
+        k0 = 3 * n
+        if kind:
+            out["key_state"] = list(r[k0:k0 + n])
+            out["disp_state"] = list(r[k0 + n:k0 + 2 * n])
+            k0 += 2 * n
         for k, name in enumerate(("path", "key", "display")):
             if not (want >> k) & 1:
                 continue
-            o = a["off_out"][k * (n + 1): k * (n + 1) + n + 1]
-            raw = a["text%d" % k][: int(o[n])].tobytes().decode("ascii")
+            o = r[k0 + k * (n + 1): k0 + (k + 1) * (n + 1)]
+            t0 = self._text0[k]
+            raw = bytes(mv[t0:t0 + o[n]]).decode("ascii")
             out[name] = [raw[o[i]:o[i + 1]] if o[i + 1] > o[i] else None for i in range(n)]
         return out
+
+
+class LineHost:
+    """K5h (``avdb_vcf_line_host``): one VCF line -> its COPY rows and .mapping
+    line, rendered by the library's host code with the kernels' own per-line
+    definitions (K0 parse_line, K2 infer_end/classify, K5 format_line).  The
+    loader's per-line ``parse_variant`` uses it: no GPU launch per line."""
+
+    def __init__(self, engine: "Engine", cap: int = 1 << 16):
+        self.eng = engine
+        self.res = N.LineResult()
+        self.opts = N.FormatOpts()
+        self.rendered = 0  # lines this entry rendered (the rest went to the caller)
+        self._grow(cap)
+
+    def _grow(self, cap: int):
+        self.cap = int(cap)
+        self._copy = ctypes.create_string_buffer(self.cap)
+        self._map = ctypes.create_string_buffer(self.cap)
+        self._ca, self._ma = ctypes.addressof(self._copy), ctypes.addressof(self._map)
+
+    def run(self, line: bytes, alg_id: bytes, max_seq_len: int = 50, adsp: bool = False):
+        """``(state, copy_text, mapping_text, result)``; the texts are None unless
+        state == LINE_GPU (rendered)."""
+        o = self.opts
+        o.alg_id, o.max_seq_len, o.flags = alg_id, max_seq_len, N.FORMAT_ADSP if adsp else 0
+        r = self.res
+        rc = self.eng.lib.avdb_vcf_line_host(self.eng.ctx, line, len(line), ctypes.byref(o), self._ca, self.cap,
+                                             self._ma, self.cap, ctypes.byref(r))
+        if rc == N.AVDB_ERANGE:
+            self._grow(2 * max(r.copy_bytes, r.map_bytes))
+            rc = self.eng.lib.avdb_vcf_line_host(self.eng.ctx, line, len(line), ctypes.byref(o), self._ca, self.cap,
+                                                 self._ma, self.cap, ctypes.byref(r))
+        N.check("avdb_vcf_line_host", rc)
+        if r.state != N.LINE_GPU:
+            return r.state, None, None, r
+        self.rendered += 1
+        return (r.state, ctypes.string_at(self._ca, r.copy_bytes).decode("ascii"),
+                ctypes.string_at(self._ma, r.map_bytes).decode("ascii"), r)
 
 
 # ---------------------------------------------------------------------------
@@ -388,6 +506,13 @@ class Engine:
         if sp is None:
             sp = self._small = SmallPrep(self)
         return sp
+
+    def line_host(self) -> LineHost:
+        """The engine's K5h per-line renderer (created on first use)."""
+        lh = getattr(self, "_line_host", None)
+        if lh is None:
+            lh = self._line_host = LineHost(self)
+        return lh
 
     def set_sequence_digests(self, digests: Sequence[str]):
         if len(digests) != len(self.lengths) or any(len(d) != N.DIGEST_CHARS for d in digests):

@@ -38,6 +38,7 @@ K5a (``avdb_display_attributes``); alleles must be ASCII (VCF 4.x REF/ALT).
 from __future__ import annotations
 
 import logging
+import re
 from io import StringIO
 from typing import Dict, List, Optional, Sequence
 
@@ -57,6 +58,12 @@ ALLOWABLE_COPY_FIELDS = ["chromosome", "record_primary_key", "position", "is_mul
 
 class _AltError(Exception):
     pass
+
+
+_SLOW = object()  # parse_variant: the line needs the general path
+_RS_NUM = re.compile(r"rs([1-9][0-9]{0,17})\Z")  # refSNP ids K8h renders (engine.ExtIdInterner)
+_KEY_OK = 0       # AVDB_KEY_OK
+_CHROM_CODES: Dict[str, int] = {}
 
 
 class VCFVariantLoader(object):
@@ -265,17 +272,139 @@ class VCFVariantLoader(object):
     def close(self):
         self.close_copy_buffer()
 
+    @property
+    def _current_variant(self):
+        v = self._cur_variant
+        if v.__class__ is _LineVariant:  # a K5h line: parsed on first use
+            v = self._cur_variant = v.resolve()
+        return v
+
+    @_current_variant.setter
+    def _current_variant(self, v):
+        self._cur_variant = v
+
     def get_current_variant(self, toStr=False):
         return str(self._current_variant) if toStr else self._current_variant
 
     def get_current_variant_id(self):
-        return self._current_variant.id if self._current_variant else None
+        v = self._cur_variant
+        if v.__class__ is _LineVariant:
+            return v.id
+        return v.id if v else None
 
     # ---- record prep ----------------------------------------------------------
     def parse_variant(self, line, flags=None):
         """One VCF line -> ``{variant.id: [{primary_key, bin_index}, ...]}``
-        (vcf_variant_loader.py:351-391)."""
+        (vcf_variant_loader.py:351-391).
+
+        The loader's per-line call (load_vcf_file.py:112) takes a lean path: the
+        host parse, ONE library call for all of the line's alts (K8h: end, bin,
+        key, ltree path, display JSON), the COPY rows.  A line that path does not
+        settle with certainty — a parse error, a key the PK generator must build
+        (long alleles, ':' in an allele, non-rs ids), an unmappable bin, a FREQ
+        the reference would fail on, resume/skip-existing/ADSP modes — goes
+        through ``parse_variants([line])``, which raises where the reference
+        raises (nothing is emitted before that decision)."""
+        if (flags is None and isinstance(line, str) and self._bin_indexer is not None
+                and self._pk_generator is not None and self._existing is None and not self.is_adsp()
+                and self._resume is True):
+            out = _SLOW
+            if self._chromosome_map is None and not self._vcf_header_fields:
+                out = self._parse_line_k5h(line)
+            if out is _SLOW:
+                out = self._parse_line_k8h(line)
+            if out is not _SLOW:
+                return out
         return self.parse_variants([line], flags)[0]
+
+    def _parse_line_k5h(self, line):
+        """The whole line in one library call (K5h, ``avdb_vcf_line_host``): COPY
+        rows and the .mapping line as the K5 kernels render them."""
+        try:
+            raw = line.encode("ascii")
+        except UnicodeEncodeError:
+            return _SLOW
+        st, copy, mp, r = self._engine.line_host().run(raw, _xstr(self._alg_invocation_id).encode(),
+                                                       self._pk_generator.max_sequence_length())
+        if copy is None:
+            return _SLOW
+        # .mapping line: id TAB [{'primary_key': '<pk>', 'bin_index': '<path>'}, ...] (keys and
+        # paths K5 renders hold no quote), i.e. str() of the list parse_variant returns
+        vid, rest = mp[:-1].split("\t", 1)
+        parts = rest.split("'")
+        self.increment_counter("line")
+        for _ in range(r.n_skip):
+            self.logger.warning("Skipping variant " + vid + "; no alt allele (alt = .)")
+        if r.n_skip:
+            self.increment_counter("skipped", r.n_skip)
+        self._copy_buffer.write(copy)
+        self.increment_counter("variant", r.n_rows)
+        self._current_variant = _LineVariant(line, vid, self)
+        return {vid: [{"primary_key": pk, "bin_index": p} for pk, p in zip(parts[3::8], parts[7::8])]}
+
+    def _parse_line_k8h(self, line):
+        """Host parse (chromosome map / custom header honoured) + one K8h call for
+        the line's alts (end, bin, key, path, display JSON)."""
+        try:
+            entry = VcfEntryParser(line, self._vcf_header_fields)
+            entry.update_chromosome(self._chromosome_map)
+            v = entry.get_variant(dbSNP=self.is_dbsnp(), namespace=True)
+        except Exception:  # noqa: BLE001 — parse_variants raises it with the reference's counters
+            return _SLOW
+        pos = v.position
+        ref = v.ref_allele
+        alts = [a for a in v.alt_alleles if a != "."]
+        rs = v.ref_snp_id
+        if rs is None:
+            ext = 0
+        else:
+            m = _RS_NUM.match(rs)
+            if m is None:
+                return _SLOW
+            ext = int(m.group(1))
+        chrom = _xstr(v.chromosome)
+        ps = _xstr(pos)
+        n = len(alts)
+        if n:
+            if not (0 < pos < 4294967296):
+                return _SLOW
+            code = _CHROM_CODES.get(chrom)
+            if code is None:
+                code = _CHROM_CODES[chrom] = min(bin_index_chrom_code(chrom), 255)
+            rb = ref.encode()
+            res = self._engine.small().run([code] * n, [pos] * n, refs=[rb] * n, alts=[a.encode() for a in alts],
+                                           ext=[ext] * n, want=7, max_seq_len=self._pk_generator.max_sequence_length())
+            if res is None:
+                return _SLOW
+            ks, paths, keys, disp, dst = res["key_state"], res["path"], res["key"], res["display"], res["disp_state"]
+            freqs = []
+            for i in range(n):
+                if ks[i] != _KEY_OK or paths[i] is None or dst[i] != 0:
+                    return _SLOW
+                try:
+                    freqs.append(_freq_str(entry, alts[i]))
+                except Exception:  # noqa: BLE001
+                    return _SLOW
+        # -- the line is settled: emit exactly as vcf_variant_loader.py:273-348 --
+        self.increment_counter("line")
+        self._current_variant = v
+        head = "chr" + chrom
+        tail = "#".join((_xstr(self._alg_invocation_id), _xstr(rs, nullStr="NULL"),
+                         "True" if v.is_multi_allelic else "NULL"))
+        mapping = []
+        i = 0
+        for alt in v.alt_alleles:
+            if alt == ".":
+                self.logger.warning("Skipping variant " + v.id + "; no alt allele (alt = .)")
+                self.increment_counter("skipped")
+                continue
+            pk, path = keys[i], paths[i]
+            self._copy_buffer.write("#".join((head, pk, ps, ":".join((chrom, ps, ref, alt)), path, tail, disp[i],
+                                              freqs[i])) + "\n")
+            self.increment_counter("variant")
+            mapping.append({"primary_key": pk, "bin_index": path})
+            i += 1
+        return {v.id: mapping}
 
     def parse_variants(self, lines: Sequence, flags=None, errors: str = "raise", dedup: bool = False,
                        keep_override=None):
@@ -858,6 +987,22 @@ class VCFVariantLoader(object):
                 continue
             out.append({v.id: mapping})
         return out
+
+class _LineVariant:
+    """The current variant of a line K5h rendered: its id is known, the
+    namespace (VcfEntryParser.get_variant) is built only if someone asks."""
+
+    __slots__ = ("line", "id", "loader")
+
+    def __init__(self, line, vid, loader):
+        self.line, self.id, self.loader = line, vid, loader
+
+    def resolve(self):
+        ld = self.loader
+        e = VcfEntryParser(self.line, ld._vcf_header_fields)
+        e.update_chromosome(ld._chromosome_map)
+        return e.get_variant(dbSNP=ld.is_dbsnp(), namespace=True)
+
 
 class _LazyEntry:
     """Stands in for a parsed VcfEntryParser when only INFO FREQ may be needed."""

@@ -11,13 +11,34 @@ delegated to the GPU-backed ``VariantAnnotator``.
 
 from __future__ import annotations
 
+import re
 from types import SimpleNamespace
 
 from .variant_annotator import VariantAnnotator
 
+# Every ASCII string int() or float() accepts matches this (a superset: the
+# characters of a number, or nan / inf / infinity, between str.isspace()
+# whitespace); a string that does not match is returned without trying either.
+_NUMISH = re.compile(r"[\s\x1c-\x1f+\-]*(?:[0-9_.eE+\-]+|nan|inf|infinity)[\s\x1c-\x1f]*", re.I)
+_NOT_INT = re.compile(r"[.eEnNiIaAfFtTyY]")  # int() accepts none of these
+
 
 def to_numeric(value):
-    """int, else float, else the value (GenomicsDBData ``to_numeric`` behaviour)."""
+    """int, else float, else the value (GenomicsDBData ``to_numeric`` behaviour).
+    ASCII strings take a fast path with the same result: plain digits go to
+    int(), text that cannot be a number is returned as is, and text int()
+    cannot accept goes straight to float() (the conversions that would raise
+    and be caught are skipped)."""
+    if value.__class__ is str and value.isascii():
+        if value.isdigit() and len(value) < 4000:
+            return int(value)
+        if _NUMISH.fullmatch(value) is None:
+            return value
+        if _NOT_INT.search(value) is not None:
+            try:
+                return float(value)
+            except (ValueError, TypeError):
+                return value
     try:
         return int(value)
     except (ValueError, TypeError):
@@ -39,6 +60,8 @@ def _xstr(v, nullStr="", falseAsNull=False):
     return str(v)
 
 
+_MISSING = object()
+
 DEFAULT_FIELDS = ["chrom", "pos", "id", "ref", "alt", "qual", "filter", "info"]
 
 
@@ -50,10 +73,13 @@ class _LazyInfo(object):
     def __init__(self, s: str):
         self.s = s
 
-    def resolve(self) -> dict:
+    def raw(self) -> dict:
+        """The INFO dict before numeric coercion (vcf_parser.py:101-108)."""
         infoStr = self.s.replace("\\x59", "/").replace("#", ":")
-        info = dict(item.split("=", 1) if "=" in item else [item, True] for item in infoStr.split(";"))
-        return convert_str2numeric_values(info)
+        return dict(item.split("=", 1) if "=" in item else [item, True] for item in infoStr.split(";"))
+
+    def resolve(self) -> dict:
+        return convert_str2numeric_values(self.raw())
 
 
 class VcfEntryParser(object):
@@ -66,6 +92,7 @@ class VcfEntryParser(object):
         self._header_fields = ["chrom", "pos", "id", "ref", "alt"] if identityOnly \
             else DEFAULT_FIELDS if headerFields is None \
             else [x.lower().replace("#", "") for x in headerFields]
+        self.__raw_info = None
         self.__entry = None if entry is None else self.parse_entry(entry)
 
     def parse_entry(self, inputStr):
@@ -121,9 +148,22 @@ class VcfEntryParser(object):
         self.__verify_entry()
         if "rs" in self.__entry["id"]:
             return self.__entry["id"]
-        if "info" in self.__entry and "RS" in self._info():
-            return "rs" + str(self._info()["RS"])
+        if "info" in self.__entry:
+            rs = self._info_value("RS")
+            if rs is not _MISSING:
+                return "rs" + str(rs)
         return None
+
+    def _info_value(self, key):
+        """One coerced INFO value (or _MISSING) without coercing the whole dict."""
+        info = self.__entry["info"]
+        if isinstance(info, _LazyInfo):
+            raw = self.__raw_info
+            if raw is None:
+                raw = self.__raw_info = info.raw()
+            v = raw.get(key, _MISSING)
+            return to_numeric(v) if v.__class__ is str else v
+        return info.get(key, _MISSING)
 
     def _info(self) -> dict:
         info = self.__entry["info"]
@@ -151,10 +191,8 @@ class VcfEntryParser(object):
         self.__verify_entry()
         if "info" not in self.__entry:
             return None
-        info = self._info()
-        if key in info:
-            return info[key]
-        return default
+        v = self._info_value(key)
+        return default if v is _MISSING else v
 
     def get_frequencies(self, allele):
         """vcf_parser.py:195-222 (INFO FREQ)."""

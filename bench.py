@@ -309,15 +309,47 @@ def dropin(a):
     res["load_vcf_text_per_line_us"] = per_call(lambda xs: ld.load_vcf_text(text if len(xs) > 20 else
                                                                             ("\n".join(xs) + "\n").encode()),
                                                 lines, reps=3)
+    res["per_line_path"] = {"k5h_rendered_lines": ld._engine.line_host().rendered,
+                            "note": "parse_variant: K5h (avdb_vcf_line_host, the kernels' per-line code in the "
+                                    "library's host code) for the lines it renders, else the general path; "
+                                    "find_bin_index misses: K8h (avdb_small_prep_host)"}
+    # the same calls through the reference-structured port on this host, same process,
+    # same inputs (oracle.load_line: VcfEntryParser-style parse, per-alt VariantAnnotator-
+    # style normalize + end, PortBinIndex with the reference's one-bin L13 cache and a
+    # BinIndexRef table search on a miss, primary key, FREQ + display attributes, COPY
+    # row and .mapping line; 0.82x the verbatim reference's per-line time in the build
+    # container, tools/calibrate_cpu_baseline.py)
+    from oracle import avdb_oracle as O
+    from annotatedvdb_amd.chromosomes import length_table
+    lens = length_table()
+    pbi = O.PortBinIndex(O.BinTable(GRCH38_LENGTHS))
+    base = {"parse_variant_per_line_us": per_call(lambda xs: [O.load_line(x, lens, bin_index=pbi) for x in xs],
+                                                  lines)}
+    pbi = O.PortBinIndex(O.BinTable(GRCH38_LENGTHS))
+    base["find_bin_index_sorted_us"] = per_call(lambda xs: [pbi.find_bin_index("chr22", p, p) for p in xs], pos)
+    pbi = O.PortBinIndex(O.BinTable(GRCH38_LENGTHS))
+    base["find_bin_index_miss_us"] = per_call(lambda xs: [pbi.find_bin_index("chr22", s, e) for s, e in xs],
+                                              spans)
+    try:
+        host_cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        host_cores = os.cpu_count() or 1
+    cpu = {"value": base["parse_variant_per_line_us"], "unit": "us/line", "cores": 1, "workers": 1,
+           "host_cores_visible": host_cores, "kind": "port", "per_call": base,
+           "sample": "the same 3,000 dbSNP-shaped lines, 200,000 sorted chr22 positions and 3,000 > 15.6 kb spans, "
+                     "one process on this host, per call as the reference's loader calls it (single-threaded per "
+                     "process, load_vcf_file.py:307-313); the miss cost excludes the Postgres round trip the "
+                     "reference pays (no database here)"}
     res["reference_build_container"] = {"parse_variant_per_line_us": 94.0, "find_bin_index_hit_us": 0.81,
                                         "find_bin_index_miss_us_fake_db": 8.2,
                                         "source": "SURVEY.md 6 / tools/calibrate_cpu_baseline.py (verbatim "
-                                                  "reference with an in-process table-search DB: a real "
-                                                  "Postgres round trip per miss costs more)"}
+                                                  "reference with an in-process table-search DB, build container)"}
+    res["vs_cpu_baseline"] = {k: base[k] / res[k] for k in ("parse_variant_per_line_us", "find_bin_index_sorted_us",
+                                                             "find_bin_index_miss_us")}
     out = {"metric": "drop-in per-call latency (find_bin_index, parse_variant)", "value":
            res["parse_variant_per_line_us"], "unit": "us/line", "n_gpus": 1, "higher_is_better": False,
            "dtype": "u8", "data": "synthetic C1 records / dbSNP-shaped VCF lines", "config":
-           {"workload": WORKLOADS["dropin"]["desc"]}, "latency": res}
+           {"workload": WORKLOADS["dropin"]["desc"]}, "latency": res, "cpu_baseline": cpu}
     print(json.dumps(out), flush=True)
 
 

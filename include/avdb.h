@@ -277,6 +277,32 @@ int avdb_vcf_format_write(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes,
                           const uint8_t* keep, const avdb_format_opts* opts, const uint64_t* copy_off,
                           const uint64_t* map_off, const uint8_t* line_state, uint8_t* copy_out,
                           uint8_t* map_out, uint64_t* counters, void* stream);
+/* K5h: ONE line of VCF text (host memory, no newline needed) -> its COPY rows and
+ * .mapping line, rendered by the library's host code with the kernels' own
+ * per-line definitions (K0 parse_line, K2 infer_end/classify, K5 format_line).
+ * The per-line call of the reference's loader (VCFVariantLoader.parse_variant,
+ * vcf_variant_loader.py:351-391, called per line by load_vcf_file.py:112) pays no
+ * GPU launch + sync this way.  res->state: AVDB_LINE_GPU = rendered (the same
+ * bytes the K5 kernels write for this line), AVDB_LINE_HOST = the caller renders
+ * it (same rules as K5: non-canonical text, long alleles, unmappable records, ...),
+ * AVDB_LINE_SKIP = comment.  opts: alg_id, max_seq_len, flags (AVDB_FORMAT_ADSP);
+ * match / adsp_dup must be NULL (batch features).  Returns AVDB_ERANGE when a
+ * buffer is short (res holds the sizes).  A context made with device = -1
+ * suffices; thread-safe per calling thread. */
+typedef struct avdb_line_result {
+  uint32_t state;
+  uint32_t flags;        /* K0 AVDB_VCF_* flags of the line */
+  uint32_t copy_bytes;   /* COPY rows written (each ends with '\n') */
+  uint32_t map_bytes;    /* .mapping line written: id '\t' [ {...}, ... ] '\n' */
+  uint32_t n_rec;        /* records (ALT != '.') */
+  uint32_t n_rows;       /* COPY rows */
+  uint32_t n_skip;       /* ALT '.' skipped */
+  uint32_t n_dup;
+  uint32_t n_upd;
+  uint32_t reserved;
+} avdb_line_result;
+int avdb_vcf_line_host(const avdb_ctx* ctx, const char* line, size_t len, const avdb_format_opts* opts,
+                       char* copy_out, size_t copy_cap, char* map_out, size_t map_cap, avdb_line_result* res);
 /* get_display_attributes (variant_annotator.py:134-241) of a record batch as
  * json.dumps text (ASCII alleles; json escaping applied).  end = K2's end.
  * Call with out == NULL first: rec_state[i] (0 ok, 1 non-ASCII allele, 2 heap
@@ -357,6 +383,22 @@ typedef struct avdb_small_batch {
   uint32_t* overflow;
 } avdb_small_batch;
 int avdb_small_prep(avdb_ctx* ctx, const avdb_small_batch* batch, void* stream);
+/* K8h: the same outputs computed by the library's host code from the kernels'
+ * own record arithmetic (infer_end / classify / bin_path / display_json are
+ * compiled for both sides), for callers that arrive one record or one VCF line
+ * at a time — BinIndex.find_bin_index (bin_index.py:59-75) and
+ * VCFVariantLoader.parse_variant (vcf_variant_loader.py:351-391) — where a GPU
+ * launch + stream sync would cost more than the reference's whole call.  All
+ * arrays are host memory; no stream, no device.  A context made with
+ * device = -1 suffices. */
+int avdb_small_prep_host(const avdb_ctx* ctx, const avdb_small_batch* batch);
+/* K1h: the bin code, status and ltree path of ONE interval [start, end] (end >=
+ * start; swapped intervals get status END_BEFORE_START as in K1) on the host —
+ * one BinIndex.find_bin_index cache miss (bin_index.py:43-56,75).  Returns the
+ * path length written to out (host, no NUL), 0 when unmappable (code ==
+ * AVDB_BIN_NONE, or a contig beyond the labelled 25), or AVDB_ERANGE. */
+int avdb_bin_path_host(const avdb_ctx* ctx, uint8_t chrom, uint32_t start, uint32_t end, uint32_t* code,
+                       uint8_t* status, char* out_host, size_t cap);
 /* Pinned host memory mapped into the device address space (hipHostMalloc,
  * mapped + coherent): the same pointer is valid on the host and in kernels. */
 int avdb_host_alloc(size_t bytes, void** ptr);

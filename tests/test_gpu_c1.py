@@ -169,11 +169,24 @@ def test_k7_states_and_edge_records(engine):
     assert int(kt0.key_off[0]) == 0
 
 
-def test_k8_small_batch_equals_multi_kernel_path(engine):
-    """K8 (one launch, host-mapped memory: the per-line drop-in path) gives the
-    same end / bin / status, key text, ltree path and display-attribute JSON as
-    K2 + K7 + K5a on the same records, across allele classes and edge records."""
+@pytest.mark.parametrize("mode", ["gpu", "host"])
+def test_k8_small_batch_equals_multi_kernel_path(engine, mode):
+    """K8 (one launch, host-mapped memory) and K8h (the same record arithmetic in
+    the library's host code: the per-call drop-in path) give the same end / bin /
+    status, key text, ltree path and display-attribute JSON as K2 + K7 + K5a on
+    the same records, across allele classes and edge records."""
     from annotatedvdb_amd import _native as N
+    sp = engine.small()
+    old_mode = sp.mode
+    sp.mode = mode
+    try:
+        _k8_vs_kernels(engine, N, sp)
+        assert sp.last_path == mode
+    finally:
+        sp.mode = old_mode
+
+
+def _k8_vs_kernels(engine, N, sp):
     from annotatedvdb_amd import synth
     from annotatedvdb_amd.engine import pack_records
     b = synth.alleles(3000, seed=81, long_frac=0.05)
@@ -188,7 +201,7 @@ def test_k8_small_batch_equals_multi_kernel_path(engine):
     refs += [e[2] for e in extra]
     alts += [e[3] for e in extra]
     ext = [int(x) for x in h["ext_id"]] + [e[4] for e in extra]
-    res = engine.small().run(chrom, pos, refs=refs, alts=alts, ext=ext,
+    res = sp.run(chrom, pos, refs=refs, alts=alts, ext=ext,
                              want=N.SMALL_PATH | N.SMALL_KEY | N.SMALL_DISPLAY)
     assert res is not None
     db = pack_records(chrom, pos, refs, alts, ext).to("cuda")
@@ -210,7 +223,7 @@ def test_k8_small_batch_equals_multi_kernel_path(engine):
     exp_disp = [raw[o[i]:o[i + 1]] if st[i] == 0 else None for i in range(db.n)]
     assert res["display"] == exp_disp
     # bins of explicit intervals (the find_bin_index miss path)
-    r2 = engine.small().run([0, 0, 21, 99], [15625, 1, 50818468, 5], ends=[15626, 248956422, 50818469, 5],
+    r2 = sp.run([0, 0, 21, 99], [15625, 1, 50818468, 5], ends=[15626, 248956422, 50818469, 5],
                             want=N.SMALL_PATH)
     assert r2["path"][0] == O.format_bin_path("1", int(r2["code"][0])) and r2["path"][1] == "chr1"
     assert r2["path"][2] is None and r2["path"][3] is None

@@ -203,3 +203,37 @@ def test_k5b_bench_size_properties(engine):
         assert err is None
         assert copy[co[li]:co[li + 1]].tobytes().decode() == "".join(x + "\n" for x in c)
         assert mapping[mo[li]:mo[li + 1]].tobytes().decode() == "".join(x + "\n" for x in m)
+
+
+def test_parse_variant_per_line_vs_reference_load_driver(engine, loader):
+    """The loader's per-line call (load_vcf_file.py:112 -> parse_variant) over every
+    line of the reference load-driver fixture: COPY rows (all columns), the
+    .mapping line the driver prints, and the exception type of every line the
+    reference raised on.  Most lines are rendered by K5h (one library call per
+    line, no GPU launch); the rest by the general path — same bytes either way."""
+    rows = load_rows()
+    lh = engine.line_host()
+    loader.reset_copy_buffer()
+    got_map, n_err = [], 0
+    for raw, err, mapping, copy in rows:
+        before = loader.copy_buffer().tell()
+        try:
+            out = loader.parse_variant(raw)
+        except Exception as e:  # noqa: BLE001
+            assert err is not None and type(e).__name__ == err, (raw, e)
+            n_err += 1
+            continue
+        assert err is None, raw
+        got_map += ["%s\t%s" % kv for kv in out.items()]
+        assert loader.get_current_variant_id() == next(iter(out))
+    exp_copy = [c for r in rows for c in r[3]]
+    assert loader.copy_buffer().getvalue().splitlines() == exp_copy
+    assert got_map == [m for r in rows if r[1] is None for m in r[2]]
+    assert loader.get_count("line") == len(rows)
+    assert loader.get_count("variant") == len(exp_copy)
+    assert lh.rendered > 0.6 * len(rows), lh.rendered
+    # the lazily built current variant equals the parser's
+    from annotatedvdb_amd.parsers import VcfEntryParser
+    last_ok = [r for r in rows if r[1] is None][-1][0]
+    loader.parse_variant(last_ok)
+    assert loader.get_current_variant() == VcfEntryParser(last_ok).get_variant(dbSNP=True, namespace=True)
