@@ -54,7 +54,8 @@ CTR_ADSP_UPDATES = 29
 FORMAT_ADSP = 1
 MATCH_NONE, MATCH_EXACT, MATCH_SWITCHED, MATCH_HOST = 0, 1, 2, 255
 LINE_GPU, LINE_HOST, LINE_SKIP = 0, 1, 2
-KEY_OK, KEY_HOST, KEY_NEED_DIGEST = 0, 1, 2
+KEY_OK, KEY_HOST, KEY_NEED_DIGEST, KEY_OVERFLOW = 0, 1, 2, 3
+PATH_OVERFLOW = 0x10
 MAX_ALG_ID = 64
 
 

@@ -365,7 +365,9 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       };
       const uint64_t ko = PF ? cur.ko : 0ull, ko1 = PF ? next_of(cur.ko, gk1) : 0ull;
       const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap && !(AVDB_K7_EXP & 16);
-      if (live && st == AVDB_KEY_OK && (PF ? ko1 : A.key_off[i + 1]) <= A.key_cap) {  // (cap: never write past the buffer)
+      if (live && st == AVDB_KEY_OK && (PF ? ko1 : A.key_off[i + 1]) > A.key_cap)
+        st = AVDB_KEY_OVERFLOW;  // never write past the buffer; say so in the state
+      if (live && st == AVDB_KEY_OK) {
         const uint64_t at = PF ? ko : A.key_off[i];
         if (kst) {
           Out<true, true> o(LdsImage{}, kimg, at - (gk0 & ~uint64_t(15)));
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
         }
       }
       // stream 1: ltree paths
-      bool pst = false;
+      bool pst = false, path_over = false;
       uint64_t gp0 = 0, gp1 = 0;
       if (A.code) {
         gp0 = A.path_off[t0];
@@ -384,7 +386,9 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
         pst = gp1 - (gp0 & ~uint64_t(15)) + 16 <= kPathWave && gp1 <= A.path_cap && !(AVDB_K7_EXP & 32);
         const uint32_t cd = live ? (PF ? cur.cd : A.code[i]) : AVDB_BIN_NONE;
         const uint64_t po1 = PF ? next_of(cur.po, gp1) : 0ull;
-        if (live && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom) && (PF ? po1 : A.path_off[i + 1]) <= A.path_cap) {
+        const bool has_path = live && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom);
+        path_over = has_path && (PF ? po1 : A.path_off[i + 1]) > A.path_cap;
+        if (has_path && !path_over) {
           const uint64_t at = PF ? cur.po : A.path_off[i];
           if (pst) {
             Out<true, true> o(LdsImage{}, pimg, at - (gp0 & ~uint64_t(15)));
@@ -395,7 +399,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
           }
         }
       }
-      if (live) A.state[i] = st;
+      if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
       wave_lds_sync();
       if (kst) flush_span(kimg, A.key_out, gk0, gk1, lane, kWave);
       if (pst) flush_span(pimg, A.path_out, gp0, gp1, lane, kWave);

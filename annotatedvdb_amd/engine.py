@@ -212,10 +212,14 @@ class KeyText:
     paths: Optional[torch.Tensor]
 
     def host(self, n: int):
-        """(keys, paths) as Python lists of str (None where not rendered)."""
+        """(keys, paths) as Python lists of str (None where not rendered).
+        Raises ``ValueError`` if a text did not fit its buffer (a reused
+        ``KeyText`` too small for this batch: state KEY_OVERFLOW / PATH_OVERFLOW)."""
         ko = self.key_off[: n + 1].cpu().numpy()
         kb = self.keys.cpu().numpy().tobytes()
         st = self.state[:n].cpu().numpy()
+        if ((st == N.KEY_OVERFLOW) | ((st & N.PATH_OVERFLOW) != 0)).any():
+            raise ValueError("primary_keys: key/path text exceeded the reused KeyText buffers")
         keys = [kb[ko[i]:ko[i + 1]].decode() if st[i] == N.KEY_OK else None for i in range(n)]
         paths = None
         if self.paths is not None:
@@ -796,8 +800,9 @@ class Engine:
         every record of ``b`` as text on the device.  Without ``out`` the size
         pass is followed by one host read of the totals; passing a ``KeyText``
         from an earlier call on a same-shaped batch reuses its buffers (no host
-        sync: a text past a buffer's end is not written, its record's state
-        stays as the size pass left it)."""
+        sync: a text that would end past a buffer is not written and its record's
+        state says so — ``KEY_OVERFLOW`` for the key, ``PATH_OVERFLOW`` ORed in
+        for the path; ``KeyText.host`` raises on either)."""
         b = b if b.device == self.device else b.to(self.device)
         self._check_alleles(b)
         n = b.n

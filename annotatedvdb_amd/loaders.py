@@ -305,17 +305,22 @@ class VCFVariantLoader(object):
         the reference would fail on, resume/skip-existing/ADSP modes — goes
         through ``parse_variants([line])``, which raises where the reference
         raises (nothing is emitted before that decision)."""
-        if (flags is None and isinstance(line, str) and self._bin_indexer is not None
-                and self._pk_generator is not None and self._existing is None and not self.is_adsp()
-                and self._resume is True):
-            out = _SLOW
-            if self._chromosome_map is None and not self._vcf_header_fields:
-                out = self._parse_line_k5h(line)
-            if out is _SLOW:
-                out = self._parse_line_k8h(line)
+        if flags is None and isinstance(line, str):
+            out = self._parse_line_fast(line)
             if out is not _SLOW:
                 return out
         return self.parse_variants([line], flags)[0]
+
+    def _parse_line_fast(self, line):
+        if (self._bin_indexer is None or self._pk_generator is None or self._existing is not None
+                or self.is_adsp() or self._resume is not True):
+            return _SLOW
+        out = _SLOW
+        if self._chromosome_map is None and not self._vcf_header_fields:
+            out = self._parse_line_k5h(line)
+        if out is _SLOW:
+            out = self._parse_line_k8h(line)
+        return out
 
     def _parse_line_k5h(self, line):
         """The whole line in one library call (K5h, ``avdb_vcf_line_host``): COPY
@@ -419,7 +424,25 @@ class VCFVariantLoader(object):
             raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
         if flags is not None:
             raise NotImplementedError("update flags are a database-update feature; out of scope")
+        if not dedup and keep_override is None and len(lines) <= self.PER_LINE_MAX:
+            # a batch too small to pay for the GPU launches: the per-line path line by
+            # line (the same results; lines it does not settle take this function's
+            # general path one at a time, which raises / records where the reference raises)
+            out = []
+            for line in lines:
+                r = self._parse_line_fast(line) if isinstance(line, str) else _SLOW
+                if r is _SLOW:
+                    r = self._parse_batch([line], errors, dedup, keep_override)[0]
+                out.append(r)
+            return out
+        return self._parse_batch(lines, errors, dedup, keep_override)
 
+    #: parse_variants batches up to this many lines run line by line on the host
+    #: path (K5h / K8h, ~5 us per line on the MI355X box's host); larger ones as
+    #: device batches (load_vcf_text is the bulk path: K0 + K2 + K5 on the GPU)
+    PER_LINE_MAX = 1 << 20
+
+    def _parse_batch(self, lines, errors, dedup, keep_override):
         # ---- phase 1: host parse (stops at the first parse error) --------------
         parsed = []  # (entry, variant) | ("skip",) | ("error", exc)
         for line in lines:

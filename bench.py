@@ -311,8 +311,8 @@ def dropin(a):
                                                 lines, reps=3)
     res["per_line_path"] = {"k5h_rendered_lines": ld._engine.line_host().rendered,
                             "note": "parse_variant: K5h (avdb_vcf_line_host, the kernels' per-line code in the "
-                                    "library's host code) for the lines it renders, else the general path; "
-                                    "find_bin_index misses: K8h (avdb_small_prep_host)"}
+                                    "library's host code) for the lines it renders, else K8h (avdb_small_prep_host) "
+                                    "or the general path; find_bin_index misses: K1h (avdb_bin_path_host)"}
     # the same calls through the reference-structured port on this host, same process,
     # same inputs (oracle.load_line: VcfEntryParser-style parse, per-alt VariantAnnotator-
     # style normalize + end, PortBinIndex with the reference's one-bin L13 cache and a

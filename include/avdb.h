@@ -326,12 +326,15 @@ int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
  * Call with key_out == NULL first: exclusive offsets key_off[n+1] (and
  * path_off[n+1]) from the SoA alone; then with key_out (and path_out), 8-byte
  * aligned, of key_cap (path_cap) bytes >= the totals, which writes the text and
- * key_state[n] (a text that would end past its cap is not written): */
+ * key_state[n] (a text that would end past its cap is not written, and its record's
+ * state says so: AVDB_KEY_OVERFLOW / AVDB_PATH_OVERFLOW): */
 #define AVDB_KEY_OK 0
 #define AVDB_KEY_HOST 1          /* ':' in an allele (the reference raises ValueError),
                                   * non-ASCII bytes, a contig without label or an
                                   * interned (non-rs) external id: caller renders */
 #define AVDB_KEY_NEED_DIGEST 2   /* long record and digest == NULL */
+#define AVDB_KEY_OVERFLOW 3      /* the key would end past key_cap: not written */
+#define AVDB_PATH_OVERFLOW 0x10u /* ORed in: the path would end past path_cap: not written */
 int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
                       const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap,
                       size_t heap_bytes, const uint64_t* ext_id, const uint32_t* bin_code,

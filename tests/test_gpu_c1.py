@@ -228,3 +228,23 @@ def _k8_vs_kernels(engine, N, sp):
     assert r2["path"][0] == O.format_bin_path("1", int(r2["code"][0])) and r2["path"][1] == "chr1"
     assert r2["path"][2] is None and r2["path"][3] is None
     assert list(r2["status"]) == [0, 0, 2, 1]
+
+
+def test_k7_reused_buffers_flag_overflow(engine):
+    """A KeyText reused for a batch whose keys and paths are longer: the texts
+    that do not fit are not written and their records say so (KEY_OVERFLOW,
+    PATH_OVERFLOW); KeyText.host refuses the batch instead of returning stale text."""
+    from annotatedvdb_amd import _native as N
+    from annotatedvdb_amd.engine import pack_records
+    a = pack_records([0] * 64, [100] * 64, [b"A"] * 64, [b"G"] * 64).to("cuda")
+    _, code, _, _ = engine.record_prep(a, want_lcp=False)
+    kt = engine.primary_keys(a, code=code)
+    assert kt.host(64)[0][0] == "1:100:A:G"
+    b = pack_records([9] * 64, [100000] * 64, [b"ACGTACGTAC"] * 64, [b"G"] * 64).to("cuda")  # leaf bins: 87-byte paths
+    _, code2, _, _ = engine.record_prep(b, want_lcp=False)
+    kt2 = engine.primary_keys(b, code=code2, out=kt)
+    st = kt2.state[:64].cpu().numpy()
+    assert ((st & 0x0F) == N.KEY_OVERFLOW).sum() > 0 and ((st & N.PATH_OVERFLOW) != 0).sum() > 0
+    assert ((st & 0x0F) == N.KEY_OK).sum() > 0  # the keys that fit were written
+    with pytest.raises(ValueError):
+        kt2.host(64)

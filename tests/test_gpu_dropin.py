@@ -52,10 +52,18 @@ def _check(lines, outs, copy_rows):
             ci += 1
 
 
-def test_loader_batch_matches_reference(loader):
+@pytest.mark.parametrize("per_line_max", [1 << 20, 0])
+def test_loader_batch_matches_reference(loader, per_line_max):
+    """parse_variants over every golden line: line by line on the host path
+    (K5h / K8h) and as one device batch (K8 / K2 + K7 + K5a)."""
     lines = golden_lines()
     loader.reset_copy_buffer()
-    outs = loader.parse_variants([l[0] for l in lines], errors="record")
+    loader._initialize_counters()
+    loader.PER_LINE_MAX = per_line_max
+    try:
+        outs = loader.parse_variants([l[0] for l in lines], errors="record")
+    finally:
+        del loader.PER_LINE_MAX
     rows = loader.copy_buffer().getvalue().splitlines()
     _check(lines, outs, rows)
     assert loader.get_count("variant") == len(rows)
