@@ -21,6 +21,7 @@ import torch  # noqa: F401  (loads torch's HIP runtime before ours; see module d
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libavdb_hip.so")
 
+ABI_VERSION = 2  # AVDB_ABI_VERSION (include/avdb.h)
 AVDB_OK = 0
 AVDB_EINVAL = -1
 AVDB_EHIP = -2
@@ -60,10 +61,13 @@ MAX_ALG_ID = 64
 
 
 class FormatOpts(ctypes.Structure):
-    """avdb_format_opts (include/avdb.h)."""
-    _fields_ = [("alg_id", ctypes.c_char_p), ("max_seq_len", ctypes.c_uint32),
+    """avdb_format_opts (include/avdb.h); ``struct_size`` is filled in."""
+    _fields_ = [("struct_size", ctypes.c_uint32), ("max_seq_len", ctypes.c_uint32), ("alg_id", ctypes.c_char_p),
                 ("flags", ctypes.c_uint32), ("match", ctypes.c_void_p), ("match_kind", ctypes.c_void_p),
                 ("frag", ctypes.c_void_p), ("frag_off", ctypes.c_void_p), ("adsp_dup", ctypes.c_void_p)]
+
+    def __init__(self, alg_id: bytes = b"", max_seq_len: int = 50, flags: int = 0):
+        super().__init__(ctypes.sizeof(FormatOpts), max_seq_len, alg_id, flags)
 
 class LineResult(ctypes.Structure):
     """avdb_line_result (include/avdb.h)."""
@@ -194,7 +198,7 @@ def load_library(path: Optional[str] = None):
                 "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
         lib = ctypes.CDLL(p)
         _sig(lib)
-        if lib.avdb_abi_version() != 1:
+        if lib.avdb_abi_version() != ABI_VERSION:
             raise NativeUnavailable("libavdb_hip ABI version mismatch")
         _lib = lib
         return lib

@@ -39,9 +39,9 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build libavdb_hip.so)")
 
 
-def _obj(src: str, flags) -> str:
+def _obj(src: str, flags, objdir: str = "obj") -> str:
     tag = "".join(f for f in flags if f.startswith("-D")).replace("-D", "_").replace("=", "")
-    return os.path.join(OUT_DIR, "obj", os.path.basename(src)[:-4] + tag + ".o")
+    return os.path.join(OUT_DIR, objdir, os.path.basename(src)[:-4] + tag + ".o")
 
 
 def _obj_stale(src: str, obj: str) -> bool:
@@ -59,19 +59,20 @@ def _reap(job) -> None:
     os.replace(obj + ".tmp", obj)
 
 
-def build(force: bool = False, verbose: bool = True, out: str = None, flags=()) -> str:
+def build(force: bool = False, verbose: bool = True, out: str = None, flags=(), objdir: str = "obj",
+          link_flags=()) -> str:
     """One object per source, compiled concurrently (each .hip is its own
     translation unit: no device code crosses files), then one link."""
     out = out or LIB
     if not force and out == LIB and not flags and not _stale():
         return LIB
-    os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
+    os.makedirs(os.path.join(OUT_DIR, objdir), exist_ok=True)
     base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", INCLUDE] + list(flags)
     procs = []
     objs = []
     jobs = max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     for src in sources():
-        obj = _obj(src, flags)
+        obj = _obj(src, flags, objdir)
         objs.append(obj)
         if force or _obj_stale(src, obj):
             cmd = base + ["-c", src, "-o", obj + ".tmp"]
@@ -83,7 +84,7 @@ def build(force: bool = False, verbose: bool = True, out: str = None, flags=()) 
     for job in procs:
         _reap(job)
     tmp = out + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + list(link_flags) + objs
     if verbose:
         print("[avdb] " + " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -446,6 +446,11 @@ static inline int fill_args(FormatArgs* A, avdb_ctx* ctx, const uint8_t* text, s
     avdb_set_error("avdb_vcf_format: null argument");
     return AVDB_EINVAL;
   }
+  if (opts && opts->struct_size != sizeof(avdb_format_opts)) {
+    avdb_set_error("avdb_vcf_format: avdb_format_opts.struct_size %u, this library expects %zu (ABI %d)",
+                   opts->struct_size, sizeof(avdb_format_opts), AVDB_ABI_VERSION);
+    return AVDB_EINVAL;
+  }
   memset(A, 0, sizeof(*A));
   A->text = text;
   A->text_bytes = text_bytes;

@@ -41,6 +41,11 @@ extern "C" int avdb_vcf_line_host(const avdb_ctx* ctx, const char* line, size_t 
     avdb_set_error("avdb_vcf_line_host: null argument");
     return AVDB_EINVAL;
   }
+  if (opts->struct_size != sizeof(avdb_format_opts)) {
+    avdb_set_error("avdb_vcf_line_host: avdb_format_opts.struct_size %u, this library expects %zu (ABI %d)",
+                   opts->struct_size, sizeof(avdb_format_opts), AVDB_ABI_VERSION);
+    return AVDB_EINVAL;
+  }
   if (opts->match || opts->adsp_dup) {
     avdb_set_error("avdb_vcf_line_host: --skipExisting / ADSP key matches are batch features (avdb_vcf_format_*)");
     return AVDB_EINVAL;

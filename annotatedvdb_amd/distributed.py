@@ -114,6 +114,14 @@ class RcclExchange:
     def allgather(self, hist: torch.Tensor, counters: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         import ctypes
         N, e = self._N, self.engine
+        # avdb_hist_allgather reads u32 bins and u64 counters from raw device pointers
+        if hist.dtype not in (torch.int32, torch.uint32) or counters.dtype not in (torch.int64, torch.uint64):
+            raise ValueError("hist must be int32/uint32 and counters int64/uint64 (got %s, %s)"
+                             % (hist.dtype, counters.dtype))
+        if not (hist.is_contiguous() and counters.is_contiguous()):
+            raise ValueError("hist and counters must be contiguous")
+        if hist.device != e.device or counters.device != e.device:
+            raise ValueError("hist and counters must be on the engine's device %s" % e.device)
         nb, nc = hist.numel(), counters.numel()
         sz = ctypes.c_size_t()
         N.check("avdb_hist_allgather_workspace_size",

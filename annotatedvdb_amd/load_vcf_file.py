@@ -9,8 +9,9 @@ the per-line loop of ``load()`` (:80-221): ``parse_variant`` per line, the
 * several files (``--dir``/``--extension``/``--chr``): files are dealt to the
   ranks by size (LPT), each rank loads its files whole, as the reference's
   workers do;
-* one file (``--fileName``) on N ranks: every rank tokenizes the text on its GPU
-  (K0) and keeps the lines the genome-piece plan gives it (K9
+* one file (``--fileName``) on N ranks: every rank streams the file in
+  ``--batchBytes`` blocks, tokenizes each on its GPU (K0) and keeps the lines
+  the genome-piece plan gives it (K9
   ``avdb_vcf_select_lines`` / ``_copy``: contigs cut at 64 Mb, pieces by LPT,
   ``shard.plan``); bins and keys need nothing from other ranks.
 
@@ -93,6 +94,28 @@ def read_text(path: str) -> bytes:
         return fh.read()
 
 
+def iter_batches(path: str, batch_bytes: int):
+    """The file as consecutive blocks of about ``batch_bytes`` cut after a newline
+    (a line longer than a block stays whole): host memory stays bounded by the
+    batch, whatever the file size (gzip streams too)."""
+    opener = gzip.open if path.endswith(".gz") else open
+    with opener(path, "rb") as fh:
+        carry = b""
+        while True:
+            block = fh.read(max(1, batch_bytes))
+            if not block:
+                break
+            buf = carry + block
+            k = buf.rfind(b"\n")
+            if k < 0:
+                carry = buf
+                continue
+            carry = buf[k + 1:]
+            yield buf[:k + 1]
+        if carry:
+            yield carry
+
+
 def make_loader(args, device: int):
     from .loaders import VCFVariantLoader
     ld = VCFVariantLoader(args.datasource, verbose=args.verbose, device=device)
@@ -114,26 +137,25 @@ def rank_text(raw: bytes, loader, plan, rank: int) -> bytes:
 
 
 def load(path: str, args, loader, rank: int, plan=None) -> Dict[str, int]:
-    """One input file (or this rank's share of it) through the GPU load path."""
+    """One input file (or this rank's share of it) through the GPU load path,
+    streamed in ``--batchBytes`` blocks cut at line boundaries.  With a piece
+    plan (one file on N ranks) every block is tokenized on this rank's GPU and
+    only the lines its pieces own are kept (K0 + K9): a line's owner depends on
+    the line alone, so block-wise selection equals whole-file selection."""
     base = os.path.join(args.outDir, os.path.basename(path))
-    raw = read_text(path)
-    if plan is not None:
-        raw = rank_text(raw, loader, plan, rank)
     before = {k: loader.get_count(k) for k in COUNTERS}
     t0 = time.perf_counter()
     with open(base + ".r%d.mapping" % rank, "w") as mfh, open(base + ".r%d.copy" % rank, "w") as cfh:
-        i = 0
-        while i < len(raw):
-            j = min(len(raw), i + args.batchBytes)
-            if j < len(raw):
-                k = raw.rfind(b"\n", i, j)
-                j = k + 1 if k >= i else (raw.find(b"\n", j) + 1 or len(raw))
+        for block in iter_batches(path, args.batchBytes):
+            if plan is not None:
+                block = rank_text(block, loader, plan, rank)
+                if not block:
+                    continue
             loader.reset_copy_buffer()
             try:
-                loader.load_vcf_text(raw[i:j], dedup=args.dedup, mapping_out=mfh)
+                loader.load_vcf_text(block, dedup=args.dedup, mapping_out=mfh, batch_bytes=args.batchBytes)
             finally:
                 cfh.write(loader.copy_buffer().getvalue())  # the rows the reference would COPY (:135-142)
-            i = j
         if loader.is_adsp():
             with open(base + ".r%d.updates" % rank, "w") as ufh:
                 for pk, chrom in loader.update_buffer():
@@ -162,15 +184,26 @@ def main(argv: Optional[Sequence[str]] = None) -> Dict[str, int]:
         mine = [(args.fileName, plan)]
     else:
         mine = [(f, None) for f in assign_files(files, ri.world)[ri.rank]]
+    failed = 0
     for f, plan in mine:
         if not os.path.exists(f):
             LOGGER.info("Input file %s not found.  SKIPPING.", f)
             continue
-        st = load(f, args, loader, ri.rank, plan)
+        before = {k: loader.get_count(k) for k in COUNTERS}
+        try:
+            st = load(f, args, loader, ri.rank, plan)
+        except Exception as err:  # noqa: BLE001 — a file fails alone, as a reference pool worker does
+            # (load_vcf_file.py:212-214: logged critical, that file stops); the other files
+            # and ranks go on, and the failure travels in the all-gathered counters
+            LOGGER.critical("rank %d: problem parsing %s at variant %s: %r", ri.rank, f,
+                            loader.get_current_variant_id(), err)
+            failed += 1
+            st = {k: loader.get_count(k) - before[k] for k in COUNTERS}
         for k in COUNTERS:
             totals[k] += st[k]
-    # node totals: one all-gather of the per-rank counters
-    mine_t = torch.tensor([totals[k] for k in COUNTERS], dtype=torch.int64,
+    # node totals: one all-gather of the per-rank counters (+ failed files), reached
+    # by every rank whatever happened to its files, so no rank waits on a dead peer
+    mine_t = torch.tensor([totals[k] for k in COUNTERS] + [failed], dtype=torch.int64,
                           device="cuda" if (args.backend or "nccl") == "nccl" and ri.distributed else "cpu")
     if ri.distributed:
         import torch.distributed as dist
@@ -179,12 +212,21 @@ def main(argv: Optional[Sequence[str]] = None) -> Dict[str, int]:
         node = torch.stack(parts).sum(0).cpu().tolist()
     else:
         node = mine_t.cpu().tolist()
-    node_totals = dict(zip(COUNTERS, node))
+    node_totals = dict(zip(COUNTERS, node[:len(COUNTERS)]))
+    node_failed = int(node[len(COUNTERS)])
     if ri.rank == 0:
-        LOGGER.info("node totals: %s", node_totals)
-        print(json.dumps({"node_totals": node_totals, "ranks": ri.world}), flush=True)
+        LOGGER.info("node totals: %s; failed files: %d", node_totals, node_failed)
+        print(json.dumps({"node_totals": node_totals, "failed_files": node_failed, "ranks": ri.world}), flush=True)
     D.finalize(ri)
+    if node_failed:
+        raise LoadFailed("%d input file(s) failed on the node (this rank: %d); see the CRITICAL log lines"
+                         % (node_failed, failed))
     return node_totals
+
+
+class LoadFailed(RuntimeError):
+    """At least one rank could not load one of its files (every rank raises it
+    after the node-wide counter exchange, so the job exits non-zero)."""
 
 
 if __name__ == "__main__":

@@ -51,7 +51,9 @@
 extern "C" {
 #endif
 
-#define AVDB_ABI_VERSION 1
+/* 2: avdb_format_opts gained struct_size (first field) and adsp_dup; K5h/K8h/K1h
+ *    host entries; AVDB_KEY_OVERFLOW / AVDB_PATH_OVERFLOW key states */
+#define AVDB_ABI_VERSION 2
 
 /* return codes */
 #define AVDB_OK 0
@@ -245,8 +247,10 @@ int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t 
 #define AVDB_FORMAT_ADSP 1u           /* opts.flags: COPY rows end with is_adsp_variant = True
                                         * (vcf_variant_loader.py:336-337) */
 typedef struct avdb_format_opts {
-  const char* alg_id;     /* xstr(row_algorithm_id), host NUL-terminated; NULL = "" */
+  uint32_t struct_size;   /* sizeof(avdb_format_opts) as the caller compiled it: the
+                           * library refuses a size it does not know (ABI check) */
   uint32_t max_seq_len;   /* primary_key_generator.py:53 (default 50) */
+  const char* alg_id;     /* xstr(row_algorithm_id), host NUL-terminated; NULL = "" */
   uint32_t flags;         /* AVDB_FORMAT_* */
   /* --skipExisting (optional, device; NULL = off): K6 match / kind per record and
    * the .mapping text each existing key contributes (its match list, rendered

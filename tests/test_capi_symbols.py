@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     lib = N.load_library()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.avdb_abi_version() == 1
+    assert lib.avdb_abi_version() == N.ABI_VERSION == 2
 
 
 def test_nm_dynamic_exports():

@@ -116,3 +116,40 @@ def test_driver_files_per_rank(engine, tmp_path):
     tot = load_vcf_file.main(["--dir", str(d), "--extension", "vcf", "--chr", "1,2,22", "--outDir", str(out)])
     n = sum(1 for ln in lines if ln.split("\t")[0] in ("1", "2", "22"))
     assert tot["line"] == n and len(_outputs(out, ".mapping")) == n
+
+
+def _driver_rc(rank, world, port, argv, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from annotatedvdb_amd import load_vcf_file
+    try:
+        q.put((rank, "ok", load_vcf_file.main(argv)))
+    except load_vcf_file.LoadFailed as err:
+        q.put((rank, "failed", str(err)))
+        raise SystemExit(1)
+
+
+def test_driver_rank_failure_reaches_every_rank(engine, tmp_path):
+    """A line that raises on one rank (an unknown contig: K9 gives it to rank 0,
+    the loader raises TypeError as the reference does) fails that rank's file
+    only; the other rank loads its share, the failure travels in the all-gathered
+    counters, and every rank exits non-zero instead of waiting on a dead peer."""
+    import torch.multiprocessing as mp
+    vcf = tmp_path / "in.vcf"
+    vcf.write_bytes(_text(6000, seed=34))
+    assert b"chrUn_KI270302v1" in vcf.read_bytes()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    argv = ["--fileName", str(vcf), "--outDir", str(tmp_path / "multi"), "--backend", "gloo",
+            "--batchBytes", str(1 << 16)]
+    procs = [ctx.Process(target=_driver_rc, args=(r, 2, port, argv, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (st, v) for r, st, v in (q.get(timeout=300) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 1
+    assert res[0][0] == res[1][0] == "failed"
+    assert "this rank: 1" in res[0][1] and "this rank: 0" in res[1][1]
+    assert os.path.getsize(tmp_path / "multi" / "in.vcf.r1.copy") > 0

@@ -182,3 +182,24 @@ def test_driver_file_assignment_lpt(tmp_path):
     a = load_vcf_file.assign_files(fs, 2)
     assert sorted(sum(a, [])) == sorted(fs)
     assert a[0] == [fs[0], fs[1], fs[4]] and a[1] == [fs[2], fs[3]]
+
+
+@pytest.mark.parametrize("gz", [False, True])
+def test_load_driver_streams_blocks_at_line_boundaries(tmp_path, gz):
+    """load_vcf_file.iter_batches: blocks of about --batchBytes ending after a
+    newline (a longer line stays whole), concatenating to the file."""
+    import gzip as gzm
+    from annotatedvdb_amd.load_vcf_file import iter_batches
+    lines = [("%d\t" % i) + "A" * (i * 37 % 300) for i in range(500)]
+    data = ("\n".join(lines)).encode()  # no final newline
+    p = tmp_path / ("x.vcf.gz" if gz else "x.vcf")
+    if gz:
+        with gzm.open(p, "wb") as fh:
+            fh.write(data)
+    else:
+        p.write_bytes(data)
+    for bb in (1, 64, 1000, 1 << 20):
+        blocks = list(iter_batches(str(p), bb))
+        assert b"".join(blocks) == data
+        assert all(b.endswith(b"\n") for b in blocks[:-1])
+        assert all(len(b) <= bb + 400 for b in blocks)

@@ -246,3 +246,16 @@ def test_k5h_edges(lib, ctx):
     opts = N.FormatOpts(b"1", 50, 0)
     assert lib.avdb_vcf_line_host(None, b"x", 1, ctypes.byref(opts), None, 0, None, 0,
                                   ctypes.byref(N.LineResult())) == N.AVDB_EINVAL
+
+
+def test_format_opts_struct_size_checked(lib, ctx):
+    """avdb_format_opts carries its size (ABI 2): a caller built against another
+    layout is refused instead of read past its struct."""
+    opts = N.FormatOpts(b"1", 50, 0)
+    opts.struct_size = ctypes.sizeof(N.FormatOpts) - 8
+    res = N.LineResult()
+    b = b"1\t100\trs5\tA\tG\t.\t.\tRS=5"
+    cb = ctypes.create_string_buffer(4096)
+    assert lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), cb, 4096, cb, 4096,
+                                  ctypes.byref(res)) == N.AVDB_EINVAL
+    assert b"struct_size" in lib.avdb_last_error()
