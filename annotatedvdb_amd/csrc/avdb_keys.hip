@@ -68,6 +68,12 @@ struct KeyArgs {
   uint8_t* state;
   uint16_t* key_sz;   // SIZE: sizes as u16 in the workspace (scanned into key_off), or NULL
   uint16_t* path_sz;
+  // one pass (MODE 2): tiles taken in order from tile_ctr; per tile a status word
+  // and the inclusive prefixes (keys, paths) of the decoupled look-back scan
+  uint32_t* tile_ctr;
+  uint32_t* scan_err;     // look-backs that gave up waiting (never expected: a bug signal)
+  uint64_t* tile_status;
+  uint64_t* tile_pre;
 };
 
 // WRITE renders each wave's 64 records as a tile: each stream's span (the
@@ -162,6 +168,105 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---------------------------------------------------------------------------
+// K7 in one pass (MODE 2): each wave takes the next 64-record tile in launch
+// order, computes its records' key and path sizes from the SoA, and finds the
+// tile's output offsets with a decoupled look-back scan over the tiles before
+// it (status word per tile: flag 1 = aggregate, 2 = inclusive prefix published);
+// then it renders as the two-pass write does.  No size pass, no scans, no
+// offset reads: the SoA is read once and the offsets are written, not read.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kTileAgg = 1ull << 62, kTilePre = 2ull << 62;
+constexpr uint64_t kAggMask = 0x7FFFFFFFull;
+constexpr uint32_t kSpinLimit = 1u << 24;  // a look-back wait this long is a bug: count it and go on
+
+__device__ __forceinline__ uint32_t ndigits64(uint64_t v) {
+  if (v <= 0xFFFFFFFFull) return ndigits(uint32_t(v));
+  const uint64_t q = v / 1000000000ull;
+  return 9u + (q <= 0xFFFFFFFFull ? ndigits(uint32_t(q)) : 9u + ndigits(uint32_t(q / 1000000000ull)));
+}
+
+// bytes of primary_key_generator.py:106-122's key for a labelled contig
+__device__ __forceinline__ uint32_t key_size(uint32_t c, uint32_t p, uint32_t r, uint32_t a, uint64_t e, bool lng) {
+  const uint32_t label = (c >= 9 && c < 22) ? 2u : 1u;
+  return label + 2u + ndigits(p) + (lng ? uint32_t(AVDB_DIGEST_CHARS) : r + 1u + a) +
+         ((e && !(e >> 63)) ? 3u + ndigits64(e) : 0u);
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const uint64_t o = (uint64_t(uint32_t(__shfl_xor(uint32_t(v >> 32), d, kWave))) << 32) |
+                       uint32_t(__shfl_xor(uint32_t(v), d, kWave));
+    v += o;
+  }
+  return v;
+}
+
+// exclusive (keys, paths) prefix of tile T whose totals are (K, P); the whole wave
+// calls it.  Waits only on tiles < T, which were taken earlier by running waves.
+__device__ __forceinline__ void tile_prefix(const KeyArgs& A, uint64_t T, uint32_t K, uint32_t P, uint64_t* EK,
+                                            uint64_t* EP) {
+  const uint32_t lane = __lane_id();
+  uint64_t* st = A.tile_status;
+  uint64_t* pre = A.tile_pre;
+  uint64_t sk = 0, sp = 0;
+  if (T > 0) {
+    if (lane == 0)
+      __hip_atomic_store(st + T, kTileAgg | (uint64_t(K) << 31) | P, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t base = int64_t(T) - 1;
+    uint32_t spins = 0;
+    while (true) {
+      const int64_t j = base - int64_t(lane);
+      uint64_t v = kTilePre;  // before tile 0: a zero prefix
+      bool ready = true;
+      if (j >= 0) {
+        v = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        ready = (v >> 62) != 0;
+      }
+      while (!__all(ready)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (!ready) {
+          v = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          ready = (v >> 62) != 0;
+        }
+        if (++spins > kSpinLimit) {
+          if (lane == 0) atomicAdd(A.scan_err, 1u);
+          if (!ready) v = kTilePre;
+          ready = true;
+        }
+      }
+      const uint64_t pm = __ballot((v >> 62) == 2);
+      uint64_t ak = 0, ap = 0;
+      if (pm) {
+        const uint32_t l = uint32_t(__ffsll((unsigned long long)pm)) - 1;  // nearest published prefix
+        if (lane < l) {
+          ak = (v >> 31) & kAggMask;
+          ap = v & kAggMask;
+        } else if (lane == l && j >= 0) {
+          ak = __hip_atomic_load(pre + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ap = __hip_atomic_load(pre + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sk += wave_sum64(ak);
+        sp += wave_sum64(ap);
+        break;
+      }
+      ak = (v >> 31) & kAggMask;
+      ap = v & kAggMask;
+      sk += wave_sum64(ak);
+      sp += wave_sum64(ap);
+      base -= kWave;
+    }
+  }
+  if (lane == 0) {
+    __hip_atomic_store(pre + 2 * T, sk + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(pre + 2 * T + 1, sp + P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(st + T, kTilePre, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  *EK = sk;
+  *EP = sp;
+}
+
 #ifndef AVDB_K7_PREFETCH
 #define AVDB_K7_PREFETCH 1  // the next tile's SoA and offsets are loaded before this one renders (0: A/B)
 #endif
@@ -175,11 +280,16 @@ struct KeyTileIn {
   bool in_regs;
 };
 
-template <bool WRITE>
+// MODE 0: size pass; 1: write pass (offsets given); 2: one pass (sizes, look-back
+// scan, offsets written, text)
+template <int MODE>
 #ifndef AVDB_K7_WAVES
 #define AVDB_K7_WAVES (AVDB_K7_PREFETCH ? 4 : 5)
 #endif
 __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A) {
+  constexpr bool WRITE = MODE != 0;
+  constexpr bool ONEP = MODE == 2;
+  static_assert(!ONEP || AVDB_K7_PREFETCH, "the one-pass form reads each tile's SoA ahead");
   __shared__ uint64_t s_kimg[WRITE ? kWavesPerBlock * kKeyWave / 8 : 1];
   __shared__ uint64_t s_pimg[WRITE ? kWavesPerBlock * kPathWave / 8 : 1];
   const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
@@ -204,10 +314,10 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       v.a = A.al[j];
       v.e = A.ext ? A.ext[j] : 0ull;
       v.off = A.off[j];
-      v.ko = A.key_off[j];
+      if constexpr (!ONEP) v.ko = A.key_off[j];
       if (A.code) {
         v.cd = A.code[j];
-        v.po = A.path_off[j];
+        if constexpr (!ONEP) v.po = A.path_off[j];
       }
     }
     return v;
@@ -239,16 +349,24 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
         if (k < nw) v.w[k] = heap_word(aw + 8 * k, h);
     }
   };
+  // ONEP: the next tile in launch order (every tile before it was taken by a running wave)
+  auto acquire = [&]() -> size_t {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(A.tile_ctr, 1u);
+    return size_t(uint32_t(__shfl(t, 0, kWave))) * kWave;
+  };
+  size_t t0 = ONEP ? acquire() : size_t(bid) * blockDim.x + size_t(wv) * kWave;
   KeyTileIn nx{};
-  if (PF && size_t(bid) * blockDim.x + size_t(wv) * kWave < A.n) {
-    nx = load_in(size_t(bid) * blockDim.x + size_t(wv) * kWave);
-    if (PFW) load_window(nx, size_t(bid) * blockDim.x + size_t(wv) * kWave + lane);
+  if (PF && t0 < A.n) {
+    nx = load_in(t0);
+    if (PFW) load_window(nx, t0 + lane);
   }
-  for (size_t t0 = size_t(bid) * blockDim.x + size_t(wv) * kWave; t0 < A.n; t0 += stride) {
+  for (size_t tn = 0; t0 < A.n; t0 = tn) {
+    tn = ONEP ? acquire() : t0 + stride;
     const size_t i = t0 + lane;
     const bool live = i < A.n;
     const KeyTileIn cur = nx;
-    if (PF && t0 + stride < A.n) nx = load_in(t0 + stride);
+    if (PF && tn < A.n) nx = load_in(tn);
     uint32_t c = 0, p = 0, r = 0, a = 0;
     uint64_t e = 0;
     bool lng = false;
@@ -264,6 +382,13 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       st = AVDB_KEY_OK;
       if (c >= uint32_t(A.n_chrom) || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
       else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
+    }
+    // ONEP: sizes from the SoA alone (what the size pass would write)
+    uint32_t ksz = 0, psz = 0;
+    if constexpr (ONEP) {
+      if (live && st == AVDB_KEY_OK) ksz = key_size(c, p, r, a, e, lng);
+      if (live && A.code && cur.cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom))
+        psz = bin_path(Out<false>(nullptr, 0), c, cur.cd).size();
     }
     // WRITE: the bytes a key copies — a short record's ref+alt, or a long record's
     // 32 digest characters — are loaded into a 7-word register window up front,
@@ -354,21 +479,72 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
         }
       }
       const size_t last = t0 + kWave < A.n ? t0 + kWave : A.n;
+      // the tile's spans [gk0, gk1) / [gp0, gp1) and each record's [ko, ko1) / [po, po1)
+      uint64_t gk0, gk1, ko = 0, ko1 = 0, gp0 = 0, gp1 = 0, po = 0, po1 = 0;
+      if constexpr (ONEP) {
+        uint32_t xk = ksz, xp = psz;  // wave inclusive scans
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+          const uint32_t uk = __shfl_up(xk, d, kWave), up = __shfl_up(xp, d, kWave);
+          if (lane >= uint32_t(d)) {
+            xk += uk;
+            xp += up;
+          }
+        }
+        const uint32_t K = __shfl(xk, kWave - 1, kWave), P = __shfl(xp, kWave - 1, kWave);
+        uint64_t EK, EP;
+        tile_prefix(A, t0 / kWave, K, P, &EK, &EP);
+        gk0 = EK;
+        gk1 = EK + K;
+        ko = EK + xk - ksz;
+        ko1 = EK + xk;
+        gp0 = EP;
+        gp1 = EP + P;
+        po = EP + xp - psz;
+        po1 = EP + xp;
+        if (live) {
+          A.key_off[i] = ko;
+          if (A.code) A.path_off[i] = po;
+          if (i + 1 == A.n) {
+            A.key_off[A.n] = ko1;
+            if (A.code) A.path_off[A.n] = po1;
+          }
+        }
+      } else {
+        gk0 = A.key_off[t0];
+        gk1 = A.key_off[last];
+        // (PF: a record's end offset is the next lane's start; the tile's last live
+        // record ends at gk1 / gp1)
+        auto next_of = [&](uint64_t v, uint64_t g1) -> uint64_t {
+          const uint64_t nv = (uint64_t(uint32_t(__shfl_down(uint32_t(v >> 32), 1, kWave))) << 32) |
+                              uint32_t(__shfl_down(uint32_t(v), 1, kWave));
+          return i + 1 == last ? g1 : nv;
+        };
+        if (PF) {
+          ko = cur.ko;
+          ko1 = next_of(cur.ko, gk1);
+        } else if (live) {
+          ko = A.key_off[i];
+          ko1 = A.key_off[i + 1];
+        }
+        if (A.code) {
+          gp0 = A.path_off[t0];
+          gp1 = A.path_off[last];
+          if (PF) {
+            po = cur.po;
+            po1 = next_of(cur.po, gp1);
+          } else if (live) {
+            po = A.path_off[i];
+            po1 = A.path_off[i + 1];
+          }
+        }
+      }
       // stream 0: keys
-      const uint64_t gk0 = A.key_off[t0], gk1 = A.key_off[last];
-      // (PF: a record's end offset is the next lane's start; the tile's last live
-      // record ends at gk1 / gp1)
-      auto next_of = [&](uint64_t v, uint64_t g1) -> uint64_t {
-        const uint64_t nv = (uint64_t(uint32_t(__shfl_down(uint32_t(v >> 32), 1, kWave))) << 32) |
-                            uint32_t(__shfl_down(uint32_t(v), 1, kWave));
-        return i + 1 == last ? g1 : nv;
-      };
-      const uint64_t ko = PF ? cur.ko : 0ull, ko1 = PF ? next_of(cur.ko, gk1) : 0ull;
       const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap && !(AVDB_K7_EXP & 16);
-      if (live && st == AVDB_KEY_OK && (PF ? ko1 : A.key_off[i + 1]) > A.key_cap)
+      if (live && st == AVDB_KEY_OK && ko1 > A.key_cap)
         st = AVDB_KEY_OVERFLOW;  // never write past the buffer; say so in the state
       if (live && st == AVDB_KEY_OK) {
-        const uint64_t at = PF ? ko : A.key_off[i];
+        const uint64_t at = ko;
         if (kst) {
           Out<true, true> o(LdsImage{}, kimg, at - (gk0 & ~uint64_t(15)));
           key(o).finish();
@@ -379,17 +555,13 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       }
       // stream 1: ltree paths
       bool pst = false, path_over = false;
-      uint64_t gp0 = 0, gp1 = 0;
       if (A.code) {
-        gp0 = A.path_off[t0];
-        gp1 = A.path_off[last];
         pst = gp1 - (gp0 & ~uint64_t(15)) + 16 <= kPathWave && gp1 <= A.path_cap && !(AVDB_K7_EXP & 32);
         const uint32_t cd = live ? (PF ? cur.cd : A.code[i]) : AVDB_BIN_NONE;
-        const uint64_t po1 = PF ? next_of(cur.po, gp1) : 0ull;
         const bool has_path = live && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom);
-        path_over = has_path && (PF ? po1 : A.path_off[i + 1]) > A.path_cap;
+        path_over = has_path && po1 > A.path_cap;
         if (has_path && !path_over) {
-          const uint64_t at = PF ? cur.po : A.path_off[i];
+          const uint64_t at = po;
           if (pst) {
             Out<true, true> o(LdsImage{}, pimg, at - (gp0 & ~uint64_t(15)));
             bin_path(o, c, cd).finish();
@@ -404,7 +576,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       if (kst) flush_span(kimg, A.key_out, gk0, gk1, lane, kWave);
       if (pst) flush_span(pimg, A.path_out, gp0, gp1, lane, kWave);
       // the next tile's key window: its offsets have arrived by now
-      if (PFW && t0 + stride < A.n) load_window(nx, t0 + stride + lane);
+      if (PFW && tn < A.n) load_window(nx, tn + lane);
       wave_lds_sync();
     } else if (live) {
       const uint32_t ks = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;
@@ -560,14 +732,14 @@ extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint
       AVDB_HIP_TRY(hipMemsetAsync(psz + n, 0, 2, s));
       A.key_sz = ksz;
       A.path_sz = bin_code ? psz : nullptr;
-      hipLaunchKernelGGL(k_record_keys<false>, dim3(grid), dim3(kBlock), 0, s, A);
+      hipLaunchKernelGGL(k_record_keys<0>, dim3(grid), dim3(kBlock), 0, s, A);
       AVDB_LAUNCH_CHECK("k_record_keys<size>");
       AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, Wide16It(ksz, Widen16()), ko, n + 1, s));
       if (bin_code)
         AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, Wide16It(psz, Widen16()), po, n + 1, s));
       return AVDB_OK;
     }
-    hipLaunchKernelGGL(k_record_keys<false>, dim3(grid), dim3(kBlock), 0, s, A);
+    hipLaunchKernelGGL(k_record_keys<0>, dim3(grid), dim3(kBlock), 0, s, A);
     AVDB_LAUNCH_CHECK("k_record_keys<size>");
     size_t tb = scan_bytes(n + 1);
     AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, ko, ko, n + 1, s));
@@ -586,7 +758,94 @@ extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint
   // (one resident generation, 5 workgroups per CU, ran 12.3 vs 10.2 ms on C4k,
   // with or without XCD-aware renumbering: the finer grid balances better)
   const unsigned grid = stream_grid(n, kBlock, AVDB_K7_GRID);
-  hipLaunchKernelGGL(k_record_keys<true>, dim3(grid), dim3(kBlock), 0, s, A);
+  hipLaunchKernelGGL(k_record_keys<1>, dim3(grid), dim3(kBlock), 0, s, A);
   AVDB_LAUNCH_CHECK("k_record_keys<write>");
+  return AVDB_OK;
+}
+
+// ---- K7 in one pass -------------------------------------------------------------
+static size_t onepass_tiles(size_t n) { return (n + kWave - 1) / kWave; }
+
+extern "C" int avdb_primary_keys_onepass_workspace_size(size_t n, size_t* bytes) {
+  if (!bytes) return AVDB_EINVAL;
+  *bytes = 512 + 24 * onepass_tiles(n);
+  return AVDB_OK;
+}
+
+extern "C" int avdb_primary_keys_bound(size_t n, size_t heap_bytes, size_t* key_cap, size_t* path_cap) {
+  if (!key_cap || !path_cap) return AVDB_EINVAL;
+  // key: label (2) ':' pos (10) ':' ref ':' alt | digest (32), ':rs' + 19 digits
+  *key_cap = 69 * n + heap_bytes + 8;
+  // path: "chr" + label (2) + 13 levels of <= 7 bytes, B up to 3 digits at L1
+  *path_cap = 98 * n + 8;
+  return AVDB_OK;
+}
+
+extern "C" int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                         const uint64_t* allele_off, const uint32_t* ref_len,
+                                         const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                                         const uint64_t* ext_id, const uint32_t* bin_code, const char* digest,
+                                         size_t n, uint32_t max_seq_len, void* workspace, size_t workspace_bytes,
+                                         uint64_t* key_off, uint64_t* path_off, uint8_t* key_out, size_t key_cap,
+                                         uint8_t* path_out, size_t path_cap, uint8_t* key_state, void* stream) {
+  if (!ctx || !key_off || (bin_code && !path_off) || !key_state || !key_out || (bin_code && !path_out)) {
+    avdb_set_error("avdb_primary_keys_onepass: null argument");
+    return AVDB_EINVAL;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (n == 0) {
+    AVDB_HIP_TRY(hipMemsetAsync(key_off, 0, 8, s));
+    if (bin_code) AVDB_HIP_TRY(hipMemsetAsync(path_off, 0, 8, s));
+    return AVDB_OK;
+  }
+  if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap) {
+    avdb_set_error("avdb_primary_keys_onepass: null array");
+    return AVDB_EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(key_out) % 8 || (path_out && reinterpret_cast<uintptr_t>(path_out) % 8)) {
+    avdb_set_error("avdb_primary_keys_onepass: outputs must be 8-byte aligned");
+    return AVDB_EINVAL;
+  }
+  size_t need = 0;
+  avdb_primary_keys_onepass_workspace_size(n, &need);
+  if (!workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(workspace) % 8) {
+    avdb_set_error("avdb_primary_keys_onepass: 8-byte aligned workspace of %zu bytes required", need);
+    return AVDB_ERANGE;
+  }
+  const size_t tiles = onepass_tiles(n);
+  char* ws = static_cast<char*>(workspace);
+  // tile counter, error counter and the status words start at zero; the prefixes
+  // are written before their status says so
+  AVDB_HIP_TRY(hipMemsetAsync(ws, 0, 512 + 8 * tiles, s));
+  KeyArgs A;
+  memset(&A, 0, sizeof(A));
+  A.chrom = chrom;
+  A.pos = pos;
+  A.off = allele_off;
+  A.rl = ref_len;
+  A.al = alt_len;
+  A.heap = heap;
+  A.ext = ext_id;
+  A.code = bin_code;
+  A.digest = digest;
+  A.heap_bytes = heap_bytes;
+  A.n = n;
+  A.max_seq_len = max_seq_len;
+  A.n_chrom = ctx->tab.n < 25 ? ctx->tab.n : 25;
+  A.key_off = key_off;
+  A.path_off = path_off;
+  A.key_cap = key_cap;
+  A.path_cap = path_cap;
+  A.key_out = key_out;
+  A.path_out = path_out;
+  A.state = key_state;
+  A.tile_ctr = reinterpret_cast<uint32_t*>(ws);
+  A.scan_err = reinterpret_cast<uint32_t*>(ws + 256);
+  A.tile_status = reinterpret_cast<uint64_t*>(ws + 512);
+  A.tile_pre = reinterpret_cast<uint64_t*>(ws + 512 + 8 * tiles);
+  const unsigned grid = stream_grid(n, kBlock, AVDB_K7_GRID);
+  hipLaunchKernelGGL(k_record_keys<2>, dim3(grid), dim3(kBlock), 0, s, A);
+  AVDB_LAUNCH_CHECK("k_record_keys<onepass>");
   return AVDB_OK;
 }

@@ -216,7 +216,7 @@ class KeyText:
         Raises ``ValueError`` if a text did not fit its buffer (a reused
         ``KeyText`` too small for this batch: state KEY_OVERFLOW / PATH_OVERFLOW)."""
         ko = self.key_off[: n + 1].cpu().numpy()
-        kb = self.keys.cpu().numpy().tobytes()
+        kb = self.keys[: int(ko[n])].cpu().numpy().tobytes()
         st = self.state[:n].cpu().numpy()
         if ((st == N.KEY_OVERFLOW) | ((st & N.PATH_OVERFLOW) != 0)).any():
             raise ValueError("primary_keys: key/path text exceeded the reused KeyText buffers")
@@ -224,7 +224,7 @@ class KeyText:
         paths = None
         if self.paths is not None:
             po = self.path_off[: n + 1].cpu().numpy()
-            pb = self.paths.cpu().numpy().tobytes()
+            pb = self.paths[: int(po[n])].cpu().numpy().tobytes()
             paths = [pb[po[i]:po[i + 1]].decode() or None for i in range(n)]
         return keys, paths
 
@@ -795,7 +795,7 @@ class Engine:
     # -- K7: primary keys + bin paths as text ------------------------------------
     def primary_keys(self, b: RecordBatch, code: Optional[torch.Tensor] = None,
                      digest: Optional[torch.Tensor] = None, max_seq_len: int = 50, *,
-                     out: Optional["KeyText"] = None) -> "KeyText":
+                     out: Optional["KeyText"] = None, onepass: bool = True) -> "KeyText":
         """``generate_primary_key`` (and, with ``code``, the ltree bin path) for
         every record of ``b`` as text on the device.  Without ``out`` the size
         pass is followed by one host read of the totals; passing a ``KeyText``
@@ -809,6 +809,8 @@ class Engine:
         s = self._stream()
         code = self._dev(code)
         digest = self._dev(digest)
+        if onepass:
+            return self._primary_keys_onepass(b, code, digest, max_seq_len, out)
         if out is None:
             sz = ctypes.c_size_t()
             self.lib.avdb_format_workspace_size(n, ctypes.byref(sz))
@@ -828,6 +830,34 @@ class Engine:
                 *args, N.ptr(out.keys), out.keys.numel(), N.ptr(out.paths),
                 out.paths.numel() if out.paths is not None else 0, N.ptr(out.state), s))
         return out
+
+    def _primary_keys_onepass(self, b: RecordBatch, code, digest, max_seq_len: int, out) -> "KeyText":
+        """K7 in one launch (``avdb_primary_keys_onepass``): sizes, offsets
+        (look-back scan) and text; the text buffers are sized by
+        ``avdb_primary_keys_bound``, so no host sync is needed even the first time."""
+        n = b.n
+        sz = ctypes.c_size_t()
+        self.lib.avdb_primary_keys_onepass_workspace_size(n, ctypes.byref(sz))
+        kc, pc = ctypes.c_size_t(), ctypes.c_size_t()
+        self.lib.avdb_primary_keys_bound(n, b.heap.numel(), ctypes.byref(kc), ctypes.byref(pc))
+        if out is None:
+            out = KeyText(ws=self.empty(int(sz.value), torch.uint8), key_off=self.empty(n + 1, torch.int64),
+                          path_off=self.empty(n + 1, torch.int64) if code is not None else None,
+                          state=self.empty(max(1, n), torch.uint8), keys=self.empty(int(kc.value), torch.uint8),
+                          paths=self.empty(int(pc.value), torch.uint8) if code is not None else None)
+        if out.ws.numel() < sz.value:
+            out.ws = self.empty(int(sz.value), torch.uint8)
+        N.check("avdb_primary_keys_onepass", self.lib.avdb_primary_keys_onepass(
+            self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
+            N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), N.ptr(code), N.ptr(digest), n, int(max_seq_len),
+            N.ptr(out.ws), out.ws.numel(), N.ptr(out.key_off), N.ptr(out.path_off), N.ptr(out.keys), out.keys.numel(),
+            N.ptr(out.paths), out.paths.numel() if out.paths is not None else 0, N.ptr(out.state), self._stream()))
+        return out
+
+    def scan_errors(self, kt: "KeyText") -> int:
+        """Look-back waits of the last one-pass K7 launch on ``kt`` that gave up (0
+        unless something is broken; the tests check it)."""
+        return int(kt.ws[256:260].view(torch.int32).item())
 
     # -- K6: existing-variant key set ----------------------------------------
     def keyset_build(self, keys: torch.Tensor, key_off: torch.Tensor) -> torch.Tensor:

@@ -347,6 +347,23 @@ int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, 
                       size_t key_cap, uint8_t* path_out, size_t path_cap, uint8_t* key_state,
                       void* stream);
 
+/* K7 in ONE pass: each record's key and path sizes, their offsets (a decoupled
+ * look-back scan over 64-record tiles taken in launch order) and the text, in
+ * one launch that reads the SoA once.  Same inputs and outputs as
+ * avdb_primary_keys, except that key_off[n+1] / path_off[n+1] are OUTPUTS and the
+ * text buffers are sized in advance: avdb_primary_keys_bound gives capacities no
+ * batch of n records with heap_bytes of alleles can exceed.  workspace:
+ * avdb_primary_keys_onepass_workspace_size(n) bytes, 8-byte aligned. */
+int avdb_primary_keys_bound(size_t n, size_t heap_bytes, size_t* key_cap, size_t* path_cap);
+int avdb_primary_keys_onepass_workspace_size(size_t n, size_t* bytes);
+int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                              const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap,
+                              size_t heap_bytes, const uint64_t* ext_id, const uint32_t* bin_code,
+                              const char* digest, size_t n, uint32_t max_seq_len, void* workspace,
+                              size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off, uint8_t* key_out,
+                              size_t key_cap, uint8_t* path_out, size_t path_cap, uint8_t* key_state,
+                              void* stream);
+
 /* ---- K8: the per-record drop-in path in one launch -------------------------
  * The reference calls its per-record API once per alt allele
  * (vcf_variant_loader.py:282-311: __generate_primary_key, infer_variant_end_location,

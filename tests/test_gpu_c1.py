@@ -248,3 +248,27 @@ def test_k7_reused_buffers_flag_overflow(engine):
     assert ((st & 0x0F) == N.KEY_OK).sum() > 0  # the keys that fit were written
     with pytest.raises(ValueError):
         kt2.host(64)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 300001])
+def test_k7_onepass_equals_two_pass(engine, n):
+    """K7 in one launch (look-back scan over 64-record tiles) == the size pass +
+    scans + write pass: offsets, states, key and path text, at sizes that end off
+    every tile boundary; no look-back ever gave up."""
+    from annotatedvdb_amd import synth
+    digs = ["%032d" % (7 * i) for i in range(25)]
+    engine.set_sequence_digests(digs)
+    b = synth.alleles(n, seed=90 + n % 7, long_frac=0.05, device="cuda")
+    end, code, status, _ = engine.record_prep(b, want_lcp=False)
+    dig, _ = engine.vrs_digest(b, 50)
+    one = engine.primary_keys(b, code=code, digest=dig)
+    two = engine.primary_keys(b, code=code, digest=dig, onepass=False)
+    assert engine.scan_errors(one) == 0
+    for a, c in ((one.key_off, two.key_off), (one.path_off, two.path_off)):
+        assert torch.equal(a[: n + 1], c[: n + 1])
+    assert torch.equal(one.state[:n], two.state[:n])
+    kn, pn = int(two.key_off[n]), int(two.path_off[n])
+    assert torch.equal(one.keys[:kn], two.keys[:kn]) and torch.equal(one.paths[:pn], two.paths[:pn])
+    # and reused buffers: a second launch over the same KeyText
+    again = engine.primary_keys(b, code=code, digest=dig, out=one)
+    assert engine.scan_errors(again) == 0 and torch.equal(again.keys[:kn], two.keys[:kn])
