@@ -69,6 +69,14 @@ class FormatOpts(ctypes.Structure):
     def __init__(self, alg_id: bytes = b"", max_seq_len: int = 50, flags: int = 0):
         super().__init__(ctypes.sizeof(FormatOpts), max_seq_len, alg_id, flags)
 
+class VcfOpts(ctypes.Structure):
+    """avdb_vcf_opts (include/avdb.h); ``struct_size`` is filled in."""
+    _fields_ = [("struct_size", ctypes.c_uint32), ("min_fields", ctypes.c_uint32), ("chrom_map", ctypes.c_void_p)]
+
+    def __init__(self, min_fields: int = 0, chrom_map=None):
+        super().__init__(ctypes.sizeof(VcfOpts), min_fields, chrom_map)
+
+
 class LineResult(ctypes.Structure):
     """avdb_line_result (include/avdb.h)."""
     _fields_ = [(name, ctypes.c_uint32) for name in ("state", "flags", "copy_bytes", "map_bytes", "n_rec", "n_rows",
@@ -84,6 +92,7 @@ EXPORTED_SYMBOLS = [
     "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest",
     "avdb_format_bin_path", "avdb_format_bin_paths",
     "avdb_vcf_workspace_size", "avdb_vcf_count_lines", "avdb_vcf_parse_lines", "avdb_vcf_emit",
+    "avdb_chrom_map_create", "avdb_chrom_map_destroy",
     "avdb_format_workspace_size", "avdb_vcf_format_size", "avdb_vcf_format_write", "avdb_vcf_line_host",
     "avdb_display_attributes",
     "avdb_keyset_workspace_size", "avdb_keyset_build", "avdb_keyset_probe",
@@ -153,15 +162,17 @@ def _sig(lib):
     f.avdb_format_bin_paths.argtypes = [P, P, P, SZ, P, SZ, P]
     f.avdb_vcf_workspace_size.argtypes = [SZ, SZ, ctypes.POINTER(SZ)]
     f.avdb_vcf_count_lines.argtypes = [P, P, SZ, P, SZ, P, P]
-    f.avdb_vcf_parse_lines.argtypes = [P, P, SZ, SZ, P, P, SZ, P, P, P, P]
+    f.avdb_vcf_parse_lines.argtypes = [P, P, SZ, SZ, P, P, SZ, P, P, P, ctypes.POINTER(VcfOpts), P]
+    f.avdb_chrom_map_create.argtypes = [P, P, P, SZ, P, ctypes.POINTER(P)]
+    f.avdb_chrom_map_destroy.argtypes = [P]
     f.avdb_vcf_emit.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, P, P, P, P, P, P]
     f.avdb_format_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_vcf_format_size.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, ctypes.POINTER(FormatOpts),
                                        P, SZ, P, P, P, P]
     f.avdb_vcf_format_write.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, ctypes.POINTER(FormatOpts),
                                         P, P, P, P, P, P, P]
-    f.avdb_vcf_line_host.argtypes = [P, ctypes.c_char_p, SZ, ctypes.POINTER(FormatOpts), P, SZ, P, SZ,
-                                     ctypes.POINTER(LineResult)]
+    f.avdb_vcf_line_host.argtypes = [P, ctypes.c_char_p, SZ, ctypes.POINTER(FormatOpts), ctypes.POINTER(VcfOpts), P, SZ,
+                                     P, SZ, ctypes.POINTER(LineResult)]
     f.avdb_display_attributes.argtypes = [P, P, P, P, P, P, P, P, SZ, SZ, P, SZ, P, P, P, P]
     f.avdb_keyset_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_build.argtypes = [P, P, P, SZ, P, SZ, P]

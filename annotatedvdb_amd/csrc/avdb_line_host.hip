@@ -35,8 +35,8 @@ thread_local LineScratch g_scratch;
 }  // namespace
 
 extern "C" int avdb_vcf_line_host(const avdb_ctx* ctx, const char* line, size_t len, const avdb_format_opts* opts,
-                                  char* copy_out, size_t copy_cap, char* map_out, size_t map_cap,
-                                  avdb_line_result* res) {
+                                  const avdb_vcf_opts* vopts, char* copy_out, size_t copy_cap, char* map_out,
+                                  size_t map_cap, avdb_line_result* res) {
   if (!ctx || (!line && len) || !opts || !res) {
     avdb_set_error("avdb_vcf_line_host: null argument");
     return AVDB_EINVAL;
@@ -44,6 +44,11 @@ extern "C" int avdb_vcf_line_host(const avdb_ctx* ctx, const char* line, size_t 
   if (opts->struct_size != sizeof(avdb_format_opts)) {
     avdb_set_error("avdb_vcf_line_host: avdb_format_opts.struct_size %u, this library expects %zu (ABI %d)",
                    opts->struct_size, sizeof(avdb_format_opts), AVDB_ABI_VERSION);
+    return AVDB_EINVAL;
+  }
+  if (vopts && vopts->struct_size != sizeof(avdb_vcf_opts)) {
+    avdb_set_error("avdb_vcf_line_host: avdb_vcf_opts.struct_size %u, this library expects %zu",
+                   vopts->struct_size, sizeof(avdb_vcf_opts));
     return AVDB_EINVAL;
   }
   if (opts->match || opts->adsp_dup) {
@@ -65,7 +70,9 @@ extern "C" int avdb_vcf_line_host(const avdb_ctx* ctx, const char* line, size_t 
   avdb_vcf_line L;
   memset(&L, 0, sizeof(L));
   uint64_t recs = 0, hbytes = 0;
-  parse_line(static_cast<const uint8_t*>(s), [lw](uint32_t k) { return lw[k]; }, 0u, uint32_t(len), L, recs, hbytes);
+  const ChromMapView cm = vopts && vopts->chrom_map ? vopts->chrom_map->host_view() : ChromMapView{};
+  parse_line(static_cast<const uint8_t*>(s), [lw](uint32_t k) { return lw[k]; }, 0u, uint32_t(len), L, recs, hbytes,
+             cm, vopts ? vopts->min_fields : 0u);
   res->flags = L.flags;
   if (L.flags & AVDB_VCF_COMMENT) {
     res->state = AVDB_LINE_SKIP;

@@ -189,7 +189,8 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
                                                       const uint64_t* __restrict__ starts,
                                                       avdb_vcf_line* __restrict__ lines,
                                                       unsigned long long* __restrict__ rec_cnt,
-                                                      unsigned long long* __restrict__ heap_cnt) {
+                                                      unsigned long long* __restrict__ heap_cnt,
+                                                      ChromMapView cm, uint32_t min_fields) {
   __shared__ u32x4 s_text[kStage / 16];
   const Heap h = make_heap(text, text_bytes);
   for (size_t base = size_t(blockIdx.x) * kBlock; base < n_lines; base += size_t(gridDim.x) * kBlock) {
@@ -208,11 +209,11 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
       if (w.staged) {
         const uint8_t* ls = reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0);
         const lds_cp64 lw = (lds_cp64)(reinterpret_cast<const uint64_t*>(ls - mis));
-        parse_line((lds_cp)ls, [lw](uint32_t k) { return lw[k]; }, mis, raw, L, recs, hbytes);
+        parse_line((lds_cp)ls, [lw](uint32_t k) { return lw[k]; }, mis, raw, L, recs, hbytes, cm, min_fields);
       } else {
         const uintptr_t la = h.lo + L.start - mis;
         parse_line((glb_cp)(text + L.start), [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); },
-                   mis, raw, L, recs, hbytes);
+                   mis, raw, L, recs, hbytes, cm, min_fields);
       }
       lines[li] = L;
       rec_cnt[li] = recs;
@@ -349,11 +350,22 @@ extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
                                     size_t n_lines, const void* line_counts, void* workspace,
                                     size_t workspace_bytes,
                                     avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off,
-                                    void* stream) {
+                                    const avdb_vcf_opts* opts, void* stream) {
   if (!ctx || !lines || !rec_off || !heap_off) {
     avdb_set_error("avdb_vcf_parse_lines: null argument");
     return AVDB_EINVAL;
   }
+  if (opts && opts->struct_size != sizeof(avdb_vcf_opts)) {
+    avdb_set_error("avdb_vcf_parse_lines: avdb_vcf_opts.struct_size %u, this library expects %zu",
+                   opts->struct_size, sizeof(avdb_vcf_opts));
+    return AVDB_EINVAL;
+  }
+  if (opts && opts->chrom_map && opts->chrom_map->device != ctx->device) {
+    avdb_set_error("avdb_vcf_parse_lines: chromosome map made for device %d", opts->chrom_map->device);
+    return AVDB_EINVAL;
+  }
+  const ChromMapView cm = opts && opts->chrom_map ? opts->chrom_map->dev : ChromMapView{};
+  const uint32_t min_fields = opts ? opts->min_fields : 0u;
   size_t need = 0;
   avdb_vcf_workspace_size(text_bytes, n_lines, &need);
   if (!workspace || workspace_bytes < need) {
@@ -382,7 +394,7 @@ extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
   AVDB_HIP_TRY(hipMemsetAsync(hc + n_lines, 0, 8, s));
   const unsigned grid = stream_grid(n_lines, kBlock, 4096);
   hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, starts,
-                     lines, rc, hc);
+                     lines, rc, hc, cm, min_fields);
   AVDB_LAUNCH_CHECK("k_vcf_parse");
   AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, rc, rc, n_lines + 1, s));
   AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, hc, hc, n_lines + 1, s));
@@ -407,5 +419,78 @@ extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_byt
                      text, text_bytes, n_lines, lines, rec_off, heap_off, chrom, pos, allele_off, ref_len,
                      alt_len, ext_id, heap, rec_line, rec_alt);
   AVDB_LAUNCH_CHECK("k_vcf_emit");
+  return AVDB_OK;
+}
+
+// ---- chromosome map (ChromosomeMap.get, chromosome_map_parser.py:84-91) ----------
+extern "C" int avdb_chrom_map_create(avdb_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, size_t n_keys,
+                                     const uint8_t* codes, avdb_chrom_map** out) {
+  if (!ctx || !out || (n_keys && (!keys || !key_off || !codes)) || n_keys >= (1u << 24)) {
+    avdb_set_error("avdb_chrom_map_create: null argument or more than 2^24-1 keys");
+    return AVDB_EINVAL;
+  }
+  *out = nullptr;
+  avdb_chrom_map* m = new (std::nothrow) avdb_chrom_map();
+  if (!m) return AVDB_ENOMEM;
+  m->device = ctx->device;
+  m->d_mem = nullptr;
+  size_t slots = 16;
+  while (slots < 2 * n_keys + 2) slots <<= 1;
+  m->slot.assign(slots, 0);
+  m->key_off.resize(n_keys + 1);
+  m->code.assign(codes, codes + n_keys);
+  const size_t total = n_keys ? key_off[n_keys] : 0;
+  if (total >= (1ull << 32)) {
+    delete m;
+    avdb_set_error("avdb_chrom_map_create: keys too long");
+    return AVDB_EINVAL;
+  }
+  m->keys.assign(keys, keys + total);
+  m->keys.push_back(0);
+  for (size_t k = 0; k <= n_keys; ++k) m->key_off[k] = uint32_t(key_off[k]);
+  for (size_t k = 0; k < n_keys; ++k) {
+    if (key_off[k + 1] < key_off[k] || key_off[k + 1] > total) {
+      delete m;
+      avdb_set_error("avdb_chrom_map_create: key_off not ascending");
+      return AVDB_EINVAL;
+    }
+    const uint64_t h = fnv1a(m->keys.data() + key_off[k], uint32_t(key_off[k + 1] - key_off[k]));
+    uint32_t q = uint32_t(h) & uint32_t(slots - 1);
+    while (m->slot[q]) q = (q + 1) & uint32_t(slots - 1);  // duplicate keys: the first stays found first
+    m->slot[q] = ((h >> 24) << 24) | uint64_t(k + 1);
+  }
+  if (ctx->device >= 0) {
+    const size_t b_slot = 8 * slots, b_off = 4 * (n_keys + 1), b_code = n_keys + 8, b_keys = m->keys.size();
+    const size_t o_off = b_slot, o_code = o_off + ((b_off + 7) & ~size_t(7)), o_keys = o_code + ((b_code + 7) & ~size_t(7));
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipMalloc(&m->d_mem, o_keys + b_keys);
+    char* d = static_cast<char*>(m->d_mem);
+    if (e == hipSuccess) e = hipMemcpy(d, m->slot.data(), b_slot, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + o_off, m->key_off.data(), b_off, hipMemcpyHostToDevice);
+    if (e == hipSuccess && n_keys) e = hipMemcpy(d + o_code, m->code.data(), n_keys, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + o_keys, m->keys.data(), b_keys, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      if (m->d_mem) (void)hipFree(m->d_mem);
+      delete m;
+      avdb_set_error("avdb_chrom_map_create: %s", hipGetErrorString(e));
+      return AVDB_EHIP;
+    }
+    m->dev = ChromMapView{reinterpret_cast<const uint64_t*>(d), reinterpret_cast<const uint8_t*>(d + o_keys),
+                          reinterpret_cast<const uint32_t*>(d + o_off), reinterpret_cast<const uint8_t*>(d + o_code),
+                          uint32_t(slots - 1)};
+  } else {
+    m->dev = ChromMapView{};
+  }
+  *out = m;
+  return AVDB_OK;
+}
+
+extern "C" int avdb_chrom_map_destroy(avdb_chrom_map* m) {
+  if (!m) return AVDB_OK;
+  if (m->d_mem) {
+    (void)hipSetDevice(m->device);
+    (void)hipFree(m->d_mem);
+  }
+  delete m;
   return AVDB_OK;
 }

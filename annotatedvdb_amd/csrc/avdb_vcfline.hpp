@@ -7,6 +7,8 @@
 
 #include "avdb_text.hpp"
 
+#include <vector>
+
 namespace avdb {
 
 // contig code of a CHROM field (vcf_parser.py:133-150 + bin_index.py:64): plain
@@ -48,6 +50,57 @@ AVDB_HD uint8_t chrom_code_of(CP p, uint32_t n, bool* host) {
     const uint32_t v = (lab[0] - '0') * 10 + (lab[1] - '0');
     return (v >= 10 && v <= 22) ? uint8_t(v - 1) : 255;
   }
+  return 255;
+}
+
+// ---- chromosome map (ChromosomeMap.get, chromosome_map_parser.py:84-91, applied
+// by VcfEntryParser.update_chromosome, vcf_parser.py:117-124): CHROM bytes ->
+// contig code through an open-addressing table built by avdb_chrom_map_create.
+// Slot = (FNV-1a hash high 40 bits << 24) | (key index + 1); 0 = empty.  code[k]
+// is the contig code of the mapped chromosome, or 0xFF when the line must be
+// rendered by the host (a key Python would coerce to a number never matches a
+// CHROM string: the reference's KeyError).  A CHROM not in the map is host too.
+struct ChromMapView {
+  const uint64_t* slot;
+  const uint8_t* keys;
+  const uint32_t* key_off;
+  const uint8_t* code;
+  uint32_t mask;  // slots - 1; 0 (with slot == nullptr): no map
+};
+
+AVDB_HD uint64_t fnv1a(const uint8_t* p, uint32_t n) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (uint32_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+  return h;
+}
+
+template <class CP>
+AVDB_HD uint64_t fnv1a_cp(CP p, uint32_t n) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (uint32_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+  return h;
+}
+
+// contig code of the mapped CHROM, or 255 with *host set
+template <class CP>
+AVDB_HD uint8_t chrom_map_code(const ChromMapView& cm, CP p, uint32_t n, bool* host) {
+  const uint64_t h = fnv1a_cp(p, n);
+  const uint64_t tag = h >> 24;
+  for (uint32_t q = uint32_t(h) & cm.mask, k = 0; k <= cm.mask; q = (q + 1) & cm.mask, ++k) {
+    const uint64_t v = cm.slot[q];
+    if (!v) break;
+    if ((v >> 24) != tag) continue;
+    const uint32_t idx = uint32_t(v & 0xFFFFFFu) - 1;
+    const uint32_t k0 = cm.key_off[idx], kn = cm.key_off[idx + 1] - k0;
+    if (kn != n) continue;
+    bool eq = true;
+    for (uint32_t i = 0; i < n && eq; ++i) eq = cm.keys[k0 + i] == p[i];
+    if (!eq) continue;
+    const uint8_t c = cm.code[idx];
+    *host = c == 0xFF;
+    return c;
+  }
+  *host = true;
   return 255;
 }
 
@@ -118,7 +171,8 @@ constexpr uint64_t kSemi = 0x3B3B3B3B3B3B3B3Bull;
 template <class CP, class WordAt>
 AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
                                            uint32_t len, avdb_vcf_line& L, uint64_t& recs,
-                                           uint64_t& hbytes) {
+                                           uint64_t& hbytes, const ChromMapView& cm = ChromMapView{},
+                                           uint32_t min_fields = 8) {
     while (len && is_ws(s[len - 1])) --len;  // str.rstrip()
     L.len = len;
     L.flags = 0;
@@ -161,7 +215,8 @@ AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
     recs = 0;
     hbytes = 0;
     if (!(L.flags & (AVDB_VCF_COMMENT | AVDB_VCF_EMPTY))) {
-      if (nf < 8) L.flags |= AVDB_VCF_FEW_FIELDS;
+      // fewer values than header fields: the reference's IndexError (vcf_parser.py:90-112)
+      if (nf < 8 || nf < min_fields) L.flags |= AVDB_VCF_FEW_FIELDS;
       const uint32_t nfields = nf < 8 ? nf : 8;
       auto fend = [&](int k) -> uint32_t {  // end of field k (exclusive)
         return (k + 1 < int(nfields)) ? L.field[k + 1] - 1 : (k == 7 ? L.field_end8 : len);
@@ -169,7 +224,7 @@ AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
       if (!(L.flags & AVDB_VCF_FEW_FIELDS)) {
         // CHROM
         bool host = false;
-        L.chrom = chrom_code_of(s, fend(0), &host);
+        L.chrom = cm.slot ? chrom_map_code(cm, s, fend(0), &host) : chrom_code_of(s, fend(0), &host);
         if (host) L.flags |= AVDB_VCF_CHROM_HOST;
         // POS: plain decimal < 2^32
         {
@@ -309,3 +364,18 @@ AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
 }
 
 }  // namespace avdb
+
+// the chromosome map object of the C ABI: the table on the host (K5h, the per-line
+// host entry) and on the device (K0's parse kernel)
+struct avdb_chrom_map {
+  int device;
+  std::vector<uint64_t> slot;
+  std::vector<uint8_t> keys;
+  std::vector<uint32_t> key_off;
+  std::vector<uint8_t> code;
+  void* d_mem;  // one device allocation: slot | key_off | code | keys
+  avdb::ChromMapView host_view() const {
+    return avdb::ChromMapView{slot.data(), keys.data(), key_off.data(), code.data(), uint32_t(slot.size() - 1)};
+  }
+  avdb::ChromMapView dev;
+};

@@ -415,6 +415,59 @@ class SmallPrep:
         return out
 
 
+class ChromMap:
+    """``avdb_chrom_map`` of a ChromosomeMap's ``source_id -> chromosome`` dict
+    (chromosome_map_parser.py:51-91).  For each source id the host decides once
+    what the reference's per-line code makes of it — ``update_chromosome`` then
+    ``get_variant`` (xstr, 'MT' -> 'M', 'chr' removed, vcf_parser.py:117-155) —
+    and gives the kernels the contig code, or 0xFF (the line is rendered by the
+    host) when the result is not a canonical contig label, or when the source id
+    is text Python would coerce to a number (a CHROM field equal to it becomes an
+    int before the lookup and never matches: KeyError)."""
+
+    def __init__(self, engine: "Engine", mapping: Dict):
+        from .chromosomes import CHROM_NAMES as names, bin_index_chrom_code
+        from .parsers import to_numeric
+        self.eng, self.mapping = engine, mapping
+        keys, codes = [], []
+        for k, v in mapping.items():
+            if not isinstance(k, str):
+                continue  # a CHROM field is a str (or a number): never this key
+            try:
+                kb = k.encode("ascii")
+            except UnicodeEncodeError:
+                continue  # K0 flags non-ASCII lines for the host anyway
+            chrom = "" if v is None else str(v)
+            if chrom == "MT":
+                chrom = "M"
+            chrom = chrom.replace("chr", "")
+            c = bin_index_chrom_code(chrom)
+            ok = c < len(names) and names[c] == chrom and isinstance(to_numeric(k), str)
+            keys.append(kb)
+            codes.append(c if ok else 0xFF)
+        off = np.zeros(len(keys) + 1, dtype=np.uint64)
+        if keys:
+            off[1:] = np.cumsum([len(k) for k in keys])
+        blob = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8)
+        cd = np.asarray(codes or [0], dtype=np.uint8)
+        h = ctypes.c_void_p()
+        N.check("avdb_chrom_map_create", engine.lib.avdb_chrom_map_create(
+            engine.ctx, blob.ctypes.data, off.ctypes.data, len(keys), cd.ctypes.data, ctypes.byref(h)))
+        self.handle = h.value
+        self.n_keys = len(keys)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.eng.lib.avdb_chrom_map_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class LineHost:
     """K5h (``avdb_vcf_line_host``): one VCF line -> its COPY rows and .mapping
     line, rendered by the library's host code with the kernels' own per-line
@@ -434,18 +487,19 @@ class LineHost:
         self._map = ctypes.create_string_buffer(self.cap)
         self._ca, self._ma = ctypes.addressof(self._copy), ctypes.addressof(self._map)
 
-    def run(self, line: bytes, alg_id: bytes, max_seq_len: int = 50, adsp: bool = False):
+    def run(self, line: bytes, alg_id: bytes, max_seq_len: int = 50, adsp: bool = False, vcf_opts=None):
         """``(state, copy_text, mapping_text, result)``; the texts are None unless
-        state == LINE_GPU (rendered)."""
+        state == LINE_GPU (rendered).  ``vcf_opts``: header width / chromosome map."""
         o = self.opts
         o.alg_id, o.max_seq_len, o.flags = alg_id, max_seq_len, N.FORMAT_ADSP if adsp else 0
         r = self.res
-        rc = self.eng.lib.avdb_vcf_line_host(self.eng.ctx, line, len(line), ctypes.byref(o), self._ca, self.cap,
+        vo = ctypes.byref(vcf_opts) if vcf_opts is not None else None
+        rc = self.eng.lib.avdb_vcf_line_host(self.eng.ctx, line, len(line), ctypes.byref(o), vo, self._ca, self.cap,
                                              self._ma, self.cap, ctypes.byref(r))
         if rc == N.AVDB_ERANGE:
             self._grow(2 * max(r.copy_bytes, r.map_bytes))
-            rc = self.eng.lib.avdb_vcf_line_host(self.eng.ctx, line, len(line), ctypes.byref(o), self._ca, self.cap,
-                                                 self._ma, self.cap, ctypes.byref(r))
+            rc = self.eng.lib.avdb_vcf_line_host(self.eng.ctx, line, len(line), ctypes.byref(o), vo, self._ca,
+                                                 self.cap, self._ma, self.cap, ctypes.byref(r))
         N.check("avdb_vcf_line_host", rc)
         if r.state != N.LINE_GPU:
             return r.state, None, None, r
@@ -510,6 +564,19 @@ class Engine:
         if sp is None:
             sp = self._small = SmallPrep(self)
         return sp
+
+    def chrom_map(self, mapping: Dict, key=None) -> "ChromMap":
+        """A ChromosomeMap's ``source_id -> chromosome`` dict as a library map
+        (device table for K0, host table for K5h), cached per ``key``."""
+        cache = self.__dict__.setdefault("_chrom_maps", {})
+        k = key if key is not None else id(mapping)
+        cm = cache.get(k)
+        if cm is None or cm.mapping is not mapping:
+            cm = cache[k] = ChromMap(self, mapping)
+        return cm
+
+    def vcf_opts(self, min_fields: int = 0, chrom_map: Optional["ChromMap"] = None) -> "N.VcfOpts":
+        return N.VcfOpts(min_fields, chrom_map.handle if chrom_map is not None else None)
 
     def line_host(self) -> LineHost:
         """The engine's K5h per-line renderer (created on first use)."""
@@ -648,9 +715,10 @@ class Engine:
         return [raw[i * 32:(i + 1) * 32].decode("ascii") for i in range(n)]
 
     # -- K0: VCF text -> records ---------------------------------------------
-    def vcf_tokenize(self, text) -> "VcfBatch":
+    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None) -> "VcfBatch":
         """Parse VCF data lines (bytes or a uint8 tensor) on the GPU into the
-        record SoA (one row per ALT != '.') plus the per-line table."""
+        record SoA (one row per ALT != '.') plus the per-line table.
+        ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map."""
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
             t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
@@ -678,7 +746,7 @@ class Engine:
         heap_off = self.empty(n_lines + 1, torch.int64)
         N.check("avdb_vcf_parse_lines", self.lib.avdb_vcf_parse_lines(
             self.ctx, tp, nb, n_lines, N.ptr(ws0), N.ptr(ws), ws.numel(), N.ptr(lines), N.ptr(rec_off),
-            N.ptr(heap_off), s))
+            N.ptr(heap_off), ctypes.byref(vcf_opts) if vcf_opts is not None else None, s))
         if n_lines:
             tot = torch.stack([rec_off[n_lines], heap_off[n_lines]]).cpu().tolist()
         else:

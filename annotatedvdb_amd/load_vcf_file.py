@@ -53,6 +53,8 @@ def parse_args(argv: Optional[Sequence[str]] = None):
                     help="chrom<TAB>refget-digest (or JSON) file for long-allele keys")
     ap.add_argument("--datasource", default="dbSNP",
                     choices=["dbSNP", "DBSNP", "dbsnp", "ADSP", "ADSP-FunGen", "NIAGADS", "EVA"])
+    ap.add_argument("-m", "--chromosomeMap", help="tab-delimited source_id -> chromosome map (e.g. RefSeq "
+                    "accessions used as CHROM), parsers.ChromosomeMap")
     ap.add_argument("--skipExisting", action="store_true")
     ap.add_argument("--existing", help="export of AnnotatedVDB.Variant: metaseq_id<TAB>record_primary_key<TAB>bin_index")
     ap.add_argument("--algInvocationId", default="0", help="row_algorithm_id of the COPY rows")
@@ -123,6 +125,9 @@ def make_loader(args, device: int):
     ld.initialize_bin_indexer(None)
     ld.set_algorithm_invocation_id(args.algInvocationId)
     ld.initialize_copy_sql()
+    if args.chromosomeMap:
+        from .parsers import ChromosomeMap
+        ld.set_chromosome_map(ChromosomeMap(args.chromosomeMap))
     if args.skipExisting:
         from .existing import ExistingVariants
         ld.set_skip_existing(True, existing=ExistingVariants.from_tsv(args.existing, engine=ld._engine))
@@ -132,7 +137,8 @@ def make_loader(args, device: int):
 def rank_text(raw: bytes, loader, plan, rank: int) -> bytes:
     """The lines of ``raw`` the piece plan gives to ``rank`` (K0 + K9 on the GPU)."""
     eng = loader._engine
-    vb = eng.vcf_tokenize(raw)
+    vo = loader._gpu_vcf_opts()  # chromosome map: lines are placed by their mapped contig
+    vb = eng.vcf_tokenize(raw, vo if isinstance(vo, type(eng.vcf_opts())) else None)
     return eng.vcf_select(vb, plan, rank).cpu().numpy().tobytes()
 
 

@@ -155,6 +155,28 @@ class VCFVariantLoader(object):
     def set_vcf_header_fields(self, fields):
         self._vcf_header_fields = fields
 
+    def _gpu_vcf_opts(self):
+        """K0 / K5h options for this loader's header fields and chromosome map, or
+        ``_SLOW`` when the text must be parsed line by line on the host: a header
+        whose first eight fields are not the standard ones (their positions would
+        move), or a chromosome map object without its ``chromosome_map()`` dict."""
+        from .parsers import DEFAULT_FIELDS
+        min_fields = 0
+        if self._vcf_header_fields:
+            hf = [x.lower().replace("#", "") for x in self._vcf_header_fields]
+            if hf[:8] != DEFAULT_FIELDS:
+                return _SLOW
+            min_fields = len(hf)
+        cm = None
+        if self._chromosome_map is not None:
+            get_map = getattr(self._chromosome_map, "chromosome_map", None)
+            if get_map is None:
+                return _SLOW
+            cm = self._engine.chrom_map(get_map(), key=id(self._chromosome_map))
+        if not min_fields and cm is None:
+            return None
+        return self._engine.vcf_opts(min_fields, cm)
+
     def vcf_header_fields(self):
         return self._vcf_header_fields
 
@@ -316,13 +338,14 @@ class VCFVariantLoader(object):
                 or self.is_adsp() or self._resume is not True):
             return _SLOW
         out = _SLOW
-        if self._chromosome_map is None and not self._vcf_header_fields:
-            out = self._parse_line_k5h(line)
+        vo = self._gpu_vcf_opts()
+        if vo is not _SLOW:
+            out = self._parse_line_k5h(line, vo)
         if out is _SLOW:
             out = self._parse_line_k8h(line)
         return out
 
-    def _parse_line_k5h(self, line):
+    def _parse_line_k5h(self, line, vcf_opts=None):
         """The whole line in one library call (K5h, ``avdb_vcf_line_host``): COPY
         rows and the .mapping line as the K5 kernels render them."""
         try:
@@ -330,7 +353,7 @@ class VCFVariantLoader(object):
         except UnicodeEncodeError:
             return _SLOW
         st, copy, mp, r = self._engine.line_host().run(raw, _xstr(self._alg_invocation_id).encode(),
-                                                       self._pk_generator.max_sequence_length())
+                                                       self._pk_generator.max_sequence_length(), vcf_opts=vcf_opts)
         if copy is None:
             return _SLOW
         # .mapping line: id TAB [{'primary_key': '<pk>', 'bin_index': '<path>'}, ...] (keys and
@@ -505,12 +528,13 @@ class VCFVariantLoader(object):
         from types import SimpleNamespace
         if self._bin_indexer is None or self._pk_generator is None:
             raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
-        if not self.resume_load() or self._chromosome_map is not None or self._vcf_header_fields:
-            # resume / chromosome maps / custom headers: exact per-line semantics
+        vo = self._gpu_vcf_opts()
+        if not self.resume_load() or vo is _SLOW:
+            # resume / a header with moved fields: exact per-line semantics
             return self.parse_variants(_data_lines(bytes(text)), errors=errors, dedup=dedup)
         raw = bytes(text)
         eng = self._engine
-        vb = eng.vcf_tokenize(raw)
+        vb = eng.vcf_tokenize(raw, vo)
         L = vb.lines_host()
         db = vb.records
         rec_line = vb.rec_line.cpu().numpy()
@@ -535,7 +559,8 @@ class VCFVariantLoader(object):
             code = int(rec["chrom"])
             try:
                 if fl & (VCF_HOST_FLAGS | 0x102) or code == 255 or int(rec["n_rec"]) == 0:
-                    entry = VcfEntryParser(line)
+                    entry = VcfEntryParser(line, self._vcf_header_fields)
+                    entry.update_chromosome(self._chromosome_map)
                     v = entry.get_variant(dbSNP=self.is_dbsnp(), namespace=True)
                     if fl & VCF_HOST_FLAGS:
                         host_patch[li] = (min(bin_index_chrom_code(v.chromosome), 255), v.position,
@@ -655,15 +680,15 @@ class VCFVariantLoader(object):
         from . import _native as N
         if self._bin_indexer is None or self._pk_generator is None:
             raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
-        if (not self.resume_load() or self._chromosome_map is not None or self._vcf_header_fields
-                or (self.is_adsp() and self._existing is None)):
-            # resume / chromosome maps / custom headers / ADSP without a validator
-            # (the reference's is_duplicate raises on it): exact per-line semantics
+        vo = self._gpu_vcf_opts()
+        if not self.resume_load() or vo is _SLOW or (self.is_adsp() and self._existing is None):
+            # resume / a header with moved fields / ADSP without a validator (the
+            # reference's is_duplicate raises on it): exact per-line semantics
             out = self.parse_variants(_data_lines(raw), errors=errors, dedup=dedup)
             return "".join("".join("%s\t%s\n" % kv for kv in o.items()) for o in out
                            if isinstance(o, dict))
         eng = self._engine
-        vb = eng.vcf_tokenize(raw)
+        vb = eng.vcf_tokenize(raw, vo)
         n = vb.n_lines
         if n == 0:
             return ""
@@ -820,8 +845,9 @@ class VCFVariantLoader(object):
             w = np.frombuffer(Lh[k].tobytes(), dtype=np.uint64)
             st, ln = int(w[0]), int(w[1] & 0xFFFFFFFF)
             try:
-                v = VcfEntryParser(raw[st:st + ln].decode("utf-8")).get_variant(dbSNP=self.is_dbsnp(),
-                                                                               namespace=True)
+                e = VcfEntryParser(raw[st:st + ln].decode("utf-8"), self._vcf_header_fields)
+                e.update_chromosome(self._chromosome_map)
+                v = e.get_variant(dbSNP=self.is_dbsnp(), namespace=True)
             except Exception:  # noqa: BLE001 — the host renderer raises it at this line
                 continue
             key = interner.key(v.ref_snp_id)

@@ -11,6 +11,7 @@ delegated to the GPU-backed ``VariantAnnotator``.
 
 from __future__ import annotations
 
+import csv
 import re
 from types import SimpleNamespace
 
@@ -216,3 +217,33 @@ class VcfEntryParser(object):
     def __verify_entry(self):
         assert self.__entry is not None, \
             "DEBUG - must set value of _entry in the VCF parser before attempting to access"
+
+
+class ChromosomeMap(object):
+    """Drop-in for ``ChromosomeMap`` (Util/lib/python/parsers/chromosome_map_parser.py:
+    27-91): a tab-delimited file with ``source_id`` and ``chromosome`` columns
+    (e.g. RefSeq accession -> chromosome); values lose their ``chr``.  ``get``
+    raises ``KeyError`` for an unknown id, as the reference's dict lookup does.
+    The loaders hand ``chromosome_map()`` to the K0 tokenizer / K5h (an
+    ``avdb_chrom_map`` table) instead of calling ``get`` per line."""
+
+    def __init__(self, fileName, verbose=False, debug=False):
+        self._verbose = verbose
+        self._debug = debug
+        self._fileName = fileName
+        with open(fileName, "r") as fh:
+            self._map = {row["source_id"]: row["chromosome"].replace("chr", "")
+                         for row in csv.DictReader(fh, delimiter="\t")}
+
+    def chromosome_map(self):
+        return self._map
+
+    def get_sequence_id(self, chrmNum):
+        """The first source id mapped to ``chrmNum`` (or 'chr' + it), else None."""
+        for sequenceId, cn in self._map.items():
+            if cn == chrmNum or cn == "chr" + _xstr(chrmNum):
+                return sequenceId
+        return None
+
+    def get(self, sequenceId):
+        return self._map[sequenceId]

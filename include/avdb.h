@@ -212,10 +212,31 @@ typedef struct avdb_vcf_line {
 int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes);
 int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
                          size_t workspace_bytes, uint64_t* n_newlines, void* stream);
+/* Parse options (nullable = the default 8-field header, no chromosome map):
+ *   min_fields  the loader's header width (VCFVariantLoader.set_vcf_header_fields,
+ *               vcf_variant_loader.py:88-93,368, for a header whose first eight fields are
+ *               the standard ones, e.g. a pVCF): a line with fewer values is flagged
+ *               AVDB_VCF_FEW_FIELDS (the reference raises IndexError there);
+ *   chrom_map   VcfEntryParser.update_chromosome (vcf_parser.py:117-124) with a
+ *               ChromosomeMap (chromosome_map_parser.py:84-91): CHROM is looked up as
+ *               bytes; a CHROM not in the map, or mapped to a key the host must
+ *               resolve, is flagged AVDB_VCF_CHROM_HOST (the reference raises KeyError). */
+typedef struct avdb_chrom_map avdb_chrom_map;
+typedef struct avdb_vcf_opts {
+  uint32_t struct_size;             /* sizeof(avdb_vcf_opts) */
+  uint32_t min_fields;
+  const avdb_chrom_map* chrom_map;  /* nullable */
+} avdb_vcf_opts;
+/* keys (host): the map's source ids, keys[key_off[k] .. key_off[k+1]); codes[k] (host):
+ * the contig code of the chromosome source id k maps to, 0xFF = lines with this CHROM
+ * are rendered by the caller.  The first of duplicate keys wins. */
+int avdb_chrom_map_create(avdb_ctx* ctx, const uint8_t* keys_host, const uint64_t* key_off_host, size_t n_keys,
+                          const uint8_t* codes_host, avdb_chrom_map** out);
+int avdb_chrom_map_destroy(avdb_chrom_map* map);
 int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
                          const void* line_counts, void* workspace, size_t workspace_bytes,
                          avdb_vcf_line* lines,
-                         uint64_t* rec_off, uint64_t* heap_off, void* stream);
+                         uint64_t* rec_off, uint64_t* heap_off, const avdb_vcf_opts* opts, void* stream);
 int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
                   const avdb_vcf_line* lines, const uint64_t* rec_off, const uint64_t* heap_off,
                   uint8_t* chrom, uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len,
@@ -290,6 +311,7 @@ int avdb_vcf_format_write(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes,
  * bytes the K5 kernels write for this line), AVDB_LINE_HOST = the caller renders
  * it (same rules as K5: non-canonical text, long alleles, unmappable records, ...),
  * AVDB_LINE_SKIP = comment.  opts: alg_id, max_seq_len, flags (AVDB_FORMAT_ADSP);
+ * vcf_opts (nullable): header width and chromosome map as for avdb_vcf_parse_lines;
  * match / adsp_dup must be NULL (batch features).  Returns AVDB_ERANGE when a
  * buffer is short (res holds the sizes).  A context made with device = -1
  * suffices; thread-safe per calling thread. */
@@ -306,7 +328,8 @@ typedef struct avdb_line_result {
   uint32_t reserved;
 } avdb_line_result;
 int avdb_vcf_line_host(const avdb_ctx* ctx, const char* line, size_t len, const avdb_format_opts* opts,
-                       char* copy_out, size_t copy_cap, char* map_out, size_t map_cap, avdb_line_result* res);
+                       const avdb_vcf_opts* vcf_opts, char* copy_out, size_t copy_cap, char* map_out,
+                       size_t map_cap, avdb_line_result* res);
 /* get_display_attributes (variant_annotator.py:134-241) of a record batch as
  * json.dumps text (ASCII alleles; json escaping applied).  end = K2's end.
  * Call with out == NULL first: rec_state[i] (0 ok, 1 non-ASCII allele, 2 heap

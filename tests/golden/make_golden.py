@@ -616,6 +616,96 @@ def run_load_driver(lines):
     return rows
 
 
+# RefSeq accessions of the GRCh38 primary assembly (NC_0000xx.yy; MT = NC_012920.1), the
+# CHROM values of NCBI's own dbSNP VCFs: what chromosome maps translate
+REFSEQ = {"1": "NC_000001.11", "2": "NC_000002.12", "3": "NC_000003.12", "4": "NC_000004.12",
+          "5": "NC_000005.10", "6": "NC_000006.12", "7": "NC_000007.14", "8": "NC_000008.11",
+          "9": "NC_000009.12", "10": "NC_000010.11", "11": "NC_000011.10", "12": "NC_000012.12",
+          "13": "NC_000013.11", "14": "NC_000014.9", "15": "NC_000015.10", "16": "NC_000016.10",
+          "17": "NC_000017.11", "18": "NC_000018.10", "19": "NC_000019.10", "20": "NC_000020.11",
+          "21": "NC_000021.9", "22": "NC_000022.11", "X": "NC_000023.11", "Y": "NC_000024.10",
+          "M": "NC_012920.1"}
+PVCF_HEADER = ["#CHROM", "POS", "ID", "REF", "ALT", "QUAL", "FILTER", "INFO", "FORMAT", "S1"]
+
+
+def write_chrmap(path):
+    """A ChromosomeMap file (source_id, chromosome, chromosome_order_num, length):
+    the 25 accessions -> chrN, plus entries the loader must get exactly right: a
+    numeric source id (Python coerces that CHROM to int before the lookup:
+    KeyError), an unplaced scaffold (-> chrUn..., no bin: TypeError), a value
+    without 'chr' and an 'MT' value."""
+    rows = [("source_id", "chromosome", "chromosome_order_num", "length")]
+    for i, c in enumerate(CHROM_NAMES):
+        rows.append((REFSEQ[c], "chr" + c, str(i + 1), str(GRCH38_LENGTHS[c])))
+    rows += [("7", "chr7", "7", str(GRCH38_LENGTHS["7"])),
+             ("NT_187361.1", "chrUn_KI270302v1", "26", "2274"),
+             ("CM000685.2", "X", "23", str(GRCH38_LENGTHS["X"])),
+             ("J01415.2", "MT", "25", "16569")]
+    with open(path, "w") as fh:
+        for r in rows:
+            fh.write("\t".join(r) + "\n")
+
+
+def gen_chrmap_lines(n, rng):
+    """gen_load_lines' records with CHROM as an accession (most lines), a
+    chromosome name (not in the map: KeyError), a numeric id that is in the map
+    (KeyError), the scaffold, the 'X'/'MT' aliases; and pVCF columns (FORMAT +
+    one sample; some lines short of the header: IndexError, some with extra)."""
+    out = []
+    alias = {"X": "CM000685.2", "M": "J01415.2"}
+    for ln in gen_load_lines(n, rng):
+        f = ln.split("\t")
+        c = f[0].replace("chr", "")
+        c = "M" if c == "MT" else c
+        u = rng.random()
+        if u < 0.85 or c not in REFSEQ:
+            f[0] = REFSEQ.get(c, f[0])
+        elif u < 0.89:
+            f[0] = c  # a plain name: not a source id
+        elif u < 0.92 and c in alias:
+            f[0] = alias[c]
+        elif u < 0.94:
+            f[0] = "7"
+        elif u < 0.96:
+            f[0] = "NT_187361.1"
+        else:
+            f[0] = REFSEQ[c]
+        u = rng.random()
+        if u < 0.9:
+            f += ["GT", rng.choice(["0/1", "1/1", "./."])]
+        elif u < 0.95:
+            f += ["GT", "0/1", "extra"]
+        out.append("\t".join(f))
+    return out
+
+
+def run_chrmap_driver(lines, map_path):
+    """run_load_driver with the loader's chromosome map and pVCF header set
+    (VCFVariantLoader.set_chromosome_map / set_vcf_header_fields)."""
+    from AnnotatedVDB.Util.loaders import VCFVariantLoader
+    from AnnotatedVDB.Util.parsers.chromosome_map_parser import ChromosomeMap
+    loader = VCFVariantLoader("dbSNP")
+    loader.initialize_pk_generator("GRCh38", "/nonexistent")
+    loader.initialize_bin_indexer(None)
+    loader._alg_invocation_id = "1"
+    loader.initialize_copy_sql()
+    loader.set_chromosome_map(ChromosomeMap(map_path))
+    loader.set_vcf_header_fields(PVCF_HEADER)
+    rows = []
+    for line in lines:
+        loader.reset_copy_buffer()
+        try:
+            pkm = loader.parse_variant(line.rstrip())
+            mapping = ["%s\t%s" % (k, v) for k, v in pkm.items()]
+            err = ""
+        except Exception as e:  # noqa: BLE001
+            mapping, err = [], type(e).__name__
+        copy = loader.copy_buffer().getvalue().splitlines()
+        rows.append((line.replace("\t", "\\t"), err, json.dumps(mapping, separators=(",", ":")),
+                     json.dumps(copy, separators=(",", ":"))))
+    return rows
+
+
 def gen_display_attrs(VariantAnnotator, n, rng):
     """(chrom, pos, ref, alt) -> json.dumps(get_display_attributes()) incl. long
     alleles (truncation at 8 and 100 characters)."""
@@ -837,7 +927,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
-    ap.add_argument("--only", choices=["all", "load", "c1", "adsp"], default="all",
+    ap.add_argument("--only", choices=["all", "load", "c1", "adsp", "chrmap"], default="all",
                     help="'load': only the load-driver fixtures (vcf_load, display_attrs); "
                          "'c1': only the C1 prefix fixture")
     a = ap.parse_args()
@@ -859,6 +949,14 @@ def main():
         wtsv("adsp_load.tsv.gz", ["line", "error", "mapping", "copy_rows", "updates", "counter_deltas"],
              run_adsp_driver(lines, M, P))
         print("existing: %d metaseq ids, %d primary keys" % (len(M), len(P)))
+        print("done")
+        return
+    if a.only == "chrmap":
+        mp = os.path.join(HERE, "chrmap_grch38.tsv")
+        write_chrmap(mp)
+        crng = random.Random(a.seed + 3)
+        wtsv("chrmap_load.tsv.gz", ["line", "error", "mapping", "copy_rows"],
+             run_chrmap_driver(gen_chrmap_lines(int(3000 * k), crng), mp))
         print("done")
         return
     if a.only == "c1":

@@ -238,3 +238,58 @@ def test_parse_variant_per_line_vs_reference_load_driver(engine, loader):
     last_ok = [r for r in rows if r[1] is None][-1][0]
     loader.parse_variant(last_ok)
     assert loader.get_current_variant() == VcfEntryParser(last_ok).get_variant(dbSNP=True, namespace=True)
+
+
+def chrmap_rows():
+    with gzip.open(os.path.join(GOLDEN, "chrmap_load.tsv.gz"), "rt") as fh:
+        fh.readline()
+        out = []
+        for line in fh:
+            raw, err, mapping, copy = line.rstrip("\n").split("\t")
+            out.append((raw.replace("\\t", "\t"), err or None, json.loads(mapping), json.loads(copy)))
+        return out
+
+
+@pytest.fixture()
+def map_loader(loader):
+    from annotatedvdb_amd.parsers import ChromosomeMap
+    loader.set_chromosome_map(ChromosomeMap(os.path.join(GOLDEN, "chrmap_grch38.tsv")))
+    loader.set_vcf_header_fields(["#CHROM", "POS", "ID", "REF", "ALT", "QUAL", "FILTER", "INFO", "FORMAT", "S1"])
+    return loader
+
+
+def test_chromosome_map_pvcf_gpu_load_vs_reference(engine, map_loader):
+    """A ChromosomeMap (RefSeq accessions as CHROM) and a pVCF header stay on the GPU
+    load path (K0 looks CHROM up in the map's device table; the header width flags
+    short lines) and give the reference loader's exact COPY rows and .mapping lines
+    (chrmap_load.tsv.gz: the reference run with the same map and header)."""
+    rows = chrmap_rows()
+    text = ("\n".join(r[0] for r in rows) + "\n").encode()
+    map_loader.reset_copy_buffer()
+    mapping = map_loader.load_vcf_text(text, errors="record")
+    assert map_loader.copy_buffer().getvalue().splitlines() == [c for r in rows for c in r[3]]
+    assert mapping.splitlines() == [m for r in rows if r[1] is None for m in r[2]]
+    st = map_loader.last_load_stats
+    ok = sum(1 for r in rows if r[1] is None)
+    assert st["lines"] == len(rows) and st["gpu_lines"] > 0.8 * ok, st
+
+
+def test_chromosome_map_pvcf_per_line_vs_reference(engine, map_loader):
+    """The same fixture through parse_variant line by line (K5h with the map's host
+    table, else the general path): rows, .mapping lines and exception types."""
+    rows = chrmap_rows()
+    map_loader.reset_copy_buffer()
+    lh = map_loader._engine.line_host()
+    r0 = lh.rendered
+    got_map = []
+    for raw, err, mapping, copy in rows:
+        try:
+            out = map_loader.parse_variant(raw)
+        except Exception as e:  # noqa: BLE001
+            assert err is not None and type(e).__name__ == err, (raw, e)
+            continue
+        assert err is None, raw
+        got_map += ["%s\t%s" % kv for kv in out.items()]
+    assert map_loader.copy_buffer().getvalue().splitlines() == [c for r in rows for c in r[3]]
+    assert got_map == [m for r in rows if r[1] is None for m in r[2]]
+    assert lh.rendered - r0 > 0.8 * sum(1 for r in rows if r[1] is None)

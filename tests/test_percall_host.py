@@ -209,7 +209,7 @@ def test_k5h_lines_vs_reference_load_driver(lib, ctx):
         opts = N.FormatOpts(b"1", 50, 0)
         res = N.LineResult()
         cb, mb = ctypes.create_string_buffer(1 << 16), ctypes.create_string_buffer(1 << 16)
-        N.check("k5h", lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), cb, 1 << 16, mb, 1 << 16,
+        N.check("k5h", lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), None, cb, 1 << 16, mb, 1 << 16,
                                               ctypes.byref(res)))
         if res.state != N.LINE_GPU:
             continue
@@ -230,7 +230,7 @@ def test_k5h_edges(lib, ctx):
         opts = N.FormatOpts(b"7", 50, 0)
         res = N.LineResult()
         cb, mb = ctypes.create_string_buffer(cap), ctypes.create_string_buffer(cap)
-        rc = lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), cb, cap, mb, cap, ctypes.byref(res))
+        rc = lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), None, cb, cap, mb, cap, ctypes.byref(res))
         return rc, res, cb.raw[:res.copy_bytes].decode(errors="replace"), mb.raw[:res.map_bytes].decode(errors="replace")
     assert run(b"#CHROM\tPOS")[1].state == N.LINE_SKIP
     assert run(b"1\t100\t.\tA")[1].state == N.LINE_HOST
@@ -244,7 +244,7 @@ def test_k5h_edges(lib, ctx):
     rc, res, _, _ = run(b"1\t100\trs5\tA\tG\t.\t.\tRS=5", cap=16)
     assert rc == N.AVDB_ERANGE and res.copy_bytes > 16
     opts = N.FormatOpts(b"1", 50, 0)
-    assert lib.avdb_vcf_line_host(None, b"x", 1, ctypes.byref(opts), None, 0, None, 0,
+    assert lib.avdb_vcf_line_host(None, b"x", 1, ctypes.byref(opts), None, None, 0, None, 0,
                                   ctypes.byref(N.LineResult())) == N.AVDB_EINVAL
 
 
@@ -256,6 +256,41 @@ def test_format_opts_struct_size_checked(lib, ctx):
     res = N.LineResult()
     b = b"1\t100\trs5\tA\tG\t.\t.\tRS=5"
     cb = ctypes.create_string_buffer(4096)
-    assert lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), cb, 4096, cb, 4096,
+    assert lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), None, cb, 4096, cb, 4096,
                                   ctypes.byref(res)) == N.AVDB_EINVAL
     assert b"struct_size" in lib.avdb_last_error()
+
+
+def test_k5h_chromosome_map_and_pvcf_header_vs_reference(lib, ctx):
+    """K5h with a ChromosomeMap (RefSeq accessions as CHROM) and a pVCF header
+    (FORMAT + a sample column) against the reference loader run with the same map
+    and header (chrmap_load.tsv.gz, make_golden.py --only chrmap): every line K5h
+    renders is byte-exact; lines the reference raised on (KeyError for unmapped /
+    numeric CHROM, IndexError for lines short of the header, ...) are never rendered."""
+    from annotatedvdb_amd.engine import ChromMap
+    from annotatedvdb_amd.parsers import ChromosomeMap
+
+    class _Eng:  # what ChromMap needs of an engine
+        pass
+    e = _Eng()
+    e.lib, e.ctx = lib, ctx
+    cmap = ChromMap(e, ChromosomeMap(os.path.join(GOLDEN, "chrmap_grch38.tsv")).chromosome_map())
+    vo = N.VcfOpts(10, cmap.handle)
+    with gzip.open(os.path.join(GOLDEN, "chrmap_load.tsv.gz"), "rt") as fh:
+        fh.readline()
+        rows = [ln.rstrip("\n").split("\t") for ln in fh]
+    rendered = 0
+    for raw, err, mapping, copy in rows:
+        b = raw.replace("\\t", "\t").encode()
+        opts, res = N.FormatOpts(b"1", 50, 0), N.LineResult()
+        cb, mb = ctypes.create_string_buffer(1 << 16), ctypes.create_string_buffer(1 << 16)
+        N.check("k5h", lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), ctypes.byref(vo), cb, 1 << 16,
+                                              mb, 1 << 16, ctypes.byref(res)))
+        if res.state != N.LINE_GPU:
+            continue
+        assert not err, (raw, err)
+        rendered += 1
+        assert cb.raw[:res.copy_bytes].decode().splitlines() == json.loads(copy), raw
+        assert mb.raw[:res.map_bytes].decode() == "".join(m + "\n" for m in json.loads(mapping)), raw
+    assert rendered > 0.8 * sum(1 for r in rows if not r[1]), rendered
+    cmap.close()
