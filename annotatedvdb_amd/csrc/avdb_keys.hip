@@ -203,60 +203,76 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
-// exclusive (keys, paths) prefix of tile T whose totals are (K, P); the whole wave
-// calls it.  Waits only on tiles < T, which were taken earlier by running waves.
-__device__ __forceinline__ void tile_prefix(const KeyArgs& A, uint64_t T, uint32_t K, uint32_t P, uint64_t* EK,
-                                            uint64_t* EP) {
+// Tile T's totals (K, P) go out as soon as its SoA has arrived — before the wave
+// renders the tile it holds before T — so no tile waits on a whole tile of work
+// (tile 0 publishes its inclusive prefix right away).
+__device__ __forceinline__ void tile_publish(const KeyArgs& A, uint64_t T, uint32_t K, uint32_t P) {
+  if (__lane_id() != 0) return;
+  if (T == 0) {
+    __hip_atomic_store(A.tile_pre, uint64_t(K), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(A.tile_pre + 1, uint64_t(P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(A.tile_status, kTilePre, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store(A.tile_status + T, kTileAgg | (uint64_t(K) << 31) | P, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// exclusive (keys, paths) prefix of tile T (totals K, P, already published); the
+// whole wave calls it.  It waits only on tiles < T, each published by its wave
+// right after that wave took it.
+__device__ __forceinline__ void tile_lookback(const KeyArgs& A, uint64_t T, uint32_t K, uint32_t P, uint64_t* EK,
+                                              uint64_t* EP) {
   const uint32_t lane = __lane_id();
   uint64_t* st = A.tile_status;
   uint64_t* pre = A.tile_pre;
   uint64_t sk = 0, sp = 0;
-  if (T > 0) {
-    if (lane == 0)
-      __hip_atomic_store(st + T, kTileAgg | (uint64_t(K) << 31) | P, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    int64_t base = int64_t(T) - 1;
-    uint32_t spins = 0;
-    while (true) {
-      const int64_t j = base - int64_t(lane);
-      uint64_t v = kTilePre;  // before tile 0: a zero prefix
-      bool ready = true;
-      if (j >= 0) {
+  if (T == 0) {
+    *EK = *EP = 0;
+    return;
+  }
+  int64_t base = int64_t(T) - 1;
+  uint32_t spins = 0;
+  while (true) {
+    const int64_t j = base - int64_t(lane);
+    uint64_t v = kTilePre;  // before tile 0: a zero prefix
+    bool ready = true;
+    if (j >= 0) {
+      v = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      ready = (v >> 62) != 0;
+    }
+    while (!__all(ready)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (!ready) {
         v = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         ready = (v >> 62) != 0;
       }
-      while (!__all(ready)) {
-        __builtin_amdgcn_s_sleep(1);
-        if (!ready) {
-          v = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          ready = (v >> 62) != 0;
-        }
-        if (++spins > kSpinLimit) {
-          if (lane == 0) atomicAdd(A.scan_err, 1u);
-          if (!ready) v = kTilePre;
-          ready = true;
-        }
+      if (++spins > kSpinLimit) {
+        if (lane == 0) atomicAdd(A.scan_err, 1u);
+        if (!ready) v = kTilePre;
+        ready = true;
       }
-      const uint64_t pm = __ballot((v >> 62) == 2);
-      uint64_t ak = 0, ap = 0;
-      if (pm) {
-        const uint32_t l = uint32_t(__ffsll((unsigned long long)pm)) - 1;  // nearest published prefix
-        if (lane < l) {
-          ak = (v >> 31) & kAggMask;
-          ap = v & kAggMask;
-        } else if (lane == l && j >= 0) {
-          ak = __hip_atomic_load(pre + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ap = __hip_atomic_load(pre + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        sk += wave_sum64(ak);
-        sp += wave_sum64(ap);
-        break;
+    }
+    const uint64_t pm = __ballot((v >> 62) == 2);
+    uint64_t ak = 0, ap = 0;
+    if (pm) {
+      const uint32_t l = uint32_t(__ffsll((unsigned long long)pm)) - 1;  // nearest published prefix
+      if (lane < l) {
+        ak = (v >> 31) & kAggMask;
+        ap = v & kAggMask;
+      } else if (lane == l && j >= 0) {
+        ak = __hip_atomic_load(pre + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ap = __hip_atomic_load(pre + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      ak = (v >> 31) & kAggMask;
-      ap = v & kAggMask;
       sk += wave_sum64(ak);
       sp += wave_sum64(ap);
-      base -= kWave;
+      break;
     }
+    ak = (v >> 31) & kAggMask;
+    ap = v & kAggMask;
+    sk += wave_sum64(ak);
+    sp += wave_sum64(ap);
+    base -= kWave;
   }
   if (lane == 0) {
     __hip_atomic_store(pre + 2 * T, sk + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -266,6 +282,11 @@ __device__ __forceinline__ void tile_prefix(const KeyArgs& A, uint64_t T, uint32
   *EK = sk;
   *EP = sp;
 }
+
+// a tile's key / path sizes (what the size pass writes) and their wave scans
+struct TileScan {
+  uint32_t ksz, psz, xk, xp, K, P;
+};
 
 #ifndef AVDB_K7_PREFETCH
 #define AVDB_K7_PREFETCH 1  // the next tile's SoA and offsets are loaded before this one renders (0: A/B)
@@ -355,18 +376,52 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
     if (lane == 0) t = atomicAdd(A.tile_ctr, 1u);
     return size_t(uint32_t(__shfl(t, 0, kWave))) * kWave;
   };
+  // ONEP: sizes of the tile whose SoA is in v (first record t), scanned over the wave
+  auto tile_sizes = [&](const KeyTileIn& v, size_t t) {
+    TileScan q{};
+    const bool lv = t + lane < A.n;
+    const bool lg = uint64_t(v.r) + v.a > A.max_seq_len;
+    if (lv && v.c < uint32_t(A.n_chrom) && !(v.e >> 63) && !(lg && !A.digest)) q.ksz = key_size(v.c, v.p, v.r, v.a, v.e, lg);
+    if (lv && A.code && v.cd != AVDB_BIN_NONE && v.c < uint32_t(A.n_chrom))
+      q.psz = bin_path(Out<false>(nullptr, 0), v.c, v.cd).size();
+    q.xk = q.ksz;
+    q.xp = q.psz;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t uk = __shfl_up(q.xk, d, kWave), up = __shfl_up(q.xp, d, kWave);
+      if (lane >= uint32_t(d)) {
+        q.xk += uk;
+        q.xp += up;
+      }
+    }
+    q.K = __shfl(q.xk, kWave - 1, kWave);
+    q.P = __shfl(q.xp, kWave - 1, kWave);
+    return q;
+  };
   size_t t0 = ONEP ? acquire() : size_t(bid) * blockDim.x + size_t(wv) * kWave;
   KeyTileIn nx{};
+  TileScan sn{};
   if (PF && t0 < A.n) {
     nx = load_in(t0);
     if (PFW) load_window(nx, t0 + lane);
+    if constexpr (ONEP) {
+      sn = tile_sizes(nx, t0);
+      tile_publish(A, t0 / kWave, sn.K, sn.P);
+    }
   }
   for (size_t tn = 0; t0 < A.n; t0 = tn) {
     tn = ONEP ? acquire() : t0 + stride;
     const size_t i = t0 + lane;
     const bool live = i < A.n;
     const KeyTileIn cur = nx;
-    if (PF && tn < A.n) nx = load_in(tn);
+    const TileScan sc = sn;
+    if (PF && tn < A.n) {
+      nx = load_in(tn);
+      if constexpr (ONEP) {  // the next tile's totals go out now (its loads are waited on here)
+        sn = tile_sizes(nx, tn);
+        tile_publish(A, tn / kWave, sn.K, sn.P);
+      }
+    }
     uint32_t c = 0, p = 0, r = 0, a = 0;
     uint64_t e = 0;
     bool lng = false;
@@ -383,13 +438,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       if (c >= uint32_t(A.n_chrom) || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
       else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
     }
-    // ONEP: sizes from the SoA alone (what the size pass would write)
-    uint32_t ksz = 0, psz = 0;
-    if constexpr (ONEP) {
-      if (live && st == AVDB_KEY_OK) ksz = key_size(c, p, r, a, e, lng);
-      if (live && A.code && cur.cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom))
-        psz = bin_path(Out<false>(nullptr, 0), c, cur.cd).size();
-    }
+
     // WRITE: the bytes a key copies — a short record's ref+alt, or a long record's
     // 32 digest characters — are loaded into a 7-word register window up front,
     // all loads independent and outside any branch.  Loads inside the per-lane
@@ -482,26 +531,16 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       // the tile's spans [gk0, gk1) / [gp0, gp1) and each record's [ko, ko1) / [po, po1)
       uint64_t gk0, gk1, ko = 0, ko1 = 0, gp0 = 0, gp1 = 0, po = 0, po1 = 0;
       if constexpr (ONEP) {
-        uint32_t xk = ksz, xp = psz;  // wave inclusive scans
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-          const uint32_t uk = __shfl_up(xk, d, kWave), up = __shfl_up(xp, d, kWave);
-          if (lane >= uint32_t(d)) {
-            xk += uk;
-            xp += up;
-          }
-        }
-        const uint32_t K = __shfl(xk, kWave - 1, kWave), P = __shfl(xp, kWave - 1, kWave);
         uint64_t EK, EP;
-        tile_prefix(A, t0 / kWave, K, P, &EK, &EP);
+        tile_lookback(A, t0 / kWave, sc.K, sc.P, &EK, &EP);
         gk0 = EK;
-        gk1 = EK + K;
-        ko = EK + xk - ksz;
-        ko1 = EK + xk;
+        gk1 = EK + sc.K;
+        ko = EK + sc.xk - sc.ksz;
+        ko1 = EK + sc.xk;
         gp0 = EP;
-        gp1 = EP + P;
-        po = EP + xp - psz;
-        po1 = EP + xp;
+        gp1 = EP + sc.P;
+        po = EP + sc.xp - sc.psz;
+        po1 = EP + sc.xp;
         if (live) {
           A.key_off[i] = ko;
           if (A.code) A.path_off[i] = po;

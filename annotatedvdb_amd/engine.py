@@ -885,6 +885,9 @@ class Engine:
             out = KeyText(ws=self.empty(int(sz.value), torch.uint8), key_off=self.empty(n + 1, torch.int64),
                           path_off=self.empty(n + 1, torch.int64) if code is not None else None,
                           state=self.empty(max(1, n), torch.uint8), keys=None, paths=None)
+        if out.key_off.numel() < n + 1 or out.state.numel() < max(1, n) or \
+                (code is not None and (out.path_off is None or out.path_off.numel() < n + 1)):
+            raise ValueError("primary_keys: the reused KeyText holds fewer records (or no paths)")
         args = (self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
                 N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), N.ptr(code), N.ptr(digest), n, int(max_seq_len),
                 N.ptr(out.ws), out.ws.numel(), N.ptr(out.key_off), N.ptr(out.path_off))
@@ -913,6 +916,9 @@ class Engine:
                           path_off=self.empty(n + 1, torch.int64) if code is not None else None,
                           state=self.empty(max(1, n), torch.uint8), keys=self.empty(int(kc.value), torch.uint8),
                           paths=self.empty(int(pc.value), torch.uint8) if code is not None else None)
+        if out.key_off.numel() < n + 1 or out.state.numel() < max(1, n) or \
+                (code is not None and (out.path_off is None or out.path_off.numel() < n + 1 or out.paths is None)):
+            raise ValueError("primary_keys: the reused KeyText holds fewer records (or no paths)")
         if out.ws.numel() < sz.value:
             out.ws = self.empty(int(sz.value), torch.uint8)
         N.check("avdb_primary_keys_onepass", self.lib.avdb_primary_keys_onepass(

@@ -230,7 +230,8 @@ def _k8_vs_kernels(engine, N, sp):
     assert list(r2["status"]) == [0, 0, 2, 1]
 
 
-def test_k7_reused_buffers_flag_overflow(engine):
+@pytest.mark.parametrize("onepass", [False, True])
+def test_k7_reused_buffers_flag_overflow(engine, onepass):
     """A KeyText reused for a batch whose keys and paths are longer: the texts
     that do not fit are not written and their records say so (KEY_OVERFLOW,
     PATH_OVERFLOW); KeyText.host refuses the batch instead of returning stale text."""
@@ -238,11 +239,13 @@ def test_k7_reused_buffers_flag_overflow(engine):
     from annotatedvdb_amd.engine import pack_records
     a = pack_records([0] * 64, [100] * 64, [b"A"] * 64, [b"G"] * 64).to("cuda")
     _, code, _, _ = engine.record_prep(a, want_lcp=False)
-    kt = engine.primary_keys(a, code=code)
+    kt = engine.primary_keys(a, code=code, onepass=onepass)
     assert kt.host(64)[0][0] == "1:100:A:G"
+    if onepass:  # buffers sized by avdb_primary_keys_bound: shrink them to the first batch's text
+        kt.keys, kt.paths = kt.keys[: int(kt.key_off[64])], kt.paths[: int(kt.path_off[64])]
     b = pack_records([9] * 64, [100000] * 64, [b"ACGTACGTAC"] * 64, [b"G"] * 64).to("cuda")  # leaf bins: 87-byte paths
     _, code2, _, _ = engine.record_prep(b, want_lcp=False)
-    kt2 = engine.primary_keys(b, code=code2, out=kt)
+    kt2 = engine.primary_keys(b, code=code2, out=kt, onepass=onepass)
     st = kt2.state[:64].cpu().numpy()
     assert ((st & 0x0F) == N.KEY_OVERFLOW).sum() > 0 and ((st & N.PATH_OVERFLOW) != 0).sum() > 0
     assert ((st & 0x0F) == N.KEY_OK).sum() > 0  # the keys that fit were written
