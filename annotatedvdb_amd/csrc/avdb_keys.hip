@@ -68,12 +68,10 @@ struct KeyArgs {
   uint8_t* state;
   uint16_t* key_sz;   // SIZE: sizes as u16 in the workspace (scanned into key_off), or NULL
   uint16_t* path_sz;
-  // one pass (MODE 2): tiles taken in order from tile_ctr; per tile a status word
-  // and the inclusive prefixes (keys, paths) of the decoupled look-back scan
-  uint32_t* tile_ctr;
-  uint32_t* scan_err;     // look-backs that gave up waiting (never expected: a bug signal)
-  uint64_t* tile_status;
-  uint64_t* tile_pre;
+  // MODE 2: per 256-record group the (keys, paths) offset of its first record =
+  // blk_pre[2*(g / kGroupsPerBlock) + {0,1}] + grp_pre[g].{x,y}
+  const uint2* grp_pre;
+  const uint64_t* blk_pre;
 };
 
 // WRITE renders each wave's 64 records as a tile: each stream's span (the
@@ -169,16 +167,18 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // ---------------------------------------------------------------------------
-// K7 in one pass (MODE 2): each wave takes the next 64-record tile in launch
-// order, computes its records' key and path sizes from the SoA, and finds the
-// tile's output offsets with a decoupled look-back scan over the tiles before
-// it (status word per tile: flag 1 = aggregate, 2 = inclusive prefix published);
-// then it renders as the two-pass write does.  No size pass, no scans, no
-// offset reads: the SoA is read once and the offsets are written, not read.
+// K7 with group offsets (MODE 2): the size pass writes one (keys, paths) total
+// per 256-record group, two small kernels scan them (per block of 4,096 groups,
+// then the block totals), and the write pass recomputes each record's sizes
+// from the SoA it reads anyway, scans them over the wave, and writes the u64
+// offsets itself.  A device-wide decoupled look-back over 64-record tiles was
+// built first (one launch, tiles in launch order): the agent-scope status loads
+// of each look-back window cost more than the tile (168 ms for C4k's 1.25e8
+// records), so the scan runs over group totals instead.
 // ---------------------------------------------------------------------------
-constexpr uint64_t kTileAgg = 1ull << 62, kTilePre = 2ull << 62;
-constexpr uint64_t kAggMask = 0x7FFFFFFFull;
-constexpr uint32_t kSpinLimit = 1u << 24;  // a look-back wait this long is a bug: count it and go on
+constexpr uint32_t kGroup = 256;              // records per scan group (4 tiles of 64)
+constexpr uint32_t kGroupsPerBlock = 4096;    // groups per block of the local scan
+constexpr uint32_t kScanThreads = 1024;       // 4 groups per thread
 
 __device__ __forceinline__ uint32_t ndigits64(uint64_t v) {
   if (v <= 0xFFFFFFFFull) return ndigits(uint32_t(v));
@@ -193,94 +193,145 @@ __device__ __forceinline__ uint32_t key_size(uint32_t c, uint32_t p, uint32_t r,
          ((e && !(e >> 63)) ? 3u + ndigits64(e) : 0u);
 }
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+// the sizes the size pass gives record j (SoA-decidable key state only)
+__device__ __forceinline__ void record_sizes(const KeyArgs& A, uint32_t c, uint32_t p, uint32_t r, uint32_t a,
+                                             uint64_t e, uint32_t cd, uint32_t* ks, uint32_t* ps) {
+  const bool lg = uint64_t(r) + a > A.max_seq_len;
+  *ks = (c < uint32_t(A.n_chrom) && !(e >> 63) && !(lg && !A.digest)) ? key_size(c, p, r, a, e, lg) : 0u;
+  *ps = (A.code && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom)) ? bin_path(Out<false>(nullptr, 0), c, cd).size()
+                                                                    : 0u;
+}
+
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    const uint64_t o = (uint64_t(uint32_t(__shfl_xor(uint32_t(v >> 32), d, kWave))) << 32) |
-                       uint32_t(__shfl_xor(uint32_t(v), d, kWave));
-    v += o;
-  }
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
   return v;
 }
 
-// Tile T's totals (K, P) go out as soon as its SoA has arrived — before the wave
-// renders the tile it holds before T — so no tile waits on a whole tile of work
-// (tile 0 publishes its inclusive prefix right away).
-__device__ __forceinline__ void tile_publish(const KeyArgs& A, uint64_t T, uint32_t K, uint32_t P) {
-  if (__lane_id() != 0) return;
-  if (T == 0) {
-    __hip_atomic_store(A.tile_pre, uint64_t(K), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(A.tile_pre + 1, uint64_t(P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(A.tile_status, kTilePre, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    __hip_atomic_store(A.tile_status + T, kTileAgg | (uint64_t(K) << 31) | P, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_AGENT);
+// group totals: one wave per 256-record group (records g*256 + 64k + lane)
+__global__ __launch_bounds__(kBlock) void k_key_group_totals(KeyArgs A, uint2* __restrict__ tot, size_t n_groups) {
+  const uint32_t lane = __lane_id();
+  const size_t w0 = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const size_t nw = size_t(gridDim.x) * blockDim.x / kWave;
+  for (size_t g = w0; g < n_groups; g += nw) {
+    uint32_t K = 0, P = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kGroup / kWave; ++k) {
+      const size_t j = g * kGroup + k * kWave + lane;
+      if (j < A.n) {
+        uint32_t ks, ps;
+        record_sizes(A, A.chrom[j], A.pos[j], A.rl[j], A.al[j], A.ext ? A.ext[j] : 0ull,
+                     A.code ? A.code[j] : AVDB_BIN_NONE, &ks, &ps);
+        K += ks;
+        P += ps;
+      }
+    }
+    K = wave_sum32(K);
+    P = wave_sum32(P);
+    if (lane == 0) tot[g] = make_uint2(K, P);
   }
 }
 
-// exclusive (keys, paths) prefix of tile T (totals K, P, already published); the
-// whole wave calls it.  It waits only on tiles < T, each published by its wave
-// right after that wave took it.
-__device__ __forceinline__ void tile_lookback(const KeyArgs& A, uint64_t T, uint32_t K, uint32_t P, uint64_t* EK,
-                                              uint64_t* EP) {
-  const uint32_t lane = __lane_id();
-  uint64_t* st = A.tile_status;
-  uint64_t* pre = A.tile_pre;
-  uint64_t sk = 0, sp = 0;
-  if (T == 0) {
-    *EK = *EP = 0;
-    return;
+// exclusive scan of the group totals inside each block of 4,096 groups (u32: a
+// block's text is < 4 GB) and the block totals
+__global__ __launch_bounds__(kScanThreads) void k_key_group_scan(const uint2* __restrict__ tot, size_t n_groups,
+                                                                  uint2* __restrict__ pre, uint64_t* __restrict__ btot) {
+  __shared__ uint32_t s_k[kScanThreads / kWave], s_p[kScanThreads / kWave];
+  const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
+  const size_t g0 = size_t(blockIdx.x) * kGroupsPerBlock + 4 * threadIdx.x;
+  uint2 v[4];
+  uint32_t k = 0, p = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = g0 + q < n_groups ? tot[g0 + q] : make_uint2(0, 0);
+    k += v[q].x;
+    p += v[q].y;
   }
-  int64_t base = int64_t(T) - 1;
-  uint32_t spins = 0;
-  while (true) {
-    const int64_t j = base - int64_t(lane);
-    uint64_t v = kTilePre;  // before tile 0: a zero prefix
-    bool ready = true;
-    if (j >= 0) {
-      v = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      ready = (v >> 62) != 0;
+  uint32_t xk = k, xp = p;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t uk = __shfl_up(xk, d, kWave), up = __shfl_up(xp, d, kWave);
+    if (lane >= uint32_t(d)) {
+      xk += uk;
+      xp += up;
     }
-    while (!__all(ready)) {
-      __builtin_amdgcn_s_sleep(1);
-      if (!ready) {
-        v = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        ready = (v >> 62) != 0;
-      }
-      if (++spins > kSpinLimit) {
-        if (lane == 0) atomicAdd(A.scan_err, 1u);
-        if (!ready) v = kTilePre;
-        ready = true;
-      }
-    }
-    const uint64_t pm = __ballot((v >> 62) == 2);
-    uint64_t ak = 0, ap = 0;
-    if (pm) {
-      const uint32_t l = uint32_t(__ffsll((unsigned long long)pm)) - 1;  // nearest published prefix
-      if (lane < l) {
-        ak = (v >> 31) & kAggMask;
-        ap = v & kAggMask;
-      } else if (lane == l && j >= 0) {
-        ak = __hip_atomic_load(pre + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ap = __hip_atomic_load(pre + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      sk += wave_sum64(ak);
-      sp += wave_sum64(ap);
-      break;
-    }
-    ak = (v >> 31) & kAggMask;
-    ap = v & kAggMask;
-    sk += wave_sum64(ak);
-    sp += wave_sum64(ap);
-    base -= kWave;
   }
-  if (lane == 0) {
-    __hip_atomic_store(pre + 2 * T, sk + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(pre + 2 * T + 1, sp + P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(st + T, kTilePre, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == kWave - 1) {
+    s_k[wv] = xk;
+    s_p[wv] = xp;
   }
-  *EK = sk;
-  *EP = sp;
+  __syncthreads();
+  uint32_t bk = 0, bp = 0, tk = 0, tp = 0;
+  for (uint32_t w = 0; w < kScanThreads / kWave; ++w) {
+    if (w < wv) {
+      bk += s_k[w];
+      bp += s_p[w];
+    }
+    tk += s_k[w];
+    tp += s_p[w];
+  }
+  uint32_t ek = bk + xk - k, ep = bp + xp - p;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (g0 + q < n_groups) pre[g0 + q] = make_uint2(ek, ep);
+    ek += v[q].x;
+    ep += v[q].y;
+  }
+  if (threadIdx.x == 0) {
+    btot[2 * blockIdx.x] = tk;
+    btot[2 * blockIdx.x + 1] = tp;
+  }
+}
+
+// exclusive scan of the block totals in place (one workgroup, sequential chunks),
+// and the grand totals into key_off[n] / path_off[n]
+__global__ __launch_bounds__(kScanThreads) void k_key_block_scan(uint64_t* __restrict__ b, size_t nb,
+                                                                 uint64_t* __restrict__ key_end,
+                                                                 uint64_t* __restrict__ path_end) {
+  __shared__ uint64_t s_k[kScanThreads / kWave], s_p[kScanThreads / kWave];
+  const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
+  uint64_t run_k = 0, run_p = 0;
+  for (size_t c0 = 0; c0 < nb; c0 += kScanThreads) {
+    const size_t i = c0 + threadIdx.x;
+    const uint64_t k = i < nb ? b[2 * i] : 0ull, p = i < nb ? b[2 * i + 1] : 0ull;
+    uint64_t xk = k, xp = p;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint64_t uk = (uint64_t(uint32_t(__shfl_up(uint32_t(xk >> 32), d, kWave))) << 32) |
+                          uint32_t(__shfl_up(uint32_t(xk), d, kWave));
+      const uint64_t up = (uint64_t(uint32_t(__shfl_up(uint32_t(xp >> 32), d, kWave))) << 32) |
+                          uint32_t(__shfl_up(uint32_t(xp), d, kWave));
+      if (lane >= uint32_t(d)) {
+        xk += uk;
+        xp += up;
+      }
+    }
+    if (lane == kWave - 1) {
+      s_k[wv] = xk;
+      s_p[wv] = xp;
+    }
+    __syncthreads();
+    uint64_t bk = 0, bp = 0, tk = 0, tp = 0;
+    for (uint32_t w = 0; w < kScanThreads / kWave; ++w) {
+      if (w < wv) {
+        bk += s_k[w];
+        bp += s_p[w];
+      }
+      tk += s_k[w];
+      tp += s_p[w];
+    }
+    if (i < nb) {
+      b[2 * i] = run_k + bk + xk - k;
+      b[2 * i + 1] = run_p + bp + xp - p;
+    }
+    run_k += tk;
+    run_p += tp;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *key_end = run_k;
+    if (path_end) *path_end = run_p;
+  }
 }
 
 // a tile's key / path sizes (what the size pass writes) and their wave scans
@@ -310,7 +361,7 @@ template <int MODE>
 __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A) {
   constexpr bool WRITE = MODE != 0;
   constexpr bool ONEP = MODE == 2;
-  static_assert(!ONEP || AVDB_K7_PREFETCH, "the one-pass form reads each tile's SoA ahead");
+  static_assert(!ONEP || AVDB_K7_PREFETCH, "the group-offset form reads each tile's SoA ahead");
   __shared__ uint64_t s_kimg[WRITE ? kWavesPerBlock * kKeyWave / 8 : 1];
   __shared__ uint64_t s_pimg[WRITE ? kWavesPerBlock * kPathWave / 8 : 1];
   const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
@@ -370,20 +421,17 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
         if (k < nw) v.w[k] = heap_word(aw + 8 * k, h);
     }
   };
-  // ONEP: the next tile in launch order (every tile before it was taken by a running wave)
-  auto acquire = [&]() -> size_t {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(A.tile_ctr, 1u);
-    return size_t(uint32_t(__shfl(t, 0, kWave))) * kWave;
+  // ONEP: a wave takes 256-record groups (grid-stride) and their four 64-record
+  // tiles in order, carrying the running offsets from the group's scanned base
+  const size_t gwave = size_t(bid) * kWavesPerBlock + wv, n_gw = size_t(gridDim.x) * kWavesPerBlock;
+  auto next_tile = [&](size_t t) -> size_t {
+    return ((t / kWave) % (kGroup / kWave)) != kGroup / kWave - 1 ? t + kWave
+                                                                    : t - (kGroup - kWave) + n_gw * kGroup;
   };
   // ONEP: sizes of the tile whose SoA is in v (first record t), scanned over the wave
   auto tile_sizes = [&](const KeyTileIn& v, size_t t) {
     TileScan q{};
-    const bool lv = t + lane < A.n;
-    const bool lg = uint64_t(v.r) + v.a > A.max_seq_len;
-    if (lv && v.c < uint32_t(A.n_chrom) && !(v.e >> 63) && !(lg && !A.digest)) q.ksz = key_size(v.c, v.p, v.r, v.a, v.e, lg);
-    if (lv && A.code && v.cd != AVDB_BIN_NONE && v.c < uint32_t(A.n_chrom))
-      q.psz = bin_path(Out<false>(nullptr, 0), v.c, v.cd).size();
+    if (t + lane < A.n) record_sizes(A, v.c, v.p, v.r, v.a, v.e, v.cd, &q.ksz, &q.psz);
     q.xk = q.ksz;
     q.xp = q.psz;
 #pragma unroll
@@ -398,29 +446,28 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
     q.P = __shfl(q.xp, kWave - 1, kWave);
     return q;
   };
-  size_t t0 = ONEP ? acquire() : size_t(bid) * blockDim.x + size_t(wv) * kWave;
+  size_t t0 = ONEP ? gwave * kGroup : size_t(bid) * blockDim.x + size_t(wv) * kWave;
   KeyTileIn nx{};
-  TileScan sn{};
+  uint64_t run_k = 0, run_p = 0;  // ONEP: offsets of the current tile's first record
   if (PF && t0 < A.n) {
     nx = load_in(t0);
     if (PFW) load_window(nx, t0 + lane);
-    if constexpr (ONEP) {
-      sn = tile_sizes(nx, t0);
-      tile_publish(A, t0 / kWave, sn.K, sn.P);
-    }
   }
   for (size_t tn = 0; t0 < A.n; t0 = tn) {
-    tn = ONEP ? acquire() : t0 + stride;
+    tn = ONEP ? next_tile(t0) : t0 + stride;
     const size_t i = t0 + lane;
     const bool live = i < A.n;
     const KeyTileIn cur = nx;
-    const TileScan sc = sn;
-    if (PF && tn < A.n) {
-      nx = load_in(tn);
-      if constexpr (ONEP) {  // the next tile's totals go out now (its loads are waited on here)
-        sn = tile_sizes(nx, tn);
-        tile_publish(A, tn / kWave, sn.K, sn.P);
+    if (PF && tn < A.n) nx = load_in(tn);
+    TileScan sc{};
+    if constexpr (ONEP) {
+      if ((t0 / kWave) % (kGroup / kWave) == 0) {  // a new group: its scanned base
+        const size_t g = t0 / kGroup;
+        const uint2 gp = A.grp_pre[g];
+        run_k = A.blk_pre[2 * (g / kGroupsPerBlock)] + gp.x;
+        run_p = A.blk_pre[2 * (g / kGroupsPerBlock) + 1] + gp.y;
       }
+      sc = tile_sizes(cur, t0);
     }
     uint32_t c = 0, p = 0, r = 0, a = 0;
     uint64_t e = 0;
@@ -531,8 +578,9 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
       // the tile's spans [gk0, gk1) / [gp0, gp1) and each record's [ko, ko1) / [po, po1)
       uint64_t gk0, gk1, ko = 0, ko1 = 0, gp0 = 0, gp1 = 0, po = 0, po1 = 0;
       if constexpr (ONEP) {
-        uint64_t EK, EP;
-        tile_lookback(A, t0 / kWave, sc.K, sc.P, &EK, &EP);
+        const uint64_t EK = run_k, EP = run_p;
+        run_k += sc.K;
+        run_p += sc.P;
         gk0 = EK;
         gk1 = EK + sc.K;
         ko = EK + sc.xk - sc.ksz;
@@ -544,10 +592,6 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
         if (live) {
           A.key_off[i] = ko;
           if (A.code) A.path_off[i] = po;
-          if (i + 1 == A.n) {
-            A.key_off[A.n] = ko1;
-            if (A.code) A.path_off[A.n] = po1;
-          }
         }
       } else {
         gk0 = A.key_off[t0];
@@ -802,12 +846,13 @@ extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint
   return AVDB_OK;
 }
 
-// ---- K7 in one pass -------------------------------------------------------------
-static size_t onepass_tiles(size_t n) { return (n + kWave - 1) / kWave; }
+// ---- K7 with group offsets --------------------------------------------------------
+static size_t key_groups(size_t n) { return (n + kGroup - 1) / kGroup; }
+static size_t key_group_blocks(size_t n) { return (key_groups(n) + kGroupsPerBlock - 1) / kGroupsPerBlock; }
 
 extern "C" int avdb_primary_keys_onepass_workspace_size(size_t n, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
-  *bytes = 512 + 24 * onepass_tiles(n);
+  *bytes = 256 + 16 * ((key_groups(n) + 1) & ~size_t(1)) + 16 * key_group_blocks(n);
   return AVDB_OK;
 }
 
@@ -842,21 +887,25 @@ extern "C" int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, co
     avdb_set_error("avdb_primary_keys_onepass: null array");
     return AVDB_EINVAL;
   }
+  if (n >= (size_t(1) << 32)) {
+    avdb_set_error("avdb_primary_keys_onepass: n must be < 2^32");
+    return AVDB_EINVAL;
+  }
   if (reinterpret_cast<uintptr_t>(key_out) % 8 || (path_out && reinterpret_cast<uintptr_t>(path_out) % 8)) {
     avdb_set_error("avdb_primary_keys_onepass: outputs must be 8-byte aligned");
     return AVDB_EINVAL;
   }
   size_t need = 0;
   avdb_primary_keys_onepass_workspace_size(n, &need);
-  if (!workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(workspace) % 8) {
-    avdb_set_error("avdb_primary_keys_onepass: 8-byte aligned workspace of %zu bytes required", need);
+  if (!workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(workspace) % 16) {
+    avdb_set_error("avdb_primary_keys_onepass: 16-byte aligned workspace of %zu bytes required", need);
     return AVDB_ERANGE;
   }
-  const size_t tiles = onepass_tiles(n);
-  char* ws = static_cast<char*>(workspace);
-  // tile counter, error counter and the status words start at zero; the prefixes
-  // are written before their status says so
-  AVDB_HIP_TRY(hipMemsetAsync(ws, 0, 512 + 8 * tiles, s));
+  const size_t ng = key_groups(n), nb = key_group_blocks(n);
+  char* ws = static_cast<char*>(workspace) + 256;
+  auto* tot = reinterpret_cast<uint2*>(ws);
+  auto* gpre = tot + ((ng + 1) & ~size_t(1));
+  auto* bpre = reinterpret_cast<uint64_t*>(gpre + ((ng + 1) & ~size_t(1)));
   KeyArgs A;
   memset(&A, 0, sizeof(A));
   A.chrom = chrom;
@@ -879,12 +928,19 @@ extern "C" int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, co
   A.key_out = key_out;
   A.path_out = path_out;
   A.state = key_state;
-  A.tile_ctr = reinterpret_cast<uint32_t*>(ws);
-  A.scan_err = reinterpret_cast<uint32_t*>(ws + 256);
-  A.tile_status = reinterpret_cast<uint64_t*>(ws + 512);
-  A.tile_pre = reinterpret_cast<uint64_t*>(ws + 512 + 8 * tiles);
-  const unsigned grid = stream_grid(n, kBlock, AVDB_K7_GRID);
+  A.grp_pre = gpre;
+  A.blk_pre = bpre;
+  hipLaunchKernelGGL(k_key_group_totals, dim3(stream_grid(ng * kWave, kBlock, 4096)), dim3(kBlock), 0, s, A, tot,
+                     ng);
+  AVDB_LAUNCH_CHECK("k_key_group_totals");
+  hipLaunchKernelGGL(k_key_group_scan, dim3(unsigned(nb)), dim3(kScanThreads), 0, s, tot, ng, gpre, bpre);
+  AVDB_LAUNCH_CHECK("k_key_group_scan");
+  hipLaunchKernelGGL(k_key_block_scan, dim3(1), dim3(kScanThreads), 0, s, bpre, nb, key_off + n,
+                     bin_code ? path_off + n : nullptr);
+  AVDB_LAUNCH_CHECK("k_key_block_scan");
+  const unsigned grid = unsigned((ng + kWavesPerBlock - 1) / kWavesPerBlock < AVDB_K7_GRID
+                                     ? (ng + kWavesPerBlock - 1) / kWavesPerBlock : AVDB_K7_GRID);
   hipLaunchKernelGGL(k_record_keys<2>, dim3(grid), dim3(kBlock), 0, s, A);
-  AVDB_LAUNCH_CHECK("k_record_keys<onepass>");
+  AVDB_LAUNCH_CHECK("k_record_keys<groups>");
   return AVDB_OK;
 }

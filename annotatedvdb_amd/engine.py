@@ -903,9 +903,10 @@ class Engine:
         return out
 
     def _primary_keys_onepass(self, b: RecordBatch, code, digest, max_seq_len: int, out) -> "KeyText":
-        """K7 in one launch (``avdb_primary_keys_onepass``): sizes, offsets
-        (look-back scan) and text; the text buffers are sized by
-        ``avdb_primary_keys_bound``, so no host sync is needed even the first time."""
+        """K7 without a host round trip (``avdb_primary_keys_onepass``): per-group
+        size totals, two small scans, then the write pass that recomputes each
+        record's sizes, writes its offsets and the text; the text buffers are sized
+        by ``avdb_primary_keys_bound``, so no host sync is needed even the first time."""
         n = b.n
         sz = ctypes.c_size_t()
         self.lib.avdb_primary_keys_onepass_workspace_size(n, ctypes.byref(sz))
@@ -927,11 +928,6 @@ class Engine:
             N.ptr(out.ws), out.ws.numel(), N.ptr(out.key_off), N.ptr(out.path_off), N.ptr(out.keys), out.keys.numel(),
             N.ptr(out.paths), out.paths.numel() if out.paths is not None else 0, N.ptr(out.state), self._stream()))
         return out
-
-    def scan_errors(self, kt: "KeyText") -> int:
-        """Look-back waits of the last one-pass K7 launch on ``kt`` that gave up (0
-        unless something is broken; the tests check it)."""
-        return int(kt.ws[256:260].view(torch.int32).item())
 
     # -- K6: existing-variant key set ----------------------------------------
     def keyset_build(self, keys: torch.Tensor, key_off: torch.Tensor) -> torch.Tensor:
