@@ -107,6 +107,13 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     const int v = atoi(s);
     if (v >= 1 && v <= 64) c->k2_blocks_per_cu = v;
   }
+  // K4 (SHA-512, VALU-bound) persistent grid: its occupancy by default; fewer
+  // workgroups leave CUs to a kernel running beside it on another stream
+  c->k4_blocks_per_cu = 3;
+  if (const char* s = getenv("AVDB_K4_BLOCKS_PER_CU")) {
+    const int v = atoi(s);
+    if (v >= 1 && v <= 3) c->k4_blocks_per_cu = v;
+  }
   *out = c;
   return AVDB_OK;
 }

@@ -799,7 +799,8 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
                        max_seq_len, counts, list);
   AVDB_LAUNCH_CHECK("k_long_scatter");
   // persistent grid over the grouped list
-  hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * kDigestWavesPerSimd), dim3(kBlock), 0, s, chrom, pos,
+  const int per_cu = ctx->k4_blocks_per_cu < kDigestWavesPerSimd ? ctx->k4_blocks_per_cu : kDigestWavesPerSimd;
+  hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * per_cu), dim3(kBlock), 0, s, chrom, pos,
                      allele_off,
                      ref_len, alt_len, heap, heap_bytes, list, total, ctx->d_seq_digest, ctx->tab.n,
                      digest_out);
