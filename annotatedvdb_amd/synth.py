@@ -209,14 +209,19 @@ def np_point_snvs(n: int, seed: int = 2, lengths=None):
     return chrom[order], pos[order].astype(np.int32)
 
 
-def np_spans(n: int, seed: int = 3, lengths=None):
+def np_spans(n: int, seed: int = 3, lengths=None, mix: str = "c3"):
+    """C3 spans (or the C4 mix: 90 % SNV / 8 % indel <= 50 bp / 2 % log-uniform
+    <= 1 Mb) on the host, numpy PCG64 (the CPU baselines' sample)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     lengths = np.asarray(lengths if lengths is not None else length_table(), dtype=np.int64)
     chrom, start = np_point_snvs(n, seed, lengths)
     u = rng.random(n)
     geo = rng.geometric(1 / 8, n) - 1
     logu = (10 ** rng.uniform(np.log10(50), 6, n)).astype(np.int64)
-    span = np.where(u < 0.5, 0, np.where(u < 0.8, geo, logu))
+    if mix == "c4":
+        span = np.where(u < 0.9, 0, np.where(u < 0.98, rng.integers(1, 51, n), logu))
+    else:
+        span = np.where(u < 0.5, 0, np.where(u < 0.8, geo, logu))
     end = np.minimum(start.astype(np.int64) + span, lengths[chrom]).astype(np.int32)
     return chrom, start, end
 

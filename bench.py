@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--n", type=int, default=None, help="records per GPU (default: config size)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="target seconds per CPU worker")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the step as a captured HIP graph (auto: the launch-bound C1 step)")
     return ap.parse_args()
 
 
@@ -166,10 +168,12 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
     from annotatedvdb_amd.chromosomes import CHROM_NAMES, GRCH38_LENGTHS
     from oracle import avdb_oracle as O
     try:
-        cores = len(os.sched_getaffinity(0))
+        host_cores = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    workers = max(1, min(16, cores))
+        host_cores = os.cpu_count() or 1
+    # one process per core, at most 16: the GPU box gives one GPU's job a 16-CPU share
+    # (its affinity mask shows the whole machine)
+    workers = max(1, min(16, host_cores))
     if workload == "c1":
         # the reference parallelises one process per chromosome file
         # (load_vcf_file.py:307-313): C1 is one file (chr22), so one process
@@ -182,7 +186,8 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
                     ["rs%d" % e if e else None for e in d["ext_id"].tolist()])]
         _TABLE = O.BinTable(GRCH38_LENGTHS)
         n, t = _cpu_c1_worker(0)
-        return {"value": n / t, "unit": "variants/s", "cores": 1, "kind": "port",
+        return {"value": n / t, "unit": "variants/s", "cores": 1, "workers": 1, "host_cores_visible": host_cores,
+                "kind": "port",
                 "per_core": n / t,
                 "sample": f"the whole C1 set ({n:,} chr22 records), one process as the reference runs one "
                           f"chromosome file (load_vcf_file.py:307-313); oracle.c1_port_loop = metaseq id + "
@@ -202,7 +207,8 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
             res = pool.map(_cpu_load_worker, range(workers))
         wall = time.perf_counter() - t0
         n = sum(r[0] for r in res)
-        return {"value": n / wall, "unit": "variants/s", "cores": workers, "kind": "port",
+        return {"value": n / wall, "unit": "variants/s", "cores": workers, "workers": workers,
+                "host_cores_visible": host_cores, "kind": "port",
                 "sample": f"{per * workers:,} synthetic dbSNP-shaped VCF lines ({n:,} COPY rows), "
                           f"{workers} processes x {per:,} lines; reference-structured loader port "
                           f"(oracle/avdb_oracle.py load_line + PortBinIndex; 0.82x the verbatim "
@@ -230,7 +236,8 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
             res = pool.map(_cpu_c5_worker, range(workers))
         wall = time.perf_counter() - t0
         n = sum(r[0] for r in res)
-        return {"value": n / wall, "unit": "variants/s", "cores": workers, "kind": "port",
+        return {"value": n / wall, "unit": "variants/s", "cores": workers, "workers": workers,
+                "host_cores_visible": host_cores, "kind": "port",
                 "sample": f"{n:,} {'ADSP-style' if workload == 'c5' else 'dbSNP-mix'} records "
                           f"({workload.upper()} generator on the CPU), {workers} processes x "
                           f"{per:,} records; reference-structured end inference + PortBinIndex + primary "
@@ -242,7 +249,7 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
         chrom, pos = synth.np_point_snvs(total, seed=2)
         end = None
     else:
-        chrom, pos, end = synth.np_spans(total, seed=3)
+        chrom, pos, end = synth.np_spans(total, seed=3 if workload == "c3" else 4, mix=workload)
     names = [CHROM_NAMES[c] for c in chrom.tolist()]
     pos = pos.tolist()
     end = end.tolist() if end is not None else None
@@ -255,7 +262,8 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
         res = pool.map(_cpu_worker, range(workers))
     wall = time.perf_counter() - t0
     n = sum(r[0] for r in res)
-    return {"value": n / wall, "unit": "variants/s", "cores": workers, "kind": "port",
+    return {"value": n / wall, "unit": "variants/s", "cores": workers, "workers": workers,
+            "host_cores_visible": host_cores, "kind": "port",
             "sample": f"{n:,} records of the {workload.upper()} workload (numpy PCG64, sorted), "
                       f"{workers} processes x {per:,} records; reference-structured PortBinIndex "
                       f"(oracle/avdb_oracle.py), per-process {np.mean([r[1] for r in res]):.2f} s"}
@@ -364,7 +372,7 @@ def main():
     # CPU baseline first, before this process touches the GPU (its worker
     # processes are forked and must not inherit an initialised HIP runtime)
     want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and ri.world == 1
-                                          and a.workload in ("c1", "c2", "c3", "c5", "c4k", "load"))
+                                          and a.workload in ("c1", "c2", "c3", "c4", "c5", "c4k", "load"))
     cpu = cpu_baseline(a.workload, a.cpu_seconds) if (ri.rank == 0 and want_cpu) else None
     ri = D.init("nccl")
     dev = torch.device("cuda", D.device_index(ri))
@@ -486,6 +494,18 @@ def main():
         last["ws4"] = torch.empty(int(sz.value), dtype=torch.uint8, device=dev)
     for _ in range(a.warmup):
         step(False)
+    use_graph = a.graph == "on" or (a.graph == "auto" and a.workload == "c1")
+    graph = None
+    if use_graph:
+        # the step captured once as a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and
+        # replayed: the same kernels on the same resident batch, without one host launch each
+        # (C1's 1.1 M records take less GPU time than its launches do)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step(False)
+        graph.replay()
+        torch.cuda.synchronize()
     # the job-level collective once untimed, so any lazy RCCL setup for the
     # all-gather is not charged to the timed region
     D.allgather_stats(hist, ctr, ri)
@@ -496,7 +516,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step(True)
+        if graph is not None:
+            graph.replay()
+        else:
+            step(True)
     # job-level exchange: per-rank L8 histograms + counters (RCCL all-gather)
     node_hist, node_ctr = D.allgather_stats(hist, ctr, ri)
     torch.cuda.synchronize()
@@ -504,6 +527,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, ri, device=dev)
     stage_ms = {k: float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])) for k, v in evs.items()}
+    if graph is not None:
+        stage_ms["graph_replay"] = True
     kname = {"c5": "record_prep", "vcf": "vcf_tokenize", "load": "format_write"}.get(a.workload, "bin_assign")
     kern_ms = stage_ms.get(kname)
     if a.workload == "c1":
