@@ -114,6 +114,12 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     const int v = atoi(s);
     if (v >= 1 && v <= 3) c->k4_blocks_per_cu = v;
   }
+  // K0 one-pass tokenizer: resident workgroups per CU (each stages a 20 KB window)
+  c->k0_blocks_per_cu = 6;
+  if (const char* s = getenv("AVDB_K0_BLOCKS_PER_CU")) {
+    const int v = atoi(s);
+    if (v >= 1 && v <= 7) c->k0_blocks_per_cu = v;
+  }
   *out = c;
   return AVDB_OK;
 }

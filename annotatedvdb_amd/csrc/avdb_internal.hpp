@@ -243,6 +243,7 @@ struct avdb_ctx {
   int k2_unroll;         // K2 groups of 4 records per lane per trip (env AVDB_K2_UNROLL: 1, 2, 4)
   int k2_blocks_per_cu;  // K2 grid = n_cu * this (env AVDB_K2_BLOCKS_PER_CU)
   int k4_blocks_per_cu;  // K4 digest grid = n_cu * this (env AVDB_K4_BLOCKS_PER_CU; default: its occupancy, 3)
+  int k0_blocks_per_cu;  // K0 one-pass grid = n_cu * this (env AVDB_K0_BLOCKS_PER_CU)
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
   bool has_digests;

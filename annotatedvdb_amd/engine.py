@@ -715,10 +715,17 @@ class Engine:
         return [raw[i * 32:(i + 1) * 32].decode("ascii") for i in range(n)]
 
     # -- K0: VCF text -> records ---------------------------------------------
-    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None) -> "VcfBatch":
+    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None, *,
+                     fused: Optional[bool] = None) -> "VcfBatch":
         """Parse VCF data lines (bytes or a uint8 tensor) on the GPU into the
         record SoA (one row per ALT != '.') plus the per-line table.
-        ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map."""
+        ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map.
+        ``fused`` (default): count pass + the one-pass tokenizer
+        (``avdb_vcf_tokenize``); False: the four-kernel path (count, parse with
+        line starts, scans, emit) — the same outputs; None: env AVDB_VCF_FUSED
+        (default 0 until the one-pass path is validated on the GPU)."""
+        if fused is None:
+            fused = os.environ.get("AVDB_VCF_FUSED", "0") != "0"
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
             t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
@@ -731,6 +738,8 @@ class Engine:
             last_nl = bool(text_t.numel() == 0 or int(text_t[-1].item()) == 10)
         nb = int(text_t.numel())
         tp = N.ptr(text_t) if nb else None
+        if fused:
+            return self._vcf_tokenize_onepass(text_t, nb, tp, last_nl, vcf_opts)
         s = self._stream()
         ws0 = self.empty(N.VCF_COUNT_WORKSPACE_BYTES, torch.uint8)
         nl = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -766,6 +775,71 @@ class Engine:
                 N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s))
         return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
                         records=b, rec_line=rec_line, rec_alt=rec_alt)
+
+    def _vcf_tokenize_onepass(self, text_t, nb: int, tp, last_nl: bool, vcf_opts) -> "VcfBatch":
+        """Count pass ('\\n' and ',' bytes: the line count and a bound on the
+        records), one host read, then ``avdb_vcf_tokenize`` (text read once) and
+        one host read of its totals.  The allele heap is sized by an estimate
+        (text bytes + 4 KB); a batch whose heap is larger runs the pass again
+        with the exact size."""
+        s = self._stream()
+        ws0 = self.empty(N.VCF_COUNT_WORKSPACE_BYTES, torch.uint8)
+        cnt = self.empty(2, torch.int64)
+        N.check("avdb_vcf_count_text", self.lib.avdb_vcf_count_text(
+            self.ctx, tp, nb, N.ptr(ws0), ws0.numel(), N.ptr(cnt), s))
+        n_nl, n_comma = (int(x) for x in cnt.cpu().tolist())
+        n_lines = n_nl + (0 if (last_nl or nb == 0) else 1)
+        rec_cap = n_lines + n_comma
+        heap_cap = nb + 4096
+        sz = ctypes.c_size_t()
+        self.lib.avdb_vcf_tokenize_workspace_size(nb, ctypes.byref(sz))
+        ws = self.empty(max(256, int(sz.value)), torch.uint8)
+        lines = self.empty(max(1, n_lines) * VCF_LINE_DTYPE.itemsize, torch.uint8)
+        rec_off = self.empty(n_lines + 1, torch.int64)
+        heap_off = self.empty(n_lines + 1, torch.int64)
+        tot = self.empty(4, torch.int64)
+        rc = max(1, rec_cap)
+        chrom, pos = self.empty(rc, torch.uint8), self.empty(rc, torch.int32)
+        allele_off, ref_len, alt_len = self.empty(rc, torch.int64), self.empty(rc, torch.int32), \
+            self.empty(rc, torch.int32)
+        ext_id, rec_line, rec_alt = self.empty(rc, torch.int64), self.empty(rc, torch.int32), \
+            self.empty(rc, torch.int32)
+        opts = ctypes.byref(vcf_opts) if vcf_opts is not None else None
+        while True:
+            heap = self.empty(max(1, heap_cap), torch.uint8)
+            N.check("avdb_vcf_tokenize", self.lib.avdb_vcf_tokenize(
+                self.ctx, tp, nb, N.ptr(ws), ws.numel(), n_lines, N.ptr(lines), N.ptr(rec_off), N.ptr(heap_off),
+                rec_cap, N.ptr(chrom), N.ptr(pos), N.ptr(allele_off), N.ptr(ref_len), N.ptr(alt_len),
+                N.ptr(ext_id), N.ptr(rec_line), N.ptr(rec_alt), heap_cap, N.ptr(heap), N.ptr(tot), opts, s))
+            t_lines, n_rec, n_heap, lb_err = (int(x) for x in tot.cpu().tolist())
+            if lb_err:
+                nc = -(-nb // 16384)
+                stuck = [x & ((1 << 64) - 1) for x in ws[64:128].view(torch.int64).cpu().tolist()]
+                t0 = 256 + 8 * nc + 48 * nc
+                trace = ws[t0:t0 + 4 * nc].view(torch.int32).cpu().numpy()
+                c0 = t0 + 4 * ((nc + 1) & ~1)
+                clk = ws[c0:c0 + 16 * nc].view(torch.int64).cpu().numpy().reshape(nc, 2)
+                phases = {int(k): int(v) for k, v in zip(*np.unique(trace, return_counts=True))}
+                c, j = int(stuck[0]), int(stuck[1])
+                rel = lambda t: (int(t) - int(clk[0, 1])) / 100.0  # us (100 MHz) after chunk 0's prefix
+                raise N.NativeError("avdb_vcf_tokenize", -1,
+                                    f"{lb_err} look-back waits gave up (outputs invalid); first: chunk {c} "
+                                    f"waited on {j} (status now {stuck[2]:#x}, phase {stuck[3]}; loop last read "
+                                    f"{stuck[4]:#x} from chunk {stuck[5]}, not-ready lanes {stuck[6]:#x}); gave up at "
+                                    f"{rel(stuck[7])} us, chunk {j} published agg at {rel(clk[j, 0])} us, prefix at "
+                                    f"{rel(clk[j, 1])} us, chunk {c} agg at {rel(clk[c, 0])} us; "
+                                    f"{nc} chunks by last phase {phases}")
+            if t_lines != n_lines or n_rec > rec_cap:  # the count pass bounds both: never expected
+                raise N.NativeError("avdb_vcf_tokenize", -1,
+                                    f"lines {t_lines} (counted {n_lines}), records {n_rec} (bound {rec_cap})")
+            if n_heap <= heap_cap:
+                break
+            heap_cap = n_heap
+        b = RecordBatch(chrom=chrom[:n_rec], pos=pos[:n_rec], allele_off=allele_off[:n_rec],
+                        ref_len=ref_len[:n_rec], alt_len=alt_len[:n_rec], heap=heap[:max(1, n_heap)],
+                        ext_id=ext_id[:n_rec])
+        return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
+                        records=b, rec_line=rec_line[:n_rec], rec_alt=rec_alt[:n_rec])
 
     # -- K9: this rank's lines of a VCF text -----------------------------------
     def vcf_select(self, vb: "VcfBatch", assignment, rank: int, cut: int = 64_000_000) -> torch.Tensor:

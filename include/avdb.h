@@ -242,6 +242,27 @@ int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t 
                   uint8_t* chrom, uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len,
                   uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line,
                   uint32_t* rec_alt, void* stream);
+/* K0 in one text pass (the same outputs as steps 2 + 3, the text read once):
+ *   avdb_vcf_count_text  -> counts[0] = '\n' bytes, counts[1] = ',' bytes (device u64[2];
+ *      workspace AVDB_VCF_COUNT_WORKSPACE_BYTES).  n_lines follows as for step 1, and
+ *      n_lines + commas bounds the records (each is a line's first ALT or follows a comma).
+ *   avdb_vcf_tokenize    -> the line table, rec_off / heap_off (n_lines + 1 entries), the
+ *      record SoA and the allele heap, as avdb_vcf_parse_lines + avdb_vcf_emit give them.
+ *      Outputs are written up to the capacities given (lines_cap lines, rec_cap records,
+ *      heap_cap heap bytes; a line whose records or heap bytes would pass a capacity is
+ *      not emitted); totals (device u64[4]) = lines, records, heap bytes, and [3] = 0
+ *      (nonzero: an internal scan wait gave up; the outputs are then invalid).  When a
+ *      total exceeds its capacity, call again with larger buffers.  The workspace must
+ *      not be shared by calls in flight on different streams. */
+int avdb_vcf_count_text(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
+                        size_t workspace_bytes, uint64_t* counts, void* stream);
+int avdb_vcf_tokenize_workspace_size(size_t text_bytes, size_t* bytes);
+int avdb_vcf_tokenize(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
+                      size_t workspace_bytes, size_t lines_cap, avdb_vcf_line* lines, uint64_t* rec_off,
+                      uint64_t* heap_off, size_t rec_cap, uint8_t* chrom, uint32_t* pos, uint64_t* allele_off,
+                      uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id, uint32_t* rec_line,
+                      uint32_t* rec_alt, size_t heap_cap, uint8_t* heap, uint64_t* totals,
+                      const avdb_vcf_opts* opts, void* stream);
 
 /* ---- K5: the load driver's text outputs ---------------------------------
  * Replaces the per-alt COPY row assembly of VCFVariantLoader.__parse_alt_alleles

@@ -26,6 +26,9 @@ for s in "$@"; do
     dropin) step bench_dropin 600 python bench.py --workload dropin ;;
     c2) step bench_c2 600 python bench.py --steps 20 --warmup 3 ;;
     c1|c3|c4|c4k|c5|load|vcf) step "bench_$s" 600 python bench.py --steps 10 --warmup 3 --workload "$s" ;;
+    ab:*) # ab:NAME=VALUE:workload  — one bench line with an env knob set (A/B)
+      kv=${s#ab:}; w=${kv##*:}; kv=${kv%:*}
+      step "bench_${w}_${kv//=/_}" 600 env "$kv" python bench.py --steps 10 --warmup 3 --cpu-baseline off --workload "$w" ;;
     prof:*) w=${s#prof:}
       step "rocprof_$w" 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$w" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-baseline off --workload "$w" ;;
     *) echo "unknown step $s"; exit 2 ;;
