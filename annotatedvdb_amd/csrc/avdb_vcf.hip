@@ -382,29 +382,45 @@ __device__ __forceinline__ void block_scan2(uint64_t a, uint64_t b, uint64_t* ea
   __syncthreads();  // s_scr is reused by the next call
 }
 
-// The look-back's cross-workgroup words are read and written ONLY with 8-byte
-// agent-scope atomic read-modify-writes (MI355X_MICROARCH.md, "Valid forms":
-// 8-B agent atomics both sides).  Per-XCD L2s are not coherent: an acquire load
-// poll is L2-served, and a status line this XCD cached while it was still zero
-// read as zero until evicted (the first form of this pass gave up waiting on
-// most chunks); atomics are performed where every XCD sees the same value.
-// (a compare-exchange of 0 for 0: LLVM lowers an idempotent fetch_or / fetch_add
-// of 0 to a plain atomic load, which is L2-served again)
+// The look-back's cross-workgroup words: relaxed agent-scope loads and stores
+// (global_load/store sc1, as rocPRIM's look-back scan), the status word stored
+// after an explicit s_waitcnt for the payload stores before it
+// (MI355X_MICROARCH.md, compiler hazard).  tools/handoff_probe.hip measured this
+// form and 8-byte agent atomics on both sides equally (no lost or stale hand-off).
 __device__ __forceinline__ uint64_t tok_read(uint64_t* p) {
-  uint64_t e = 0;
-  __hip_atomic_compare_exchange_strong(p, &e, 0ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return e;
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void tok_write(uint64_t* p, uint64_t v) {
-  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// a status word after the payload words it announces
 __device__ __forceinline__ void tok_publish(uint64_t* st, uint64_t v) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   tok_write(st, v);
 }
 
-// the chunk's exclusive (lines, records, heap) prefix; wave 0 calls it
+// aggregate (lines, records, heap) of a status word with flag 1 or 3
+__device__ __forceinline__ void tok_agg(const TokArgs& A, uint64_t v, int64_t j, uint64_t& a0, uint64_t& a1,
+                                        uint64_t& a2) {
+  if ((v >> 62) == 1) {
+    a0 += (v >> 42) & 0xFFFFFull;
+    a1 += (v >> 22) & 0xFFFFFull;
+    a2 += v & 0x3FFFFFull;
+  } else {
+    a0 += tok_read(A.agg + 3 * j);
+    a1 += tok_read(A.agg + 3 * j + 1);
+    a2 += tok_read(A.agg + 3 * j + 2);
+  }
+}
+
+// the chunk's exclusive (lines, records, heap) prefix; wave 0 calls it.  Each
+// poll step reads kLbPer status words per lane (512 chunks per round trip): all
+// workgroups finish their parse at about the same time, so a chunk far from the
+// last published prefix would otherwise walk back one 64-chunk window per round
+// trip (tools/handoff_probe.hip: ~90 ns per chunk that way).
+#ifndef AVDB_TOK_LBPER
+#define AVDB_TOK_LBPER 8
+#endif
+constexpr int kLbPer = AVDB_TOK_LBPER;
 __device__ __forceinline__ void tok_lookback(const TokArgs& A, size_t c, uint64_t T, uint64_t R, uint64_t H,
                                              uint64_t* ex) {
   const uint32_t lane = __lane_id();
@@ -424,66 +440,74 @@ __device__ __forceinline__ void tok_lookback(const TokArgs& A, size_t c, uint64_
     int64_t base = int64_t(c) - 1;
     uint32_t spins = 0;
     while (true) {
-      const int64_t j = base - int64_t(lane);
-      uint64_t v = kTokInc;  // before chunk 0: a zero prefix
-      bool ready = true;
-      if (j >= 0) {
-        v = tok_read(A.status + j);
-        ready = (v >> 62) != 0;
+      uint64_t v[kLbPer];
+      uint32_t nr = 0;  // bit k: status k not published yet
+#pragma unroll
+      for (int k = 0; k < kLbPer; ++k) {
+        const int64_t j = base - kLbPer * int64_t(lane) - k;
+        v[k] = j >= 0 ? tok_read(A.status + j) : kTokInc;  // before chunk 0: a zero prefix
       }
-      while (!__all(ready)) {
+#pragma unroll
+      for (int k = 0; k < kLbPer; ++k) nr |= ((v[k] >> 62) == 0 ? 1u : 0u) << k;
+      while (!__all(nr == 0)) {
         __builtin_amdgcn_s_sleep(2);
-        if (!ready) {
-          v = tok_read(A.status + j);
-          ready = (v >> 62) != 0;
+#pragma unroll
+        for (int k = 0; k < kLbPer; ++k) {
+          if (nr >> k & 1u) {
+            v[k] = tok_read(A.status + (base - kLbPer * int64_t(lane) - k));
+            if (v[k] >> 62) nr &= ~(1u << k);
+          }
         }
         if (++spins > kTokSpinLimit) {  // never expected: count it, never hang
-          {
-            const uint64_t nr = __ballot(!ready);
-            const uint32_t l0 = nr ? uint32_t(__ffsll((unsigned long long)nr)) - 1 : 0u;
-            const uint64_t vl = (uint64_t(uint32_t(__shfl(uint32_t(v >> 32), l0, kWave))) << 32) |
-                                uint32_t(__shfl(uint32_t(v), l0, kWave));
-            const uint64_t jl = uint64_t(__shfl(uint32_t(j), l0, kWave));
-            if (lane == 0 && atomicAdd(A.totals + 3, 1ull) == 0) {
-              const int64_t jj = base - int64_t(l0);
-              A.stuck[0] = c;
-              A.stuck[1] = uint64_t(jj);
-              A.stuck[2] = jj >= 0 ? tok_read(A.status + jj) : ~0ull;
-              A.stuck[3] = jj >= 0 ? A.trace[jj] : ~0u;
-              A.stuck[4] = vl;  // what the poll loop last read
-              A.stuck[5] = jl;  // the chunk the poll loop read it from
-              A.stuck[6] = nr;
-              A.stuck[7] = __builtin_amdgcn_s_memrealtime();
-            }
+          const uint64_t nrb = __ballot(nr != 0);
+          const uint32_t l0 = nrb ? uint32_t(__ffsll((unsigned long long)nrb)) - 1 : 0u;
+          const uint32_t nr0 = __shfl(nr, l0, kWave);
+          if (lane == 0 && atomicAdd(A.totals + 3, 1ull) == 0) {
+            const int64_t jj = base - kLbPer * int64_t(l0) - (nr0 ? __builtin_ctz(nr0) : 0);
+            A.stuck[0] = c;
+            A.stuck[1] = uint64_t(jj);
+            A.stuck[2] = jj >= 0 ? tok_read(A.status + jj) : ~0ull;
+            A.stuck[3] = jj >= 0 ? A.trace[jj] : ~0u;
+            A.stuck[4] = 0;
+            A.stuck[5] = 0;
+            A.stuck[6] = nrb;
+            A.stuck[7] = __builtin_amdgcn_s_memrealtime();
           }
-          if (!ready) v = kTokInc;
-          ready = true;
+#pragma unroll
+          for (int k = 0; k < kLbPer; ++k)
+            if (nr >> k & 1u) v[k] = kTokInc;
+          nr = 0;
         }
       }
-      const uint64_t f = v >> 62;
-      const uint64_t pm = __ballot(f == 2);
-      const uint32_t l = pm ? uint32_t(__ffsll((unsigned long long)pm)) - 1 : kWave;  // nearest inclusive
+      // the nearest published prefix: lane l, its status kf
+      uint32_t kf = kLbPer;
+#pragma unroll
+      for (int k = kLbPer - 1; k >= 0; --k)
+        if ((v[k] >> 62) == 2) kf = k;
+      const uint64_t pm = __ballot(kf < uint32_t(kLbPer));
+      const uint32_t l = pm ? uint32_t(__ffsll((unsigned long long)pm)) - 1 : kWave;
       uint64_t a0 = 0, a1 = 0, a2 = 0;
-      if (lane < l) {
-        if (f == 1) {
-          a0 = (v >> 42) & 0xFFFFFull;
-          a1 = (v >> 22) & 0xFFFFFull;
-          a2 = v & 0x3FFFFFull;
-        } else if (f == 3) {
-          a0 = tok_read(A.agg + 3 * j);
-          a1 = tok_read(A.agg + 3 * j + 1);
-          a2 = tok_read(A.agg + 3 * j + 2);
+      if (lane <= l) {
+        const uint32_t kn = lane < l ? uint32_t(kLbPer) : kf;  // aggregates before the prefix
+#pragma unroll
+        for (int k = 0; k < kLbPer; ++k) {
+          const int64_t j = base - kLbPer * int64_t(lane) - k;
+          if (uint32_t(k) < kn && j >= 0) tok_agg(A, v[k], j, a0, a1, a2);
         }
-      } else if (lane == l && j >= 0) {
-        a0 = tok_read(A.pre + 3 * j);
-        a1 = tok_read(A.pre + 3 * j + 1);
-        a2 = tok_read(A.pre + 3 * j + 2);
+        if (lane == l && kf < uint32_t(kLbPer)) {
+          const int64_t j = base - kLbPer * int64_t(lane) - kf;
+          if (j >= 0) {
+            a0 += tok_read(A.pre + 3 * j);
+            a1 += tok_read(A.pre + 3 * j + 1);
+            a2 += tok_read(A.pre + 3 * j + 2);
+          }
+        }
       }
       s0 += wave_sum64(a0);
       s1 += wave_sum64(a1);
       s2 += wave_sum64(a2);
       if (pm) break;
-      base -= kWave;
+      base -= kLbPer * kWave;
     }
   }
   if (lane == 0) {
@@ -498,7 +522,10 @@ __device__ __forceinline__ void tok_lookback(const TokArgs& A, size_t c, uint64_
   ex[2] = s2;
 }
 
-__global__ __launch_bounds__(kBlock) void k_vcf_tokenize(TokArgs A) {
+#ifndef AVDB_TOK_WAVES
+#define AVDB_TOK_WAVES 1  // min waves per SIMD the register allocation must allow (A/B knob)
+#endif
+__global__ __launch_bounds__(kBlock, AVDB_TOK_WAVES) void k_vcf_tokenize(TokArgs A) {
   __shared__ u32x4 s_text[kTokStage16];
   __shared__ uint32_t s_start[kBlock + 1];  // line starts of the round, relative to c0
   __shared__ uint64_t s_scr[2 * kVcfWaves];
@@ -823,9 +850,13 @@ extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
     avdb_set_error("avdb_vcf_parse_lines: workspace of %zu bytes required", need);
     return AVDB_ERANGE;
   }
-  if (n_lines == 0) return AVDB_OK;
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (n_lines == 0) {  // rec_off[0] = heap_off[0] = 0 (the totals of no lines)
+    AVDB_HIP_TRY(hipMemsetAsync(rec_off, 0, 8, s));
+    AVDB_HIP_TRY(hipMemsetAsync(heap_off, 0, 8, s));
+    return AVDB_OK;
+  }
   auto* starts = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + AVDB_VCF_COUNT_WORKSPACE_BYTES);
   void* tmp = reinterpret_cast<char*>(starts) + ((8 * n_lines + 255) & ~size_t(255));
   size_t tmp_bytes = scan_temp_bytes(n_lines + 1);

@@ -811,6 +811,7 @@ class Engine:
                 self.ctx, tp, nb, N.ptr(ws), ws.numel(), n_lines, N.ptr(lines), N.ptr(rec_off), N.ptr(heap_off),
                 rec_cap, N.ptr(chrom), N.ptr(pos), N.ptr(allele_off), N.ptr(ref_len), N.ptr(alt_len),
                 N.ptr(ext_id), N.ptr(rec_line), N.ptr(rec_alt), heap_cap, N.ptr(heap), N.ptr(tot), opts, s))
+            self._tok_ws = ws  # (diagnostics: tools/k0_onepass_probe.py reads the per-chunk clocks)
             t_lines, n_rec, n_heap, lb_err = (int(x) for x in tot.cpu().tolist())
             if lb_err:
                 nc = -(-nb // 16384)
