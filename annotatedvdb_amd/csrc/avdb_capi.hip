@@ -41,6 +41,7 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
   memset(&c->tab, 0, sizeof(c->tab));
   c->device = device;
   c->d_seq_digest = nullptr;
+  c->d_loc_tail = nullptr;
   c->has_digests = false;
   c->tab.n = n_chrom;
   uint32_t off = 0;
@@ -130,6 +131,10 @@ extern "C" int avdb_ctx_destroy(avdb_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipFree(ctx->d_seq_digest);
   }
+  if (ctx->d_loc_tail) {
+    (void)hipSetDevice(ctx->device);
+    (void)hipFree(ctx->d_loc_tail);
+  }
   delete ctx;
   return AVDB_OK;
 }
@@ -152,6 +157,11 @@ extern "C" int avdb_ctx_set_sequence_digests(avdb_ctx* ctx, const char* digests,
     AVDB_HIP_TRY(hipMalloc(&ctx->d_seq_digest, size_t(AVDB_MAX_CHROM) * AVDB_DIGEST_CHARS));
   AVDB_HIP_TRY(hipMemcpy(ctx->d_seq_digest, digests, size_t(n_chrom) * AVDB_DIGEST_CHARS,
                          hipMemcpyHostToDevice));
+  std::vector<uint64_t> tail;
+  avdb::location_tail_table(digests, n_chrom, tail);
+  if (!ctx->d_loc_tail)
+    AVDB_HIP_TRY(hipMalloc(&ctx->d_loc_tail, size_t(AVDB_MAX_CHROM) * 19 * 16 * sizeof(uint64_t)));
+  AVDB_HIP_TRY(hipMemcpy(ctx->d_loc_tail, tail.data(), tail.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
   ctx->has_digests = true;
   return AVDB_OK;
 }

@@ -19,7 +19,9 @@
 // words at segment boundaries are assembled bytewise.  The SHA-512 state and
 // the 16-word schedule stay in registers; the compression has a single call
 // site per kernel.
-#include "avdb_internal.hpp"
+#include "avdb_fmt.hpp"  // ascii8 / ndigits (SWAR decimal text)
+
+#include <vector>
 
 namespace avdb {
 
@@ -213,11 +215,6 @@ __device__ __forceinline__ uint8_t word_char(const uint64_t* w4, uint32_t k) {  
   return uint8_t(x >> (8 * (k & 7)));
 }
 
-__device__ __forceinline__ uint32_t ndigits(uint32_t v) {
-  uint32_t d = 1;
-  while (v >= 10u) { v /= 10u; ++d; }
-  return d;
-}
 
 
 __device__ __forceinline__ void store_digest(char* o, const uint64_t* cw) {
@@ -504,18 +501,10 @@ struct MsgSink {
       append(x, t);
     }
   }
-  __device__ __forceinline__ void digits(uint32_t v) {  // decimal, no leading zeros
-    uint64_t d = 0;
-    uint32_t nd = 0;
-    do { d = (d << 4) | (v % 10u); v /= 10u; ++nd; } while (v);
-    for (uint32_t h = 0; h < nd; h += 8, d >>= 32) {  // nibbles -> ASCII bytes
-      uint64_t y = d & 0xFFFFFFFFull;
-      y = (y | (y << 16)) & 0x0000FFFF0000FFFFull;
-      y = (y | (y << 8)) & 0x00FF00FF00FF00FFull;
-      y = (y | (y << 4)) & 0x0F0F0F0F0F0F0F0Full;
-      const uint32_t t = nd - h < 8u ? nd - h : 8u;
-      append((y + 0x3030303030303030ull) & low_bytes_mask(t), t);
-    }
+  __device__ __forceinline__ void digits(uint32_t v) {  // decimal, no leading zeros (SWAR, K7's dec_text)
+    const Dec d = dec_text(v);
+    append(d.lo, d.n < 8 ? d.n : 8);
+    if (d.n > 8) append(d.hi, d.n - 8);
   }
   // SHA padding for a T-byte message of nb blocks: 0x80, zeros, 128-bit length
   __device__ __forceinline__ void finish(uint64_t T, uint32_t nb) {
@@ -533,10 +522,14 @@ struct MsgSink {
 };
 
 // the VRS SequenceLocation serialisation of interval (S, E] on a contig whose 32
-// refget chars are dig (4 little-endian words), block `blk` of its 2
-__device__ __forceinline__ void location_block(uint64_t* slot, uint32_t blk, uint32_t S, uint32_t E,
-                                               const uint64_t* dig, uint64_t T) {
-  MsgSink m(slot, blk);
+// refget chars are dig (4 little-endian words): its first block.  The
+// serialisation is 183 + nE + nS bytes (2 SHA blocks for every 32-bit position)
+// and the digits end at byte 79 + nE + nS < 128, so block 0 is complete once the
+// digest chars are appended, and block 1 depends only on the contig and
+// nE + nS: it is read from the table avdb_ctx_set_sequence_digests builds
+// (location_tail_table) instead of being serialised again per record.
+__device__ __forceinline__ void location_block0(uint64_t* slot, uint32_t S, uint32_t E, const uint64_t* dig) {
+  MsgSink m(slot, 0);
   m.lit(LOC0);
   m.digits(E);
   m.lit(LOC1);
@@ -544,8 +537,6 @@ __device__ __forceinline__ void location_block(uint64_t* slot, uint32_t blk, uin
   m.lit(LOC2);
 #pragma unroll
   for (int q = 0; q < 4; ++q) m.append(dig[q], 8);
-  m.lit(LOC3);
-  m.finish(T, sha_blocks(T));
 }
 
 // compile-time little-endian 8-byte chunk of a string literal (zero past its end)
@@ -641,11 +632,58 @@ __device__ __forceinline__ void allele_block(uint64_t* w, uint32_t ab, const uin
                                              uint64_t altoff, uint32_t a, uint64_t TA, uint32_t nb,
                                              const uint64_t* s_suf) {
   const int64_t Q = int64_t(kAlPrefix) + a;  // first suffix byte
+  // a block wholly inside the ALT bytes for every lane of the wave (lanes are
+  // grouped by block count, so all but the last two blocks of a long ALT are):
+  // each word is one heap load, byte-swapped — no prefix, mask or suffix window
+  const bool inside = ab >= 1 && int64_t(ab) * 128 + 128 <= Q;
+  if (__all(inside)) {
+    const uint64_t b0 = altoff + 128 * uint64_t(ab) - kAlPrefix;
+    if (hp.lo + b0 + 128 <= hp.hi) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap64(alt_word<false>(hp, b0 + 8 * j));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap64(alt_word<true>(hp, b0 + 8 * j));
+    }
+    return;
+  }
   if (hp.lo + altoff + 128 * uint64_t(ab) + 128 <= hp.hi)
     allele_words<false>(w, ab, locw, hp, altoff, Q, s_suf);
   else
     allele_words<true>(w, ab, locw, hp, altoff, Q, s_suf);
   if (ab + 1 == nb) w[15] = TA * 8;  // (w[14], the high length word, is 0 from the table)
+}
+
+constexpr uint32_t kLocTailS = 19;  // nE + nS = 2..20
+
+// Host: block 1 of every contig's SequenceLocation serialisation for each digit
+// count nE + nS, as the big-endian message words SHA-512 consumes (the digit
+// values lie in block 0; block 1 = the rest of LOC2, the digest chars, LOC3, the
+// padding and the bit length 8 * (183 + nE + nS)).
+void location_tail_table(const char* digests, int n_chrom, std::vector<uint64_t>& out) {
+  out.assign(size_t(n_chrom) * kLocTailS * 16, 0);
+  for (int c = 0; c < n_chrom; ++c) {
+    for (uint32_t s = 2; s <= 20; ++s) {
+      uint8_t m[256] = {0};
+      size_t k = 0;
+      auto put = [&](const char* t, size_t n) { for (size_t q = 0; q < n; ++q) m[k++] = uint8_t(t[q]); };
+      put(LOC0, nL0);
+      for (uint32_t q = 0; q < s; ++q) m[k++] = '0';  // E and S digits: their values lie in block 0
+      put(LOC1, nL1);
+      put(LOC2, nL2);
+      put(digests + size_t(c) * AVDB_DIGEST_CHARS, AVDB_DIGEST_CHARS);
+      put(LOC3, nL3);
+      const uint64_t T = k;  // 183 + s
+      m[k] = 0x80;
+      for (int q = 0; q < 8; ++q) m[255 - q] = uint8_t((T * 8) >> (8 * q));
+      uint64_t* o = &out[(size_t(c) * kLocTailS + (s - 2)) * 16];
+      for (int j = 0; j < 16; ++j) {
+        uint64_t v = 0;
+        for (int q = 0; q < 8; ++q) v = (v << 8) | m[128 + 8 * j + q];
+        o[j] = v;
+      }
+    }
+  }
 }
 
 // Waves per SIMD (launch bound and persistent grid).  3: <= 168 VGPRs, no
@@ -659,7 +697,8 @@ __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
     const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
     const uint32_t* __restrict__ list, const unsigned int* __restrict__ count,
-    const char* __restrict__ seq_digest, int n_chrom, char* __restrict__ out) {
+    const char* __restrict__ seq_digest, const uint64_t* __restrict__ loc_tail, int n_chrom,
+    char* __restrict__ out) {
   __shared__ uint64_t s_w[16 * kBlock];
   __shared__ uint64_t s_suf[kSufTab];
   if (threadIdx.x < kSufTab) {  // 8-byte windows of (8 zero bytes | AL2 | 0x80 | zeros)
@@ -686,8 +725,9 @@ __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     }
     // gnomAD chr-pos-ref-alt -> interbase interval (pos-1, pos-1+len(ref)]
     const uint32_t S = pos[i] - 1u, E = S + r;
-    const uint64_t TL = uint64_t(nL0 + nL1 + nL2 + nL3 + AVDB_DIGEST_CHARS) + ndigits(E) + ndigits(S);
-    const uint32_t nbL = sha_blocks(TL);  // 2 for every 32-bit position
+    const uint32_t nES = ndigits(E) + ndigits(S);  // 2..20
+    constexpr uint32_t nbL = 2;  // sha_blocks(183 + nES) for every 32-bit position
+    const uint64_t* tail = loc_tail + (size_t(c) * kLocTailS + (nES - 2)) * 16;
     const uint64_t* dg = reinterpret_cast<const uint64_t*>(seq_digest + size_t(c) * AVDB_DIGEST_CHARS);
     const uint64_t dig[4] = {dg[0], dg[1], dg[2], dg[3]};
     const uint64_t altoff = off[i] + r;
@@ -702,10 +742,18 @@ __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     // b is uniform across the wave, so the branch does not diverge.
     for (uint32_t b = 0; b < nbL + nbA; ++b) {
       uint64_t w[16];
-      if (b < nbL) {
-        location_block(slot, b, S, E, dig, TL);
+      if (b == 0) {
+        location_block0(slot, S, E, dig);
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j] = slot[j * kBlock];
+      } else if (b == 1) {
+        const u32x4* t4 = reinterpret_cast<const u32x4*>(tail);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const u32x4 v = t4[j];
+          w[2 * j] = uint64_t(v.x) | (uint64_t(v.y) << 32);
+          w[2 * j + 1] = uint64_t(v.z) | (uint64_t(v.w) << 32);
+        }
       } else {
         allele_block(w, b - nbL, locw, hp, altoff, a, TA, nbA, s_suf);
       }
@@ -757,7 +805,7 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
     avdb_set_error("avdb_vrs_digest: null array");
     return AVDB_EINVAL;
   }
-  if (!ctx->has_digests || !ctx->d_seq_digest) {
+  if (!ctx->has_digests || !ctx->d_seq_digest || !ctx->d_loc_tail) {
     avdb_set_error("avdb_vrs_digest: sequence digests not set (avdb_ctx_set_sequence_digests)");
     return AVDB_EINVAL;
   }
@@ -802,8 +850,8 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   const int per_cu = ctx->k4_blocks_per_cu < kDigestWavesPerSimd ? ctx->k4_blocks_per_cu : kDigestWavesPerSimd;
   hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * per_cu), dim3(kBlock), 0, s, chrom, pos,
                      allele_off,
-                     ref_len, alt_len, heap, heap_bytes, list, total, ctx->d_seq_digest, ctx->tab.n,
-                     digest_out);
+                     ref_len, alt_len, heap, heap_bytes, list, total, ctx->d_seq_digest, ctx->d_loc_tail,
+                     ctx->tab.n, digest_out);
   AVDB_LAUNCH_CHECK("k_vrs_digest");
   return AVDB_OK;
 }

@@ -246,14 +246,18 @@ struct avdb_ctx {
   int k0_blocks_per_cu;  // K0 one-pass grid = n_cu * this (env AVDB_K0_BLOCKS_PER_CU)
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
+  uint64_t* d_loc_tail;  // K4: block 1 of each contig's SequenceLocation message per digit count (avdb_digest.hip)
   bool has_digests;
 };
 
 void avdb_set_error(const char* fmt, ...);
 
+#include <vector>
 namespace avdb {
 // workspace bytes K7's size pass needs for n records (u16 sizes + their scan)
 size_t key_size_workspace(size_t n);
+// K4's per-(contig, digit count) SequenceLocation block-1 table (host)
+void location_tail_table(const char* digests, int n_chrom, std::vector<uint64_t>& out);
 }  // namespace avdb
 
 #define AVDB_HIP_TRY(expr)                                                         \

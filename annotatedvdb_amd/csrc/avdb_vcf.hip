@@ -418,7 +418,7 @@ __device__ __forceinline__ void tok_agg(const TokArgs& A, uint64_t v, int64_t j,
 // last published prefix would otherwise walk back one 64-chunk window per round
 // trip (tools/handoff_probe.hip: ~90 ns per chunk that way).
 #ifndef AVDB_TOK_LBPER
-#define AVDB_TOK_LBPER 8
+#define AVDB_TOK_LBPER 1  // status words per lane per poll (A/B at 2 waves/SIMD: 8 4.13 ms, 1 3.84)
 #endif
 constexpr int kLbPer = AVDB_TOK_LBPER;
 __device__ __forceinline__ void tok_lookback(const TokArgs& A, size_t c, uint64_t T, uint64_t R, uint64_t H,
@@ -523,7 +523,7 @@ __device__ __forceinline__ void tok_lookback(const TokArgs& A, size_t c, uint64_
 }
 
 #ifndef AVDB_TOK_WAVES
-#define AVDB_TOK_WAVES 1  // min waves per SIMD the register allocation must allow (A/B knob)
+#define AVDB_TOK_WAVES 4  // min waves per SIMD the register allocation must allow (A/B: 2 4.13 ms, 3 3.34, 4 3.15)
 #endif
 __global__ __launch_bounds__(kBlock, AVDB_TOK_WAVES) void k_vcf_tokenize(TokArgs A) {
   __shared__ u32x4 s_text[kTokStage16];
