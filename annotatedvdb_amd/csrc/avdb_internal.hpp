@@ -244,6 +244,7 @@ struct avdb_ctx {
   int k2_blocks_per_cu;  // K2 grid = n_cu * this (env AVDB_K2_BLOCKS_PER_CU)
   int k4_blocks_per_cu;  // K4 digest grid = n_cu * this (env AVDB_K4_BLOCKS_PER_CU; default: its occupancy, 3)
   int k0_blocks_per_cu;  // K0 one-pass grid = n_cu * this (env AVDB_K0_BLOCKS_PER_CU)
+  size_t k3_list_min;    // K3 grouped: two-phase list form from this many records on (env AVDB_K3_LIST_MIN)
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
   uint64_t* d_loc_tail;  // K4: block 1 of each contig's SequenceLocation message per digit count (avdb_digest.hip)

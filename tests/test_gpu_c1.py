@@ -253,11 +253,12 @@ def test_k7_reused_buffers_flag_overflow(engine, onepass):
         kt2.host(64)
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 257, 4097, 300001, 1048577 + 300])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 257, 4097, 300001, 1048577 + 300, (4 << 20) - 1, (4 << 20) + 4097])
 def test_k7_onepass_equals_two_pass(engine, n):
     """K7 with group offsets (group totals + two scans + a write pass that writes
     the offsets) == the size pass + hipCUB scans + write pass: offsets, states, key
-    and path text, at sizes that end off every tile, group and scan-block boundary."""
+    and path text, at sizes that end off every tile, group and scan-block boundary,
+    with one-tile groups (below 4 M records) and four-tile groups (from 4 M on)."""
     from annotatedvdb_amd import synth
     digs = ["%032d" % (7 * i) for i in range(25)]
     engine.set_sequence_digests(digs)
