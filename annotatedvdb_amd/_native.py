@@ -98,7 +98,8 @@ EXPORTED_SYMBOLS = [
     "avdb_display_attributes",
     "avdb_keyset_workspace_size", "avdb_keyset_build", "avdb_keyset_probe",
     "avdb_primary_keys", "avdb_keyset_probe_text", "avdb_primary_keys_bound",
-    "avdb_primary_keys_onepass_workspace_size", "avdb_primary_keys_onepass",
+    "avdb_primary_keys_onepass_workspace_size", "avdb_primary_keys_onepass", "avdb_primary_keys_onepass_ex",
+    "avdb_record_prep_keyed",
     "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
     "avdb_small_prep", "avdb_small_prep_host", "avdb_bin_path_host", "avdb_host_alloc", "avdb_host_free",
     "avdb_rccl_unique_id", "avdb_rccl_comm_init", "avdb_rccl_comm_destroy",
@@ -107,6 +108,7 @@ EXPORTED_SYMBOLS = [
 
 
 SMALL_PATH, SMALL_KEY, SMALL_DISPLAY = 1, 2, 4
+KEYS_TOTALS_READY = 1  # AVDB_KEYS_TOTALS_READY
 SMALL_MAX = 65536
 
 
@@ -184,6 +186,9 @@ def _sig(lib):
     f.avdb_keyset_probe.argtypes = [P, P, SZ, P, P, SZ, P, P, P, P, P, P, SZ, SZ, I32, P, P, P, P]
     f.avdb_primary_keys.argtypes = [P, P, P, P, P, P, P, SZ, P, P, P, SZ, U32, P, SZ, P, P, P, SZ, P, SZ, P, P]
     f.avdb_primary_keys_onepass.argtypes = list(f.avdb_primary_keys.argtypes)  # same signature
+    f.avdb_primary_keys_onepass_ex.argtypes = list(f.avdb_primary_keys.argtypes)[:-1] + [U32, P]
+    f.avdb_record_prep_keyed.argtypes = list(f.avdb_record_prep.argtypes)[:-1] + [P, U32, I32, I32, P, SZ,
+                                                                                 ctypes.POINTER(I32), P]
     f.avdb_primary_keys_bound.argtypes = [SZ, SZ, ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
     f.avdb_primary_keys_onepass_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]

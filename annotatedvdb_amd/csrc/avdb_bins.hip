@@ -15,7 +15,7 @@
 // batch (so a position-sorted batch hits a narrow, LDS-resident slice of the
 // histogram), per-contig lengths and L8 offsets staged in LDS, and
 // wave-ballot run aggregation for the histogram atomics.
-#include "avdb_internal.hpp"
+#include "avdb_fmt.hpp"  // K7 key / path sizes for the keyed K2
 
 namespace avdb {
 
@@ -367,13 +367,26 @@ __global__ __launch_bounds__(kBlock) void k_record_prep(
 // the heap.  Grid-stride over a resident grid, as K1.
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-template <bool HIST, int UNROLL>
+// The keyed form (KEYS, avdb_record_prep_keyed) also gives K7 its group totals:
+// a wave's 64 lanes x 4 records per step are exactly one of K7's 256-record scan
+// groups, so the key / path sizes of its records (the SoA is in registers; only
+// the refSNP ids are read in addition) are summed over the wave and stored as
+// that group's totals — K7's own totals pass re-read 25 B per record.
+struct KeyTotals {
+  const u64x2* ext2;    // refSNP keys, 2 per u64x2 (nullable: none)
+  uint2* tot;           // K7 group totals (avdb::key_totals_of(workspace))
+  uint32_t max_seq_len;
+  uint32_t n_key_chrom; // labelled contigs
+  uint32_t has_digest, with_paths;
+};
+
+template <bool HIST, int UNROLL, bool KEYS = false>
 __global__ __launch_bounds__(kK1Block) void k_record_prep4(
     const uint32_t* __restrict__ chromv, const u32x4* __restrict__ pos4, const u64x2* __restrict__ off2,
     const u32x4* __restrict__ rl4, const u32x4* __restrict__ al4, const uint8_t* __restrict__ heap,
     size_t heap_bytes, size_t ngroups, u32x4* __restrict__ end4, u32x4* __restrict__ code4,
     uint32_t* __restrict__ statusv, u32x4* __restrict__ lcp4, ChromTable tab, uint32_t* __restrict__ g_hist,
-    unsigned long long* __restrict__ g_ctr, int lds_hist,
+    unsigned long long* __restrict__ g_ctr, int lds_hist, KeyTotals kt,
     // scalar tail [tail_begin, n): block 0, wave 0
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ rl, const uint32_t* __restrict__ al, size_t tail_begin, size_t n,
@@ -407,6 +420,16 @@ __global__ __launch_bounds__(kK1Block) void k_record_prep4(
       o23[u] = __builtin_nontemporal_load(&off2[2 * jj + 1]);
       r4[u] = __builtin_nontemporal_load(&rl4[jj]);
       a4[u] = __builtin_nontemporal_load(&al4[jj]);
+    }
+    u64x2 x01[UNROLL], x23[UNROLL];  // KEYS: refSNP keys
+    if constexpr (KEYS) {
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const size_t j = base + size_t(u) * bdim + threadIdx.x;
+        const size_t jj = j < ngroups ? j : 0;
+        x01[u] = kt.ext2 ? __builtin_nontemporal_load(&kt.ext2[2 * jj]) : u64x2{0, 0};
+        x23[u] = kt.ext2 ? __builtin_nontemporal_load(&kt.ext2[2 * jj + 1]) : u64x2{0, 0};
+      }
     }
     // first 8 bytes of ref and alt of every non-SNV record, all issued first
     uint64_t wr[UNROLL][4], wa[UNROLL][4];
@@ -468,6 +491,28 @@ __global__ __launch_bounds__(kK1Block) void k_record_prep4(
 #pragma unroll
           for (int k = 0; k < 4; ++k) wave_hist_add(key[k], hist);
         }
+      }
+      if constexpr (KEYS) {  // this wave's 256 records are one K7 group
+        uint32_t K = 0, P = 0;
+        if (live) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t c = (cw[u] >> (8 * k)) & 0xFFu;
+            const uint64_t ev = k < 2 ? x01[u][k] : x23[u][k - 2];
+            uint32_t ks, ps;
+            key_path_sizes(c, p4[u][k], r4[u][k], a4[u][k], ev, cv[k], kt.max_seq_len, kt.n_key_chrom,
+                           kt.has_digest != 0, kt.with_paths != 0, &ks, &ps);
+            K += ks;
+            P += ps;
+          }
+        }
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) {
+          K += __shfl_xor(K, d, kWave);
+          P += __shfl_xor(P, d, kWave);
+        }
+        const size_t j0 = base + size_t(u) * bdim + (threadIdx.x & ~uint32_t(kWave - 1));
+        if (__lane_id() == 0 && j0 < ngroups) kt.tot[j0 / kWave] = make_uint2(K, P);
       }
       if (live) {
         __builtin_nontemporal_store(e, &end4[j]);
@@ -598,12 +643,56 @@ extern "C" int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   return AVDB_OK;
 }
 
+static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                            const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap,
+                            size_t heap_bytes, size_t n, uint32_t* end_out, uint32_t* bin_code, uint8_t* status,
+                            uint32_t* lcp, uint32_t* hist_l8, uint64_t* counters, void* stream, const KeyTotals* keyed,
+                            int* totals_written);
+
 extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                 const uint64_t* allele_off, const uint32_t* ref_len,
                                 const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
                                 size_t n, uint32_t* end_out, uint32_t* bin_code, uint8_t* status,
                                 uint32_t* lcp, uint32_t* hist_l8, uint64_t* counters,
                                 void* stream) {
+  return record_prep_impl(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, n, end_out, bin_code,
+                          status, lcp, hist_l8, counters, stream, nullptr, nullptr);
+}
+
+extern "C" int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                      const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                                      const uint8_t* heap, size_t heap_bytes, size_t n, uint32_t* end_out,
+                                      uint32_t* bin_code, uint8_t* status, uint32_t* lcp, uint32_t* hist_l8,
+                                      uint64_t* counters, const uint64_t* ext_id, uint32_t max_seq_len,
+                                      int has_digest, int with_paths, void* key_workspace,
+                                      size_t key_workspace_bytes, int* totals_written, void* stream) {
+  if (!totals_written) {
+    avdb_set_error("avdb_record_prep_keyed: null totals_written");
+    return AVDB_EINVAL;
+  }
+  *totals_written = 0;
+  size_t need = 0;
+  avdb_primary_keys_onepass_workspace_size(n, &need);
+  if (!key_workspace || key_workspace_bytes < need || reinterpret_cast<uintptr_t>(key_workspace) % 16) {
+    avdb_set_error("avdb_record_prep_keyed: 16-byte aligned K7 one-pass workspace of %zu bytes required", need);
+    return AVDB_ERANGE;
+  }
+  KeyTotals kt;
+  kt.ext2 = reinterpret_cast<const u64x2*>(ext_id);
+  kt.tot = avdb::key_totals_of(key_workspace);
+  kt.max_seq_len = max_seq_len;
+  kt.n_key_chrom = uint32_t(ctx && ctx->tab.n < 25 ? ctx->tab.n : 25);
+  kt.has_digest = has_digest ? 1u : 0u;
+  kt.with_paths = with_paths ? 1u : 0u;
+  return record_prep_impl(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, n, end_out, bin_code,
+                          status, lcp, hist_l8, counters, stream, &kt, totals_written);
+}
+
+static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                            const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap,
+                            size_t heap_bytes, size_t n, uint32_t* end_out, uint32_t* bin_code, uint8_t* status,
+                            uint32_t* lcp, uint32_t* hist_l8, uint64_t* counters, void* stream, const KeyTotals* keyed,
+                            int* totals_written) {
   if (int rc = check_ctx(ctx)) return rc;
   if (n == 0) return AVDB_OK;
   if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap || !end_out || !bin_code) {
@@ -619,19 +708,25 @@ extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint3
   const bool vec = ctx->k2_vector && n >= 4 && aligned(chrom, 4) && aligned(pos, 16) && aligned(allele_off, 16) &&
                    aligned(ref_len, 16) && aligned(alt_len, 16) && aligned(end_out, 16) && aligned(bin_code, 16) &&
                    (!status || aligned(status, 4)) && (!lcp || aligned(lcp, 16));
+  // keyed: K7's 256-record groups (batches of key_totals_min_records() or more)
+  // and 16-byte aligned refSNP keys
+  const bool keys = keyed && vec && n >= avdb::key_totals_min_records() && (!keyed->ext2 || aligned(keyed->ext2, 16));
+  const KeyTotals kt = keys ? *keyed : KeyTotals{};
   if (vec) {
     const size_t ngroups = n / 4;
     const unsigned bdim = unsigned(kK1Block);
-    const int U = ctx->k2_unroll;
+    const int U = keys ? ctx->k2_keyed_unroll : ctx->k2_unroll;  // (the keyed form's registers: 144 VGPRs at U=2)
     const unsigned grid = stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
 #define K2V(HI, UU)                                                                                       \
-  hipLaunchKernelGGL((k_record_prep4<HI, UU>), dim3(grid), dim3(bdim), shm, s,                           \
+  if (keys) K2VK(HI, UU, true); else K2VK(HI, UU, false)
+#define K2VK(HI, UU, KK)                                                                                  \
+  hipLaunchKernelGGL((k_record_prep4<HI, UU, KK>), dim3(grid), dim3(bdim), shm, s,                       \
                      reinterpret_cast<const uint32_t*>(chrom), reinterpret_cast<const u32x4*>(pos),      \
                      reinterpret_cast<const u64x2*>(allele_off), reinterpret_cast<const u32x4*>(ref_len), \
                      reinterpret_cast<const u32x4*>(alt_len), heap, heap_bytes, ngroups,                  \
                      reinterpret_cast<u32x4*>(end_out), reinterpret_cast<u32x4*>(bin_code),              \
                      reinterpret_cast<uint32_t*>(status), reinterpret_cast<u32x4*>(lcp), ctx->tab, hist_l8, \
-                     ctr, lds_hist, chrom, pos, allele_off, ref_len, alt_len, ngroups * 4, n, end_out,   \
+                     ctr, lds_hist, kt, chrom, pos, allele_off, ref_len, alt_len, ngroups * 4, n, end_out,  \
                      bin_code, status, lcp)
     if (U == 1) {
       if (hist) K2V(true, 1);
@@ -644,7 +739,9 @@ extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint3
       else K2V(false, 2);
     }
 #undef K2V
+#undef K2VK
     AVDB_LAUNCH_CHECK("k_record_prep4");
+    if (keys && totals_written) *totals_written = 1;
     return AVDB_OK;
   }
   const unsigned grid = stream_grid(n, kBlock * 8, 2048);

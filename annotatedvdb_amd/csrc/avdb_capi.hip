@@ -108,6 +108,11 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     const int v = atoi(s);
     if (v >= 1 && v <= 64) c->k2_blocks_per_cu = v;
   }
+  c->k2_keyed_unroll = 1;
+  if (const char* s = getenv("AVDB_K2_KEYED_UNROLL")) {
+    const int v = atoi(s);
+    if (v == 1 || v == 2 || v == 4) c->k2_keyed_unroll = v;
+  }
   // K4 (SHA-512, VALU-bound) persistent grid: its occupancy by default; fewer
   // workgroups leave CUs to a kernel running beside it on another stream
   c->k4_blocks_per_cu = 3;

@@ -486,6 +486,41 @@ AVDB_HD O bin_path(O o, uint32_t c, uint32_t code) {
   return o;
 }
 
+// ---- K7 text sizes (shared by K7's group-totals pass and the keyed K2) ----
+// bytes of bin_path(c, code) in closed form: "chr" + label + 6 bytes per level
+// up to L9, 7 from L10 on, and the extra digits of an L1 bin number >= 10
+AVDB_HD uint32_t bin_path_size(uint32_t c, uint32_t code) {
+  const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
+  const uint32_t label = c < 9 ? 1u : (c < 22 ? 2u : (c < 25 ? 1u : ndigits(c)));
+  uint32_t n = 3u + label + 6u * (level < 9u ? level : 9u) + 7u * (level > 9u ? level - 9u : 0u);
+  if (level) n += ndigits((g >> (level - 1)) + 1u) - 1u;
+  return n;
+}
+
+__device__ __forceinline__ uint32_t ndigits64(uint64_t v) {
+  if (v <= 0xFFFFFFFFull) return ndigits(uint32_t(v));
+  const uint64_t q = v / 1000000000ull;
+  return 9u + (q <= 0xFFFFFFFFull ? ndigits(uint32_t(q)) : 9u + ndigits(uint32_t(q / 1000000000ull)));
+}
+
+// bytes of primary_key_generator.py:106-122's key for a labelled contig
+__device__ __forceinline__ uint32_t key_size(uint32_t c, uint32_t p, uint32_t r, uint32_t a, uint64_t e, bool lng) {
+  const uint32_t label = (c >= 9 && c < 22) ? 2u : 1u;
+  return label + 2u + ndigits(p) + (lng ? uint32_t(AVDB_DIGEST_CHARS) : r + 1u + a) +
+         ((e && !(e >> 63)) ? 3u + ndigits64(e) : 0u);
+}
+
+// the key and path sizes K7's write pass gives a record (SoA-decidable states only):
+// n_key_chrom labelled contigs, keys of long records only with digests, paths only
+// with bin codes
+__device__ __forceinline__ void key_path_sizes(uint32_t c, uint32_t p, uint32_t r, uint32_t a, uint64_t e, uint32_t cd,
+                                               uint32_t max_seq_len, uint32_t n_key_chrom, bool has_digest,
+                                               bool has_code, uint32_t* ks, uint32_t* ps) {
+  const bool lg = uint64_t(r) + a > max_seq_len;
+  *ks = (c < n_key_chrom && !(e >> 63) && !(lg && !has_digest)) ? key_size(c, p, r, a, e, lg) : 0u;
+  *ps = (has_code && cd != AVDB_BIN_NONE && c < n_key_chrom) ? bin_path_size(c, cd) : 0u;
+}
+
 // ---------------------------------------------------------------------------
 // JSON strings (json.dumps, ensure_ascii): '"' '\\' and the short escapes,
 // other bytes outside ' '..'~' as \u00XX (lowercase hex)

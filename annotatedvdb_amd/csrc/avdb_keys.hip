@@ -185,26 +185,11 @@ constexpr size_t kSmallGroupN = size_t(4) << 20;
 constexpr uint32_t kGroupsPerBlock = 4096;    // groups per block of the local scan
 constexpr uint32_t kScanThreads = 1024;       // 4 groups per thread
 
-__device__ __forceinline__ uint32_t ndigits64(uint64_t v) {
-  if (v <= 0xFFFFFFFFull) return ndigits(uint32_t(v));
-  const uint64_t q = v / 1000000000ull;
-  return 9u + (q <= 0xFFFFFFFFull ? ndigits(uint32_t(q)) : 9u + ndigits(uint32_t(q / 1000000000ull)));
-}
-
-// bytes of primary_key_generator.py:106-122's key for a labelled contig
-__device__ __forceinline__ uint32_t key_size(uint32_t c, uint32_t p, uint32_t r, uint32_t a, uint64_t e, bool lng) {
-  const uint32_t label = (c >= 9 && c < 22) ? 2u : 1u;
-  return label + 2u + ndigits(p) + (lng ? uint32_t(AVDB_DIGEST_CHARS) : r + 1u + a) +
-         ((e && !(e >> 63)) ? 3u + ndigits64(e) : 0u);
-}
-
 // the sizes the size pass gives record j (SoA-decidable key state only)
 __device__ __forceinline__ void record_sizes(const KeyArgs& A, uint32_t c, uint32_t p, uint32_t r, uint32_t a,
                                              uint64_t e, uint32_t cd, uint32_t* ks, uint32_t* ps) {
-  const bool lg = uint64_t(r) + a > A.max_seq_len;
-  *ks = (c < uint32_t(A.n_chrom) && !(e >> 63) && !(lg && !A.digest)) ? key_size(c, p, r, a, e, lg) : 0u;
-  *ps = (A.code && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom)) ? bin_path(Out<false>(nullptr, 0), c, cd).size()
-                                                                    : 0u;
+  key_path_sizes(c, p, r, a, e, cd, A.max_seq_len, uint32_t(A.n_chrom), A.digest != nullptr, A.code != nullptr, ks,
+                 ps);
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -215,9 +200,10 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 
 // group totals: one wave per group of 64 << group_log2 records (records
 // (g << group_log2 + k) * 64 + lane)
-__global__ __launch_bounds__(kBlock) void k_key_group_totals(KeyArgs A, uint2* __restrict__ tot, size_t n_groups) {
+__global__ __launch_bounds__(kBlock) void k_key_group_totals(KeyArgs A, uint2* __restrict__ tot, size_t n_groups,
+                                                              size_t g_begin) {
   const uint32_t lane = __lane_id();
-  const size_t w0 = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const size_t w0 = g_begin + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
   const size_t nw = size_t(gridDim.x) * blockDim.x / kWave;
   const uint32_t tpg = 1u << A.group_log2;
   for (size_t g = w0; g < n_groups; g += nw) {
@@ -862,6 +848,13 @@ static size_t key_groups(size_t n) {
 }
 static size_t key_group_blocks(size_t n) { return (key_groups(n) + kGroupsPerBlock - 1) / kGroupsPerBlock; }
 
+namespace avdb {
+// the keyed K2 (avdb_record_prep_keyed) writes K7's group totals straight into the
+// one-pass workspace: 256-record groups only (batches of kSmallGroupN records or more)
+size_t key_totals_min_records() { return kSmallGroupN; }
+uint2* key_totals_of(void* workspace) { return reinterpret_cast<uint2*>(static_cast<char*>(workspace) + 256); }
+}  // namespace avdb
+
 extern "C" int avdb_primary_keys_onepass_workspace_size(size_t n, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
   *bytes = 256 + 16 * ((key_groups(n) + 1) & ~size_t(1)) + 16 * key_group_blocks(n);
@@ -877,13 +870,14 @@ extern "C" int avdb_primary_keys_bound(size_t n, size_t heap_bytes, size_t* key_
   return AVDB_OK;
 }
 
-extern "C" int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
-                                         const uint64_t* allele_off, const uint32_t* ref_len,
-                                         const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
-                                         const uint64_t* ext_id, const uint32_t* bin_code, const char* digest,
-                                         size_t n, uint32_t max_seq_len, void* workspace, size_t workspace_bytes,
-                                         uint64_t* key_off, uint64_t* path_off, uint8_t* key_out, size_t key_cap,
-                                         uint8_t* path_out, size_t path_cap, uint8_t* key_state, void* stream) {
+extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                            const uint64_t* allele_off, const uint32_t* ref_len,
+                                            const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                                            const uint64_t* ext_id, const uint32_t* bin_code, const char* digest,
+                                            size_t n, uint32_t max_seq_len, void* workspace, size_t workspace_bytes,
+                                            uint64_t* key_off, uint64_t* path_off, uint8_t* key_out, size_t key_cap,
+                                            uint8_t* path_out, size_t path_cap, uint8_t* key_state, uint32_t flags,
+                                            void* stream) {
   if (!ctx || !key_off || (bin_code && !path_off) || !key_state || !key_out || (bin_code && !path_out)) {
     avdb_set_error("avdb_primary_keys_onepass: null argument");
     return AVDB_EINVAL;
@@ -943,8 +937,14 @@ extern "C" int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, co
   A.grp_pre = gpre;
   A.blk_pre = bpre;
   A.group_log2 = key_group_log2(n);
-  hipLaunchKernelGGL(k_key_group_totals, dim3(stream_grid(ng * kWave, kBlock, 4096)), dim3(kBlock), 0, s, A, tot,
-                     ng);
+  if ((flags & AVDB_KEYS_TOTALS_READY) && A.group_log2 == kGroupLog2) {
+    // the keyed K2 wrote every group's totals but the last one's, which may hold
+    // the < 4 records its vector form leaves to a scalar tail: that one again
+    hipLaunchKernelGGL(k_key_group_totals, dim3(1), dim3(kWave), 0, s, A, tot, ng, ng - 1);
+  } else {
+    hipLaunchKernelGGL(k_key_group_totals, dim3(stream_grid(ng * kWave, kBlock, 4096)), dim3(kBlock), 0, s, A, tot,
+                       ng, size_t(0));
+  }
   AVDB_LAUNCH_CHECK("k_key_group_totals");
   hipLaunchKernelGGL(k_key_group_scan, dim3(unsigned(nb)), dim3(kScanThreads), 0, s, tot, ng, gpre, bpre);
   AVDB_LAUNCH_CHECK("k_key_group_scan");
@@ -958,4 +958,16 @@ extern "C" int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, co
   hipLaunchKernelGGL(k_record_keys<2>, dim3(grid), dim3(kBlock), 0, s, A);
   AVDB_LAUNCH_CHECK("k_record_keys<groups>");
   return AVDB_OK;
+}
+
+extern "C" int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                         const uint64_t* allele_off, const uint32_t* ref_len,
+                                         const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                                         const uint64_t* ext_id, const uint32_t* bin_code, const char* digest,
+                                         size_t n, uint32_t max_seq_len, void* workspace, size_t workspace_bytes,
+                                         uint64_t* key_off, uint64_t* path_off, uint8_t* key_out, size_t key_cap,
+                                         uint8_t* path_out, size_t path_cap, uint8_t* key_state, void* stream) {
+  return avdb_primary_keys_onepass_ex(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id,
+                                      bin_code, digest, n, max_seq_len, workspace, workspace_bytes, key_off, path_off,
+                                      key_out, key_cap, path_out, path_cap, key_state, 0u, stream);
 }

@@ -210,6 +210,9 @@ class KeyText:
     state: torch.Tensor
     keys: Optional[torch.Tensor]
     paths: Optional[torch.Tensor]
+    # (n, max_seq_len, has_digest, with_paths) of the group totals a keyed
+    # record_prep left in ``ws`` for the next primary_keys call, or None
+    totals_for: Optional[tuple] = None
 
     def host(self, n: int):
         """(keys, paths) as Python lists of str (None where not rendered).
@@ -634,8 +637,13 @@ class Engine:
 
     # -- K2 ----------------------------------------------------------------
     def record_prep(self, b: RecordBatch, *, want_lcp: bool = True, hist: Optional[torch.Tensor] = None,
-                    counters: Optional[torch.Tensor] = None):
-        """Returns ``(end, code, status, lcp)`` device tensors."""
+                    counters: Optional[torch.Tensor] = None, keys: Optional["KeyText"] = None,
+                    key_digest: bool = False, key_paths: bool = True, max_seq_len: int = 50):
+        """Returns ``(end, code, status, lcp)`` device tensors.  With ``keys`` (a
+        one-pass ``KeyText`` from an earlier ``primary_keys`` on a same-sized
+        batch) K2 also writes K7's group totals into its workspace
+        (``avdb_record_prep_keyed``), so the next ``primary_keys(b, code,
+        digest if key_digest, out=keys)`` skips its totals pass."""
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
@@ -643,11 +651,19 @@ class Engine:
         code = self.empty(n, torch.int32)
         status = self.empty(n, torch.uint8)
         lcp = self.empty(n, torch.int32) if want_lcp else None
-        N.check("avdb_record_prep", self.lib.avdb_record_prep(
-            self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
-            N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, N.ptr(end), N.ptr(code), N.ptr(status),
-            N.ptr(lcp),
-            N.ptr(hist), N.ptr(counters), self._stream()))
+        args = (self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
+                N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, N.ptr(end), N.ptr(code), N.ptr(status),
+                N.ptr(lcp), N.ptr(hist), N.ptr(counters))
+        if keys is None:
+            N.check("avdb_record_prep", self.lib.avdb_record_prep(*args, self._stream()))
+            return end, code, status, lcp
+        keys.totals_for = None
+        done = ctypes.c_int(0)
+        N.check("avdb_record_prep_keyed", self.lib.avdb_record_prep_keyed(
+            *args, N.ptr(b.ext_id), int(max_seq_len), 1 if key_digest else 0, 1 if key_paths else 0,
+            N.ptr(keys.ws), keys.ws.numel(), ctypes.byref(done), self._stream()))
+        if done.value:
+            keys.totals_for = (n, int(max_seq_len), bool(key_digest), bool(key_paths))
         return end, code, status, lcp
 
     # -- K3 ----------------------------------------------------------------
@@ -997,11 +1013,15 @@ class Engine:
             raise ValueError("primary_keys: the reused KeyText holds fewer records (or no paths)")
         if out.ws.numel() < sz.value:
             out.ws = self.empty(int(sz.value), torch.uint8)
-        N.check("avdb_primary_keys_onepass", self.lib.avdb_primary_keys_onepass(
+            out.totals_for = None
+        ready = out.totals_for == (n, int(max_seq_len), digest is not None, code is not None)
+        out.totals_for = None
+        N.check("avdb_primary_keys_onepass_ex", self.lib.avdb_primary_keys_onepass_ex(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
             N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), N.ptr(code), N.ptr(digest), n, int(max_seq_len),
             N.ptr(out.ws), out.ws.numel(), N.ptr(out.key_off), N.ptr(out.path_off), N.ptr(out.keys), out.keys.numel(),
-            N.ptr(out.paths), out.paths.numel() if out.paths is not None else 0, N.ptr(out.state), self._stream()))
+            N.ptr(out.paths), out.paths.numel() if out.paths is not None else 0, N.ptr(out.state),
+            N.KEYS_TOTALS_READY if ready else 0, self._stream()))
         return out
 
     # -- K6: existing-variant key set ----------------------------------------

@@ -447,8 +447,11 @@ def main():
 
     def c4k_step(record: bool):
         box = {}
+        # (K2 also writes K7's group totals into the reused KeyText's workspace:
+        # avdb_record_prep_keyed; the first step allocates the KeyText)
         timed("record_prep", record, lambda: box.setdefault(
-            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr)))
+            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr, keys=last.get("kt"),
+                                    key_digest=True)))
         timed("pk_dedup", record, lambda: box.setdefault(
             "keep", eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3"))))
         timed("vrs_digest", record, lambda: box.setdefault(
@@ -704,8 +707,10 @@ def main():
         out["data"] = "synthetic dbSNP-shaped VCF text (numpy PCG64 lines tiled on the device)"
         out["config"].update(lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
                              records_processed=None)
-        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (5 kernels + "
-                                   "2 host syncs for the line and record totals)")
+        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (count pass, one host "
+                                   "read, the one-pass tokenizer, one host read of its totals; "
+                                   "AVDB_VCF_FUSED=0: the four-kernel path); the line table and line offsets "
+                                   "it also writes (96 B per line) are not counted")
     if ri.rank == 0:
         print(json.dumps(out), flush=True)
     D.finalize(ri)

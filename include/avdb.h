@@ -407,6 +407,29 @@ int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, const uint32_
                               size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off, uint8_t* key_out,
                               size_t key_cap, uint8_t* path_out, size_t path_cap, uint8_t* key_state,
                               void* stream);
+/* The same with flags: AVDB_KEYS_TOTALS_READY = the workspace already holds the
+ * group totals avdb_record_prep_keyed wrote for this batch (same n, max_seq_len,
+ * digest presence and paths), so the totals pass over the SoA is skipped (only
+ * the last group is summed again). */
+#define AVDB_KEYS_TOTALS_READY 1u
+int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                 const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                                 const uint8_t* heap, size_t heap_bytes, const uint64_t* ext_id,
+                                 const uint32_t* bin_code, const char* digest, size_t n, uint32_t max_seq_len,
+                                 void* workspace, size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off,
+                                 uint8_t* key_out, size_t key_cap, uint8_t* path_out, size_t path_cap,
+                                 uint8_t* key_state, uint32_t flags, void* stream);
+/* K2 that also writes K7's group totals (key / path bytes per 256 records) into a
+ * one-pass K7 workspace, from the SoA it reads anyway plus the refSNP ids: the
+ * record-prep half of the keyed pipeline (C4k).  *totals_written = 1 when it did
+ * (batches of 4 Mi records or more, aligned arrays); pass AVDB_KEYS_TOTALS_READY
+ * to avdb_primary_keys_onepass_ex then.  Otherwise it is avdb_record_prep. */
+int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                           const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                           size_t n, uint32_t* end_out, uint32_t* bin_code, uint8_t* status, uint32_t* lcp,
+                           uint32_t* hist_l8, uint64_t* counters, const uint64_t* ext_id, uint32_t max_seq_len,
+                           int has_digest, int with_paths, void* key_workspace, size_t key_workspace_bytes,
+                           int* totals_written, void* stream);
 
 /* ---- K8: the per-record drop-in path in one launch -------------------------
  * The reference calls its per-record API once per alt allele

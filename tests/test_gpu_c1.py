@@ -275,3 +275,31 @@ def test_k7_onepass_equals_two_pass(engine, n):
     # and reused buffers: a second launch over the same KeyText
     again = engine.primary_keys(b, code=code, digest=dig, out=one)
     assert torch.equal(again.keys[:kn], two.keys[:kn]) and torch.equal(again.key_off[: n + 1], two.key_off[: n + 1])
+
+
+@pytest.mark.parametrize("n", [(4 << 20) + 4099, (4 << 20) + 256 * 7, 300001])
+def test_keyed_record_prep_feeds_k7(engine, n):
+    """K2 writing K7's group totals (avdb_record_prep_keyed, the C4k pipeline) then
+    K7 without its totals pass == plain K2 + K7: end / bin / status and every key,
+    path, offset and state; below 4 Mi records the keyed call is plain K2 and K7
+    sums the totals itself."""
+    from annotatedvdb_amd import synth
+    digs = ["%032d" % (5 * i) for i in range(25)]
+    engine.set_sequence_digests(digs)
+    b = synth.alleles(n, seed=11 + n % 5, long_frac=0.03, device="cuda")
+    end, code, status, _ = engine.record_prep(b, want_lcp=False)
+    dig, _ = engine.vrs_digest(b, 50)
+    ref = engine.primary_keys(b, code=code, digest=dig)
+    kt = engine.primary_keys(b, code=code, digest=dig)  # the reused buffers
+    kt.state.fill_(77)
+    kt.key_off.fill_(0)
+    end2, code2, status2, _ = engine.record_prep(b, want_lcp=False, keys=kt, key_digest=True)
+    assert (kt.totals_for is not None) == (n >= (4 << 20))
+    assert torch.equal(end, end2) and torch.equal(code, code2) and torch.equal(status, status2)
+    out = engine.primary_keys(b, code=code2, digest=dig, out=kt)
+    assert out.totals_for is None
+    assert torch.equal(out.key_off[: n + 1], ref.key_off[: n + 1])
+    assert torch.equal(out.path_off[: n + 1], ref.path_off[: n + 1])
+    assert torch.equal(out.state[:n], ref.state[:n])
+    kn, pn = int(ref.key_off[n]), int(ref.path_off[n])
+    assert torch.equal(out.keys[:kn], ref.keys[:kn]) and torch.equal(out.paths[:pn], ref.paths[:pn])
