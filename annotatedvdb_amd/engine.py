@@ -210,8 +210,9 @@ class KeyText:
     state: torch.Tensor
     keys: Optional[torch.Tensor]
     paths: Optional[torch.Tensor]
-    # (n, max_seq_len, has_digest, with_paths) of the group totals a keyed
-    # record_prep left in ``ws`` for the next primary_keys call, or None
+    # (n, max_seq_len, has_digest, with_paths, the batch's array addresses) of the
+    # group totals a keyed record_prep left in ``ws`` for the next primary_keys
+    # call on the same batch, or None
     totals_for: Optional[tuple] = None
 
     def host(self, n: int):
@@ -662,8 +663,9 @@ class Engine:
         N.check("avdb_record_prep_keyed", self.lib.avdb_record_prep_keyed(
             *args, N.ptr(b.ext_id), int(max_seq_len), 1 if key_digest else 0, 1 if key_paths else 0,
             N.ptr(keys.ws), keys.ws.numel(), ctypes.byref(done), self._stream()))
-        if done.value:
-            keys.totals_for = (n, int(max_seq_len), bool(key_digest), bool(key_paths))
+        if done.value:  # (tied to this batch's arrays: another batch of the same size recomputes)
+            keys.totals_for = (n, int(max_seq_len), bool(key_digest), bool(key_paths), b.chrom.data_ptr(),
+                               b.pos.data_ptr(), b.ref_len.data_ptr(), b.alt_len.data_ptr(), b.ext_id.data_ptr())
         return end, code, status, lcp
 
     # -- K3 ----------------------------------------------------------------
@@ -1014,7 +1016,9 @@ class Engine:
         if out.ws.numel() < sz.value:
             out.ws = self.empty(int(sz.value), torch.uint8)
             out.totals_for = None
-        ready = out.totals_for == (n, int(max_seq_len), digest is not None, code is not None)
+        ready = out.totals_for == (n, int(max_seq_len), digest is not None, code is not None, b.chrom.data_ptr(),
+                                   b.pos.data_ptr(), b.ref_len.data_ptr(), b.alt_len.data_ptr(),
+                                   b.ext_id.data_ptr())
         out.totals_for = None
         N.check("avdb_primary_keys_onepass_ex", self.lib.avdb_primary_keys_onepass_ex(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),

@@ -303,3 +303,24 @@ def test_keyed_record_prep_feeds_k7(engine, n):
     assert torch.equal(out.state[:n], ref.state[:n])
     kn, pn = int(ref.key_off[n]), int(ref.path_off[n])
     assert torch.equal(out.keys[:kn], ref.keys[:kn]) and torch.equal(out.paths[:pn], ref.paths[:pn])
+
+
+def test_keyed_totals_not_reused_for_another_batch(engine):
+    """Group totals a keyed K2 left for batch A are not taken for batch B of the
+    same size: B's keys and offsets are B's own."""
+    from annotatedvdb_amd import synth
+    n = (4 << 20) + 17
+    engine.set_sequence_digests(["%032d" % (3 * i) for i in range(25)])
+    a = synth.alleles(n, seed=21, long_frac=0.02, device="cuda")
+    b = synth.alleles(n, seed=22, long_frac=0.02, device="cuda")
+    _, ca, _, _ = engine.record_prep(a, want_lcp=False)
+    _, cb, _, _ = engine.record_prep(b, want_lcp=False)
+    da, _ = engine.vrs_digest(a, 50)
+    db, _ = engine.vrs_digest(b, 50)
+    ref = engine.primary_keys(b, code=cb, digest=db)
+    kt = engine.primary_keys(a, code=ca, digest=da)
+    engine.record_prep(a, want_lcp=False, keys=kt, key_digest=True)
+    assert kt.totals_for is not None
+    out = engine.primary_keys(b, code=cb, digest=db, out=kt)
+    assert torch.equal(out.key_off[: n + 1], ref.key_off[: n + 1])
+    assert torch.equal(out.path_off[: n + 1], ref.path_off[: n + 1])
