@@ -378,10 +378,15 @@ struct KeyTotals {
   uint32_t max_seq_len;
   uint32_t n_key_chrom; // labelled contigs
   uint32_t has_digest, with_paths;
+  uint32_t group_log2;  // K7's groups: 64 << group_log2 records (0: 16 lanes' records, 2: the wave's)
 };
 
-template <bool HIST, int UNROLL, bool KEYS = false>
-__global__ __launch_bounds__(kK1Block) void k_record_prep4(
+// KEYS: 0 plain; 1 keyed; 2 keyed with registers for 6 waves per SIMD — for
+// batches whose K7 groups are 64 records (below 4 Mi records), where the launch is
+// one generation of workgroups only if 3 fit per CU (C1: 0.110 -> 0.107 ms); at
+// C4k's size the unconstrained form is faster (record prep 1.19 vs 1.25 ms)
+template <bool HIST, int UNROLL, int KEYS = 0>
+__global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
     const uint32_t* __restrict__ chromv, const u32x4* __restrict__ pos4, const u64x2* __restrict__ off2,
     const u32x4* __restrict__ rl4, const u32x4* __restrict__ al4, const uint8_t* __restrict__ heap,
     size_t heap_bytes, size_t ngroups, u32x4* __restrict__ end4, u32x4* __restrict__ code4,
@@ -422,7 +427,7 @@ __global__ __launch_bounds__(kK1Block) void k_record_prep4(
       a4[u] = __builtin_nontemporal_load(&al4[jj]);
     }
     u64x2 x01[UNROLL], x23[UNROLL];  // KEYS: refSNP keys
-    if constexpr (KEYS) {
+    if constexpr (KEYS != 0) {
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         const size_t j = base + size_t(u) * bdim + threadIdx.x;
@@ -492,7 +497,7 @@ __global__ __launch_bounds__(kK1Block) void k_record_prep4(
           for (int k = 0; k < 4; ++k) wave_hist_add(key[k], hist);
         }
       }
-      if constexpr (KEYS) {  // this wave's 256 records are one K7 group
+      if constexpr (KEYS != 0) {  // this wave's 256 records are one K7 group
         uint32_t K = 0, P = 0;
         if (live) {
 #pragma unroll
@@ -507,12 +512,20 @@ __global__ __launch_bounds__(kK1Block) void k_record_prep4(
           }
         }
 #pragma unroll
-        for (int d = 32; d > 0; d >>= 1) {
+        for (int d = 8; d > 0; d >>= 1) {  // over each 16 lanes: 64 records
           K += __shfl_xor(K, d, kWave);
           P += __shfl_xor(P, d, kWave);
         }
-        const size_t j0 = base + size_t(u) * bdim + (threadIdx.x & ~uint32_t(kWave - 1));
-        if (__lane_id() == 0 && j0 < ngroups) kt.tot[j0 / kWave] = make_uint2(K, P);
+        if (kt.group_log2 == 0) {  // four 64-record groups per wave step
+          if ((__lane_id() & 15u) == 0 && j < ngroups) kt.tot[j >> 4] = make_uint2(K, P);
+        } else {  // one 256-record group
+          K += __shfl_xor(K, 16, kWave);
+          P += __shfl_xor(P, 16, kWave);
+          K += __shfl_xor(K, 32, kWave);
+          P += __shfl_xor(P, 32, kWave);
+          const size_t j0 = base + size_t(u) * bdim + (threadIdx.x & ~uint32_t(kWave - 1));
+          if (__lane_id() == 0 && j0 < ngroups) kt.tot[j0 / kWave] = make_uint2(K, P);
+        }
       }
       if (live) {
         __builtin_nontemporal_store(e, &end4[j]);
@@ -684,6 +697,7 @@ extern "C" int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const
   kt.n_key_chrom = uint32_t(ctx && ctx->tab.n < 25 ? ctx->tab.n : 25);
   kt.has_digest = has_digest ? 1u : 0u;
   kt.with_paths = with_paths ? 1u : 0u;
+  kt.group_log2 = avdb::key_totals_group_log2(n);
   return record_prep_impl(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, n, end_out, bin_code,
                           status, lcp, hist_l8, counters, stream, &kt, totals_written);
 }
@@ -708,9 +722,8 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
   const bool vec = ctx->k2_vector && n >= 4 && aligned(chrom, 4) && aligned(pos, 16) && aligned(allele_off, 16) &&
                    aligned(ref_len, 16) && aligned(alt_len, 16) && aligned(end_out, 16) && aligned(bin_code, 16) &&
                    (!status || aligned(status, 4)) && (!lcp || aligned(lcp, 16));
-  // keyed: K7's 256-record groups (batches of key_totals_min_records() or more)
-  // and 16-byte aligned refSNP keys
-  const bool keys = keyed && vec && n >= avdb::key_totals_min_records() && (!keyed->ext2 || aligned(keyed->ext2, 16));
+  // keyed: the vector form with 16-byte aligned refSNP keys
+  const bool keys = keyed && vec && (!keyed->ext2 || aligned(keyed->ext2, 16));
   const KeyTotals kt = keys ? *keyed : KeyTotals{};
   if (vec) {
     const size_t ngroups = n / 4;
@@ -718,7 +731,7 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
     const int U = keys ? ctx->k2_keyed_unroll : ctx->k2_unroll;  // (the keyed form's registers: 144 VGPRs at U=2)
     const unsigned grid = stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
 #define K2V(HI, UU)                                                                                       \
-  if (keys) K2VK(HI, UU, true); else K2VK(HI, UU, false)
+  if (keys && kt.group_log2 == 0) K2VK(HI, UU, 2); else if (keys) K2VK(HI, UU, 1); else K2VK(HI, UU, 0)
 #define K2VK(HI, UU, KK)                                                                                  \
   hipLaunchKernelGGL((k_record_prep4<HI, UU, KK>), dim3(grid), dim3(bdim), shm, s,                       \
                      reinterpret_cast<const uint32_t*>(chrom), reinterpret_cast<const u32x4*>(pos),      \

@@ -128,6 +128,8 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
   }
   // (the one-kernel run scan for C1's 1.1 M records measured 22.2 us against 5.7 + 7.6 us
   // for the list form: the list form is the default at every size)
+  c->k7_raw_blocks = 256;
+  if (const char* s = getenv("AVDB_K7_RAW_BLOCKS")) c->k7_raw_blocks = size_t(strtoull(s, nullptr, 10));
   c->k3_list_min = 0;
   if (const char* s = getenv("AVDB_K3_LIST_MIN")) c->k3_list_min = size_t(strtoull(s, nullptr, 10));
   *out = c;

@@ -245,6 +245,7 @@ struct avdb_ctx {
   int k2_keyed_unroll;   // keyed K2 (K7 group totals) groups per lane per trip (env AVDB_K2_KEYED_UNROLL)
   int k4_blocks_per_cu;  // K4 digest grid = n_cu * this (env AVDB_K4_BLOCKS_PER_CU; default: its occupancy, 3)
   int k0_blocks_per_cu;  // K0 one-pass grid = n_cu * this (env AVDB_K0_BLOCKS_PER_CU)
+  size_t k7_raw_blocks;  // K7 one-pass: write pass sums up to this many block totals itself (env AVDB_K7_RAW_BLOCKS)
   size_t k3_list_min;    // K3 grouped: two-phase list form from this many records on (env AVDB_K3_LIST_MIN)
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
@@ -259,7 +260,7 @@ namespace avdb {
 // workspace bytes K7's size pass needs for n records (u16 sizes + their scan)
 size_t key_size_workspace(size_t n);
 // K7 one-pass workspace: group totals the keyed K2 fills (avdb_keys.hip)
-size_t key_totals_min_records();
+uint32_t key_totals_group_log2(size_t n);
 uint2* key_totals_of(void* workspace);
 // K4's per-(contig, digit count) SequenceLocation block-1 table (host)
 void location_tail_table(const char* digests, int n_chrom, std::vector<uint64_t>& out);

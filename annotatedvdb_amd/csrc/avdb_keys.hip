@@ -73,6 +73,7 @@ struct KeyArgs {
   const uint2* grp_pre;
   const uint64_t* blk_pre;
   uint32_t group_log2;  // MODE 2: records per scan group = 64 << group_log2 (tiles per group = 1 << group_log2)
+  uint32_t blk_raw;     // MODE 2: blk_pre holds each block's totals, not their exclusive scan
 };
 
 // WRITE renders each wave's 64 records as a tile: each stream's span (the
@@ -106,6 +107,9 @@ struct KeyArgs {
 // 10.21 vs 10.19 ms on C4k keys + paths; not kept.)
 #ifndef AVDB_K7_EXP
 #define AVDB_K7_EXP 0
+#endif
+#ifndef AVDB_K7_WINCHECK
+#define AVDB_K7_WINCHECK 1  // key window: one bounds check per record (0: per word, A/B)
 #endif
 constexpr uint32_t kKeyWave = 2560;
 constexpr uint32_t kPathWave = 5632;
@@ -181,9 +185,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 // for large batches; 64 (one tile) below kSmallGroupN records, where a wave per
 // tile gives the launch 4x the waves (C1, 1.1 M records: one generation of waves).
 constexpr uint32_t kGroupLog2 = 2;
-constexpr size_t kSmallGroupN = size_t(4) << 20;
+#ifndef AVDB_K7_SMALL_GROUP_N
+#define AVDB_K7_SMALL_GROUP_N (size_t(4) << 20)
+#endif
+constexpr size_t kSmallGroupN = AVDB_K7_SMALL_GROUP_N;
 constexpr uint32_t kGroupsPerBlock = 4096;    // groups per block of the local scan
 constexpr uint32_t kScanThreads = 1024;       // 4 groups per thread
+// up to ctx->k7_raw_blocks (256) blocks of groups, the write pass sums the block
+// totals before its group itself (<= 4 loads per lane at a group's start) instead
+// of a separate one-workgroup scan launch
 
 // the sizes the size pass gives record j (SoA-decidable key state only)
 __device__ __forceinline__ void record_sizes(const KeyArgs& A, uint32_t c, uint32_t p, uint32_t r, uint32_t a,
@@ -197,46 +207,68 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
   for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
   return v;
 }
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1)
+    v += (uint64_t(uint32_t(__shfl_xor(uint32_t(v >> 32), d, kWave))) << 32) | uint32_t(__shfl_xor(uint32_t(v), d, kWave));
+  return v;
+}
 
-// group totals: one wave per group of 64 << group_log2 records (records
-// (g << group_log2 + k) * 64 + lane)
+// the (keys, paths) bytes of group g (records (g << group_log2 + k) * 64 + lane),
+// summed over the wave
+__device__ __forceinline__ uint2 group_total(const KeyArgs& A, size_t g, uint32_t lane) {
+  const uint32_t tpg = 1u << A.group_log2;
+  uint32_t K = 0, P = 0;
+#pragma unroll 4
+  for (uint32_t k = 0; k < tpg; ++k) {
+    const size_t j = ((g << A.group_log2) + k) * kWave + lane;
+    if (j < A.n) {
+      uint32_t ks, ps;
+      record_sizes(A, A.chrom[j], A.pos[j], A.rl[j], A.al[j], A.ext ? A.ext[j] : 0ull,
+                   A.code ? A.code[j] : AVDB_BIN_NONE, &ks, &ps);
+      K += ks;
+      P += ps;
+    }
+  }
+  return make_uint2(wave_sum32(K), wave_sum32(P));
+}
+
+// group totals: one wave per group of 64 << group_log2 records
 __global__ __launch_bounds__(kBlock) void k_key_group_totals(KeyArgs A, uint2* __restrict__ tot, size_t n_groups,
                                                               size_t g_begin) {
   const uint32_t lane = __lane_id();
   const size_t w0 = g_begin + (size_t(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
   const size_t nw = size_t(gridDim.x) * blockDim.x / kWave;
-  const uint32_t tpg = 1u << A.group_log2;
   for (size_t g = w0; g < n_groups; g += nw) {
-    uint32_t K = 0, P = 0;
-#pragma unroll 4
-    for (uint32_t k = 0; k < tpg; ++k) {
-      const size_t j = ((g << A.group_log2) + k) * kWave + lane;
-      if (j < A.n) {
-        uint32_t ks, ps;
-        record_sizes(A, A.chrom[j], A.pos[j], A.rl[j], A.al[j], A.ext ? A.ext[j] : 0ull,
-                     A.code ? A.code[j] : AVDB_BIN_NONE, &ks, &ps);
-        K += ks;
-        P += ps;
-      }
-    }
-    K = wave_sum32(K);
-    P = wave_sum32(P);
-    if (lane == 0) tot[g] = make_uint2(K, P);
+    const uint2 t = group_total(A, g, lane);
+    if (lane == 0) tot[g] = t;
   }
 }
 
 // exclusive scan of the group totals inside each block of 4,096 groups (u32: a
-// block's text is < 4 GB) and the block totals
+// block's text is < 4 GB) and the block totals.  redo_last: the totals came from
+// the keyed K2, whose vector form may leave the last group's final < 4 records to
+// a scalar tail — the last block's first wave sums that group again here.
 __global__ __launch_bounds__(kScanThreads) void k_key_group_scan(const uint2* __restrict__ tot, size_t n_groups,
-                                                                  uint2* __restrict__ pre, uint64_t* __restrict__ btot) {
+                                                                  uint2* __restrict__ pre, uint64_t* __restrict__ btot,
+                                                                  KeyArgs A, int redo_last) {
   __shared__ uint32_t s_k[kScanThreads / kWave], s_p[kScanThreads / kWave];
+  __shared__ uint2 s_last;
   const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
+  const bool redo = redo_last && blockIdx.x == gridDim.x - 1;  // (block-uniform)
+  if (redo) {
+    if (wv == 0) {
+      const uint2 t = group_total(A, n_groups - 1, lane);
+      if (lane == 0) s_last = t;
+    }
+    __syncthreads();
+  }
   const size_t g0 = size_t(blockIdx.x) * kGroupsPerBlock + 4 * threadIdx.x;
   uint2 v[4];
   uint32_t k = 0, p = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    v[q] = g0 + q < n_groups ? tot[g0 + q] : make_uint2(0, 0);
+    v[q] = g0 + q < n_groups ? (redo && g0 + q == n_groups - 1 ? s_last : tot[g0 + q]) : make_uint2(0, 0);
     k += v[q].x;
     p += v[q].y;
   }
@@ -457,9 +489,20 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
     if constexpr (ONEP) {
       if (((t0 / kWave) & ((1u << A.group_log2) - 1)) == 0) {  // a new group: its scanned base
         const size_t g = (t0 / kWave) >> A.group_log2;
+        const size_t b = g / kGroupsPerBlock;
         const uint2 gp = A.grp_pre[g];
-        run_k = A.blk_pre[2 * (g / kGroupsPerBlock)] + gp.x;
-        run_p = A.blk_pre[2 * (g / kGroupsPerBlock) + 1] + gp.y;
+        if (A.blk_raw) {  // the totals of the blocks before b, summed over the wave
+          uint64_t bk = 0, bp = 0;
+          for (size_t q = lane; q < b; q += kWave) {
+            bk += A.blk_pre[2 * q];
+            bp += A.blk_pre[2 * q + 1];
+          }
+          run_k = wave_sum64(bk) + gp.x;
+          run_p = wave_sum64(bp) + gp.y;
+        } else {
+          run_k = A.blk_pre[2 * b] + gp.x;
+          run_p = A.blk_pre[2 * b + 1] + gp.y;
+        }
       }
       sc = tile_sizes(cur, t0);
     }
@@ -545,9 +588,16 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
             const uint32_t nw = (wmis + nb + 7) >> 3;
             // (bytes outside the digest row / the heap allocation read as 0)
             const Heap h = lng ? Heap{src, src + AVDB_DIGEST_CHARS} : make_heap(A.heap, A.heap_bytes);
+            if (AVDB_K7_WINCHECK && aw >= h.lo && aw + 8 * nw <= h.hi) {
+              // the whole window inside: plain loads, one bounds check per record instead of per word
 #pragma unroll
-            for (uint32_t k = 0; k < kKeyWords; ++k)
-              if (k < nw) w[k] = heap_word(aw + 8 * k, h);
+              for (uint32_t k = 0; k < kKeyWords; ++k)
+                if (k < nw) w[k] = *reinterpret_cast<const uint64_t*>(aw + 8 * k);
+            } else {
+#pragma unroll
+              for (uint32_t k = 0; k < kKeyWords; ++k)
+                if (k < nw) w[k] = heap_word(aw + 8 * k, h);
+            }
           }
         }
         if (!lng && st == AVDB_KEY_OK && !(AVDB_K7_EXP & 4)) {
@@ -586,6 +636,10 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
         if (live) {
           A.key_off[i] = ko;
           if (A.code) A.path_off[i] = po;
+          if (i + 1 == A.n) {  // the totals (also from k_key_block_scan when it runs)
+            A.key_off[A.n] = ko1;
+            if (A.code) A.path_off[A.n] = po1;
+          }
         }
       } else {
         gk0 = A.key_off[t0];
@@ -850,8 +904,8 @@ static size_t key_group_blocks(size_t n) { return (key_groups(n) + kGroupsPerBlo
 
 namespace avdb {
 // the keyed K2 (avdb_record_prep_keyed) writes K7's group totals straight into the
-// one-pass workspace: 256-record groups only (batches of kSmallGroupN records or more)
-size_t key_totals_min_records() { return kSmallGroupN; }
+// one-pass workspace, at the group size K7 uses for n records
+uint32_t key_totals_group_log2(size_t n) { return key_group_log2(n); }
 uint2* key_totals_of(void* workspace) { return reinterpret_cast<uint2*>(static_cast<char*>(workspace) + 256); }
 }  // namespace avdb
 
@@ -937,22 +991,25 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   A.grp_pre = gpre;
   A.blk_pre = bpre;
   A.group_log2 = key_group_log2(n);
-  if ((flags & AVDB_KEYS_TOTALS_READY) && A.group_log2 == kGroupLog2) {
-    // the keyed K2 wrote every group's totals but the last one's, which may hold
-    // the < 4 records its vector form leaves to a scalar tail: that one again
-    hipLaunchKernelGGL(k_key_group_totals, dim3(1), dim3(kWave), 0, s, A, tot, ng, ng - 1);
-  } else {
+  A.blk_raw = nb <= ctx->k7_raw_blocks ? 1u : 0u;
+  // the keyed K2 wrote every group's totals but the last one's, which may hold the
+  // < 4 records its vector form leaves to a scalar tail: the scan sums that one again
+  const int ready = (flags & AVDB_KEYS_TOTALS_READY) ? 1 : 0;
+  if (!ready) {
     hipLaunchKernelGGL(k_key_group_totals, dim3(stream_grid(ng * kWave, kBlock, 4096)), dim3(kBlock), 0, s, A, tot,
                        ng, size_t(0));
+    AVDB_LAUNCH_CHECK("k_key_group_totals");
   }
-  AVDB_LAUNCH_CHECK("k_key_group_totals");
-  hipLaunchKernelGGL(k_key_group_scan, dim3(unsigned(nb)), dim3(kScanThreads), 0, s, tot, ng, gpre, bpre);
+  hipLaunchKernelGGL(k_key_group_scan, dim3(unsigned(nb)), dim3(kScanThreads), 0, s, tot, ng, gpre, bpre, A, ready);
   AVDB_LAUNCH_CHECK("k_key_group_scan");
-  hipLaunchKernelGGL(k_key_block_scan, dim3(1), dim3(kScanThreads), 0, s, bpre, nb, key_off + n,
-                     bin_code ? path_off + n : nullptr);
-  AVDB_LAUNCH_CHECK("k_key_block_scan");
+  if (!A.blk_raw) {
+    hipLaunchKernelGGL(k_key_block_scan, dim3(1), dim3(kScanThreads), 0, s, bpre, nb, key_off + n,
+                       bin_code ? path_off + n : nullptr);
+    AVDB_LAUNCH_CHECK("k_key_block_scan");
+  }
   // (one workgroup doing both scans for C1's 17 K groups measured 11.9 us against
-  // 5.2 + 4.9 us for the two launches: not kept)
+  // 5.2 + 4.9 us for the two launches: not kept; up to k7_raw_blocks blocks the
+  // write pass sums the block totals itself)
   const unsigned grid = unsigned((ng + kWavesPerBlock - 1) / kWavesPerBlock < AVDB_K7_GRID
                                      ? (ng + kWavesPerBlock - 1) / kWavesPerBlock : AVDB_K7_GRID);
   hipLaunchKernelGGL(k_record_keys<2>, dim3(grid), dim3(kBlock), 0, s, A);

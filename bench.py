@@ -435,8 +435,9 @@ def main():
 
     def c1_step(record: bool):
         box = {}
+        # (K2 also writes K7's group totals into the reused KeyText's workspace)
         timed("record_prep", record, lambda: box.setdefault(
-            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr)))
+            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr, keys=last.get("kt"))))
         timed("pk_dedup", record, lambda: box.setdefault(
             "keep", eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3"))))
         code_ = box["prep"][1]

@@ -410,7 +410,7 @@ int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, const uint32_
 /* The same with flags: AVDB_KEYS_TOTALS_READY = the workspace already holds the
  * group totals avdb_record_prep_keyed wrote for this batch (same n, max_seq_len,
  * digest presence and paths), so the totals pass over the SoA is skipped (only
- * the last group is summed again). */
+ * the last group is summed again, inside the scan). */
 #define AVDB_KEYS_TOTALS_READY 1u
 int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                  const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
@@ -422,7 +422,7 @@ int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint
 /* K2 that also writes K7's group totals (key / path bytes per 256 records) into a
  * one-pass K7 workspace, from the SoA it reads anyway plus the refSNP ids: the
  * record-prep half of the keyed pipeline (C4k).  *totals_written = 1 when it did
- * (batches of 4 Mi records or more, aligned arrays); pass AVDB_KEYS_TOTALS_READY
+ * (16-byte aligned arrays); pass AVDB_KEYS_TOTALS_READY
  * to avdb_primary_keys_onepass_ex then.  Otherwise it is avdb_record_prep. */
 int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
                            const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,

@@ -277,12 +277,13 @@ def test_k7_onepass_equals_two_pass(engine, n):
     assert torch.equal(again.keys[:kn], two.keys[:kn]) and torch.equal(again.key_off[: n + 1], two.key_off[: n + 1])
 
 
-@pytest.mark.parametrize("n", [(4 << 20) + 4099, (4 << 20) + 256 * 7, 300001])
+@pytest.mark.parametrize("n", [(4 << 20) + 4099, (4 << 20) + 256 * 7, 1100000, 300001, 4097, 130, 64, 5, 3])
 def test_keyed_record_prep_feeds_k7(engine, n):
-    """K2 writing K7's group totals (avdb_record_prep_keyed, the C4k pipeline) then
-    K7 without its totals pass == plain K2 + K7: end / bin / status and every key,
-    path, offset and state; below 4 Mi records the keyed call is plain K2 and K7
-    sums the totals itself."""
+    """K2 writing K7's group totals (avdb_record_prep_keyed, the C4k and C1
+    pipelines) then K7 without its totals pass == plain K2 + K7: end / bin / status
+    and every key, path, offset and state — 256-record groups from 4 Mi records on,
+    64-record groups (four per K2 wave step) below; under 4 records the keyed call
+    is plain K2 and K7 sums the totals itself."""
     from annotatedvdb_amd import synth
     digs = ["%032d" % (5 * i) for i in range(25)]
     engine.set_sequence_digests(digs)
@@ -294,7 +295,7 @@ def test_keyed_record_prep_feeds_k7(engine, n):
     kt.state.fill_(77)
     kt.key_off.fill_(0)
     end2, code2, status2, _ = engine.record_prep(b, want_lcp=False, keys=kt, key_digest=True)
-    assert (kt.totals_for is not None) == (n >= (4 << 20))
+    assert (kt.totals_for is not None) == (n >= 4)
     assert torch.equal(end, end2) and torch.equal(code, code2) and torch.equal(status, status2)
     out = engine.primary_keys(b, code=code2, digest=dig, out=kt)
     assert out.totals_for is None
@@ -324,3 +325,27 @@ def test_keyed_totals_not_reused_for_another_batch(engine):
     out = engine.primary_keys(b, code=cb, digest=db, out=kt)
     assert torch.equal(out.key_off[: n + 1], ref.key_off[: n + 1])
     assert torch.equal(out.path_off[: n + 1], ref.path_off[: n + 1])
+
+
+def test_k7_block_scan_launch_equals_raw_block_sums(engine):
+    """Past ctx->k7_raw_blocks blocks of 4,096 groups K7 scans the block totals in
+    a launch of its own; below, the write pass sums them.  Both give the same
+    offsets and text (forced here with AVDB_K7_RAW_BLOCKS=0 on a second context)."""
+    import os
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.engine import Engine
+    n = 3 * 4096 * 64 + 77  # four blocks of 64-record groups
+    b = synth.alleles(n, seed=5, long_frac=0.0, device="cuda")
+    _, code, _, _ = engine.record_prep(b, want_lcp=False)
+    raw = engine.primary_keys(b, code=code)
+    os.environ["AVDB_K7_RAW_BLOCKS"] = "0"
+    try:
+        e2 = Engine(0)
+    finally:
+        del os.environ["AVDB_K7_RAW_BLOCKS"]
+    scanned = e2.primary_keys(b, code=code)
+    assert torch.equal(raw.key_off[: n + 1], scanned.key_off[: n + 1])
+    assert torch.equal(raw.path_off[: n + 1], scanned.path_off[: n + 1])
+    assert torch.equal(raw.state[:n], scanned.state[:n])
+    kn, pn = int(raw.key_off[n]), int(raw.path_off[n])
+    assert torch.equal(raw.keys[:kn], scanned.keys[:kn]) and torch.equal(raw.paths[:pn], scanned.paths[:pn])
