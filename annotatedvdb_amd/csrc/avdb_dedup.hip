@@ -321,6 +321,9 @@ __global__ __launch_bounds__(kBlock) void k_dedup_mark4(const uint8_t* __restric
   if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt;
 }
 
+#ifndef AVDB_K3_FASTPATH
+#define AVDB_K3_FASTPATH 1  // A/B knob: 0 sends every suspect through dedup_record
+#endif
 __global__ __launch_bounds__(kBlock) void k_dedup_resolve_list(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
@@ -338,7 +341,33 @@ __global__ __launch_bounds__(kBlock) void k_dedup_resolve_list(
     const uint32_t t = base + threadIdx.x;
     const bool live = t < cnt;
     const size_t i = live ? mine[t] : 0;
-    const uint8_t k = dedup_record(h, chrom, pos, off, rl, al, ext, i, live, live);
+    // A suspect shares (chrom, pos) with record i-1 (k_dedup_mark4).  The usual run
+    // is two records, so i-1's lengths / id / offset and i-2's (chrom, pos) are
+    // loaded together with i's, and a short compare against i-1 settles most
+    // suspects in two dependent memory trips; dedup_record's serial look-back
+    // (chrom / pos, then lengths, then bytes, per candidate) takes the rest.
+    bool settled = false;
+    uint8_t k = 1;
+    if (AVDB_K3_FASTPATH && live) {
+      const uint32_t r = rl[i], a = al[i], r1 = rl[i - 1], a1 = al[i - 1];
+      const uint64_t e = ext ? ext[i] : 0ull, e1 = ext ? ext[i - 1] : 0ull;
+      const uint64_t o = off[i], o1 = off[i - 1];
+      const bool run3 = i >= 2 && chrom[i - 2] == chrom[i] && pos[i - 2] == pos[i];
+      const uint32_t L = r + a;
+      const bool cand = r1 == r && a1 == a && e1 == e;
+      if (cand && L <= kCoopBytes) {
+        if (heap_equal(h, o, o1, L)) {
+          k = 0;
+          settled = true;
+        } else {
+          settled = !run3;
+        }
+      } else if (!cand) {
+        settled = !run3;
+      }
+    }
+    const uint8_t ks = dedup_record(h, chrom, pos, off, rl, al, ext, i, live, live && !settled);
+    if (!settled) k = ks;
     if (live && !k) {
       keep[i] = 0;
       ++dups;
