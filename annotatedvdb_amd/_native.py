@@ -89,7 +89,7 @@ EXPORTED_SYMBOLS = [
     "avdb_ctx_set_sequence_digests", "avdb_l8_bin_count",
     "avdb_bin_assign", "avdb_record_prep",
     "avdb_pk_dedup_workspace_size", "avdb_pk_dedup",
-    "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest",
+    "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest", "avdb_vrs_digest_ex",
     "avdb_format_bin_path", "avdb_format_bin_paths",
     "avdb_vcf_workspace_size", "avdb_vcf_count_lines", "avdb_vcf_parse_lines", "avdb_vcf_emit",
     "avdb_vcf_count_text", "avdb_vcf_tokenize_workspace_size", "avdb_vcf_tokenize",
@@ -109,6 +109,8 @@ EXPORTED_SYMBOLS = [
 
 SMALL_PATH, SMALL_KEY, SMALL_DISPLAY = 1, 2, 4
 KEYS_TOTALS_READY = 1  # AVDB_KEYS_TOTALS_READY
+KEYED_TOTALS, KEYED_LONG_CODES = 1, 2  # avdb_record_prep_keyed's *totals_written bits
+DIGEST_CODES_READY = 1  # AVDB_DIGEST_CODES_READY
 SMALL_MAX = 65536
 
 
@@ -161,6 +163,7 @@ def _sig(lib):
     f.avdb_sha512t24u.argtypes = [P, P, P, P, SZ, P, P]
     f.avdb_vrs_digest_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_vrs_digest.argtypes = [P, P, P, P, P, P, P, SZ, SZ, U32, P, SZ, P, P, P]
+    f.avdb_vrs_digest_ex.argtypes = [P, P, P, P, P, P, P, SZ, SZ, U32, P, SZ, P, P, U32, P]
     f.avdb_format_bin_path.argtypes = [P, U8, U32, ctypes.c_char_p, SZ]
     f.avdb_format_bin_paths.argtypes = [P, P, P, SZ, P, SZ, P]
     f.avdb_vcf_workspace_size.argtypes = [SZ, SZ, ctypes.POINTER(SZ)]
@@ -187,7 +190,7 @@ def _sig(lib):
     f.avdb_primary_keys.argtypes = [P, P, P, P, P, P, P, SZ, P, P, P, SZ, U32, P, SZ, P, P, P, SZ, P, SZ, P, P]
     f.avdb_primary_keys_onepass.argtypes = list(f.avdb_primary_keys.argtypes)  # same signature
     f.avdb_primary_keys_onepass_ex.argtypes = list(f.avdb_primary_keys.argtypes)[:-1] + [U32, P]
-    f.avdb_record_prep_keyed.argtypes = list(f.avdb_record_prep.argtypes)[:-1] + [P, U32, I32, I32, P, SZ,
+    f.avdb_record_prep_keyed.argtypes = list(f.avdb_record_prep.argtypes)[:-1] + [P, U32, I32, I32, P, SZ, P, SZ,
                                                                                  ctypes.POINTER(I32), P]
     f.avdb_primary_keys_bound.argtypes = [SZ, SZ, ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
     f.avdb_primary_keys_onepass_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]

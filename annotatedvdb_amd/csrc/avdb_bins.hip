@@ -379,6 +379,7 @@ struct KeyTotals {
   uint32_t n_key_chrom; // labelled contigs
   uint32_t has_digest, with_paths;
   uint32_t group_log2;  // K7's groups: 64 << group_log2 records (0: 16 lanes' records, 2: the wave's)
+  uint8_t* long_codes;  // nullable: K4's long_code per record (avdb::vrs_long_codes_of(digest workspace))
 };
 
 // KEYS: 0 plain; 1 keyed; 2 keyed with registers for 6 waves per SIMD — for
@@ -527,6 +528,14 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
           if (__lane_id() == 0 && j0 < ngroups) kt.tot[j0 / kWave] = make_uint2(K, P);
         }
       }
+      if constexpr (KEYS != 0) {
+        if (kt.long_codes && live) {
+          uint32_t lc = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) lc |= long_code(r4[u][k], a4[u][k], kt.max_seq_len) << (8 * k);
+          __builtin_nontemporal_store(lc, reinterpret_cast<uint32_t*>(kt.long_codes) + j);
+        }
+      }
       if (live) {
         __builtin_nontemporal_store(e, &end4[j]);
         __builtin_nontemporal_store(cv, &code4[j]);
@@ -555,6 +564,7 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
       code[i] = cv;
       if (status) status[i] = uint8_t(s_k);
       if (lcp) lcp[i] = l;
+      if (KEYS != 0 && kt.long_codes) kt.long_codes[i] = uint8_t(long_code(r, a, kt.max_seq_len));
       nrec += 1;
       err += s_k ? (1u << (8 * (s_k - 1))) : 0u;
       key = l8_key(c, p, cv, s_l8off);
@@ -678,7 +688,8 @@ extern "C" int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const
                                       uint32_t* bin_code, uint8_t* status, uint32_t* lcp, uint32_t* hist_l8,
                                       uint64_t* counters, const uint64_t* ext_id, uint32_t max_seq_len,
                                       int has_digest, int with_paths, void* key_workspace,
-                                      size_t key_workspace_bytes, int* totals_written, void* stream) {
+                                      size_t key_workspace_bytes, void* digest_workspace,
+                                      size_t digest_workspace_bytes, int* totals_written, void* stream) {
   if (!totals_written) {
     avdb_set_error("avdb_record_prep_keyed: null totals_written");
     return AVDB_EINVAL;
@@ -698,6 +709,16 @@ extern "C" int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const
   kt.has_digest = has_digest ? 1u : 0u;
   kt.with_paths = with_paths ? 1u : 0u;
   kt.group_log2 = avdb::key_totals_group_log2(n);
+  kt.long_codes = nullptr;
+  if (digest_workspace) {
+    size_t dneed = 0;
+    avdb_vrs_digest_workspace_size(n, &dneed);
+    if (digest_workspace_bytes < dneed || reinterpret_cast<uintptr_t>(digest_workspace) % 16) {
+      avdb_set_error("avdb_record_prep_keyed: 16-byte aligned K4 workspace of %zu bytes required", dneed);
+      return AVDB_ERANGE;
+    }
+    kt.long_codes = avdb::vrs_long_codes_of(digest_workspace, n);
+  }
   return record_prep_impl(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, n, end_out, bin_code,
                           status, lcp, hist_l8, counters, stream, &kt, totals_written);
 }
@@ -754,7 +775,7 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
 #undef K2V
 #undef K2VK
     AVDB_LAUNCH_CHECK("k_record_prep4");
-    if (keys && totals_written) *totals_written = 1;
+    if (keys && totals_written) *totals_written = AVDB_KEYED_TOTALS | (kt.long_codes ? AVDB_KEYED_LONG_CODES : 0);
     return AVDB_OK;
   }
   const unsigned grid = stream_grid(n, kBlock * 8, 2048);

@@ -81,7 +81,8 @@ constexpr uint32_t kAlPrefix = nA0 + AVDB_DIGEST_CHARS + nA1;  // ALT starts her
 #endif
 static_assert(kAlPrefix == 68, "allele prefix");
 
-constexpr int kLongBuckets = 32;  // allele-message block counts (the last bucket takes the rest)
+// (kLongBuckets, long_bucket, long_code: avdb_internal.hpp)
+static_assert(kAlPrefix + nA2 == kVrsAlleleFixedBytes, "VRS Allele message length");
 constexpr int kCompactGrid = 2048;  // 8 workgroups per CU for the streaming passes
 
 __device__ __forceinline__ uint32_t sha_blocks(uint64_t msg_bytes) {
@@ -278,10 +279,7 @@ __device__ __forceinline__ bool is_long_rec(uint32_t r, uint32_t a, uint32_t max
   return uint64_t(r) + a > max_len;
 }
 
-__device__ __forceinline__ uint32_t bucket_of(uint32_t a) {
-  const uint32_t nb = allele_blocks(a);
-  return nb < kLongBuckets ? nb : kLongBuckets - 1;
-}
+__device__ __forceinline__ uint32_t bucket_of(uint32_t a) { return long_bucket(a); }
 
 // f(i, ref_len, alt_len) for every record of this workgroup's contiguous chunk;
 // 4 records per lane per step through 16-byte loads when VEC (the chunk size is
@@ -443,6 +441,66 @@ __global__ __launch_bounds__(kBlock) void k_long_scatter_flags(const uint8_t* __
     if (j2 < i1 && j2 + 4 > i1)
       for (size_t k = j2; k < i1; ++k)
         if (is_long[k]) list[atomicAdd(&s_cur[bucket_of(al[k])], 1u)] = uint32_t(k);
+  }
+}
+
+// The keyed K2 already classified every record (long_code: 0 or 1 + bucket, one
+// byte per record in the workspace): the histogram reads those bytes (1 B per
+// record instead of both lengths, 8 B) and writes the is_long flags from them
+__global__ __launch_bounds__(kBlock) void k_long_hist_codes(const uint8_t* __restrict__ codes, size_t n,
+                                                            uint8_t* __restrict__ is_long,
+                                                            uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_cnt[kLongBuckets];
+  if (threadIdx.x < kLongBuckets) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t per = (((n + gridDim.x - 1) / gridDim.x) + 3) & ~size_t(3);  // k_long_hist's chunks
+  const size_t i0 = size_t(blockIdx.x) * per;
+  const size_t i1 = i0 + per < n ? i0 + per : n;
+  for (size_t j = i0 + 4 * size_t(threadIdx.x); j < i1; j += 4 * size_t(blockDim.x)) {
+    if (j + 4 <= i1) {
+      const uint32_t c4 = *reinterpret_cast<const uint32_t*>(codes + j);
+      uint32_t f = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t c = (c4 >> (8 * k)) & 0xFFu;
+        if (c) {
+          f |= 1u << (8 * k);
+          atomicAdd(&s_cnt[c - 1], 1u);
+        }
+      }
+      if (is_long) *reinterpret_cast<uint32_t*>(is_long + j) = f;
+    } else {
+      for (size_t k = j; k < i1; ++k) {
+        const uint32_t c = codes[k];
+        if (c) atomicAdd(&s_cnt[c - 1], 1u);
+        if (is_long) is_long[k] = c ? 1 : 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kLongBuckets) counts[threadIdx.x * gridDim.x + blockIdx.x] = s_cnt[threadIdx.x];
+}
+
+// the scatter over the same chunks, buckets from the codes (no length reads)
+__global__ __launch_bounds__(kBlock) void k_long_scatter_codes(const uint8_t* __restrict__ codes, size_t n,
+                                                               const uint32_t* __restrict__ offs,
+                                                               uint32_t* __restrict__ list) {
+  __shared__ uint32_t s_cur[kLongBuckets];
+  if (threadIdx.x < kLongBuckets) s_cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const size_t per = (((n + gridDim.x - 1) / gridDim.x) + 3) & ~size_t(3);
+  const size_t i0 = size_t(blockIdx.x) * per;
+  const size_t i1 = i0 + per < n ? i0 + per : n;
+  for (size_t j = i0 + 4 * size_t(threadIdx.x); j < i1; j += 4 * size_t(blockDim.x)) {
+    const uint32_t c4 = j + 4 <= i1 ? *reinterpret_cast<const uint32_t*>(codes + j) : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t c = (c4 >> (8 * k)) & 0xFFu;
+      if (c) list[atomicAdd(&s_cur[c - 1], 1u)] = uint32_t(j + k);
+    }
+    if (j + 4 > i1)
+      for (size_t k = j; k < i1; ++k)
+        if (codes[k]) list[atomicAdd(&s_cur[codes[k] - 1], 1u)] = uint32_t(k);
   }
 }
 
@@ -787,11 +845,19 @@ extern "C" int avdb_sha512t24u(avdb_ctx* ctx, const uint8_t* data, const uint64_
   return AVDB_OK;
 }
 
+// workspace: 256 (total) | counts u32[kLongBuckets * kCompactGrid] | list u32[n]
+// | codes u8[n] (the keyed K2's long_code per record)
 extern "C" int avdb_vrs_digest_workspace_size(size_t n, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
-  *bytes = 256 + 4 * size_t(kLongBuckets) * kCompactGrid + 4 * n;
+  *bytes = 256 + 4 * size_t(kLongBuckets) * kCompactGrid + 4 * n + ((n + 15) & ~size_t(15));
   return AVDB_OK;
 }
+
+namespace avdb {
+uint8_t* vrs_long_codes_of(void* workspace, size_t n) {
+  return static_cast<uint8_t*>(workspace) + 256 + 4 * size_t(kLongBuckets) * kCompactGrid + 4 * n;
+}
+}  // namespace avdb
 
 extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                const uint64_t* allele_off, const uint32_t* ref_len,
@@ -799,6 +865,16 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
                                size_t n, uint32_t max_seq_len, void* workspace,
                                size_t workspace_bytes, char* digest_out, uint8_t* is_long,
                                void* stream) {
+  return avdb_vrs_digest_ex(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, n, max_seq_len,
+                            workspace, workspace_bytes, digest_out, is_long, 0u, stream);
+}
+
+extern "C" int avdb_vrs_digest_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                  const uint64_t* allele_off, const uint32_t* ref_len,
+                                  const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                                  size_t n, uint32_t max_seq_len, void* workspace,
+                                  size_t workspace_bytes, char* digest_out, uint8_t* is_long,
+                                  uint32_t flags, void* stream) {
   if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
   if (n == 0) return AVDB_OK;
   if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap || !digest_out) {
@@ -827,7 +903,11 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   auto* list = counts + size_t(kLongBuckets) * kCompactGrid;
   const bool vec = (reinterpret_cast<uintptr_t>(ref_len) | reinterpret_cast<uintptr_t>(alt_len)) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(is_long) % 4 == 0;
-  if (vec)
+  const bool codes_ready = (flags & AVDB_DIGEST_CODES_READY) && reinterpret_cast<uintptr_t>(is_long) % 4 == 0;
+  const uint8_t* codes = vrs_long_codes_of(workspace, n);
+  if (codes_ready)
+    hipLaunchKernelGGL(k_long_hist_codes, dim3(kCompactGrid), dim3(kBlock), 0, s, codes, n, is_long, counts);
+  else if (vec)
     hipLaunchKernelGGL(k_long_hist<true>, dim3(kCompactGrid), dim3(kBlock), 0, s, ref_len, alt_len, n,
                        max_seq_len, is_long, counts);
   else
@@ -836,7 +916,9 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   AVDB_LAUNCH_CHECK("k_long_hist");
   hipLaunchKernelGGL(k_long_scan, dim3(1), dim3(1024), 0, s, counts, total);
   AVDB_LAUNCH_CHECK("k_long_scan");
-  if (vec && is_long && AVDB_K4_SCATTER_FLAGS)
+  if (codes_ready)
+    hipLaunchKernelGGL(k_long_scatter_codes, dim3(kCompactGrid), dim3(kBlock), 0, s, codes, n, counts, list);
+  else if (vec && is_long && AVDB_K4_SCATTER_FLAGS)
     hipLaunchKernelGGL(k_long_scatter_flags, dim3(kCompactGrid), dim3(kBlock), 0, s, is_long, alt_len, n, counts,
                        list);
   else if (vec)

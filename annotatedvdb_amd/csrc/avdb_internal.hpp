@@ -231,6 +231,20 @@ __device__ __forceinline__ void wave_hist_add(uint32_t key, uint32_t* hist) {
   }
 }
 
+// ---- K4's long-record bucket code (shared by K4 and the keyed K2) ----------
+// 0: short (ref + alt <= max_len, keyed by its alleles); else 1 + the record's
+// bucket = the SHA-512 block count of its VRS Allele message (68 bytes before
+// the ALT, 54 after; avdb_digest.hip), the last bucket taking the rest
+constexpr int kLongBuckets = 32;
+constexpr uint32_t kVrsAlleleFixedBytes = 68 + 54;
+__device__ __forceinline__ uint32_t long_bucket(uint32_t a) {
+  const uint32_t nb = uint32_t((uint64_t(kVrsAlleleFixedBytes) + a + 17 + 127) / 128);
+  return nb < uint32_t(kLongBuckets) ? nb : uint32_t(kLongBuckets) - 1;
+}
+__device__ __forceinline__ uint32_t long_code(uint32_t r, uint32_t a, uint32_t max_len) {
+  return uint64_t(r) + a > max_len ? 1u + long_bucket(a) : 0u;
+}
+
 }  // namespace avdb
 
 struct avdb_ctx {
@@ -262,6 +276,8 @@ size_t key_size_workspace(size_t n);
 // K7 one-pass workspace: group totals the keyed K2 fills (avdb_keys.hip)
 uint32_t key_totals_group_log2(size_t n);
 uint2* key_totals_of(void* workspace);
+// K4 workspace: the per-record bucket codes the keyed K2 fills (avdb_digest.hip)
+uint8_t* vrs_long_codes_of(void* workspace, size_t n);
 // K4's per-(contig, digit count) SequenceLocation block-1 table (host)
 void location_tail_table(const char* digests, int n_chrom, std::vector<uint64_t>& out);
 }  // namespace avdb

@@ -535,6 +535,8 @@ class Engine:
         nb = ctypes.c_uint32()
         self.lib.avdb_l8_bin_count(self._ctx, ctypes.byref(nb))
         self.n_l8 = int(nb.value)
+        # K4 workspaces the keyed K2 classified a batch into: data_ptr -> (n, max_seq_len, length arrays)
+        self._codes_for: Dict[int, tuple] = {}
         if sequence_digests is not None:
             self.set_sequence_digests(sequence_digests)
 
@@ -639,12 +641,15 @@ class Engine:
     # -- K2 ----------------------------------------------------------------
     def record_prep(self, b: RecordBatch, *, want_lcp: bool = True, hist: Optional[torch.Tensor] = None,
                     counters: Optional[torch.Tensor] = None, keys: Optional["KeyText"] = None,
-                    key_digest: bool = False, key_paths: bool = True, max_seq_len: int = 50):
+                    key_digest: bool = False, key_paths: bool = True, max_seq_len: int = 50,
+                    digest_workspace: Optional[torch.Tensor] = None):
         """Returns ``(end, code, status, lcp)`` device tensors.  With ``keys`` (a
         one-pass ``KeyText`` from an earlier ``primary_keys`` on a same-sized
         batch) K2 also writes K7's group totals into its workspace
         (``avdb_record_prep_keyed``), so the next ``primary_keys(b, code,
-        digest if key_digest, out=keys)`` skips its totals pass."""
+        digest if key_digest, out=keys)`` skips its totals pass; with
+        ``digest_workspace`` too (the K4 workspace the next ``vrs_digest(b,
+        max_seq_len, workspace=...)`` gets) it classifies the long records for K4."""
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
@@ -659,13 +664,24 @@ class Engine:
             N.check("avdb_record_prep", self.lib.avdb_record_prep(*args, self._stream()))
             return end, code, status, lcp
         keys.totals_for = None
+        dws = digest_workspace
+        if dws is not None:
+            self._codes_for.pop(dws.data_ptr(), None)
+            sz = ctypes.c_size_t()
+            self.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
+            if dws.numel() < sz.value:
+                raise ValueError("record_prep: digest_workspace needs %d bytes" % sz.value)
         done = ctypes.c_int(0)
         N.check("avdb_record_prep_keyed", self.lib.avdb_record_prep_keyed(
             *args, N.ptr(b.ext_id), int(max_seq_len), 1 if key_digest else 0, 1 if key_paths else 0,
-            N.ptr(keys.ws), keys.ws.numel(), ctypes.byref(done), self._stream()))
-        if done.value:  # (tied to this batch's arrays: another batch of the same size recomputes)
+            N.ptr(keys.ws), keys.ws.numel(), N.ptr(dws), dws.numel() if dws is not None else 0,
+            ctypes.byref(done), self._stream()))
+        # (tied to this batch's arrays: another batch of the same size recomputes)
+        if done.value & N.KEYED_TOTALS:
             keys.totals_for = (n, int(max_seq_len), bool(key_digest), bool(key_paths), b.chrom.data_ptr(),
                                b.pos.data_ptr(), b.ref_len.data_ptr(), b.alt_len.data_ptr(), b.ext_id.data_ptr())
+        if done.value & N.KEYED_LONG_CODES:
+            self._codes_for[dws.data_ptr()] = (n, int(max_seq_len), b.ref_len.data_ptr(), b.alt_len.data_ptr())
         return end, code, status, lcp
 
     # -- K3 ----------------------------------------------------------------
@@ -709,10 +725,13 @@ class Engine:
         self.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
         ws = workspace if workspace is not None and workspace.numel() >= sz.value else \
             self.empty(int(sz.value), torch.uint8)
-        N.check("avdb_vrs_digest", self.lib.avdb_vrs_digest(
+        # the keyed K2 classified this batch's records into this workspace
+        ready = self._codes_for.pop(ws.data_ptr(), None) == (n, int(max_seq_len), b.ref_len.data_ptr(),
+                                                              b.alt_len.data_ptr())
+        N.check("avdb_vrs_digest_ex", self.lib.avdb_vrs_digest_ex(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
             N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, int(max_seq_len), N.ptr(ws), int(sz.value),
-            N.ptr(dig), N.ptr(is_long), self._stream()))
+            N.ptr(dig), N.ptr(is_long), N.DIGEST_CODES_READY if ready else 0, self._stream()))
         return dig, is_long
 
     def sha512t24u(self, blobs: Sequence[bytes]) -> List[str]:

@@ -446,13 +446,16 @@ def main():
         last.setdefault("kt", box["kt"])
         last["prep"], last["keep"] = box["prep"], box["keep"]
 
+    # (AVDB_BENCH_K4_CODES=0: K4 classifies the records itself; A/B of the keyed K2's long-record codes)
+    k4_codes = os.environ.get("AVDB_BENCH_K4_CODES", "1") != "0"
+
     def c4k_step(record: bool):
         box = {}
         # (K2 also writes K7's group totals into the reused KeyText's workspace:
         # avdb_record_prep_keyed; the first step allocates the KeyText)
         timed("record_prep", record, lambda: box.setdefault(
             "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr, keys=last.get("kt"),
-                                    key_digest=True)))
+                                    key_digest=True, digest_workspace=last.get("ws4") if k4_codes else None)))
         timed("pk_dedup", record, lambda: box.setdefault(
             "keep", eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3"))))
         timed("vrs_digest", record, lambda: box.setdefault(

@@ -166,6 +166,14 @@ int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                     const uint8_t* heap, size_t heap_bytes, size_t n, uint32_t max_seq_len,
                     void* workspace,
                     size_t workspace_bytes, char* digest_out, uint8_t* is_long, void* stream);
+/* The same with flags: AVDB_DIGEST_CODES_READY = avdb_record_prep_keyed already
+ * classified this batch's records into the workspace (same n and max_seq_len), so
+ * the pass over both length arrays is replaced by one over those bytes. */
+#define AVDB_DIGEST_CODES_READY 1u
+int avdb_vrs_digest_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                       const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                       size_t n, uint32_t max_seq_len, void* workspace, size_t workspace_bytes, char* digest_out,
+                       uint8_t* is_long, uint32_t flags, void* stream);
 
 /* ---- K0: VCF text -> per-alt record SoA ----------------------------------
  * Replaces the text half of VcfEntryParser.parse_entry / get_variant / get_refsnp
@@ -419,17 +427,24 @@ int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint
                                  void* workspace, size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off,
                                  uint8_t* key_out, size_t key_cap, uint8_t* path_out, size_t path_cap,
                                  uint8_t* key_state, uint32_t flags, void* stream);
-/* K2 that also writes K7's group totals (key / path bytes per 256 records) into a
- * one-pass K7 workspace, from the SoA it reads anyway plus the refSNP ids: the
- * record-prep half of the keyed pipeline (C4k).  *totals_written = 1 when it did
- * (16-byte aligned arrays); pass AVDB_KEYS_TOTALS_READY
- * to avdb_primary_keys_onepass_ex then.  Otherwise it is avdb_record_prep. */
+/* K2 that also writes K7's group totals (key / path bytes per group of 64 or 256
+ * records) into a one-pass K7 workspace, from the SoA it reads anyway plus the
+ * refSNP ids: the record-prep half of the keyed pipeline (C4k, C1).  With a K4
+ * workspace (avdb_vrs_digest_workspace_size(n) bytes, 16-byte aligned; nullable)
+ * it also classifies every record for K4 (short, or long and its SHA-512 block
+ * bucket).  *totals_written = AVDB_KEYED_TOTALS | AVDB_KEYED_LONG_CODES for what it
+ * wrote (16-byte aligned arrays; else 0 and it is avdb_record_prep): pass
+ * AVDB_KEYS_TOTALS_READY to avdb_primary_keys_onepass_ex and
+ * AVDB_DIGEST_CODES_READY to avdb_vrs_digest_ex (same n and max_seq_len) then. */
+#define AVDB_KEYED_TOTALS 1
+#define AVDB_KEYED_LONG_CODES 2
 int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
                            const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
                            size_t n, uint32_t* end_out, uint32_t* bin_code, uint8_t* status, uint32_t* lcp,
                            uint32_t* hist_l8, uint64_t* counters, const uint64_t* ext_id, uint32_t max_seq_len,
                            int has_digest, int with_paths, void* key_workspace, size_t key_workspace_bytes,
-                           int* totals_written, void* stream);
+                           void* digest_workspace, size_t digest_workspace_bytes, int* totals_written,
+                           void* stream);
 
 /* ---- K8: the per-record drop-in path in one launch -------------------------
  * The reference calls its per-record API once per alt allele
