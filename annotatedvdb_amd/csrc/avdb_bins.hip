@@ -517,16 +517,17 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
           K += __shfl_xor(K, d, kWave);
           P += __shfl_xor(P, d, kWave);
         }
-        if (kt.group_log2 == 0) {  // four 64-record groups per wave step
-          if ((__lane_id() & 15u) == 0 && j < ngroups) kt.tot[j >> 4] = make_uint2(K, P);
-        } else {  // one 256-record group
+        // a K7 group is 64 << group_log2 records = the records of 16 << group_log2 lanes
+        if (kt.group_log2 >= 1) {
           K += __shfl_xor(K, 16, kWave);
           P += __shfl_xor(P, 16, kWave);
+        }
+        if (kt.group_log2 >= 2) {
           K += __shfl_xor(K, 32, kWave);
           P += __shfl_xor(P, 32, kWave);
-          const size_t j0 = base + size_t(u) * bdim + (threadIdx.x & ~uint32_t(kWave - 1));
-          if (__lane_id() == 0 && j0 < ngroups) kt.tot[j0 / kWave] = make_uint2(K, P);
         }
+        if ((__lane_id() & ((16u << kt.group_log2) - 1)) == 0 && j < ngroups)
+          kt.tot[j >> (4 + kt.group_log2)] = make_uint2(K, P);
       }
       if constexpr (KEYS != 0) {
         if (kt.long_codes && live) {
@@ -752,7 +753,7 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
     const int U = keys ? ctx->k2_keyed_unroll : ctx->k2_unroll;  // (the keyed form's registers: 144 VGPRs at U=2)
     const unsigned grid = stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
 #define K2V(HI, UU)                                                                                       \
-  if (keys && kt.group_log2 == 0) K2VK(HI, UU, 2); else if (keys) K2VK(HI, UU, 1); else K2VK(HI, UU, 0)
+  if (keys && kt.group_log2 < 2) K2VK(HI, UU, 2); else if (keys) K2VK(HI, UU, 1); else K2VK(HI, UU, 0)
 #define K2VK(HI, UU, KK)                                                                                  \
   hipLaunchKernelGGL((k_record_prep4<HI, UU, KK>), dim3(grid), dim3(bdim), shm, s,                       \
                      reinterpret_cast<const uint32_t*>(chrom), reinterpret_cast<const u32x4*>(pos),      \

@@ -895,7 +895,10 @@ extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint
 }
 
 // ---- K7 with group offsets --------------------------------------------------------
-static uint32_t key_group_log2(size_t n) { return n < kSmallGroupN ? 0u : kGroupLog2; }
+#ifndef AVDB_K7_SMALL_LOG2
+#define AVDB_K7_SMALL_LOG2 0u  // group size below kSmallGroupN records (A/B knob: 64 << this)
+#endif
+static uint32_t key_group_log2(size_t n) { return n < kSmallGroupN ? uint32_t(AVDB_K7_SMALL_LOG2) : kGroupLog2; }
 static size_t key_groups(size_t n) {
   const size_t g = size_t(kWave) << key_group_log2(n);
   return (n + g - 1) / g;
