@@ -49,6 +49,9 @@ namespace avdb {
 // than it saves.
 typedef __attribute__((address_space(1))) uint8_t gbyte;
 typedef __attribute__((address_space(1))) U64u* gw_u64u;
+#ifndef AVDB_SINK_NT
+#define AVDB_SINK_NT 0  // A/B knob: the global sink's 8-byte stores as nontemporal stores
+#endif
 // per SIMD: the text window's LDS allows 4 workgroups per CU (re-checked after
 // the append sink: 4 waves with ~100 B of spills 5.5 ms, 3 waves without 6.2 ms)
 #ifndef AVDB_K5_WAVES
@@ -179,7 +182,10 @@ struct Out {
       const uint32_t k = pend.k;  // 0..7
       pend.w |= x << (8 * k);
       if (k + t >= 8) {
-        reinterpret_cast<gw_u64u>(base + p - k)->v = pend.w;
+        if constexpr (AVDB_SINK_NT)
+          __builtin_nontemporal_store(pend.w, reinterpret_cast<__attribute__((address_space(1))) uint64_t*>(base + p - k));
+        else
+          reinterpret_cast<gw_u64u>(base + p - k)->v = pend.w;
         pend.w = k ? x >> (64 - 8 * k) : 0ull;
         pend.k = k + t - 8;
       } else {
