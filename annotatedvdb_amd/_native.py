@@ -88,7 +88,7 @@ EXPORTED_SYMBOLS = [
     "avdb_ctx_create", "avdb_ctx_destroy", "avdb_ctx_n_chrom",
     "avdb_ctx_set_sequence_digests", "avdb_l8_bin_count",
     "avdb_bin_assign", "avdb_record_prep",
-    "avdb_pk_dedup_workspace_size", "avdb_pk_dedup",
+    "avdb_pk_dedup_workspace_size", "avdb_pk_dedup", "avdb_pk_dedup_ex",
     "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest", "avdb_vrs_digest_ex",
     "avdb_format_bin_path", "avdb_format_bin_paths",
     "avdb_vcf_workspace_size", "avdb_vcf_count_lines", "avdb_vcf_parse_lines", "avdb_vcf_emit",
@@ -109,7 +109,8 @@ EXPORTED_SYMBOLS = [
 
 SMALL_PATH, SMALL_KEY, SMALL_DISPLAY = 1, 2, 4
 KEYS_TOTALS_READY = 1  # AVDB_KEYS_TOTALS_READY
-KEYED_TOTALS, KEYED_LONG_CODES = 1, 2  # avdb_record_prep_keyed's *totals_written bits
+KEYED_TOTALS, KEYED_LONG_CODES, KEYED_DEDUP_MARKS = 1, 2, 4  # avdb_record_prep_keyed's *totals_written bits
+DEDUP_MARKED = 1  # AVDB_DEDUP_MARKED
 DIGEST_CODES_READY = 1  # AVDB_DIGEST_CODES_READY
 SMALL_MAX = 65536
 
@@ -160,6 +161,7 @@ def _sig(lib):
     f.avdb_record_prep.argtypes = [P, P, P, P, P, P, P, SZ, SZ, P, P, P, P, P, P, P]
     f.avdb_pk_dedup_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_pk_dedup.argtypes = [P, P, P, P, P, P, P, SZ, P, SZ, I32, P, SZ, P, P, P]
+    f.avdb_pk_dedup_ex.argtypes = [P, P, P, P, P, P, P, SZ, P, SZ, P, SZ, P, P, U32, P]
     f.avdb_sha512t24u.argtypes = [P, P, P, P, SZ, P, P]
     f.avdb_vrs_digest_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_vrs_digest.argtypes = [P, P, P, P, P, P, P, SZ, SZ, U32, P, SZ, P, P, P]
@@ -191,7 +193,7 @@ def _sig(lib):
     f.avdb_primary_keys_onepass.argtypes = list(f.avdb_primary_keys.argtypes)  # same signature
     f.avdb_primary_keys_onepass_ex.argtypes = list(f.avdb_primary_keys.argtypes)[:-1] + [U32, P]
     f.avdb_record_prep_keyed.argtypes = list(f.avdb_record_prep.argtypes)[:-1] + [P, U32, I32, I32, P, SZ, P, SZ,
-                                                                                 ctypes.POINTER(I32), P]
+                                                                                 P, SZ, P, ctypes.POINTER(I32), P]
     f.avdb_primary_keys_bound.argtypes = [SZ, SZ, ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
     f.avdb_primary_keys_onepass_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]

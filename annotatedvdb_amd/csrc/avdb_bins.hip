@@ -380,6 +380,13 @@ struct KeyTotals {
   uint32_t has_digest, with_paths;
   uint32_t group_log2;  // K7's groups: 64 << group_log2 records (0: 16 lanes' records, 2: the wave's)
   uint8_t* long_codes;  // nullable: K4's long_code per record (avdb::vrs_long_codes_of(digest workspace))
+  // nullable: K3's first phase (k_dedup_mark4) — keep = 1 for every record and the
+  // records sharing their predecessor's (chrom, pos), listed in this workgroup's
+  // slice of dd_list (dd_slice entries), their count in dd_counts[workgroup]
+  uint8_t* keep;
+  uint32_t* dd_counts;
+  uint32_t* dd_list;
+  size_t dd_slice;
 };
 
 // KEYS: 0 plain; 1 keyed; 2 keyed with registers for 6 waves per SIMD — for
@@ -403,12 +410,15 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
   __shared__ uint32_t s_len[AVDB_MAX_CHROM];
   __shared__ uint32_t s_l8off[AVDB_MAX_CHROM];
   __shared__ unsigned long long s_ctr[AVDB_N_COUNTERS];
+  __shared__ uint32_t s_dd;  // KEYS with dd_list: suspects this workgroup listed
+  if (threadIdx.x == 0) s_dd = 0;
   const bool use_lds = HIST && lds_hist;
   stage_table(tab, s_len, s_l8off, s_ctr, s_hist, use_lds);
   uint32_t* hist = use_lds ? s_hist : g_hist;
   const bool ctrs = g_ctr != nullptr;
   const int n_chrom = tab.n;
   const size_t bdim = blockDim.x;
+  uint32_t* dd_mine = (KEYS != 0 && kt.dd_list) ? kt.dd_list + size_t(blockIdx.x) * kt.dd_slice : nullptr;
   uint32_t err = 0, nrec = 0;
   int since_flush = 0;
   uint32_t run_key = 0xFFFFFFFFu, run_cnt = 0;
@@ -530,6 +540,37 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
           kt.tot[j >> (4 + kt.group_log2)] = make_uint2(K, P);
       }
       if constexpr (KEYS != 0) {
+        if (dd_mine) {  // K3's mark phase on the (chrom, pos) already in registers
+          const uint32_t c4 = cw[u];
+          const u32x4 q4 = p4[u];
+          uint32_t pc = __shfl_up(c4 >> 24, 1, kWave), pp = __shfl_up(q4.w, 1, kWave);
+          if (__lane_id() == 0 && live && j > 0) {
+            pc = chrom[4 * j - 1];
+            pp = pos[4 * j - 1];
+          }
+          uint32_t same = 0;
+          if (live) {
+            same |= uint32_t(j > 0 && (c4 & 0xFFu) == pc && q4.x == pp);
+            same |= uint32_t(((c4 >> 8) & 0xFFu) == (c4 & 0xFFu) && q4.y == q4.x) << 1;
+            same |= uint32_t(((c4 >> 16) & 0xFFu) == ((c4 >> 8) & 0xFFu) && q4.z == q4.y) << 2;
+            same |= uint32_t((c4 >> 24) == ((c4 >> 16) & 0xFFu) && q4.w == q4.z) << 3;
+          }
+          const uint32_t cnt = __popc(same);
+          uint32_t incl = cnt;
+#pragma unroll
+          for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t up = __shfl_up(incl, d, kWave);
+            if (__lane_id() >= uint32_t(d)) incl += up;
+          }
+          const uint32_t total = __shfl(incl, kWave - 1, kWave);
+          if (total) {
+            uint32_t at = 0;
+            if (__lane_id() == kWave - 1) at = atomicAdd(&s_dd, total);
+            at = __shfl(at, kWave - 1, kWave) + incl - cnt;
+            for (uint32_t m = same; m; m &= m - 1) dd_mine[at++] = uint32_t(4 * j + __builtin_ctz(m));
+          }
+          if (live) reinterpret_cast<uint32_t*>(kt.keep)[j] = 0x01010101u;
+        }
         if (kt.long_codes && live) {
           uint32_t lc = 0;
 #pragma unroll
@@ -566,6 +607,10 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
       if (status) status[i] = uint8_t(s_k);
       if (lcp) lcp[i] = l;
       if (KEYS != 0 && kt.long_codes) kt.long_codes[i] = uint8_t(long_code(r, a, kt.max_seq_len));
+      if (KEYS != 0 && dd_mine) {
+        if (i > 0 && chrom[i - 1] == c && pos[i - 1] == p) dd_mine[atomicAdd(&s_dd, 1u)] = uint32_t(i);
+        kt.keep[i] = 1;
+      }
       nrec += 1;
       err += s_k ? (1u << (8 * (s_k - 1))) : 0u;
       key = l8_key(c, p, cv, s_l8off);
@@ -583,7 +628,8 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
       s_ctr[AVDB_CTR_STATUS0] = s_ctr[AVDB_CTR_RECORDS] - bad;
     }
   }
-  publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);
+  publish(tab, s_ctr, s_hist, use_lds, HIST, g_hist, g_ctr);  // (begins with a barrier)
+  if (KEYS != 0 && dd_mine && threadIdx.x == 0) kt.dd_counts[blockIdx.x] = s_dd;
 }
 
 }  // namespace avdb
@@ -673,6 +719,26 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
                             uint32_t* lcp, uint32_t* hist_l8, uint64_t* counters, void* stream, const KeyTotals* keyed,
                             int* totals_written);
 
+// the keyed K2's grid, and the most records one of its workgroups handles (its
+// grid-stride trips of bdim * U groups of 4, plus the < 4 records of block 0's
+// scalar tail): one K3 list slice each
+static unsigned keyed_grid(const avdb_ctx* ctx, size_t n) {
+  return stream_grid(n / 4, unsigned(kK1Block) * unsigned(ctx->k2_keyed_unroll),
+                     unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
+}
+namespace avdb {
+void keyed_prep_layout(const avdb_ctx* ctx, size_t n, unsigned* grid, size_t* slice) {
+  *grid = 0;
+  *slice = 0;
+  if (!ctx || n < 4) return;
+  const unsigned g = keyed_grid(ctx, n);
+  const size_t per_trip = size_t(kK1Block) * size_t(ctx->k2_keyed_unroll) * g;  // groups of 4 per grid trip
+  const size_t trips = (n / 4 + per_trip - 1) / per_trip;
+  *grid = g;
+  *slice = 4 * size_t(kK1Block) * size_t(ctx->k2_keyed_unroll) * trips + 4;
+}
+}  // namespace avdb
+
 extern "C" int avdb_record_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                 const uint64_t* allele_off, const uint32_t* ref_len,
                                 const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
@@ -690,7 +756,9 @@ extern "C" int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const
                                       uint64_t* counters, const uint64_t* ext_id, uint32_t max_seq_len,
                                       int has_digest, int with_paths, void* key_workspace,
                                       size_t key_workspace_bytes, void* digest_workspace,
-                                      size_t digest_workspace_bytes, int* totals_written, void* stream) {
+                                      size_t digest_workspace_bytes, void* dedup_workspace,
+                                      size_t dedup_workspace_bytes, uint8_t* keep, int* totals_written,
+                                      void* stream) {
   if (!totals_written) {
     avdb_set_error("avdb_record_prep_keyed: null totals_written");
     return AVDB_EINVAL;
@@ -719,6 +787,22 @@ extern "C" int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const
       return AVDB_ERANGE;
     }
     kt.long_codes = avdb::vrs_long_codes_of(digest_workspace, n);
+  }
+  kt.keep = nullptr;
+  kt.dd_counts = kt.dd_list = nullptr;
+  kt.dd_slice = 0;
+  if (dedup_workspace && keep) {  // K3's mark phase too, when the layout fits
+    unsigned grid = 0;
+    size_t slice = 0;
+    avdb::keyed_prep_layout(ctx, n, &grid, &slice);
+    if (grid && grid <= avdb::kDedupMaxGroups && reinterpret_cast<uintptr_t>(dedup_workspace) % 16 == 0 &&
+        reinterpret_cast<uintptr_t>(keep) % 4 == 0 &&
+        dedup_workspace_bytes >= avdb::kDedupListHead + 4 * size_t(grid) * slice) {
+      kt.keep = keep;
+      kt.dd_counts = static_cast<uint32_t*>(dedup_workspace);
+      kt.dd_list = reinterpret_cast<uint32_t*>(static_cast<char*>(dedup_workspace) + avdb::kDedupListHead);
+      kt.dd_slice = slice;
+    }
   }
   return record_prep_impl(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, n, end_out, bin_code,
                           status, lcp, hist_l8, counters, stream, &kt, totals_written);
@@ -751,7 +835,7 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
     const size_t ngroups = n / 4;
     const unsigned bdim = unsigned(kK1Block);
     const int U = keys ? ctx->k2_keyed_unroll : ctx->k2_unroll;  // (the keyed form's registers: 144 VGPRs at U=2)
-    const unsigned grid = stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
+    const unsigned grid = keys ? keyed_grid(ctx, n) : stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
 #define K2V(HI, UU)                                                                                       \
   if (keys && kt.group_log2 < 2) K2VK(HI, UU, 2); else if (keys) K2VK(HI, UU, 1); else K2VK(HI, UU, 0)
 #define K2VK(HI, UU, KK)                                                                                  \
@@ -776,7 +860,9 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
 #undef K2V
 #undef K2VK
     AVDB_LAUNCH_CHECK("k_record_prep4");
-    if (keys && totals_written) *totals_written = AVDB_KEYED_TOTALS | (kt.long_codes ? AVDB_KEYED_LONG_CODES : 0);
+    if (keys && totals_written)
+      *totals_written = AVDB_KEYED_TOTALS | (kt.long_codes ? AVDB_KEYED_LONG_CODES : 0) |
+                        (kt.dd_list ? AVDB_KEYED_DEDUP_MARKS : 0);
     return AVDB_OK;
   }
   const unsigned grid = stream_grid(n, kBlock * 8, 2048);

@@ -250,6 +250,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_grouped4(
 // 64 suspects instead of once per wave of mostly unique records.
 constexpr int kListGridMax = 4096;
 constexpr size_t kListHead = 4 * kListGridMax;  // per-workgroup suspect counts
+static_assert(kListHead == kDedupListHead && unsigned(kListGridMax) == kDedupMaxGroups, "K3 list layout");
 
 __device__ __forceinline__ void chunk_of(size_t items, size_t* lo, size_t* hi) {
   const size_t per = (items + gridDim.x - 1) / gridDim.x;
@@ -329,11 +330,14 @@ __global__ __launch_bounds__(kBlock) void k_dedup_resolve_list(
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
     const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
     const uint64_t* __restrict__ ext, size_t n, const uint32_t* __restrict__ counts,
-    const uint32_t* __restrict__ list, uint8_t* __restrict__ keep, unsigned long long* __restrict__ g_ctr) {
+    const uint32_t* __restrict__ list, uint8_t* __restrict__ keep, unsigned long long* __restrict__ g_ctr,
+    size_t slice) {
   const Heap h = make_heap(heap, heap_bytes);
   size_t g0, g1;
   chunk_of((n + 3) / 4, &g0, &g1);
-  const uint32_t* mine = list + 4 * g0;
+  // slice: the keyed K2 listed the suspects (one slice of `slice` entries per K2
+  // workgroup, as many resolve workgroups); else k_dedup_mark4's chunks
+  const uint32_t* mine = slice ? list + size_t(blockIdx.x) * slice : list + 4 * g0;
   const uint32_t cnt = counts[blockIdx.x];
   uint32_t dups = 0;
   // wave-uniform trip count (dedup_record's cooperative compares need the whole wave)
@@ -475,6 +479,37 @@ extern "C" int avdb_pk_dedup_workspace_size(size_t n, size_t* bytes) {
   return AVDB_OK;
 }
 
+extern "C" int avdb_pk_dedup_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                                const uint8_t* heap, size_t heap_bytes, const uint64_t* ext_id, size_t n,
+                                void* workspace, size_t workspace_bytes, uint8_t* keep, uint64_t* counters,
+                                uint32_t flags, void* stream) {
+  if (!(flags & AVDB_DEDUP_MARKED))
+    return avdb_pk_dedup(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id, n, 1, workspace,
+                         workspace_bytes, keep, counters, stream);
+  if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
+  if (n == 0) return AVDB_OK;
+  if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap || !keep || !workspace) {
+    avdb_set_error("avdb_pk_dedup_ex: null array");
+    return AVDB_EINVAL;
+  }
+  unsigned grid = 0;
+  size_t slice = 0;
+  keyed_prep_layout(ctx, n, &grid, &slice);
+  if (!grid || workspace_bytes < kListHead + 4 * size_t(grid) * slice) {
+    avdb_set_error("avdb_pk_dedup_ex: the workspace does not hold the keyed K2's suspect lists");
+    return AVDB_ERANGE;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  auto* counts = static_cast<uint32_t*>(workspace);
+  auto* list = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + kListHead);
+  hipLaunchKernelGGL(k_dedup_resolve_list, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), chrom,
+                     pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id, n, counts, list, keep,
+                     reinterpret_cast<unsigned long long*>(counters), slice);
+  AVDB_LAUNCH_CHECK("k_dedup_resolve_list");
+  return AVDB_OK;
+}
+
 extern "C" int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                              const uint64_t* allele_off, const uint32_t* ref_len,
                              const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
@@ -505,7 +540,7 @@ extern "C" int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t
       hipLaunchKernelGGL(k_dedup_mark4, dim3(grid4), dim3(kBlock), 0, s, chrom, pos, n, keep, counts, list);
       AVDB_LAUNCH_CHECK("k_dedup_mark4");
       hipLaunchKernelGGL(k_dedup_resolve_list, dim3(grid4), dim3(kBlock), 0, s, chrom, pos, allele_off,
-                         ref_len, alt_len, heap, heap_bytes, ext_id, n, counts, list, keep, ctr);
+                         ref_len, alt_len, heap, heap_bytes, ext_id, n, counts, list, keep, ctr, size_t(0));
       AVDB_LAUNCH_CHECK("k_dedup_resolve_list");
     } else if (vec) {
       hipLaunchKernelGGL(k_dedup_grouped4, dim3(grid4), dim3(kBlock), 0, s, chrom, pos, allele_off,

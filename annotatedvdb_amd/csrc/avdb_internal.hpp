@@ -276,6 +276,12 @@ size_t key_size_workspace(size_t n);
 // K7 one-pass workspace: group totals the keyed K2 fills (avdb_keys.hip)
 uint32_t key_totals_group_log2(size_t n);
 uint2* key_totals_of(void* workspace);
+// K3 list-form workspace: per-workgroup suspect counts, then the suspect list
+constexpr size_t kDedupListHead = 16384;
+constexpr unsigned kDedupMaxGroups = kDedupListHead / 4;
+// the keyed K2's workgroups and the records each may list as suspects (one slice
+// of the K3 list per workgroup; avdb_bins.hip), for K3's resolve over them
+void keyed_prep_layout(const avdb_ctx* ctx, size_t n, unsigned* grid, size_t* slice);
 // K4 workspace: the per-record bucket codes the keyed K2 fills (avdb_digest.hip)
 uint8_t* vrs_long_codes_of(void* workspace, size_t n);
 // K4's per-(contig, digit count) SequenceLocation block-1 table (host)

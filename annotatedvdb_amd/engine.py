@@ -537,6 +537,8 @@ class Engine:
         self.n_l8 = int(nb.value)
         # K4 workspaces the keyed K2 classified a batch into: data_ptr -> (n, max_seq_len, length arrays)
         self._codes_for: Dict[int, tuple] = {}
+        # K3 workspaces the keyed K2 ran the mark phase into: data_ptr -> ((n, chrom, pos), keep)
+        self._marks_for: Dict[int, tuple] = {}
         if sequence_digests is not None:
             self.set_sequence_digests(sequence_digests)
 
@@ -642,14 +644,17 @@ class Engine:
     def record_prep(self, b: RecordBatch, *, want_lcp: bool = True, hist: Optional[torch.Tensor] = None,
                     counters: Optional[torch.Tensor] = None, keys: Optional["KeyText"] = None,
                     key_digest: bool = False, key_paths: bool = True, max_seq_len: int = 50,
-                    digest_workspace: Optional[torch.Tensor] = None):
+                    digest_workspace: Optional[torch.Tensor] = None,
+                    dedup_workspace: Optional[torch.Tensor] = None):
         """Returns ``(end, code, status, lcp)`` device tensors.  With ``keys`` (a
         one-pass ``KeyText`` from an earlier ``primary_keys`` on a same-sized
         batch) K2 also writes K7's group totals into its workspace
         (``avdb_record_prep_keyed``), so the next ``primary_keys(b, code,
         digest if key_digest, out=keys)`` skips its totals pass; with
         ``digest_workspace`` too (the K4 workspace the next ``vrs_digest(b,
-        max_seq_len, workspace=...)`` gets) it classifies the long records for K4."""
+        max_seq_len, workspace=...)`` gets) it classifies the long records for K4,
+        and with ``dedup_workspace`` (the one the next ``pk_dedup(b, workspace=...)``
+        gets) it runs K3's first phase, so that call only resolves the listed runs."""
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
@@ -671,17 +676,24 @@ class Engine:
             self.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
             if dws.numel() < sz.value:
                 raise ValueError("record_prep: digest_workspace needs %d bytes" % sz.value)
+        ddw = dedup_workspace
+        keep = None
+        if ddw is not None:
+            self._marks_for.pop(ddw.data_ptr(), None)
+            keep = self.empty(max(4, n), torch.uint8)
         done = ctypes.c_int(0)
         N.check("avdb_record_prep_keyed", self.lib.avdb_record_prep_keyed(
             *args, N.ptr(b.ext_id), int(max_seq_len), 1 if key_digest else 0, 1 if key_paths else 0,
             N.ptr(keys.ws), keys.ws.numel(), N.ptr(dws), dws.numel() if dws is not None else 0,
-            ctypes.byref(done), self._stream()))
+            N.ptr(ddw), ddw.numel() if ddw is not None else 0, N.ptr(keep), ctypes.byref(done), self._stream()))
         # (tied to this batch's arrays: another batch of the same size recomputes)
         if done.value & N.KEYED_TOTALS:
             keys.totals_for = (n, int(max_seq_len), bool(key_digest), bool(key_paths), b.chrom.data_ptr(),
                                b.pos.data_ptr(), b.ref_len.data_ptr(), b.alt_len.data_ptr(), b.ext_id.data_ptr())
         if done.value & N.KEYED_LONG_CODES:
             self._codes_for[dws.data_ptr()] = (n, int(max_seq_len), b.ref_len.data_ptr(), b.alt_len.data_ptr())
+        if done.value & N.KEYED_DEDUP_MARKS:
+            self._marks_for[ddw.data_ptr()] = ((n, b.chrom.data_ptr(), b.pos.data_ptr()), keep)
         return end, code, status, lcp
 
     # -- K3 ----------------------------------------------------------------
@@ -691,6 +703,15 @@ class Engine:
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
+        marks = self._marks_for.pop(workspace.data_ptr(), None) if workspace is not None else None
+        if grouped and marks is not None and marks[0] == (n, b.chrom.data_ptr(), b.pos.data_ptr()):
+            # the keyed K2 already wrote keep = 1 and listed the runs: resolve them
+            keep = marks[1]
+            N.check("avdb_pk_dedup_ex", self.lib.avdb_pk_dedup_ex(
+                self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
+                N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), n, N.ptr(workspace),
+                workspace.numel(), N.ptr(keep), N.ptr(counters), N.DEDUP_MARKED, self._stream()))
+            return keep[:n]
         keep = self.empty(n, torch.uint8)
         ws = None
         ws_bytes = 0

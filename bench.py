@@ -437,7 +437,8 @@ def main():
         box = {}
         # (K2 also writes K7's group totals into the reused KeyText's workspace)
         timed("record_prep", record, lambda: box.setdefault(
-            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr, keys=last.get("kt"))))
+            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr, keys=last.get("kt"),
+                                    dedup_workspace=last.get("ws3") if k3_marks else None)))
         timed("pk_dedup", record, lambda: box.setdefault(
             "keep", eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3"))))
         code_ = box["prep"][1]
@@ -448,6 +449,8 @@ def main():
 
     # (AVDB_BENCH_K4_CODES=0: K4 classifies the records itself; A/B of the keyed K2's long-record codes)
     k4_codes = os.environ.get("AVDB_BENCH_K4_CODES", "1") != "0"
+    # (AVDB_BENCH_K3_MARKS=0: K3 runs its own mark pass; A/B of the keyed K2's K3 first phase)
+    k3_marks = os.environ.get("AVDB_BENCH_K3_MARKS", "1") != "0"
 
     def c4k_step(record: bool):
         box = {}
@@ -455,7 +458,8 @@ def main():
         # avdb_record_prep_keyed; the first step allocates the KeyText)
         timed("record_prep", record, lambda: box.setdefault(
             "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr, keys=last.get("kt"),
-                                    key_digest=True, digest_workspace=last.get("ws4") if k4_codes else None)))
+                                    key_digest=True, digest_workspace=last.get("ws4") if k4_codes else None,
+                                    dedup_workspace=last.get("ws3") if k3_marks else None)))
         timed("pk_dedup", record, lambda: box.setdefault(
             "keep", eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3"))))
         timed("vrs_digest", record, lambda: box.setdefault(
@@ -493,7 +497,8 @@ def main():
 
     last = {}
     if a.workload in ("c1", "c4k"):  # dedup workspace, allocated once
-        last["ws3"] = torch.empty(16384 + 4 * ((n + 3) & ~3), dtype=torch.uint8, device=dev)
+        # (+ 2^22 entries: the keyed K2's per-workgroup suspect slices round up)
+        last["ws3"] = torch.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), dtype=torch.uint8, device=dev)
     if a.workload == "c4k":  # K4 compaction workspace, allocated once
         import ctypes
         sz = ctypes.c_size_t()

@@ -149,6 +149,15 @@ int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                   int grouped,
                   void* workspace, size_t workspace_bytes, uint8_t* keep, uint64_t* counters,
                   void* stream);
+/* The same (grouped, list form) with flags: AVDB_DEDUP_MARKED = avdb_record_prep_keyed
+ * already ran the first phase for this batch (keep = 1 everywhere, the records that
+ * share their predecessor's position listed in `workspace`, which must be the one it
+ * was given, with `keep` its keep array): only the run scan over those lists runs. */
+#define AVDB_DEDUP_MARKED 1u
+int avdb_pk_dedup_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                     const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                     const uint64_t* ext_id, size_t n, void* workspace, size_t workspace_bytes, uint8_t* keep,
+                     uint64_t* counters, uint32_t flags, void* stream);
 
 /* ---- K4: digests ---------------------------------------------------------
  * sha512t24u of n byte strings (data + off[i], len[i]) -> out[i*32..] base64url. */
@@ -432,19 +441,25 @@ int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint
  * refSNP ids: the record-prep half of the keyed pipeline (C4k, C1).  With a K4
  * workspace (avdb_vrs_digest_workspace_size(n) bytes, 16-byte aligned; nullable)
  * it also classifies every record for K4 (short, or long and its SHA-512 block
- * bucket).  *totals_written = AVDB_KEYED_TOTALS | AVDB_KEYED_LONG_CODES for what it
- * wrote (16-byte aligned arrays; else 0 and it is avdb_record_prep): pass
- * AVDB_KEYS_TOTALS_READY to avdb_primary_keys_onepass_ex and
- * AVDB_DIGEST_CODES_READY to avdb_vrs_digest_ex (same n and max_seq_len) then. */
+ * bucket).  With a K3 list workspace and a keep array (nullable) it also runs K3's
+ * first phase (keep = 1, same-position records listed per workgroup) when its
+ * lists fit (kDedupListHead + 4 * grid * slice bytes: at most 16 KB + 4 (n + 2^22)
+ * at the default unroll).
+ * *totals_written = AVDB_KEYED_TOTALS | AVDB_KEYED_LONG_CODES | AVDB_KEYED_DEDUP_MARKS
+ * for what it wrote (16-byte aligned arrays; else 0 and it is avdb_record_prep):
+ * pass AVDB_KEYS_TOTALS_READY to avdb_primary_keys_onepass_ex, AVDB_DIGEST_CODES_READY
+ * to avdb_vrs_digest_ex (same n and max_seq_len) and AVDB_DEDUP_MARKED to
+ * avdb_pk_dedup_ex then. */
 #define AVDB_KEYED_TOTALS 1
 #define AVDB_KEYED_LONG_CODES 2
+#define AVDB_KEYED_DEDUP_MARKS 4
 int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
                            const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
                            size_t n, uint32_t* end_out, uint32_t* bin_code, uint8_t* status, uint32_t* lcp,
                            uint32_t* hist_l8, uint64_t* counters, const uint64_t* ext_id, uint32_t max_seq_len,
                            int has_digest, int with_paths, void* key_workspace, size_t key_workspace_bytes,
-                           void* digest_workspace, size_t digest_workspace_bytes, int* totals_written,
-                           void* stream);
+                           void* digest_workspace, size_t digest_workspace_bytes, void* dedup_workspace,
+                           size_t dedup_workspace_bytes, uint8_t* keep, int* totals_written, void* stream);
 
 /* ---- K8: the per-record drop-in path in one launch -------------------------
  * The reference calls its per-record API once per alt allele

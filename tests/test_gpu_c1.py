@@ -382,3 +382,32 @@ def test_keyed_record_prep_classifies_for_k4(engine, n, long_frac):
     assert torch.equal(is_long2[:n], ref2_long[:n])
     sel2 = ref2_long.bool()
     assert torch.equal(dig2[sel2], ref2_dig[sel2])
+
+
+@pytest.mark.parametrize("n,dup", [((4 << 20) + 4099, 0.01), (1100000, 0.05), (300001, 0.3), (4097, 0.5), (130, 0.5),
+                                   (7, 0.5), (5, 0.0)])
+def test_keyed_record_prep_marks_for_k3(engine, n, dup):
+    """The keyed K2 with a K3 workspace runs K3's first phase (keep = 1, the records
+    sharing their predecessor's position listed per K2 workgroup; avdb_pk_dedup_ex +
+    AVDB_DEDUP_MARKED resolves them): the same keep flags and duplicate count as
+    K3 on its own; a workspace marked for one batch is not taken for another."""
+    from annotatedvdb_amd import _native as N
+    from annotatedvdb_amd import synth
+    b = synth.alleles(n, seed=17 + n % 5, long_frac=0.02, dup_frac=dup, device="cuda")
+    ctr0 = torch.zeros(N.N_COUNTERS, dtype=torch.int64, device="cuda")
+    ref_keep = engine.pk_dedup(b, grouped=True, counters=ctr0)
+    kt = engine.primary_keys(b, code=engine.record_prep(b, want_lcp=False)[1])
+    ws = torch.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), dtype=torch.uint8, device="cuda")
+    engine.record_prep(b, want_lcp=False, keys=kt, dedup_workspace=ws)
+    assert bool(engine._marks_for) == (n >= 4)
+    ctr1 = torch.zeros(N.N_COUNTERS, dtype=torch.int64, device="cuda")
+    keep = engine.pk_dedup(b, grouped=True, counters=ctr1, workspace=ws)
+    assert not engine._marks_for
+    assert torch.equal(keep[:n], ref_keep[:n])
+    assert torch.equal(ctr0, ctr1)
+    if dup:
+        assert int((keep[:n] == 0).sum()) > 0
+    # marked for batch b, then asked for batch c of the same size: c's own result
+    c = synth.alleles(n, seed=99 + n % 5, long_frac=0.02, dup_frac=dup, device="cuda")
+    engine.record_prep(b, want_lcp=False, keys=kt, dedup_workspace=ws)
+    assert torch.equal(engine.pk_dedup(c, grouped=True, workspace=ws)[:n], engine.pk_dedup(c, grouped=True)[:n])

@@ -4,8 +4,8 @@ the bench's own generator and seeds: 8 ranks' length-balanced pieces x 1.25e8
 records = 1e9) runs shard by shard on one GPU through K2 (end, bin), K3
 (keep-first dedup), K4 (VRS digests of the long records) and K7 (primary-key and
 ltree-path text), in the keyed form bench.py times (K2 also writing K7's group
-totals and K4's long-record codes); every output of every record is compared
-with the C oracle.
+totals, K4's long-record codes and K3's first phase); every output of every
+record is compared with the C oracle.
 The oracle runs in chunks on a thread pool (ctypes releases the GIL).
 
 The long-record digests are checked against the oracle's restatement of the
@@ -42,21 +42,23 @@ def _check_shard(engine, n, seed, pieces):
     sz = ctypes.c_size_t()
     engine.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
     ws4 = torch.empty(int(sz.value), dtype=torch.uint8, device="cuda")
+    ws3 = torch.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), dtype=torch.uint8, device="cuda")
     end, code, status, _ = engine.record_prep(b, want_lcp=False)
     keep = engine.pk_dedup(b, grouped=True)
     dig, is_long = engine.vrs_digest(b, 50, workspace=ws4)
     kt = engine.primary_keys(b, code=code, digest=dig)
     del end, code, status, keep, dig, is_long
     # then the bench's keyed step on the same batch, reusing the key text buffers:
-    # K2 writes K7's group totals and K4's long-record codes, K4 and K7 skip their
-    # own passes over the SoA (what bench.py --workload c4k times)
-    end, code, status, _ = engine.record_prep(b, want_lcp=False, keys=kt, key_digest=True, digest_workspace=ws4)
-    assert kt.totals_for is not None and engine._codes_for
-    keep = engine.pk_dedup(b, grouped=True)
+    # K2 writes K7's group totals, K4's long-record codes and K3's first phase, and
+    # K7, K4 and K3 skip their own passes over the SoA (what bench.py --workload c4k times)
+    end, code, status, _ = engine.record_prep(b, want_lcp=False, keys=kt, key_digest=True, digest_workspace=ws4,
+                                              dedup_workspace=ws3)
+    assert kt.totals_for is not None and engine._codes_for and engine._marks_for
+    keep = engine.pk_dedup(b, grouped=True, workspace=ws3)
     dig, is_long = engine.vrs_digest(b, 50, workspace=ws4)
     kt = engine.primary_keys(b, code=code, digest=dig, out=kt)
     torch.cuda.synchronize()
-    del ws4
+    del ws4, ws3
     assert not kt.state[:n].cpu().numpy().any()
     h = {k: getattr(b, k).cpu().numpy() for k in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap",
                                                   "ext_id")}
