@@ -92,7 +92,6 @@ EXPORTED_SYMBOLS = [
     "avdb_sha512t24u", "avdb_vrs_digest_workspace_size", "avdb_vrs_digest", "avdb_vrs_digest_ex",
     "avdb_format_bin_path", "avdb_format_bin_paths",
     "avdb_vcf_workspace_size", "avdb_vcf_count_lines", "avdb_vcf_parse_lines", "avdb_vcf_emit",
-    "avdb_vcf_count_text", "avdb_vcf_tokenize_workspace_size", "avdb_vcf_tokenize",
     "avdb_chrom_map_create", "avdb_chrom_map_destroy",
     "avdb_format_workspace_size", "avdb_vcf_format_size", "avdb_vcf_format_write", "avdb_vcf_line_host",
     "avdb_display_attributes",
@@ -101,7 +100,7 @@ EXPORTED_SYMBOLS = [
     "avdb_primary_keys_onepass_workspace_size", "avdb_primary_keys_onepass", "avdb_primary_keys_onepass_ex",
     "avdb_record_prep_keyed",
     "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
-    "avdb_small_prep", "avdb_small_prep_host", "avdb_bin_path_host", "avdb_host_alloc", "avdb_host_free",
+    "avdb_small_prep", "avdb_small_prep_host", "avdb_bin_path_host", "avdb_annotate_host", "avdb_host_alloc", "avdb_host_free",
     "avdb_rccl_unique_id", "avdb_rccl_comm_init", "avdb_rccl_comm_destroy",
     "avdb_hist_allgather_workspace_size", "avdb_hist_allgather",
 ]
@@ -174,10 +173,6 @@ def _sig(lib):
     f.avdb_chrom_map_create.argtypes = [P, P, P, SZ, P, ctypes.POINTER(P)]
     f.avdb_chrom_map_destroy.argtypes = [P]
     f.avdb_vcf_emit.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, P, P, P, P, P, P]
-    f.avdb_vcf_count_text.argtypes = [P, P, SZ, P, SZ, P, P]
-    f.avdb_vcf_tokenize_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
-    f.avdb_vcf_tokenize.argtypes = [P, P, SZ, P, SZ, SZ, P, P, P, SZ, P, P, P, P, P, P, P, P, SZ, P, P,
-                                    ctypes.POINTER(VcfOpts), P]
     f.avdb_format_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_vcf_format_size.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, ctypes.POINTER(FormatOpts),
                                        P, SZ, P, P, P, P]
@@ -200,6 +195,7 @@ def _sig(lib):
     f.avdb_small_prep.argtypes = [P, ctypes.POINTER(SmallBatch), P]
     f.avdb_small_prep_host.argtypes = [P, ctypes.POINTER(SmallBatch)]
     f.avdb_bin_path_host.argtypes = [P, U8, U32, U32, ctypes.POINTER(U32), ctypes.POINTER(U8), P, SZ]
+    f.avdb_annotate_host.argtypes = [P, ctypes.c_char_p, U32, U32, U32, I32, P, P, SZ]
     f.avdb_host_alloc.argtypes = [SZ, ctypes.POINTER(P)]
     f.avdb_host_free.argtypes = [P]
     f.avdb_shard_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
@@ -259,3 +255,26 @@ def require_gpu():
     if not torch.cuda.is_available():
         raise NativeUnavailable("no ROCm GPU visible (torch.cuda.is_available() is False); "
                                 "the avdb kernels run only on gfx950 — there is no CPU fallback")
+
+
+_host_ctx = None
+
+
+def host_ctx():
+    """A process-wide context for the library's per-call host entries (K8a
+    ``avdb_annotate_host`` and friends): made with device -1, so it needs no
+    GPU — those entries run the kernels' record arithmetic in the library's host
+    code and never launch.  Batch kernels take an ``Engine`` on a GPU."""
+    global _host_ctx
+    lib = load_library()
+    with _lock:
+        if _host_ctx is None:
+            from .chromosomes import length_table
+            lens = length_table("GRCh38")
+            arr = (ctypes.c_uint32 * len(lens))(*lens)
+            h = ctypes.c_void_p()
+            rc = lib.avdb_ctx_create(-1, arr, len(lens), ctypes.byref(h))
+            if rc < 0:
+                raise NativeError("avdb_ctx_create", rc, lib.avdb_last_error().decode(errors="replace"))
+            _host_ctx = h
+        return _host_ctx

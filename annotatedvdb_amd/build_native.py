@@ -32,6 +32,33 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+PERCALL_SRC = os.path.join(CSRC, "avdb_percall.c")
+
+
+def percall_path() -> str:
+    import sysconfig
+    return os.path.join(HERE, "avdb_percall" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_percall(force: bool = False, verbose: bool = True) -> str:
+    """The CPython binding of the per-call host entries (``avdb_percall``,
+    plain C against Python.h: it calls into libavdb_hip.so through the function
+    pointers ``_native`` hands it, so it links against nothing else)."""
+    import sysconfig
+    out = percall_path()
+    deps = [PERCALL_SRC, os.path.join(INCLUDE, "avdb.h")]
+    if not force and os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+        return out
+    cc = os.environ.get("CC") or shutil.which("gcc") or "cc"
+    cmd = [cc, "-O2", "-shared", "-fPIC", "-Wall", "-I", sysconfig.get_paths()["include"], "-I", INCLUDE,
+           PERCALL_SRC, "-o", out + ".tmp"]
+    if verbose:
+        print("[avdb] " + " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):
@@ -94,4 +121,5 @@ def build(force: bool = False, verbose: bool = True, out: str = None, flags=(), 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_percall(force="--force" in sys.argv)
     print(LIB)

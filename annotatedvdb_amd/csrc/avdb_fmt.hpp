@@ -601,6 +601,94 @@ AVDB_HD void variant_class_text(O& o, int cls, bool dup) {
   }
 }
 
+// The display class and coordinates of one record (variant_annotator.py:147-239):
+// the common prefix l (__normalize_alleles :100-107; SNVs untouched, :97-98),
+// cls 0 SNV, 1 inversion, 2 substitution, 3 indel, 4 indel (insertion downstream
+// of POS), 5 insertion / duplication, 6 deletion; dup: the 'dup' prefix.
+template <class CP>
+struct DisplayShape {
+  uint32_t l, ls, le;
+  int cls;
+  bool dup, snv;
+  Al<CP> nref, nalt, orig;
+};
+
+template <class CP>
+AVDB_HD DisplayShape<CP> display_shape(uint32_t pos, uint32_t end, CP ref, uint32_t r, CP alt, uint32_t a) {
+  DisplayShape<CP> d;
+  d.snv = r == 1u && a == 1u;
+  uint32_t l = 0;
+  if (!d.snv) {
+    const uint32_t m = r < a ? r : a;
+    while (l < m && ref[l] == alt[l]) ++l;
+  }
+  const uint32_t nr = r - l, na = a - l;
+  d.l = l;
+  d.nref = Al<CP>{ref + l, nr, l > 0 && nr == 0};
+  d.nalt = Al<CP>{alt + l, na, l > 0 && na == 0};
+  d.orig = Al<CP>{r ? ref + 1 : ref, r ? r - 1 : 0, false};
+  d.ls = pos;
+  d.le = pos;
+  d.dup = false;
+  if (d.snv) {
+    d.cls = 0;
+  } else if (r == a) {  // MNV (:171-189)
+    bool inv = true;
+    for (uint32_t i = 0; i < r && inv; ++i) inv = ref[i] == alt[r - 1 - i];
+    d.cls = inv ? 1 : 2;
+    d.le = end;
+  } else if (na >= 1) {  // insertion (:192-229)
+    d.ls = pos + 1;
+    // originalRef.count(normAlt) non-overlapping and len/count == len(normAlt)
+    // <=> originalRef == normAlt * k, k >= 1
+    if (d.orig.n > 0 && d.orig.n % na == 0) {
+      d.dup = true;
+      for (uint32_t i = 0, j = 0; i < d.orig.n && d.dup; ++i) {
+        d.dup = d.orig.p[i] == d.nalt.p[j];
+        if (++j == na) j = 0;
+      }
+    }
+    if (nr >= 1) { d.cls = 3; d.le = end; }
+    else if (end != pos + 1) { d.cls = 4; d.le = end; }
+    else { d.cls = 5; d.le = pos + 1; }
+  } else {  // deletion (:231-239)
+    d.cls = 6;
+    d.ls = pos + 1;
+    d.le = end;
+  }
+  return d;
+}
+
+// the 'display_allele' value of a display shape (:167-237)
+template <bool ESC, class O, class CP>
+AVDB_HD void display_allele_text(O& o, const DisplayShape<CP>& d, CP ref, uint32_t r, CP alt, uint32_t a) {
+  const uint64_t pre = d.dup ? 0x707564ull : 0x736E69ull;  // "dup" / "ins"
+  const Al<CP> raw_ref{ref, r, false}, raw_alt{alt, a, false};
+  switch (d.cls) {
+    case 0: al_str<ESC>(o, raw_ref); o.put('>'); al_str<ESC>(o, raw_alt); break;
+    case 1: o.lit("inv"); al_str<ESC>(o, raw_ref); break;
+    case 2: al_str<ESC>(o, d.nref); o.put('>'); al_str<ESC>(o, d.nalt); break;
+    case 3: o.lit("del"); al_trunc<ESC>(o, d.nref, 100); o.append(pre, 3); al_trunc<ESC>(o, d.nalt, 100); break;
+    case 4: o.lit("del"); al_trunc<ESC>(o, d.orig, 100); o.append(pre, 3); al_trunc<ESC>(o, d.nalt, 100); break;
+    case 5: o.append(pre, 3); al_trunc<ESC>(o, d.nalt, 100); break;
+    default: o.lit("del"); al_trunc<ESC>(o, d.nref, 100); break;
+  }
+}
+
+// the 'sequence_allele' value of a display shape (:168-238)
+template <bool ESC, class O, class CP>
+AVDB_HD void sequence_allele_text(O& o, const DisplayShape<CP>& d, CP ref, uint32_t r, CP alt, uint32_t a) {
+  const uint64_t pre = d.dup ? 0x707564ull : 0x736E69ull;
+  const Al<CP> raw_ref{ref, r, false}, raw_alt{alt, a, false};
+  switch (d.cls) {
+    case 0: al_str<ESC>(o, raw_ref); o.put('/'); al_str<ESC>(o, raw_alt); break;
+    case 1: al_trunc<ESC>(o, raw_ref, 8); o.put('/'); al_trunc<ESC>(o, raw_alt, 8); break;
+    case 5: o.append(pre, 3); al_trunc<ESC>(o, d.nalt, 8); break;
+    case 6: al_trunc<ESC>(o, d.nref, 8); o.lit("/-"); break;
+    default: al_trunc<ESC>(o, d.nref, 8); o.put('/'); al_trunc<ESC>(o, d.nalt, 8); break;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // get_display_attributes (variant_annotator.py:134-241) as json.dumps text.
 // Keys in the reference's dict insertion order: location_start, location_end,
@@ -612,86 +700,33 @@ AVDB_HD void variant_class_text(O& o, int cls, bool dup) {
 template <bool ESC, class O, class CP>
 AVDB_HD O display_json(O o, uint32_t chrom, uint32_t pos, uint32_t end, CP ref, uint32_t r,
                                        CP alt, uint32_t a, Dec posd = Dec{0, 0, 0}) {
-  const bool snv = r == 1u && a == 1u;
-  uint32_t l = 0;  // common prefix (__normalize_alleles :100-107); SNVs untouched (:97-98)
-  if (!snv) {
-    const uint32_t m = r < a ? r : a;
-    while (l < m && ref[l] == alt[l]) ++l;
-  }
-  const uint32_t nr = r - l, na = a - l;
-  const Al<CP> nref{ref + l, nr, l > 0 && nr == 0}, nalt{alt + l, na, l > 0 && na == 0};
-  uint32_t ls = pos, le = pos;
-  int cls;  // 0 SNV, 1 inversion, 2 substitution, 3 indel, 4 indel (ins downstream), 5 ins/dup, 6 deletion
-  bool dup = false;
-  const Al<CP> orig{r ? ref + 1 : ref, r ? r - 1 : 0, false};
-  if (snv) {
-    cls = 0;
-  } else if (r == a) {  // MNV (:171-189)
-    bool inv = true;
-    for (uint32_t i = 0; i < r && inv; ++i) inv = ref[i] == alt[r - 1 - i];
-    cls = inv ? 1 : 2;
-    le = end;
-  } else if (na >= 1) {  // insertion (:192-229)
-    ls = pos + 1;
-    // originalRef.count(normAlt) non-overlapping and len/count == len(normAlt)
-    // <=> originalRef == normAlt * k, k >= 1
-    if (orig.n > 0 && orig.n % na == 0) {
-      dup = true;
-      for (uint32_t i = 0, j = 0; i < orig.n && dup; ++i) {
-        dup = orig.p[i] == nalt.p[j];
-        if (++j == na) j = 0;
-      }
-    }
-    if (nr >= 1) { cls = 3; le = end; }
-    else if (end != pos + 1) { cls = 4; le = end; }
-    else { cls = 5; le = pos + 1; }
-  } else {  // deletion (:231-239)
-    cls = 6;
-    ls = pos + 1;
-    le = end;
-  }
+  const DisplayShape<CP> d = display_shape(pos, end, ref, r, alt, a);
   o.lit("{\"location_start\": ");
-  if (posd.n && ls == pos) o.dec(posd);  // posd: POS as text, when the caller has it
-  else o.u32v(ls);
+  if (posd.n && d.ls == pos) o.dec(posd);  // posd: POS as text, when the caller has it
+  else o.u32v(d.ls);
   o.lit(", \"location_end\": ");
-  if (posd.n && le == pos) o.dec(posd);
-  else o.u32v(le);
-  if (!snv && l > 0) {  // normalized id differs from the metaseq id iff a prefix was trimmed
+  if (posd.n && d.le == pos) o.dec(posd);
+  else o.u32v(d.le);
+  if (!d.snv && d.l > 0) {  // normalized id differs from the metaseq id iff a prefix was trimmed
     o.lit(", \"normalized_metaseq_id\": \"");
     if (chrom < 25) chrom_name(o, chrom);
     o.put(':');
     if (posd.n) o.dec(posd);
     else o.u32v(pos);
     o.put(':');
-    al_str<ESC>(o, nref);
+    al_str<ESC>(o, d.nref);
     o.put(':');
-    al_str<ESC>(o, nalt);
+    al_str<ESC>(o, d.nalt);
     o.put('"');
   }
-  const bool order_b = cls >= 3 && cls <= 5;
-  if (!order_b) variant_class_text(o, cls, dup);
-  const uint64_t pre = dup ? 0x707564ull : 0x736E69ull;  // "dup" / "ins"
-  const Al<CP> raw_ref{ref, r, false}, raw_alt{alt, a, false};
+  const bool order_b = d.cls >= 3 && d.cls <= 5;
+  if (!order_b) variant_class_text(o, d.cls, d.dup);
   o.lit(", \"display_allele\": \"");
-  switch (cls) {
-    case 0: al_str<ESC>(o, raw_ref); o.put('>'); al_str<ESC>(o, raw_alt); break;
-    case 1: o.lit("inv"); al_str<ESC>(o, raw_ref); break;
-    case 2: al_str<ESC>(o, nref); o.put('>'); al_str<ESC>(o, nalt); break;
-    case 3: o.lit("del"); al_trunc<ESC>(o, nref, 100); o.append(pre, 3); al_trunc<ESC>(o, nalt, 100); break;
-    case 4: o.lit("del"); al_trunc<ESC>(o, orig, 100); o.append(pre, 3); al_trunc<ESC>(o, nalt, 100); break;
-    case 5: o.append(pre, 3); al_trunc<ESC>(o, nalt, 100); break;
-    default: o.lit("del"); al_trunc<ESC>(o, nref, 100); break;
-  }
+  display_allele_text<ESC>(o, d, ref, r, alt, a);
   o.lit("\", \"sequence_allele\": \"");
-  switch (cls) {
-    case 0: al_str<ESC>(o, raw_ref); o.put('/'); al_str<ESC>(o, raw_alt); break;
-    case 1: al_trunc<ESC>(o, raw_ref, 8); o.put('/'); al_trunc<ESC>(o, raw_alt, 8); break;
-    case 5: o.append(pre, 3); al_trunc<ESC>(o, nalt, 8); break;
-    case 6: al_trunc<ESC>(o, nref, 8); o.lit("/-"); break;
-    default: al_trunc<ESC>(o, nref, 8); o.put('/'); al_trunc<ESC>(o, nalt, 8); break;
-  }
+  sequence_allele_text<ESC>(o, d, ref, r, alt, a);
   o.put('"');
-  if (order_b) variant_class_text(o, cls, dup);
+  if (order_b) variant_class_text(o, d.cls, d.dup);
   o.put('}');
   return o;
 }

@@ -353,3 +353,54 @@ extern "C" int avdb_bin_path_host(const avdb_ctx* ctx, uint8_t chrom, uint32_t s
   bin_path(HostOut(reinterpret_cast<uint8_t*>(out), 0), chrom, cd);
   return int(len);
 }
+
+// K8a: one VariantAnnotator (variant_annotator.py:21-241) on the host — the
+// drop-in class the reference constructs per alt allele (vcf_parser.py:225-231).
+// infer_end (K2) and display_shape / display_allele_text / sequence_allele_text
+// (K5a) are the kernels' AVDB_HD definitions; the end is returned relative to the
+// position (infer_end at pos 0, as int32), so the caller's integer position is
+// never narrowed.
+extern "C" int avdb_annotate_host(const avdb_ctx* ctx, const uint8_t* alleles, uint32_t r, uint32_t a,
+                                  uint32_t pos, int want_display, avdb_annotation* out, char* text, size_t cap) {
+  if (!ctx || !out || (!alleles && uint64_t(r) + a) || (!text && cap)) {
+    avdb_set_error("avdb_annotate_host: null argument");
+    return AVDB_EINVAL;
+  }
+  const uint64_t n = uint64_t(r) + a;
+  const Heap hp = make_heap(alleles, size_t(n));
+  const bool snv = r == 1u && a == 1u;
+  uint32_t lcp;
+  const uint32_t rel = infer_end(hp, 0, r, a, 0u, snv ? 0 : heap_u64(hp, 0), snv ? 0 : heap_u64(hp, r), &lcp);
+  memset(out, 0, sizeof(*out));
+  out->end_rel = int32_t(rel);
+  out->lcp = lcp;
+  out->state = 2;
+  if (!want_display) return AVDB_OK;
+  // display coordinates pos, pos + 1 and the end stay in u32 (VCF positions do);
+  // a non-ASCII allele is outside the byte-level contract
+  if (!host_ascii(alleles, uint32_t(n)) || uint64_t(pos) + n + 2 > 0xFFFFFFFFull ||
+      int64_t(pos) + int32_t(rel) < 0) {
+    out->state = 1;
+    return AVDB_OK;
+  }
+  const uint8_t* alt = alleles + r;
+  const DisplayShape<const uint8_t*> d = display_shape(pos, pos + rel, alleles, r, alt, a);
+  out->location_start = d.ls;
+  out->location_end = d.le;
+  out->variant_class = d.cls == 5 ? (d.dup ? AVDB_VC_DUPLICATION : AVDB_VC_INSERTION)
+                                  : (d.cls == 6 ? AVDB_VC_DELETION : uint32_t(d.cls));
+  HostOut c0(nullptr, 0), c1(nullptr, 0);
+  display_allele_text<false>(c0, d, alleles, r, alt, a);
+  sequence_allele_text<false>(c1, d, alleles, r, alt, a);
+  out->display_bytes = c0.size();
+  out->sequence_bytes = c1.size();
+  if (uint64_t(c0.size()) + c1.size() > cap) {
+    avdb_set_error("avdb_annotate_host: %u bytes needed", c0.size() + c1.size());
+    return AVDB_ERANGE;
+  }
+  HostOut w0(reinterpret_cast<uint8_t*>(text), 0), w1(reinterpret_cast<uint8_t*>(text), c0.size());
+  display_allele_text<false>(w0, d, alleles, r, alt, a);
+  sequence_allele_text<false>(w1, d, alleles, r, alt, a);
+  out->state = 0;
+  return AVDB_OK;
+}

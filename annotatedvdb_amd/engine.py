@@ -150,6 +150,27 @@ VCF_ID_HOST = 0x200
 VCF_HOST_FLAGS = VCF_BAD_POS | VCF_EXT_HOST | VCF_CHROM_HOST | VCF_ID_HOST
 
 
+def _stamp(*ts) -> tuple:
+    """Identity + version of each tensor: what a keyed K2 hand-off is tied to.
+    A weak reference (a freed tensor whose block the caching allocator hands to a
+    new tensor at the same address does not match) and ``_version`` (an in-place
+    edit of the batch between the producer and the consumer does not match)."""
+    import weakref
+    return tuple(None if t is None else (weakref.ref(t), t._version) for t in ts)
+
+
+def _stamp_ok(stamp: tuple, *ts) -> bool:
+    if stamp is None or len(stamp) != len(ts):
+        return False
+    for st, t in zip(stamp, ts):
+        if st is None or t is None:
+            if st is not None or t is not None:
+                return False
+        elif st[0]() is not t or t._version != st[1]:
+            return False
+    return True
+
+
 @dataclass
 class VcfBatch:
     """Output of ``Engine.vcf_tokenize``: device text, per-line table, records."""
@@ -210,10 +231,6 @@ class KeyText:
     state: torch.Tensor
     keys: Optional[torch.Tensor]
     paths: Optional[torch.Tensor]
-    # (n, max_seq_len, has_digest, with_paths, the batch's array addresses) of the
-    # group totals a keyed record_prep left in ``ws`` for the next primary_keys
-    # call on the same batch, or None
-    totals_for: Optional[tuple] = None
 
     def host(self, n: int):
         """(keys, paths) as Python lists of str (None where not rendered).
@@ -281,14 +298,19 @@ class SmallPrep:
         self._text0 = [offs["text%d" % k] for k in range(3)]
 
     def _alloc(self, total: int) -> int:
-        """The arena: pinned host memory mapped into the device (avdb_host_alloc)."""
+        """The arena: pinned host memory mapped into the device (avdb_host_alloc);
+        plain host memory for a host-only engine (K8h never reads it from a kernel)."""
+        if self.eng.host_only:
+            self._host_arena = np.zeros(total + 64, dtype=np.uint8)
+            return (self._host_arena.ctypes.data + 63) & ~63
         p = ctypes.c_void_p()
         N.check("avdb_host_alloc", self.eng.lib.avdb_host_alloc(total, ctypes.byref(p)))
         return p.value
 
     def close(self):
         if getattr(self, "_ptr", None):
-            self.eng.lib.avdb_host_free(self._ptr)
+            if not self.eng.host_only:
+                self.eng.lib.avdb_host_free(self._ptr)
             self._ptr = None
 
     def __del__(self):
@@ -392,7 +414,7 @@ class SmallPrep:
         else:
             s_in.pack_into(mv, 0, *chrom, *pos, *ends)
         b.max_seq_len, b.want = int(max_seq_len), int(want)
-        on_host = self.mode == "host" or (self.mode == "auto" and n <= self.host_max)
+        on_host = self.mode == "host" or (self.mode == "auto" and n <= self.host_max) or self.eng.host_only
         if on_host:
             N.check("avdb_small_prep_host", self.eng.lib.avdb_small_prep_host(self.eng.ctx, ctypes.byref(b)))
         else:
@@ -520,25 +542,39 @@ class Engine:
 
     def __init__(self, device=None, lengths: Optional[Sequence[int]] = None, assembly: str = "GRCh38",
                  sequence_digests: Optional[Sequence[str]] = None):
-        N.require_gpu()
+        if device is None and os.environ.get("AVDB_DEVICE") == "host":
+            device = "host"
+        # "host": a host-only engine — only the library's per-call host entries
+        # (K5h, K8h, K1h: the kernels' record arithmetic compiled for the host side)
+        # work; every kernel entry raises NativeUnavailable.  Opt-in only
+        # (device="host" or AVDB_DEVICE=host), never a silent fallback.
+        self.host_only = device == "host"
+        if not self.host_only:
+            N.require_gpu()
         self.lib = N.load_library()
-        if device is None:
-            device = torch.cuda.current_device()
-        self.device = torch.device("cuda", int(device) if not isinstance(device, torch.device)
-                                   else (device.index or 0))
+        if self.host_only:
+            self.device = torch.device("cpu")
+        else:
+            if device is None:
+                device = torch.cuda.current_device()
+            self.device = torch.device("cuda", int(device) if not isinstance(device, torch.device)
+                                       else (device.index or 0))
         self.lengths = list(lengths) if lengths is not None else length_table(assembly)
         arr = (ctypes.c_uint32 * len(self.lengths))(*self.lengths)
         h = ctypes.c_void_p()
-        N.check("avdb_ctx_create", self.lib.avdb_ctx_create(self.device.index, arr, len(self.lengths),
-                                                            ctypes.byref(h)))
+        N.check("avdb_ctx_create", self.lib.avdb_ctx_create(-1 if self.host_only else self.device.index, arr,
+                                                            len(self.lengths), ctypes.byref(h)))
         self._ctx = h
         nb = ctypes.c_uint32()
         self.lib.avdb_l8_bin_count(self._ctx, ctypes.byref(nb))
         self.n_l8 = int(nb.value)
-        # K4 workspaces the keyed K2 classified a batch into: data_ptr -> (n, max_seq_len, length arrays)
-        self._codes_for: Dict[int, tuple] = {}
-        # K3 workspaces the keyed K2 ran the mark phase into: data_ptr -> ((n, chrom, pos), keep)
-        self._marks_for: Dict[int, tuple] = {}
+        # what the last keyed K2 left for its consumers, each entry tied (by _stamp)
+        # to the exact tensors it was computed from and taken by the one call it
+        # was meant for: "totals" (K7's group totals in a KeyText's workspace),
+        # "codes" (K4's long-record codes in a digest workspace), "marks" (K3's
+        # first phase in a dedup workspace + keep).  Every record_prep call drops
+        # all of them first.
+        self._pending: Dict[str, tuple] = {}
         if sequence_digests is not None:
             self.set_sequence_digests(sequence_digests)
 
@@ -564,6 +600,9 @@ class Engine:
         return self._ctx
 
     def _stream(self):
+        if self.host_only:
+            raise N.NativeUnavailable("a host-only engine (AVDB_DEVICE=host) runs the per-call host entries only; "
+                                      "this batch entry is a gfx950 kernel and needs a GPU")
         return N.stream_handle(self.device)
 
     def small(self) -> SmallPrep:
@@ -658,6 +697,7 @@ class Engine:
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
+        self._pending.clear()
         end = self.empty(n, torch.int32)
         code = self.empty(n, torch.int32)
         status = self.empty(n, torch.uint8)
@@ -668,10 +708,8 @@ class Engine:
         if keys is None:
             N.check("avdb_record_prep", self.lib.avdb_record_prep(*args, self._stream()))
             return end, code, status, lcp
-        keys.totals_for = None
         dws = digest_workspace
         if dws is not None:
-            self._codes_for.pop(dws.data_ptr(), None)
             sz = ctypes.c_size_t()
             self.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
             if dws.numel() < sz.value:
@@ -679,21 +717,22 @@ class Engine:
         ddw = dedup_workspace
         keep = None
         if ddw is not None:
-            self._marks_for.pop(ddw.data_ptr(), None)
             keep = self.empty(max(4, n), torch.uint8)
         done = ctypes.c_int(0)
         N.check("avdb_record_prep_keyed", self.lib.avdb_record_prep_keyed(
             *args, N.ptr(b.ext_id), int(max_seq_len), 1 if key_digest else 0, 1 if key_paths else 0,
             N.ptr(keys.ws), keys.ws.numel(), N.ptr(dws), dws.numel() if dws is not None else 0,
             N.ptr(ddw), ddw.numel() if ddw is not None else 0, N.ptr(keep), ctypes.byref(done), self._stream()))
-        # (tied to this batch's arrays: another batch of the same size recomputes)
+        # (tied to these exact tensors: another batch, a reallocated one or an
+        # in-place edit recomputes)
         if done.value & N.KEYED_TOTALS:
-            keys.totals_for = (n, int(max_seq_len), bool(key_digest), bool(key_paths), b.chrom.data_ptr(),
-                               b.pos.data_ptr(), b.ref_len.data_ptr(), b.alt_len.data_ptr(), b.ext_id.data_ptr())
+            self._pending["totals"] = (_stamp(keys.ws, b.chrom, b.pos, b.ref_len, b.alt_len, b.ext_id,
+                                              code if key_paths else None),
+                                       keys, n, int(max_seq_len), bool(key_digest))
         if done.value & N.KEYED_LONG_CODES:
-            self._codes_for[dws.data_ptr()] = (n, int(max_seq_len), b.ref_len.data_ptr(), b.alt_len.data_ptr())
+            self._pending["codes"] = (_stamp(dws, b.ref_len, b.alt_len), n, int(max_seq_len))
         if done.value & N.KEYED_DEDUP_MARKS:
-            self._marks_for[ddw.data_ptr()] = ((n, b.chrom.data_ptr(), b.pos.data_ptr()), keep)
+            self._pending["marks"] = (_stamp(ddw, b.chrom, b.pos), n, keep)
         return end, code, status, lcp
 
     # -- K3 ----------------------------------------------------------------
@@ -703,10 +742,11 @@ class Engine:
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
-        marks = self._marks_for.pop(workspace.data_ptr(), None) if workspace is not None else None
-        if grouped and marks is not None and marks[0] == (n, b.chrom.data_ptr(), b.pos.data_ptr()):
+        marks = self._pending.pop("marks", None)
+        if (grouped and workspace is not None and marks is not None and marks[1] == n
+                and _stamp_ok(marks[0], workspace, b.chrom, b.pos)):
             # the keyed K2 already wrote keep = 1 and listed the runs: resolve them
-            keep = marks[1]
+            keep = marks[2]
             N.check("avdb_pk_dedup_ex", self.lib.avdb_pk_dedup_ex(
                 self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
                 N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), n, N.ptr(workspace),
@@ -747,8 +787,9 @@ class Engine:
         ws = workspace if workspace is not None and workspace.numel() >= sz.value else \
             self.empty(int(sz.value), torch.uint8)
         # the keyed K2 classified this batch's records into this workspace
-        ready = self._codes_for.pop(ws.data_ptr(), None) == (n, int(max_seq_len), b.ref_len.data_ptr(),
-                                                              b.alt_len.data_ptr())
+        codes = self._pending.pop("codes", None)
+        ready = (codes is not None and codes[1:] == (n, int(max_seq_len))
+                 and _stamp_ok(codes[0], ws, b.ref_len, b.alt_len))
         N.check("avdb_vrs_digest_ex", self.lib.avdb_vrs_digest_ex(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
             N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, int(max_seq_len), N.ptr(ws), int(sz.value),
@@ -773,17 +814,10 @@ class Engine:
         return [raw[i * 32:(i + 1) * 32].decode("ascii") for i in range(n)]
 
     # -- K0: VCF text -> records ---------------------------------------------
-    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None, *,
-                     fused: Optional[bool] = None) -> "VcfBatch":
+    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None) -> "VcfBatch":
         """Parse VCF data lines (bytes or a uint8 tensor) on the GPU into the
         record SoA (one row per ALT != '.') plus the per-line table.
-        ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map.
-        ``fused`` (default): count pass + the one-pass tokenizer
-        (``avdb_vcf_tokenize``); False: the four-kernel path (count, parse with
-        line starts, scans, emit) — the same outputs; None: env AVDB_VCF_FUSED
-        (default 0 until the one-pass path is validated on the GPU)."""
-        if fused is None:
-            fused = os.environ.get("AVDB_VCF_FUSED", "0") != "0"
+        ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map."""
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
             t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
@@ -796,8 +830,6 @@ class Engine:
             last_nl = bool(text_t.numel() == 0 or int(text_t[-1].item()) == 10)
         nb = int(text_t.numel())
         tp = N.ptr(text_t) if nb else None
-        if fused:
-            return self._vcf_tokenize_onepass(text_t, nb, tp, last_nl, vcf_opts)
         s = self._stream()
         ws0 = self.empty(N.VCF_COUNT_WORKSPACE_BYTES, torch.uint8)
         nl = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -833,72 +865,6 @@ class Engine:
                 N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s))
         return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
                         records=b, rec_line=rec_line, rec_alt=rec_alt)
-
-    def _vcf_tokenize_onepass(self, text_t, nb: int, tp, last_nl: bool, vcf_opts) -> "VcfBatch":
-        """Count pass ('\\n' and ',' bytes: the line count and a bound on the
-        records), one host read, then ``avdb_vcf_tokenize`` (text read once) and
-        one host read of its totals.  The allele heap is sized by an estimate
-        (text bytes + 4 KB); a batch whose heap is larger runs the pass again
-        with the exact size."""
-        s = self._stream()
-        ws0 = self.empty(N.VCF_COUNT_WORKSPACE_BYTES, torch.uint8)
-        cnt = self.empty(2, torch.int64)
-        N.check("avdb_vcf_count_text", self.lib.avdb_vcf_count_text(
-            self.ctx, tp, nb, N.ptr(ws0), ws0.numel(), N.ptr(cnt), s))
-        n_nl, n_comma = (int(x) for x in cnt.cpu().tolist())
-        n_lines = n_nl + (0 if (last_nl or nb == 0) else 1)
-        rec_cap = n_lines + n_comma
-        heap_cap = nb + 4096
-        sz = ctypes.c_size_t()
-        self.lib.avdb_vcf_tokenize_workspace_size(nb, ctypes.byref(sz))
-        ws = self.empty(max(256, int(sz.value)), torch.uint8)
-        lines = self.empty(max(1, n_lines) * VCF_LINE_DTYPE.itemsize, torch.uint8)
-        rec_off = self.empty(n_lines + 1, torch.int64)
-        heap_off = self.empty(n_lines + 1, torch.int64)
-        tot = self.empty(4, torch.int64)
-        rc = max(1, rec_cap)
-        chrom, pos = self.empty(rc, torch.uint8), self.empty(rc, torch.int32)
-        allele_off, ref_len, alt_len = self.empty(rc, torch.int64), self.empty(rc, torch.int32), \
-            self.empty(rc, torch.int32)
-        ext_id, rec_line, rec_alt = self.empty(rc, torch.int64), self.empty(rc, torch.int32), \
-            self.empty(rc, torch.int32)
-        opts = ctypes.byref(vcf_opts) if vcf_opts is not None else None
-        while True:
-            heap = self.empty(max(1, heap_cap), torch.uint8)
-            N.check("avdb_vcf_tokenize", self.lib.avdb_vcf_tokenize(
-                self.ctx, tp, nb, N.ptr(ws), ws.numel(), n_lines, N.ptr(lines), N.ptr(rec_off), N.ptr(heap_off),
-                rec_cap, N.ptr(chrom), N.ptr(pos), N.ptr(allele_off), N.ptr(ref_len), N.ptr(alt_len),
-                N.ptr(ext_id), N.ptr(rec_line), N.ptr(rec_alt), heap_cap, N.ptr(heap), N.ptr(tot), opts, s))
-            self._tok_ws = ws  # (diagnostics: tools/k0_onepass_probe.py reads the per-chunk clocks)
-            t_lines, n_rec, n_heap, lb_err = (int(x) for x in tot.cpu().tolist())
-            if lb_err:
-                nc = -(-nb // 16384)
-                stuck = [x & ((1 << 64) - 1) for x in ws[64:128].view(torch.int64).cpu().tolist()]
-                t0 = 256 + 8 * nc + 48 * nc
-                trace = ws[t0:t0 + 4 * nc].view(torch.int32).cpu().numpy()
-                c0 = t0 + 4 * ((nc + 1) & ~1)
-                clk = ws[c0:c0 + 16 * nc].view(torch.int64).cpu().numpy().reshape(nc, 2)
-                phases = {int(k): int(v) for k, v in zip(*np.unique(trace, return_counts=True))}
-                c, j = int(stuck[0]), int(stuck[1])
-                rel = lambda t: (int(t) - int(clk[0, 1])) / 100.0  # us (100 MHz) after chunk 0's prefix
-                raise N.NativeError("avdb_vcf_tokenize", -1,
-                                    f"{lb_err} look-back waits gave up (outputs invalid); first: chunk {c} "
-                                    f"waited on {j} (status now {stuck[2]:#x}, phase {stuck[3]}; loop last read "
-                                    f"{stuck[4]:#x} from chunk {stuck[5]}, not-ready lanes {stuck[6]:#x}); gave up at "
-                                    f"{rel(stuck[7])} us, chunk {j} published agg at {rel(clk[j, 0])} us, prefix at "
-                                    f"{rel(clk[j, 1])} us, chunk {c} agg at {rel(clk[c, 0])} us; "
-                                    f"{nc} chunks by last phase {phases}")
-            if t_lines != n_lines or n_rec > rec_cap:  # the count pass bounds both: never expected
-                raise N.NativeError("avdb_vcf_tokenize", -1,
-                                    f"lines {t_lines} (counted {n_lines}), records {n_rec} (bound {rec_cap})")
-            if n_heap <= heap_cap:
-                break
-            heap_cap = n_heap
-        b = RecordBatch(chrom=chrom[:n_rec], pos=pos[:n_rec], allele_off=allele_off[:n_rec],
-                        ref_len=ref_len[:n_rec], alt_len=alt_len[:n_rec], heap=heap[:max(1, n_heap)],
-                        ext_id=ext_id[:n_rec])
-        return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
-                        records=b, rec_line=rec_line[:n_rec], rec_alt=rec_alt[:n_rec])
 
     # -- K9: this rank's lines of a VCF text -----------------------------------
     def vcf_select(self, vb: "VcfBatch", assignment, rank: int, cut: int = 64_000_000) -> torch.Tensor:
@@ -1055,11 +1021,11 @@ class Engine:
             raise ValueError("primary_keys: the reused KeyText holds fewer records (or no paths)")
         if out.ws.numel() < sz.value:
             out.ws = self.empty(int(sz.value), torch.uint8)
-            out.totals_for = None
-        ready = out.totals_for == (n, int(max_seq_len), digest is not None, code is not None, b.chrom.data_ptr(),
-                                   b.pos.data_ptr(), b.ref_len.data_ptr(), b.alt_len.data_ptr(),
-                                   b.ext_id.data_ptr())
-        out.totals_for = None
+        # the keyed K2 wrote this batch's group totals into this KeyText's workspace
+        # (sizes from these length / id arrays and, for the paths, these bin codes)
+        tot = self._pending.pop("totals", None)
+        ready = (tot is not None and tot[1] is out and tot[2:] == (n, int(max_seq_len), digest is not None)
+                 and _stamp_ok(tot[0], out.ws, b.chrom, b.pos, b.ref_len, b.alt_len, b.ext_id, code))
         N.check("avdb_primary_keys_onepass_ex", self.lib.avdb_primary_keys_onepass_ex(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
             N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), N.ptr(code), N.ptr(digest), n, int(max_seq_len),
@@ -1153,7 +1119,15 @@ _ENGINES: Dict[int, Engine] = {}
 
 
 def default_engine(device=None) -> Engine:
-    """Process-wide engine per device (GRCh38 table)."""
+    """Process-wide engine per device (GRCh38 table); ``AVDB_DEVICE=host`` (with no
+    device given) selects the host-only engine of the per-call entries."""
+    if device is None and os.environ.get("AVDB_DEVICE") == "host":
+        device = "host"
+    if device == "host":
+        eng = _ENGINES.get("host")
+        if eng is None:
+            eng = _ENGINES["host"] = Engine("host")
+        return eng
     N.require_gpu()
     idx = torch.cuda.current_device() if device is None else int(device)
     eng = _ENGINES.get(idx)

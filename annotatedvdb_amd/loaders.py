@@ -24,9 +24,15 @@ when a key cannot be built (e.g. ``':'`` inside an allele breaks
 ``metaseqId.split(':')``, primary_key_generator.py:106, through the retry
 ladder :234-256), ``TypeError`` when the location has no bin
 (bin_index.py:75).  ``--skipExisting`` checks a key set of the rows already
-loaded (``existing.ExistingVariants``, K6) instead of the database; the other
-database-backed features (``update_existing``, COPY into Postgres) are outside
-the bin/key path and raise ``NotImplementedError``.  The ADSP datasource checks
+loaded (``existing.ExistingVariants``, K6) instead of the database.  The
+loader's database hand-offs keep the reference's surface: ``set_cursor`` /
+``load_variants`` give the COPY buffer to the caller's cursor exactly as
+variant_loader.py:395-405,479-486 do (``copy_expert(copy_sql, buffer, 2**10)``,
+then a fresh buffer), ``update_variants`` hands the update buffer over as
+:457-476 do, and ``set_algorithm_invocation`` takes the AlgorithmInvocation id
+from a provider the caller installs (``set_algorithm_invocation_provider``) in
+place of the row insert (:431-437).  ``update_existing`` (rewriting loaded rows)
+stays out of scope and raises ``NotImplementedError``.  The ADSP datasource checks
 every alt's primary key against the rows already loaded (``is_duplicate(recordPK)``,
 vcf_variant_loader.py:303-307) through the same exported key set (K7 keys, K6
 text probe): a loaded key becomes an ``is_adsp_variant`` update in
@@ -58,6 +64,40 @@ ALLOWABLE_COPY_FIELDS = ["chromosome", "record_primary_key", "position", "is_mul
 
 class _AltError(Exception):
     pass
+
+
+_ALG_INVOCATION_PROVIDER = None
+
+
+def set_algorithm_invocation_provider(provider):
+    """Install ``provider(callingScript, comment, commit) -> id``, the stand-in for
+    the AlgorithmInvocation row insert ``VCFVariantLoader.set_algorithm_invocation``
+    makes in the reference (variant_loader.py:431-437, algorithm_invocation.py:28-47).
+    ``None`` removes it."""
+    global _ALG_INVOCATION_PROVIDER
+    _ALG_INVOCATION_PROVIDER = provider
+
+
+def _execute_values(cur, sql, argslist, template=None, page_size=100):
+    """psycopg2.extras.execute_values (what variant_loader.py:471 calls): the
+    ``VALUES %s`` placeholder expanded to one page of mogrified rows per
+    ``execute``.  Uses psycopg2's own when it is importable."""
+    try:
+        from psycopg2.extras import execute_values
+    except ImportError:
+        execute_values = None
+    if execute_values is not None:
+        return execute_values(cur, sql, argslist, template=template, page_size=page_size)
+    pre, post = sql.split("%s", 1) if isinstance(sql, str) else sql.split(b"%s", 1)
+    rows = list(argslist)
+    for lo in range(0, len(rows), page_size):
+        page = rows[lo:lo + page_size]
+        parts = []
+        for row in page:
+            t = template or "(" + ",".join(["%s"] * len(row)) + ")"
+            v = cur.mogrify(t, row)
+            parts.append(v.decode() if isinstance(v, bytes) else v)
+        cur.execute(pre + ",".join(parts) + post)
 
 
 _SLOW = object()  # parse_variant: the line needs the general path
@@ -94,7 +134,12 @@ class VCFVariantLoader(object):
         self.last_load_stats = None
         self._match = None
         self._adsp_dup = None
+        self._cursor = None
+        self._batch_update = False
+        self._update_sql = None
         self._update_buffer = []
+        self._fail_at_variant = None
+        self._log_skips = False
         self._initialize_counters()
         self.initialize_copy_buffer()
         self.logger.info(type(self).__name__ + " initialized")
@@ -128,8 +173,19 @@ class VCFVariantLoader(object):
         self._alg_invocation_id = _xstr(alg_id)
 
     def set_algorithm_invocation(self, callingScript, comment, commit=True):
-        raise NotImplementedError("AlgorithmInvocation rows live in the database (out of scope); "
-                                  "use set_algorithm_invocation_id()")
+        """variant_loader.py:431-437.  The reference inserts an
+        AnnotatedVDB.AlgorithmInvocation row through its own database connection
+        (algorithm_invocation.py:28-47) and keeps the returned id; here the id
+        comes from the provider installed with
+        :func:`set_algorithm_invocation_provider` (called with the same three
+        arguments), e.g. one that runs that INSERT ... RETURNING on the caller's
+        connection.  Without a provider: NotImplementedError (no database here)."""
+        provider = _ALG_INVOCATION_PROVIDER
+        if provider is None:
+            raise NotImplementedError("AlgorithmInvocation rows live in the database: install a provider with "
+                                      "annotatedvdb_amd.loaders.set_algorithm_invocation_provider(fn), or call "
+                                      "set_algorithm_invocation_id()")
+        self._alg_invocation_id = _xstr(provider(callingScript, comment, commit))
 
     def alg_invocation_id(self):
         return self._alg_invocation_id
@@ -276,23 +332,91 @@ class VCFVariantLoader(object):
     def add_copy_str(self, copyStr):
         self._copy_buffer.write(copyStr + "\n")
 
+    # ---- database hand-offs (variant_loader.py:395-405,457-486) --------------
+    def cursor(self):
+        return self._cursor
+
+    def set_cursor(self, cursor):
+        """The caller's database cursor (psycopg2 or anything with its
+        ``copy_expert`` / ``execute`` / ``mogrify``)."""
+        self._cursor = cursor
+
     def load_variants(self):
-        raise NotImplementedError("COPY into Postgres is out of scope; read copy_buffer()")
+        """COPY the buffered rows (variant_loader.py:479-486): the buffer goes to
+        the caller's cursor as ``copy_expert(copy_sql, buffer, 2**10)``, then a
+        fresh buffer starts.  Errors propagate (the reference passes them through
+        raise_pg_exception, which re-raises)."""
+        self._copy_buffer.seek(0)
+        self._cursor.copy_expert(self._copy_sql, self._copy_buffer, 2 ** 10)
+        self.reset_copy_buffer()
+
+    def get_copy_fileds(self):
+        return self._copy_fields
+
+    def set_update_sql(self, sql):
+        self._update_sql = sql
+
+    def set_batch_update(self):
+        """Updates as one SQL string buffer executed at once (variant_loader.py:146-150)."""
+        self._batch_update = True
+        self.initialize_update_buffer()
+
+    def initialize_update_buffer(self):
+        self._update_buffer = StringIO() if self._batch_update else []
+
+    def close_update_buffer(self):
+        if self._batch_update:
+            self._update_buffer.close()
+
+    def log_skips(self):
+        self._log_skips = True
+
+    def set_fail_at_variant(self, variant):
+        self._fail_at_variant = variant
+
+    def fail_at_variant(self):
+        return self._fail_at_variant
+
+    def is_fail_at_variant(self):
+        return self._fail_at_variant == self.get_current_variant_id()
+
+    def debug(self):
+        return self._debug
 
     # ---- ADSP update buffer (variant_loader.py:290-300; vcf_variant_loader.py:222-226)
     def update_buffer(self, sizeOnly=False):
         """``(record_primary_key, 'chr' + chromosome)`` per ADSP alt whose key was
-        already loaded (the values of the is_adsp_variant UPDATE)."""
+        already loaded (the values of the is_adsp_variant UPDATE,
+        vcf_variant_loader.py:222-226); a SQL string buffer after
+        ``set_batch_update()`` (variant_loader.py:298-304)."""
+        if self._batch_update:
+            return self._update_buffer.tell() if sizeOnly else self._update_buffer
         return len(self._update_buffer) if sizeOnly else self._update_buffer
 
     def reset_update_buffer(self):
-        self._update_buffer = []
+        self.close_update_buffer()
+        self.initialize_update_buffer()
 
     def update_variants(self):
-        raise NotImplementedError("UPDATE in Postgres is out of scope; read update_buffer()")
+        """Execute the update buffer on the caller's cursor (variant_loader.py:457-476):
+        ``execute_values(cursor, update_sql, buffer, page_size=2**10)`` (psycopg2's,
+        or the same paging over ``cursor.mogrify`` when psycopg2 is absent), or the
+        batch string with ``cursor.execute``; then a fresh buffer."""
+        if self._update_sql is None:
+            raise ValueError("must set update sql (VariantLoader.set_update_sql(sql) before attempting update")
+        if self.update_buffer(sizeOnly=True) > 0:
+            if self._batch_update:
+                self._update_buffer.seek(0)
+                self._cursor.execute(self._update_buffer.getvalue())
+            else:
+                _execute_values(self._cursor, self._update_sql, self._update_buffer, page_size=2 ** 10)
+            self.reset_update_buffer()
+        else:
+            self.logger.warning("update called on empty buffer")
 
     def close(self):
         self.close_copy_buffer()
+        self.close_update_buffer()
 
     @property
     def _current_variant(self):

@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--n", type=int, default=None, help="records per GPU (default: config size)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="target seconds per CPU worker")
+    ap.add_argument("--keyed", default="auto", choices=["auto", "on", "off"],
+                    help="also run the keyed C4k step and attach it as 'keyed' (auto: with the default c2 line)")
+    ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (gloo, CPU): the launcher test")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the step as a captured HIP graph (auto: the launch-bound C1 step)")
     return ap.parse_args()
@@ -107,6 +110,20 @@ def _cpu_load_worker(k):
     for ln in lines:
         _, _, rows = O.load_line(ln, lens, bin_index=bi)
         recs += len(rows)
+    return recs, time.perf_counter() - t0
+
+
+def _cpu_vcf_worker(k):
+    """Reference-structured VCF tokenize (oracle.parse_vcf_line: VcfEntryParser
+    parse_entry + get_variant, vcf_parser.py:76-169) and the per-ALT explode with
+    the '.' skip (vcf_variant_loader.py:273-280) over this worker's lines."""
+    from oracle import avdb_oracle as O
+    lines = _SAMPLE[k]
+    t0 = time.perf_counter()
+    recs = 0
+    for ln in lines:
+        v = O.parse_vcf_line(ln)
+        recs += sum(1 for x in v["alts"] if x != ".")
     return recs, time.perf_counter() - t0
 
 
@@ -214,6 +231,22 @@ def cpu_baseline(workload: str, seconds_per_worker: float):
                           f"(oracle/avdb_oracle.py load_line + PortBinIndex; 0.82x the verbatim "
                           f"reference's per-line time, tools/calibrate_cpu_baseline.py), per-process "
                           f"{np.mean([r[1] for r in res]):.2f} s"}
+    if workload == "vcf":
+        per = int(seconds_per_worker / 40e-6)  # ~40 us per line in the port
+        lines = synth.vcf_text(per * workers, seed=6).decode().splitlines()
+        _SAMPLE = [lines[k * per:(k + 1) * per] for k in range(workers)]
+        ctx = mp.get_context("fork")
+        t0 = time.perf_counter()
+        with ctx.Pool(workers) as pool:
+            res = pool.map(_cpu_vcf_worker, range(workers))
+        wall = time.perf_counter() - t0
+        n = sum(r[0] for r in res)
+        return {"value": n / wall, "unit": "variants/s", "cores": workers, "workers": workers,
+                "host_cores_visible": host_cores, "kind": "port",
+                "sample": f"{per * workers:,} synthetic dbSNP-shaped VCF lines ({n:,} per-ALT records), "
+                          f"{workers} processes x {per:,} lines; reference-structured VcfEntryParser parse + "
+                          f"get_variant + per-ALT explode (oracle/avdb_oracle.py parse_vcf_line), per-process "
+                          f"{np.mean([r[1] for r in res]):.2f} s"}
     if workload in ("c5", "c4k"):
         # ADSP-style (or dbSNP-mix) records generated on the CPU (same generator, CPU stream)
         per = int(seconds_per_worker / 6e-6)  # ~5.6 us per record in the port
@@ -317,6 +350,19 @@ def dropin(a):
     res["load_vcf_text_per_line_us"] = per_call(lambda xs: ld.load_vcf_text(text if len(xs) > 20 else
                                                                             ("\n".join(xs) + "\n").encode()),
                                                 lines, reps=3)
+    # VariantAnnotator per alt allele, as vcf_parser.py:225-231 / vcf_variant_loader.py:309
+    # construct and call it (one instance per call): K8a through the avdb_percall binding
+    from annotatedvdb_amd.variant_annotator import VariantAnnotator
+    heap = d["heap"].tobytes()
+    o_, rl_, al_ = d["allele_off"].tolist(), d["ref_len"].tolist(), d["alt_len"].tolist()
+    alle = [(heap[x:x + y].decode(), heap[x + y:x + y + z].decode(), p)
+            for x, y, z, p in zip(o_[:50000], rl_[:50000], al_[:50000], pos[:50000])]
+    res["annotator_end_us"] = per_call(
+        lambda xs: [VariantAnnotator(r, a_, "22", p).infer_variant_end_location() for r, a_, p in xs], alle)
+    res["annotator_normalized_us"] = per_call(
+        lambda xs: [VariantAnnotator(r, a_, "22", p).get_normalized_alleles() for r, a_, p in xs], alle)
+    res["annotator_display_us"] = per_call(
+        lambda xs: [VariantAnnotator(r, a_, "22", p).get_display_attributes() for r, a_, p in xs], alle)
     res["per_line_path"] = {"k5h_rendered_lines": ld._engine.line_host().rendered,
                             "note": "parse_variant: K5h (avdb_vcf_line_host, the kernels' per-line code in the "
                                     "library's host code) for the lines it renders, else K8h (avdb_small_prep_host) "
@@ -338,6 +384,13 @@ def dropin(a):
     pbi = O.PortBinIndex(O.BinTable(GRCH38_LENGTHS))
     base["find_bin_index_miss_us"] = per_call(lambda xs: [pbi.find_bin_index("chr22", s, e) for s, e in xs],
                                               spans)
+    PVA = O.PortVariantAnnotator
+    base["annotator_end_us"] = per_call(
+        lambda xs: [PVA(r, a_, "22", p).infer_variant_end_location() for r, a_, p in xs], alle)
+    base["annotator_normalized_us"] = per_call(
+        lambda xs: [PVA(r, a_, "22", p).get_normalized_alleles() for r, a_, p in xs], alle)
+    base["annotator_display_us"] = per_call(
+        lambda xs: [PVA(r, a_, "22", p).get_display_attributes() for r, a_, p in xs], alle)
     try:
         host_cores = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -353,12 +406,69 @@ def dropin(a):
                                         "source": "SURVEY.md 6 / tools/calibrate_cpu_baseline.py (verbatim "
                                                   "reference with an in-process table-search DB, build container)"}
     res["vs_cpu_baseline"] = {k: base[k] / res[k] for k in ("parse_variant_per_line_us", "find_bin_index_sorted_us",
-                                                             "find_bin_index_miss_us")}
+                                                             "find_bin_index_miss_us", "annotator_end_us",
+                                                             "annotator_normalized_us", "annotator_display_us")}
     out = {"metric": "drop-in per-call latency (find_bin_index, parse_variant)", "value":
            res["parse_variant_per_line_us"], "unit": "us/line", "n_gpus": 1, "higher_is_better": False,
            "dtype": "u8", "data": "synthetic C1 records / dbSNP-shaped VCF lines", "config":
            {"workload": WORKLOADS["dropin"]["desc"]}, "latency": res, "cpu_baseline": cpu}
     print(json.dumps(out), flush=True)
+
+
+def launch_command(a, port: int):
+    """The torchrun command that starts ``--gpus`` ranks of this script (one
+    process per GPU), as the driver's own N>1 form does."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+
+
+def launch(a) -> int:
+    """``bench.py --gpus N`` without torchrun's environment: start N ranks as a
+    child torchrun (before this process touches the GPU — nothing is re-exec'd)
+    and relay rank 0's JSON line; other output goes to stderr.  The reference's
+    driver starts its own workers too (load_vcf_file.py:307-313)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    pr = subprocess.Popen(launch_command(a, port), stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    for line in pr.stdout:
+        if line.startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return pr.wait()
+
+
+def check_world(a, env=None) -> str:
+    """'launch' (start --gpus ranks), 'run' (this process is a rank), or raise
+    on a torchrun world that disagrees with --gpus."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if a.gpus > 1 else "run"
+    if int(ws) != a.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {a.gpus}: launch N ranks with --gpus N")
+    return "run"
+
+
+def dry_run(a):
+    """--dry-run: the N-rank plumbing alone (process group, all-gather, max over
+    ranks, one JSON line from rank 0) with gloo on the CPU — the launcher's test."""
+    from annotatedvdb_amd import distributed as D
+    ri = D.init("gloo")
+    ctr = torch.zeros(32, dtype=torch.int64)
+    ctr[20] = 100
+    _, node = D.allgather_stats(torch.zeros(8, dtype=torch.int32), ctr, ri)
+    t = D.max_over_ranks(0.001 * (1 + ri.rank), ri)
+    if ri.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": ri.world, "dry_run": True,
+                          "ms_per_step": t * 1e3, "config": {"records_total": int(node[20].item())}}), flush=True)
+    D.finalize(ri)
 
 
 def main():
@@ -367,43 +477,68 @@ def main():
         torch.cuda.set_device(0)
         dropin(a)
         return
+    if check_world(a) == "launch":
+        sys.exit(launch(a))
+    if a.dry_run:
+        dry_run(a)
+        return
     from annotatedvdb_amd import distributed as D
     ri = D.rank_info()
-    # CPU baseline first, before this process touches the GPU (its worker
+    # the north_star path rides along the default line: the keyed 1B-shard step (C4k)
+    keyed = a.keyed == "on" or (a.keyed == "auto" and a.workload == "c2")
+    # CPU baselines first, before this process touches the GPU (their worker
     # processes are forked and must not inherit an initialised HIP runtime)
     want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and ri.world == 1
-                                          and a.workload in ("c1", "c2", "c3", "c4", "c5", "c4k", "load"))
+                                          and a.workload in ("c1", "c2", "c3", "c4", "c5", "c4k", "load", "vcf"))
     cpu = cpu_baseline(a.workload, a.cpu_seconds) if (ri.rank == 0 and want_cpu) else None
+    cpu_k = cpu_baseline("c4k", a.cpu_seconds) if (keyed and ri.rank == 0 and want_cpu) else None
     ri = D.init("nccl")
     dev = torch.device("cuda", D.device_index(ri))
     torch.cuda.set_device(dev)
+    out = run_workload(a, a.workload, ri, dev, cpu)
+    if keyed:
+        torch.cuda.empty_cache()
+        k = run_workload(a, "c4k", ri, dev, cpu_k)
+        out["keyed"] = {key: k[key] for key in ("metric", "value", "unit", "ms_per_step", "dtype", "config",
+                                                "roofline", "k7_roofline", "cpu_baseline")}
+        out["keyed"]["note"] = ("north_star's keyed path on BASELINE configs[3]'s per-GPU shard (1.25e8 of the "
+                                "1e9 records): K2 end + bin, K3 dedup, K4 VRS digests, K7 primary-key + ltree-path "
+                                "text; same steps / warmup, timed the same way")
+    if ri.rank == 0:
+        print(json.dumps(out), flush=True)
+    D.finalize(ri)
 
+
+def run_workload(a, name, ri, dev, cpu):
+    """One workload on this rank's GPU: resident synthetic batch, warmup, K timed
+    steps between barriers, max over ranks; returns the JSON object."""
+    from annotatedvdb_amd import distributed as D
     from annotatedvdb_amd import synth
     from annotatedvdb_amd.engine import Engine
 
-    W = WORKLOADS[a.workload]
+    W = WORKLOADS[name]
     n = a.n or W["n"]
     pieces = D.my_pieces(ri)
     eng = Engine(dev.index)
-    if a.workload in ("c5", "c4k"):
+    if name in ("c5", "c4k"):
         digs = ["%032d" % i for i in range(25)]  # synthetic refget ids (no SeqRepo offline)
         eng.set_sequence_digests(digs)
 
     # ---- resident synthetic batch (untimed) ----
     seed = 1000 * ri.rank
-    if a.workload == "c2":
+    if name == "c2":
         chrom, start = synth.point_snvs(n, seed=2 + seed, device=dev, pieces=pieces)
         end = None
-    elif a.workload in ("c3", "c4"):
-        chrom, start, end = synth.spans(n, seed=(3 if a.workload == "c3" else 4) + seed, device=dev,
-                                        pieces=pieces, mix=a.workload)
-    elif a.workload == "c1":
+    elif name in ("c3", "c4"):
+        chrom, start, end = synth.spans(n, seed=(3 if name == "c3" else 4) + seed, device=dev,
+                                        pieces=pieces, mix=name)
+    elif name == "c1":
         batch = synth.c1_batch(n, seed=1, device=dev)
         heap_bytes = int(batch.heap.numel())
-    elif a.workload == "c4k":
+    elif name == "c4k":
         batch = synth.dbsnp_alleles(n, seed=4 + seed, device=dev, pieces=pieces)
         heap_bytes = int(batch.heap.numel())
-    elif a.workload in ("vcf", "load"):
+    elif name in ("vcf", "load"):
         tile = synth.vcf_text(min(VCF_TILE, n), seed=6 + seed)
         reps = -(-n // min(VCF_TILE, n))
         text = torch.frombuffer(bytearray(tile), dtype=torch.uint8).to(dev).repeat(reps)
@@ -423,7 +558,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     evs = {}
 
-    def timed(name, record, fn):
+    def timed(stage, record, fn):
         if not record:
             fn()
             return
@@ -431,7 +566,7 @@ def main():
         e0.record(stream)
         fn()
         e1.record(stream)
-        evs.setdefault(name, []).append((e0, e1))
+        evs.setdefault(stage, []).append((e0, e1))
 
     def c1_step(record: bool):
         box = {}
@@ -471,16 +606,16 @@ def main():
         last["prep"], last["keep"], last["dig"] = box["prep"], box["keep"], box["dig"]
 
     def step(record: bool):
-        if a.workload == "c1":
+        if name == "c1":
             c1_step(record)
-        elif a.workload == "c4k":
+        elif name == "c4k":
             c4k_step(record)
-        elif a.workload in ("c2", "c3", "c4"):
+        elif name in ("c2", "c3", "c4"):
             timed("bin_assign", record, lambda: eng.bin_assign(
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
-        elif a.workload == "vcf":
+        elif name == "vcf":
             timed("vcf_tokenize", record, lambda: eng.vcf_tokenize(text))
-        elif a.workload == "load":
+        elif name == "load":
             box = {}
             timed("vcf_tokenize", record, lambda: box.setdefault("vb", eng.vcf_tokenize(text)))
             vb = box["vb"]
@@ -496,17 +631,17 @@ def main():
             timed("vrs_digest", record, lambda: eng.vrs_digest(batch, 50))
 
     last = {}
-    if a.workload in ("c1", "c4k"):  # dedup workspace, allocated once
+    if name in ("c1", "c4k"):  # dedup workspace, allocated once
         # (+ 2^22 entries: the keyed K2's per-workgroup suspect slices round up)
         last["ws3"] = torch.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), dtype=torch.uint8, device=dev)
-    if a.workload == "c4k":  # K4 compaction workspace, allocated once
+    if name == "c4k":  # K4 compaction workspace, allocated once
         import ctypes
         sz = ctypes.c_size_t()
         eng.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
         last["ws4"] = torch.empty(int(sz.value), dtype=torch.uint8, device=dev)
     for _ in range(a.warmup):
         step(False)
-    use_graph = a.graph == "on" or (a.graph == "auto" and a.workload == "c1")
+    use_graph = a.graph == "on" or (a.graph == "auto" and name == "c1")
     graph = None
     if use_graph:
         # the step captured once as a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and
@@ -541,18 +676,18 @@ def main():
     stage_ms = {k: float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])) for k, v in evs.items()}
     if graph is not None:
         stage_ms["graph_replay"] = True
-    kname = {"c5": "record_prep", "vcf": "vcf_tokenize", "load": "format_write"}.get(a.workload, "bin_assign")
+    kname = {"c5": "record_prep", "vcf": "vcf_tokenize", "load": "format_write"}.get(name, "bin_assign")
     kern_ms = stage_ms.get(kname)
-    if a.workload == "c1":
+    if name == "c1":
         kern_ms = elapsed * 1e3 / a.steps  # the whole step (launch-bound at 1.1 M records)
-    if a.workload == "c4k":
+    if name == "c4k":
         kern_ms = sum(stage_ms[k] for k in ("record_prep", "pk_dedup", "vrs_digest", "primary_keys"))
-    if a.workload in ("vcf", "load"):
+    if name in ("vcf", "load"):
         n_lines, n = n, n_rec  # the unit is emitted variant records (per-ALT rows)
     total_records = n * ri.world * a.steps
     value = total_records / elapsed
 
-    if a.workload == "c4k":
+    if name == "c4k":
         # SURVEY.md §8d per-record bytes of the keyed record path (34 + rlen + alen + 24 per
         # long record) plus the key and ltree-path text K7 writes, over the four kernels' time
         kt = last["kt"]
@@ -566,7 +701,7 @@ def main():
         short = (rl + al) <= 50
         k7_bytes = 50 * n + int((rl + al)[short].sum().item()) + 32 * n_long + text
         del rl, al, short
-    elif a.workload == "c1":
+    elif name == "c1":
         # SURVEY.md §8d per-record bytes of the C5-style record path (in chrom 1 + pos 4 +
         # heap_off 8 + rlen 4 + alen 4 + rs 4, the allele bytes, out bin 4 + end 4 +
         # keep 1) plus the text K7 writes (keys + ltree paths)
@@ -574,7 +709,7 @@ def main():
         rl, al = batch.ref_len.long(), batch.alt_len.long()
         text = int(kt.key_off[n].item()) + int(kt.path_off[n].item())
         bytes_per_launch = 34 * n + int((rl + al).sum().item()) + text
-    elif a.workload == "c5":
+    elif name == "c5":
         # K2 algorithmic bytes per record: in chrom 1 + pos 4 + allele_off 8 + ref_len 4 +
         # alt_len 4, out end 4 + code 4 + status 1 (= 30 B), plus the allele bytes end
         # inference must read: through the first ref/alt mismatch (lcp + 1, capped at each
@@ -601,14 +736,14 @@ def main():
             lines.append(idx)
         line_bytes = n * 30 + 128 * int(torch.unique(torch.cat(lines)).numel())
         del lcp, need, rl, al, off, lines
-    elif a.workload == "load":
+    elif name == "load":
         # K5 write pass: text read once + line table (80 B) + rec_off (8) + both offset
         # arrays (16) + line state (1) per line + end/code/status (9) per record, and
         # the COPY + .mapping text written
         fr = last["fr"]
         out_bytes = int(fr.copy.numel()) + int(fr.mapping.numel())
         bytes_per_launch = int(text.numel()) + 105 * n_lines + 9 * n + out_bytes
-    elif a.workload == "vcf":
+    elif name == "vcf":
         # text read once + record SoA written (chrom 1, pos 4, allele_off 8, ref_len 4,
         # alt_len 4, ext_id 8, rec_line 4, rec_alt 4 = 37 B) + allele heap written
         bytes_per_launch = int(text.numel()) + 37 * n + heap_bytes
@@ -616,7 +751,7 @@ def main():
         bytes_per_launch = n * W["bytes_per"]
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{a.workload}.json")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
@@ -646,7 +781,7 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "cpu_baseline": cpu,
     }
-    if a.workload == "c5":
+    if name == "c5":
         out["roofline"]["line_granular"] = {
             "bytes_per_launch": line_bytes, "achieved": line_bytes / (kern_ms * 1e-3) / 1e9,
             "frac": line_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -677,7 +812,7 @@ def main():
                                     "vop3_issue_peak": vop3, "sq_insts_valu_per_launch": vi,
                                     "sha512_compressions_per_launch": pk.get("sha512_compressions_per_launch"),
                                     "note": pk.get("note")}
-    if a.workload == "c4k":
+    if name == "c4k":
         kt = last["kt"]
         out["dtype"] = "u8"
         out["data"] = "synthetic dbSNP-mix records (synth.dbsnp_alleles, torch PCG on device), resident in HBM"
@@ -685,24 +820,26 @@ def main():
                              long_records=n_long, heap_bytes=heap_bytes,
                              duplicates=int(node_ctr[21].item()) // max(1, a.steps))
         k7_ms = stage_ms["primary_keys"]
-        out["k7_roofline"] = {"kernel": "avdb_primary_keys (size pass + 2 scans + LDS-staged write pass)",
+        out["k7_roofline"] = {"kernel": "avdb_primary_keys_onepass_ex (group scan + LDS-staged write pass; "
+                                        "group totals from the keyed K2)",
                               "bound": "hbm", "achieved": k7_bytes / (k7_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": k7_bytes / (k7_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                               "algorithmic_bytes_per_launch": k7_bytes, "stage_ms": k7_ms}
         out["roofline"]["note"] = ("achieved = SURVEY 8d keyed-record bytes (34 + rlen + alen + 24 if long) + "
                                    "key/path text written, over K2 + K3 + K4 + K7 HIP-event time; K4 (SHA-512) "
                                    "is VALU-bound, the others HBM-bound")
-    if a.workload == "c1":
+    if name == "c1":
         kt = last["kt"]
         out["dtype"] = "u8"
         out["data"] = "synthetic C1 records (numpy PCG64 seed 1, synth.np_c1), resident in HBM"
         out["config"].update(key_bytes=int(kt.key_off[n].item()), path_bytes=int(kt.path_off[n].item()),
                              duplicates=int(node_ctr[21].item()) // max(1, a.steps))
         out["roofline"]["note"] = ("achieved = SURVEY 8d record bytes + key/path text written / whole step "
-                                   "time; at 1.1 M records the step is launch-bound (7 launches), not HBM-bound")
+                                   "time; at 1.1 M records the step is launch-bound (4 kernels in one HIP graph), "
+                                   "not HBM-bound")
         if cpu:
             out["cpu_baseline"]["reference_survey_per_core"] = "285-306 K variants/s (SURVEY.md 6, build container)"
-    if a.workload == "load":
+    if name == "load":
         fr = last["fr"]
         out["dtype"] = "u8"
         out["data"] = "synthetic dbSNP-shaped VCF text with INFO FREQ (numpy PCG64 lines tiled on the device)"
@@ -711,18 +848,17 @@ def main():
                              records_processed=None)
         out["roofline"]["note"] = ("achieved = K5 write-pass algorithmic bytes (text + line table + offsets "
                                    "+ per-record inputs + COPY/.mapping text written) / its HIP-event time")
-    if a.workload == "vcf":
+    if name == "vcf":
         out["dtype"] = "u8"
         out["data"] = "synthetic dbSNP-shaped VCF text (numpy PCG64 lines tiled on the device)"
         out["config"].update(lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
                              records_processed=None)
-        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (count pass, one host "
-                                   "read, the one-pass tokenizer, one host read of its totals; "
-                                   "AVDB_VCF_FUSED=0: the four-kernel path); the line table and line offsets "
-                                   "it also writes (96 B per line) are not counted")
-    if ri.rank == 0:
-        print(json.dumps(out), flush=True)
-    D.finalize(ri)
+        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (count pass, line starts + "
+                                   "parse, two scans, emit, and its two host reads); the line table and line "
+                                   "offsets it also writes (96 B per line) are not counted")
+    return out
+
+
 
 
 if __name__ == "__main__":

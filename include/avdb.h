@@ -259,27 +259,6 @@ int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t 
                   uint8_t* chrom, uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len,
                   uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line,
                   uint32_t* rec_alt, void* stream);
-/* K0 in one text pass (the same outputs as steps 2 + 3, the text read once):
- *   avdb_vcf_count_text  -> counts[0] = '\n' bytes, counts[1] = ',' bytes (device u64[2];
- *      workspace AVDB_VCF_COUNT_WORKSPACE_BYTES).  n_lines follows as for step 1, and
- *      n_lines + commas bounds the records (each is a line's first ALT or follows a comma).
- *   avdb_vcf_tokenize    -> the line table, rec_off / heap_off (n_lines + 1 entries), the
- *      record SoA and the allele heap, as avdb_vcf_parse_lines + avdb_vcf_emit give them.
- *      Outputs are written up to the capacities given (lines_cap lines, rec_cap records,
- *      heap_cap heap bytes; a line whose records or heap bytes would pass a capacity is
- *      not emitted); totals (device u64[4]) = lines, records, heap bytes, and [3] = 0
- *      (nonzero: an internal scan wait gave up; the outputs are then invalid).  When a
- *      total exceeds its capacity, call again with larger buffers.  The workspace must
- *      not be shared by calls in flight on different streams. */
-int avdb_vcf_count_text(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
-                        size_t workspace_bytes, uint64_t* counts, void* stream);
-int avdb_vcf_tokenize_workspace_size(size_t text_bytes, size_t* bytes);
-int avdb_vcf_tokenize(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
-                      size_t workspace_bytes, size_t lines_cap, avdb_vcf_line* lines, uint64_t* rec_off,
-                      uint64_t* heap_off, size_t rec_cap, uint8_t* chrom, uint32_t* pos, uint64_t* allele_off,
-                      uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id, uint32_t* rec_line,
-                      uint32_t* rec_alt, size_t heap_cap, uint8_t* heap, uint64_t* totals,
-                      const avdb_vcf_opts* opts, void* stream);
 
 /* ---- K5: the load driver's text outputs ---------------------------------
  * Replaces the per-alt COPY row assembly of VCFVariantLoader.__parse_alt_alleles
@@ -520,6 +499,37 @@ int avdb_small_prep_host(const avdb_ctx* ctx, const avdb_small_batch* batch);
  * AVDB_BIN_NONE, or a contig beyond the labelled 25), or AVDB_ERANGE. */
 int avdb_bin_path_host(const avdb_ctx* ctx, uint8_t chrom, uint32_t start, uint32_t end, uint32_t* code,
                        uint8_t* status, char* out_host, size_t cap);
+/* K8a: ONE VariantAnnotator (Util/lib/python/variant_annotator.py:21-241) on the
+ * host, for the drop-in class the reference constructs per alt allele
+ * (vcf_parser.py:225-231, vcf_variant_loader.py:309-311).  alleles = REF bytes
+ * then ALT bytes (host).  end_rel = infer_variant_end_location - pos (:36-79,
+ * relative, so the caller's integer position is never narrowed); lcp = the
+ * common-prefix length __normalize_alleles trims (:82-121).  With want_display,
+ * the get_display_attributes fields (:134-241): location_start / _end, the class,
+ * and the display_allele then sequence_allele texts in text[0, display_bytes +
+ * sequence_bytes) — state 0; state 1 when they are the caller's (a non-ASCII
+ * allele, or coordinates leaving u32), 2 when not asked.  Returns 0, or
+ * AVDB_ERANGE when the two texts exceed cap (their sizes are set). */
+#define AVDB_VC_SNV 0          /* single nucleotide variant / SNV */
+#define AVDB_VC_INVERSION 1    /* inversion / MNV */
+#define AVDB_VC_SUBSTITUTION 2 /* substitution / MNV */
+#define AVDB_VC_INDEL 3        /* indel / INDEL */
+#define AVDB_VC_INDEL_DOWN 4   /* indel / INDEL (insertion downstream of POS) */
+#define AVDB_VC_INSERTION 5    /* insertion / INS */
+#define AVDB_VC_DUPLICATION 6  /* duplication / DUP */
+#define AVDB_VC_DELETION 7     /* deletion / DEL */
+typedef struct avdb_annotation {
+  int32_t end_rel;
+  uint32_t lcp;
+  uint32_t location_start;
+  uint32_t location_end;
+  uint32_t variant_class;
+  uint32_t display_bytes;
+  uint32_t sequence_bytes;
+  uint32_t state;
+} avdb_annotation;
+int avdb_annotate_host(const avdb_ctx* ctx, const uint8_t* alleles, uint32_t ref_len, uint32_t alt_len,
+                       uint32_t pos, int want_display, avdb_annotation* out, char* text, size_t cap);
 /* Pinned host memory mapped into the device address space (hipHostMalloc,
  * mapped + coherent): the same pointer is valid on the host and in kernels. */
 int avdb_host_alloc(size_t bytes, void** ptr);

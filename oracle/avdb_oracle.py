@@ -462,6 +462,61 @@ def display_attributes(chrom: str, pos: int, ref: str, alt: str) -> dict:
     return at
 
 
+class PortVariantAnnotator(object):
+    """The reference ``VariantAnnotator``'s per-call structure
+    (variant_annotator.py:21-241): the metaseq id joined in the constructor, each
+    method normalising the alleles again as the reference does (:46, :147-152).
+    The CPU baseline of the drop-in per-call figures (bench.py --workload dropin)."""
+
+    def __init__(self, refAllele, altAllele, chrom, position):
+        self.ref, self.alt, self.chrom, self.position = refAllele, altAllele, chrom, position
+        self.metaseq = ":".join((xstr(chrom), xstr(position), refAllele, altAllele))
+
+    def get_normalized_alleles(self, snvDivMinus=False):
+        ref, alt = self.ref, self.alt
+        if len(ref) == 1 and len(alt) == 1:
+            return ref, alt
+        last = -1
+        for i in range(len(ref)):  # :100-107, slice compares as the reference does
+            if ref[i:i + 1] == alt[i:i + 1]:
+                last = i
+            else:
+                break
+        if last >= 0:
+            nalt = alt[last + 1:]
+            if not nalt and snvDivMinus:
+                nalt = "-"
+            nref = ref[last + 1:]
+            if not nref and snvDivMinus:
+                nref = "-"
+            return nref, nalt
+        return ref, alt
+
+    def infer_variant_end_location(self, rsPosition=None):
+        ref, alt = self.ref, self.alt
+        nref, nalt = self.get_normalized_alleles()
+        r, a, nr, na = len(ref), len(alt), len(nref), len(nalt)
+        position = int(self.position)
+        if r == 1 and a == 1:
+            return position
+        if r == a:
+            if ref == alt[::-1]:
+                return position + r - 1
+            return position + nr - 1
+        if na >= 1:
+            if nr >= 1:
+                return position + nr
+            if nr == 0 and r > 1:
+                return position + r - 1
+            return position + 1
+        if nr == 0:
+            return position + r - 1
+        return position + nr
+
+    def get_display_attributes(self, rsPosition=None):
+        return display_attributes(xstr(self.chrom), self.position, self.ref, self.alt)
+
+
 # ---------------------------------------------------------------------------
 # §8f rank 2: INFO FREQ -> allele_frequencies, COPY row, .mapping line
 #   vcf_parser.py:76-114 (INFO parse: '\x2c'->',', '\x59'->'/', '#'->':',

@@ -53,7 +53,7 @@ def _check_shard(engine, n, seed, pieces):
     # K7, K4 and K3 skip their own passes over the SoA (what bench.py --workload c4k times)
     end, code, status, _ = engine.record_prep(b, want_lcp=False, keys=kt, key_digest=True, digest_workspace=ws4,
                                               dedup_workspace=ws3)
-    assert kt.totals_for is not None and engine._codes_for and engine._marks_for
+    assert set(engine._pending) == {"totals", "codes", "marks"}
     keep = engine.pk_dedup(b, grouped=True, workspace=ws3)
     dig, is_long = engine.vrs_digest(b, 50, workspace=ws4)
     kt = engine.primary_keys(b, code=code, digest=dig, out=kt)

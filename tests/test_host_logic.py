@@ -139,12 +139,12 @@ def test_dbsnp_allele_mix():
 
 
 def test_bench_step_does_not_shadow_main_buffers():
-    """bench.py's step() closes over main()'s resident buffers; a local of the
+    """bench.py's step() closes over run_workload()'s resident buffers; a local of the
     same name anywhere in step() breaks every workload (UnboundLocalError)."""
     import ast
     src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
     tree = ast.parse(src)
-    main = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "main")
+    main = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "run_workload")
     step = next(n for n in ast.walk(main) if isinstance(n, ast.FunctionDef) and n.name == "step")
     stored = {n.id for n in ast.walk(step) if isinstance(n, ast.Name) and isinstance(n.ctx, ast.Store)}
     assert not stored & {"chrom", "start", "end", "code", "hist", "ctr", "batch", "text", "eng"}, stored
@@ -203,3 +203,23 @@ def test_load_driver_streams_blocks_at_line_boundaries(tmp_path, gz):
         assert b"".join(blocks) == data
         assert all(b.endswith(b"\n") for b in blocks[:-1])
         assert all(len(b) <= bb + 400 for b in blocks)
+
+
+def test_keyed_handoff_stamps():
+    """engine._stamp / _stamp_ok: a hand-off matches only the same
+    tensor objects at the same versions — not a new tensor at a recycled
+    address, not an in-place edit, not a missing / extra tensor."""
+    import torch
+    from annotatedvdb_amd.engine import _stamp, _stamp_ok
+    a, b = torch.zeros(8), torch.ones(8)
+    st = _stamp(a, b, None)
+    assert _stamp_ok(st, a, b, None)
+    assert not _stamp_ok(st, a, b, a)
+    assert not _stamp_ok(st, b, a, None)
+    a.add_(0)
+    assert not _stamp_ok(st, a, b, None)
+    st = _stamp(a)
+    del a
+    c = torch.zeros(8)
+    assert not _stamp_ok(st, c)
+    assert not _stamp_ok(None, c)

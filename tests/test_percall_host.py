@@ -294,3 +294,54 @@ def test_k5h_chromosome_map_and_pvcf_header_vs_reference(lib, ctx):
         assert mb.raw[:res.map_bytes].decode() == "".join(m + "\n" for m in json.loads(mapping)), raw
     assert rendered > 0.8 * sum(1 for r in rows if not r[1]), rendered
     cmap.close()
+
+
+def test_k8a_variant_annotator_vs_reference(lib):
+    """The drop-in VariantAnnotator (one K8a call per instance through the
+    avdb_percall binding) on every golden pair: end, normalized alleles (both
+    snvDivMinus forms), metaseq id; and every reference display-attribute dict,
+    key order included."""
+    from annotatedvdb_amd.variant_annotator import VariantAnnotator
+    for r in read_tsv("end_infer.tsv.gz"):
+        va = VariantAnnotator(r["ref"], r["alt"], "1", int(r["pos"]))
+        assert va.infer_variant_end_location() == int(r["end"]), r
+        lcp = int(r["lcp"])
+        snv = len(r["ref"]) == 1 and len(r["alt"]) == 1
+        want = (r["ref"], r["alt"]) if snv or lcp == 0 else (r["ref"][lcp:], r["alt"][lcp:])
+        assert va.get_normalized_alleles() == want, r
+        if not snv and lcp:
+            assert va.get_normalized_alleles(True) == (want[0] or "-", want[1] or "-"), r
+        assert va.get_metaseq_id() == r["metaseq_id"]
+    for r in read_tsv("display_attrs.tsv.gz"):
+        d = VariantAnnotator(r["ref"], r["alt"], r["chrom"], int(r["pos"])).get_display_attributes()
+        assert json.dumps(d) == r["attributes"], r
+
+
+def test_k8a_variant_annotator_edges(lib):
+    """Quirks the reference has and the binding's edges."""
+    from annotatedvdb_amd.variant_annotator import VariantAnnotator
+    from oracle import avdb_oracle as O
+    assert VariantAnnotator("AT", "AT", "1", 100).infer_variant_end_location() == 99  # end < start
+    assert VariantAnnotator("ATA", "ATA", "1", 100).infer_variant_end_location() == 102  # palindrome
+    assert VariantAnnotator("A", "<DEL>", "1", 100).infer_variant_end_location() == 101
+    assert VariantAnnotator("A", "*", "1", 100).infer_variant_end_location() == 100
+    big = 10 ** 12  # a Python int beyond u32: the end is position + the library's relative end
+    assert VariantAnnotator("CAGT", "CG", "1", big).infer_variant_end_location() == big + 3
+    assert VariantAnnotator("CAGT", "CG", "1", "100").infer_variant_end_location() == 103
+    with pytest.raises(ValueError):
+        VariantAnnotator("CAGT", "CG", "1", "x").infer_variant_end_location()
+    with pytest.raises(ValueError):
+        VariantAnnotator("CÅ", "C", "1", 100).infer_variant_end_location()
+    # a display text beyond the binding's stack buffer (inversions keep the whole allele)
+    inv = "ACGT" * 700
+    ref, alt = inv, inv[::-1]
+    want = O.display_attributes("7", 5000, ref, alt)
+    got = VariantAnnotator(ref, alt, "7", 5000).get_display_attributes()
+    assert got == want and list(got) == list(want)
+    sub = "A" * 1500
+    want = O.display_attributes("7", 5000, "G" + sub, "GC" + sub[1:] + "T")
+    assert VariantAnnotator("G" + sub, "GC" + sub[1:] + "T", "7", 5000).get_display_attributes() == want
+    d = VariantAnnotator("CAG", "C", "chrUn_KI270302v1", 100).get_display_attributes()
+    assert d["normalized_metaseq_id"] == "chrUn_KI270302v1:100:AG:-"
+    assert list(d) == ["location_start", "location_end", "normalized_metaseq_id", "variant_class",
+                       "variant_class_abbrev", "display_allele", "sequence_allele"]
