@@ -25,6 +25,7 @@ for s in "$@"; do
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
     dropin) step bench_dropin 600 python bench.py --workload dropin ;;
     c2) step bench_c2 600 python bench.py --steps 20 --warmup 3 ;;
+    gloo2) step bench_gloo2 600 env AVDB_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 10 --warmup 3 ;;
     c1|c3|c4|c4k|c5|load|vcf) step "bench_$s" 600 python bench.py --steps 10 --warmup 3 --workload "$s" ;;
     ab:*) # ab:NAME=VALUE:workload  — one bench line with an env knob set (A/B)
       kv=${s#ab:}; w=${kv##*:}; kv=${kv%:*}
