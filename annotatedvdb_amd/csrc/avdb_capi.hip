@@ -130,6 +130,8 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
   // for the list form: the list form is the default at every size)
   c->k7_raw_blocks = 256;
   if (const char* s = getenv("AVDB_K7_RAW_BLOCKS")) c->k7_raw_blocks = size_t(strtoull(s, nullptr, 10));
+  c->k7_v2 = 1;
+  if (const char* s = getenv("AVDB_K7_V2")) c->k7_v2 = atoi(s);
   c->k3_list_min = 0;
   if (const char* s = getenv("AVDB_K3_LIST_MIN")) c->k3_list_min = size_t(strtoull(s, nullptr, 10));
   *out = c;

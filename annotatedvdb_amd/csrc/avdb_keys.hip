@@ -724,6 +724,289 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// K7 write pass, round 4 (k_record_keys_v2; the group-offset one-pass form).
+// Round 3's pass issued ~1,280 VALU wave-instructions per 64-record tile
+// (profiles/pmc_k7.json), most of them in the key stream: a seven-word join of
+// ref ':' alt with the ':' shifted in word by word, a separate seven-word ':' /
+// ASCII check, and a separate 32-character digest path — all of it executed by
+// the whole wave whenever one lane needs it (2 % long records put one in 73 % of
+// tiles).  Here:
+//  * a long record's digest row and a short record's ref are the same kind of
+//    piece, a byte range of a register window, so one code path renders both;
+//  * ref and alt come from two windows (each aligned at its own range), appended
+//    as two ranges with the ':' between — no per-word colon shifting;
+//  * a range loop stops when no lane of the wave has bytes left (the longest
+//    range of the tile decides, not a fixed seven words), full words take the
+//    constant-size append, and the ':' / non-ASCII test runs on the words as
+//    they are appended;
+//  * "label:pos:" and ":rs<id>" are assembled in two registers each and appended
+//    as one or two pieces.
+// A key that turns out HOST (':' or a non-ASCII byte) has its span written with
+// its bytes: the span is reserved from the SoA either way, and a key's text is
+// read only when its state is AVDB_KEY_OK.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kWinWords = 7;  // a range of <= 49 bytes at byte offset <= 7
+
+// bit 7 of each byte of x that is ':' (metaseqId.split raises, primary_key_generator.py:106)
+// or non-ASCII — exact as an any-test (x's bytes outside the range are zero)
+__device__ __forceinline__ uint64_t key_bad(uint64_t x) {
+  const uint64_t v = x ^ 0x3A3A3A3A3A3A3A3Aull;
+  return (((v - 0x0101010101010101ull) & ~v) | x) & kHiBits;
+}
+
+// the window: words [aw, aw + 8 * kWinWords) of the range's aligned start, loaded
+// only as far as some byte of the range needs (bytes outside [lo, hi) read as 0)
+__device__ __forceinline__ void load_win(uint64_t (&W)[kWinWords], uintptr_t src, uint32_t n, const Heap& h) {
+  const uintptr_t aw = src & ~uintptr_t(7);
+  const uint32_t nw = (uint32_t(src & 7) + n + 7) >> 3;
+  if (aw >= h.lo && aw + 8 * nw <= h.hi) {
+#pragma unroll
+    for (uint32_t k = 0; k < kWinWords; ++k)
+      W[k] = k < nw ? reinterpret_cast<const uint64_t*>(aw)[k] : 0ull;
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kWinWords; ++k) W[k] = k < nw ? heap_word(aw + 8 * k, h) : 0ull;
+  }
+}
+
+// bytes [m, m + n) of window W (m + n <= 56) to the sink, bad |= key_bad of them.
+// The loop ends when no lane has bytes left (wave-uniform).
+template <class O>
+__device__ __forceinline__ void append_win(O& o, const uint64_t (&W)[kWinWords], uint32_t m, uint32_t n,
+                                           uint64_t& bad) {
+#pragma unroll
+  for (uint32_t j = 0; j < kWinWords; ++j) {
+    if (!__any(n > 8 * j)) break;
+    if (n > 8 * j) {
+      uint64_t x = W[j] >> (8 * m);
+      if (j + 1 < kWinWords) x |= (W[j + 1] << (63 - 8 * m)) << 1;  // (m == 0: nothing)
+      if (n - 8 * j >= 8) {
+        bad |= key_bad(x);
+        o.append(x, 8);
+      } else {
+        const uint32_t t = n - 8 * j;
+        x &= low_bytes_mask(t);
+        bad |= key_bad(x);
+        o.append(x, t);
+      }
+    }
+  }
+}
+
+// "label:pos:" (contigs 0..24) as up to 14 bytes in two words
+__device__ __forceinline__ uint32_t key_prefix(uint32_t c, uint32_t p, uint64_t* p0, uint64_t* p1) {
+  const uint32_t L = (c >= 9 && c < 22) ? 2u : 1u;
+  const uint64_t lab = c < 9 ? uint64_t('1' + c)
+                             : (c < 22 ? (uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8))
+                                       : (c == 22 ? uint64_t('X') : (c == 23 ? uint64_t('Y') : uint64_t('M'))));
+  const Dec d = dec_text(p);
+  const uint32_t sh = 8 * (L + 1);  // 16 or 24
+  uint64_t a = lab | (0x3Aull << (8 * L)) | (d.lo << sh);
+  uint64_t b = (d.lo >> (64 - sh)) | (d.hi << sh);
+  const uint32_t cp = L + 1 + d.n;  // the second ':' (<= 13)
+  if (cp < 8) a |= 0x3Aull << (8 * cp);
+  else b |= 0x3Aull << (8 * (cp - 8));
+  *p0 = a;
+  *p1 = b;
+  return cp + 1;
+}
+
+template <class O>
+__device__ __forceinline__ void append2(O& o, uint64_t w0, uint64_t w1, uint32_t n) {  // n <= 16
+  if (n >= 8) {
+    o.append(w0, 8);
+    if (n > 8) o.append(w1 & low_bytes_mask(n - 8), n - 8);
+  } else {
+    o.append(w0 & low_bytes_mask(n), n);
+  }
+}
+
+#ifndef AVDB_K7_V2_WAVES
+#define AVDB_K7_V2_WAVES 4
+#endif
+__global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(KeyArgs A) {
+  __shared__ uint64_t s_kimg[kWavesPerBlock * kKeyWave / 8];
+  __shared__ uint64_t s_pimg[kWavesPerBlock * kPathWave / 8];
+  const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
+  lds_u64* kimg = (lds_u64*)s_kimg + wv * (kKeyWave / 8);
+  lds_u64* pimg = (lds_u64*)s_pimg + wv * (kPathWave / 8);
+  for (uint32_t q = lane; q < kKeyWave / 8; q += kWave) kimg[q] = 0;
+  for (uint32_t q = lane; q < kPathWave / 8; q += kWave) pimg[q] = 0;
+  wave_lds_sync();
+  const Heap hheap = make_heap(A.heap, A.heap_bytes);
+  const uint32_t n_chrom = uint32_t(A.n_chrom);
+  auto load_in = [&](size_t t) {
+    KeyTileIn v{};
+    const size_t j = t + lane;
+    if (j < A.n) {
+      v.c = A.chrom[j];
+      v.p = A.pos[j];
+      v.r = A.rl[j];
+      v.a = A.al[j];
+      v.e = A.ext ? A.ext[j] : 0ull;
+      v.off = A.off[j];
+      if (A.code) v.cd = A.code[j];
+    }
+    return v;
+  };
+  const size_t gwave = size_t(blockIdx.x) * kWavesPerBlock + wv, n_gw = size_t(gridDim.x) * kWavesPerBlock;
+  const uint32_t tpg = 1u << A.group_log2;
+  size_t t0 = gwave * (size_t(kWave) << A.group_log2);
+  KeyTileIn nx{};
+  if (t0 < A.n) nx = load_in(t0);
+  uint64_t run_k = 0, run_p = 0;
+  for (size_t tn = 0; t0 < A.n; t0 = tn) {
+    tn = ((t0 / kWave) & (tpg - 1)) != tpg - 1 ? t0 + kWave
+                                               : t0 - size_t(tpg - 1) * kWave + n_gw * (size_t(kWave) << A.group_log2);
+    const size_t i = t0 + lane;
+    const bool live = i < A.n;
+    const KeyTileIn cur = nx;
+    if (tn < A.n) nx = load_in(tn);
+    if (((t0 / kWave) & (tpg - 1)) == 0) {  // a new group: its scanned base
+      const size_t g = (t0 / kWave) >> A.group_log2;
+      const size_t b = g / kGroupsPerBlock;
+      const uint2 gp = A.grp_pre[g];
+      if (A.blk_raw) {
+        uint64_t bk = 0, bp = 0;
+        for (size_t q = lane; q < b; q += kWave) {
+          bk += A.blk_pre[2 * q];
+          bp += A.blk_pre[2 * q + 1];
+        }
+        run_k = wave_sum64(bk) + gp.x;
+        run_p = wave_sum64(bp) + gp.y;
+      } else {
+        run_k = A.blk_pre[2 * b] + gp.x;
+        run_p = A.blk_pre[2 * b + 1] + gp.y;
+      }
+    }
+    // the tile's sizes (SoA-decidable, as the group totals), scanned over the wave
+    uint32_t ksz = 0, psz = 0;
+    if (live) record_sizes(A, cur.c, cur.p, cur.r, cur.a, cur.e, cur.cd, &ksz, &psz);
+    uint32_t xk = ksz, xp = psz;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t uk = __shfl_up(xk, d, kWave), up = __shfl_up(xp, d, kWave);
+      if (lane >= uint32_t(d)) {
+        xk += uk;
+        xp += up;
+      }
+    }
+    const uint32_t K = __shfl(xk, kWave - 1, kWave), P = __shfl(xp, kWave - 1, kWave);
+    const uint64_t gk0 = run_k, gk1 = run_k + K, gp0 = run_p, gp1 = run_p + P;
+    const uint64_t ko = gk0 + xk - ksz, ko1 = gk0 + xk, po = gp0 + xp - psz, po1 = gp0 + xp;
+    run_k = gk1;
+    run_p = gp1;
+    const uint32_t c = cur.c, p = cur.p, r = cur.r, a = cur.a;
+    const uint64_t e = cur.e;
+    const bool lng = uint64_t(r) + a > A.max_seq_len;
+    uint8_t st = AVDB_KEY_HOST;
+    if (live) {
+      A.key_off[i] = ko;
+      if (A.code) A.path_off[i] = po;
+      if (i + 1 == A.n) {
+        A.key_off[A.n] = ko1;
+        if (A.code) A.path_off[A.n] = po1;
+      }
+      st = AVDB_KEY_OK;
+      if (c >= n_chrom || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
+      else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
+      else if (!lng && cur.off + r + a > A.heap_bytes) st = AVDB_KEY_HOST;
+      if (st == AVDB_KEY_OK && ko1 > A.key_cap) st = AVDB_KEY_OVERFLOW;
+    }
+    // the body's two ranges: a long record's 32 digest characters, or ref then alt
+    // (windows loaded up front, independent of each other)
+    const bool kok = st == AVDB_KEY_OK;
+    uint64_t W1[kWinWords], W2[kWinWords];
+    uint32_t m1 = 0, n1 = 0, m2 = 0, n2 = 0;
+    bool wide = false;  // a range past the window (max_seq_len > 50): the per-piece path
+    if (kok) {
+      uintptr_t s1, s2;
+      if (lng) {
+        s1 = reinterpret_cast<uintptr_t>(A.digest) + 32 * i;
+        n1 = AVDB_DIGEST_CHARS;
+        s2 = s1;
+      } else {
+        s1 = reinterpret_cast<uintptr_t>(A.heap) + cur.off;
+        n1 = r;
+        s2 = s1 + r;
+        n2 = a;
+      }
+      m1 = uint32_t(s1 & 7);
+      m2 = uint32_t(s2 & 7);
+      wide = m1 + n1 > 8 * kWinWords || m2 + n2 > 8 * kWinWords;
+      const Heap h1 = lng ? Heap{s1, s1 + AVDB_DIGEST_CHARS} : hheap;
+      load_win(W1, s1, wide ? 0u : n1, h1);
+      load_win(W2, s2, wide ? 0u : n2, hheap);
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kWinWords; ++k) W1[k] = W2[k] = 0;
+    }
+    // stream 0: keys
+    const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap;
+    uint64_t bad = 0;
+    auto render_key = [&](auto o) {  // primary_key_generator.py:106-122
+      uint64_t q0, q1;
+      const uint32_t lp = key_prefix(c, p, &q0, &q1);
+      append2(o, q0, q1, lp);
+      if (!wide) {
+        append_win(o, W1, m1, n1, bad);
+        if (!lng) o.put(':');
+        append_win(o, W2, m2, n2, bad);
+      } else {
+        const uint64_t off = cur.off;
+        if (!key_allele_ok((glb_cp)(A.heap + off), r + a)) bad = kHiBits;
+        o.bytes((glb_cp)(A.heap + off), r);
+        o.put(':');
+        o.bytes((glb_cp)(A.heap + off + r), a);
+      }
+      if (e) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
+        if (e <= 0xFFFFFFFFull) {
+          const Dec d = dec_text(uint32_t(e));
+          append2(o, 0x73723Aull | (d.lo << 24), (d.lo >> 40) | (d.hi << 24), 3 + d.n);
+        } else {
+          o.lit(":rs");
+          o.u64v(e);
+        }
+      }
+      return o;
+    };
+    if (kok) {
+      if (kst) {
+        Out<true, true> o(LdsImage{}, kimg, ko - (gk0 & ~uint64_t(15)));
+        render_key(o).finish();
+      } else {
+        Out<true> o(A.key_out, ko);
+        render_key(o).finish();
+      }
+      if (bad) st = AVDB_KEY_HOST;
+    }
+    // stream 1: ltree paths
+    bool pst = false, path_over = false;
+    if (A.code) {
+      pst = gp1 - (gp0 & ~uint64_t(15)) + 16 <= kPathWave && gp1 <= A.path_cap;
+      const uint32_t cd = live ? cur.cd : AVDB_BIN_NONE;
+      const bool has_path = live && cd != AVDB_BIN_NONE && c < n_chrom;
+      path_over = has_path && po1 > A.path_cap;
+      if (has_path && !path_over) {
+        if (pst) {
+          Out<true, true> o(LdsImage{}, pimg, po - (gp0 & ~uint64_t(15)));
+          bin_path(o, c, cd).finish();
+        } else {
+          Out<true> o(A.path_out, po);
+          bin_path(o, c, cd).finish();
+        }
+      }
+    }
+    if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
+    wave_lds_sync();
+    if (kst) flush_span(kimg, A.key_out, gk0, gk1, lane, kWave);
+    if (pst) flush_span(pimg, A.path_out, gp0, gp1, lane, kWave);
+    wave_lds_sync();
+  }
+}
+
 }  // namespace avdb
 
 using namespace avdb;
@@ -1015,8 +1298,13 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   // write pass sums the block totals itself)
   const unsigned grid = unsigned((ng + kWavesPerBlock - 1) / kWavesPerBlock < AVDB_K7_GRID
                                      ? (ng + kWavesPerBlock - 1) / kWavesPerBlock : AVDB_K7_GRID);
-  hipLaunchKernelGGL(k_record_keys<2>, dim3(grid), dim3(kBlock), 0, s, A);
-  AVDB_LAUNCH_CHECK("k_record_keys<groups>");
+  if (ctx->k7_v2) {
+    hipLaunchKernelGGL(k_record_keys_v2, dim3(grid), dim3(kBlock), 0, s, A);
+    AVDB_LAUNCH_CHECK("k_record_keys_v2");
+  } else {
+    hipLaunchKernelGGL(k_record_keys<2>, dim3(grid), dim3(kBlock), 0, s, A);
+    AVDB_LAUNCH_CHECK("k_record_keys<groups>");
+  }
   return AVDB_OK;
 }
 
