@@ -8,6 +8,7 @@ OUT=gpurun_out/$T
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 P="tools/k7_probe.py 125000000 3"
+export AVDB_K7_PROBE_MODE=both
 timeout -k 10 240 python $P > "$OUT/probe.json" 2> "$OUT/probe.err" &&
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 $P > "$OUT/prof.log" 2>&1 &&
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD -d "$OUT/pmc1" -o run --output-format csv -- python3 $P > "$OUT/pmc1.log" 2>&1 &&

@@ -41,8 +41,10 @@ def main():
     ko = eng.primary_keys(b, digest=dig)
     torch.cuda.synchronize()
     kb, pb = int(kt.key_off[n].item()), int(kt.path_off[n].item())
+    mode = os.environ.get("AVDB_K7_PROBE_MODE", "all")  # all | both (keys + paths only, for counter passes)
     t_both, all_both = timed(lambda: eng.primary_keys(b, code=code, digest=dig, out=kt), reps)
-    t_keys, all_keys = timed(lambda: eng.primary_keys(b, digest=dig, out=ko), reps)
+    t_keys, all_keys = (timed(lambda: eng.primary_keys(b, digest=dig, out=ko), reps) if mode == "all"
+                        else (None, []))
     print(json.dumps({"n": n, "key_bytes": kb, "path_bytes": pb, "keys_paths_ms": t_both, "keys_only_ms": t_keys,
                       "all_both": all_both, "all_keys": all_keys,
                       "text_TBps_both": (kb + pb) / (t_both * 1e-3) / 1e12}))
