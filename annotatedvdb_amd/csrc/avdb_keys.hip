@@ -749,6 +749,48 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
 // ---------------------------------------------------------------------------
 constexpr uint32_t kWinWords = 7;  // a range of <= 49 bytes at byte offset <= 7
 
+// inclusive wave64 prefix sum through DPP row shifts and row broadcasts: six
+// VALU adds with no LDS round trip (__shfl_up lowers to ds_bpermute: six
+// dependent LDS trips per value)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+  return x;
+}
+
+// flush_span with 32-bit chunk indices (a tile's span is < 8 KB): one 64-bit
+// address add per store instead of 64-bit index arithmetic
+__device__ __forceinline__ void flush_span32(lds_u64* img, uint8_t* out, uint64_t g0, uint64_t g1, uint32_t lane) {
+  const uint64_t a0 = g0 & ~uint64_t(15);
+  const uint64_t f0 = (g0 + 15) & ~uint64_t(15), f1 = g1 & ~uint64_t(15);  // full chunks [f0, f1)
+  u32x4* dst = reinterpret_cast<u32x4*>(out + a0);
+  if (f1 > f0) {
+    const uint32_t q1 = uint32_t(f1 - a0) >> 4;
+    for (uint32_t q = (uint32_t(f0 - a0) >> 4) + lane; q < q1; q += kWave) {
+      const uint64_t lo = img[2 * q], hi = img[2 * q + 1];
+      img[2 * q] = 0;
+      img[2 * q + 1] = 0;
+      __builtin_nontemporal_store(u32x4{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)}, dst + q);
+    }
+  }
+  const bool head = g0 != f0 || f1 < f0;
+  const bool tail = (g1 & 15) && f1 >= f0 && (f1 != a0 || !head);
+  if ((lane == 0 && head) || (lane == 1 && tail)) {
+    const uint64_t a = lane == 0 ? a0 : f1;
+    const uint32_t q = uint32_t(a - a0) >> 4;
+    const uint64_t v0 = img[2 * q], v1 = img[2 * q + 1];
+    img[2 * q] = 0;
+    img[2 * q + 1] = 0;
+    const uint32_t lo = a < g0 ? uint32_t(g0 - a) : 0u;
+    const uint32_t hi = a + 16 > g1 ? uint32_t(g1 - a) : 16u;
+    store_part16(out, a, lo, hi, v0, v1);
+  }
+}
+
 // bit 7 of each byte of x that is ':' (metaseqId.split raises, primary_key_generator.py:106)
 // or non-ASCII — exact as an any-test (x's bytes outside the range are zero)
 __device__ __forceinline__ uint64_t key_bad(uint64_t x) {
@@ -761,10 +803,11 @@ __device__ __forceinline__ uint64_t key_bad(uint64_t x) {
 __device__ __forceinline__ void load_win(uint64_t (&W)[kWinWords], uintptr_t src, uint32_t n, const Heap& h) {
   const uintptr_t aw = src & ~uintptr_t(7);
   const uint32_t nw = (uint32_t(src & 7) + n + 7) >> 3;
-  if (aw >= h.lo && aw + 8 * nw <= h.hi) {
+  if (aw >= h.lo && aw + 8 * kWinWords <= h.hi) {
+    // the whole window inside the allocation: all seven words, no per-word select
+    // (words past the range are only ever read under a byte mask)
 #pragma unroll
-    for (uint32_t k = 0; k < kWinWords; ++k)
-      W[k] = k < nw ? reinterpret_cast<const uint64_t*>(aw)[k] : 0ull;
+    for (uint32_t k = 0; k < kWinWords; ++k) W[k] = reinterpret_cast<const uint64_t*>(aw)[k];
   } else {
 #pragma unroll
     for (uint32_t k = 0; k < kWinWords; ++k) W[k] = k < nw ? heap_word(aw + 8 * k, h) : 0ull;
@@ -796,12 +839,11 @@ __device__ __forceinline__ void append_win(O& o, const uint64_t (&W)[kWinWords],
 }
 
 // "label:pos:" (contigs 0..24) as up to 14 bytes in two words
-__device__ __forceinline__ uint32_t key_prefix(uint32_t c, uint32_t p, uint64_t* p0, uint64_t* p1) {
+__device__ __forceinline__ uint32_t key_prefix(uint32_t c, const Dec& d, uint64_t* p0, uint64_t* p1) {
   const uint32_t L = (c >= 9 && c < 22) ? 2u : 1u;
   const uint64_t lab = c < 9 ? uint64_t('1' + c)
                              : (c < 22 ? (uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8))
                                        : (c == 22 ? uint64_t('X') : (c == 23 ? uint64_t('Y') : uint64_t('M'))));
-  const Dec d = dec_text(p);
   const uint32_t sh = 8 * (L + 1);  // 16 or 24
   uint64_t a = lab | (0x3Aull << (8 * L)) | (d.lo << sh);
   uint64_t b = (d.lo >> (64 - sh)) | (d.hi << sh);
@@ -881,19 +923,21 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
         run_p = A.blk_pre[2 * b + 1] + gp.y;
       }
     }
-    // the tile's sizes (SoA-decidable, as the group totals), scanned over the wave
+    // the tile's sizes (SoA-decidable, as the group totals: key_path_sizes), from
+    // the POS and refSNP digits the key renders anyway, scanned over the wave
+    const Dec dp = dec_text(cur.p);
+    const bool e32 = cur.e <= 0xFFFFFFFFull;
+    const Dec de = dec_text(uint32_t(cur.e));
     uint32_t ksz = 0, psz = 0;
-    if (live) record_sizes(A, cur.c, cur.p, cur.r, cur.a, cur.e, cur.cd, &ksz, &psz);
-    uint32_t xk = ksz, xp = psz;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t uk = __shfl_up(xk, d, kWave), up = __shfl_up(xp, d, kWave);
-      if (lane >= uint32_t(d)) {
-        xk += uk;
-        xp += up;
-      }
+    if (live) {
+      const bool lg = uint64_t(cur.r) + cur.a > A.max_seq_len;
+      if (cur.c < uint32_t(A.n_chrom) && !(cur.e >> 63) && !(lg && !A.digest))
+        ksz = ((cur.c >= 9 && cur.c < 22) ? 2u : 1u) + 2u + dp.n + (lg ? uint32_t(AVDB_DIGEST_CHARS) : cur.r + 1u + cur.a) +
+              (cur.e ? 3u + (e32 ? de.n : ndigits64(cur.e)) : 0u);
+      if (A.code && cur.cd != AVDB_BIN_NONE && cur.c < uint32_t(A.n_chrom)) psz = bin_path_size(cur.c, cur.cd);
     }
-    const uint32_t K = __shfl(xk, kWave - 1, kWave), P = __shfl(xp, kWave - 1, kWave);
+    const uint32_t xk = wave_incl_sum(ksz), xp = wave_incl_sum(psz);
+    const uint32_t K = __builtin_amdgcn_readlane(xk, kWave - 1), P = __builtin_amdgcn_readlane(xp, kWave - 1);
     const uint64_t gk0 = run_k, gk1 = run_k + K, gp0 = run_p, gp1 = run_p + P;
     const uint64_t ko = gk0 + xk - ksz, ko1 = gk0 + xk, po = gp0 + xp - psz, po1 = gp0 + xp;
     run_k = gk1;
@@ -948,7 +992,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
     uint64_t bad = 0;
     auto render_key = [&](auto o) {  // primary_key_generator.py:106-122
       uint64_t q0, q1;
-      const uint32_t lp = key_prefix(c, p, &q0, &q1);
+      const uint32_t lp = key_prefix(c, dp, &q0, &q1);
       append2(o, q0, q1, lp);
       if (!wide) {
         append_win(o, W1, m1, n1, bad);
@@ -962,9 +1006,8 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
         o.bytes((glb_cp)(A.heap + off + r), a);
       }
       if (e) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
-        if (e <= 0xFFFFFFFFull) {
-          const Dec d = dec_text(uint32_t(e));
-          append2(o, 0x73723Aull | (d.lo << 24), (d.lo >> 40) | (d.hi << 24), 3 + d.n);
+        if (e32) {
+          append2(o, 0x73723Aull | (de.lo << 24), (de.lo >> 40) | (de.hi << 24), 3 + de.n);
         } else {
           o.lit(":rs");
           o.u64v(e);
@@ -1001,8 +1044,8 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
     }
     if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
     wave_lds_sync();
-    if (kst) flush_span(kimg, A.key_out, gk0, gk1, lane, kWave);
-    if (pst) flush_span(pimg, A.path_out, gp0, gp1, lane, kWave);
+    if (kst) flush_span32(kimg, A.key_out, gk0, gk1, lane);
+    if (pst) flush_span32(pimg, A.path_out, gp0, gp1, lane);
     wave_lds_sync();
   }
 }
