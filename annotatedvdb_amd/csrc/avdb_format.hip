@@ -12,7 +12,7 @@
 //     (vcf_parser.py:200-222), both as json.dumps text;
 //   * the .mapping line: variant id TAB str([{'primary_key': .., 'bin_index': ..}, ..])
 //     (load_vcf_file.py:116-117).
-//   SIZE pass (bytes per line) -> hipCUB exclusive scans -> WRITE pass, both the
+//   SIZE pass (bytes per line) -> exclusive scans (avdb_scan.hpp) -> WRITE pass, both the
 //   same templated code.  One lane per line, 256 consecutive lines per workgroup
 //   with their text staged in LDS (as K0); each lane writes its own contiguous
 //   span of both outputs (sink and alternatives measured: see Out below).  A
@@ -25,15 +25,10 @@
 // shared sink and renderers: avdb_fmt.hpp.)
 #include "avdb_k5.hpp"
 
-#include <hipcub/hipcub.hpp>
+#include "avdb_scan.hpp"
 
 
-static size_t scan_bytes(size_t n) {
-  size_t t = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, static_cast<const unsigned long long*>(nullptr),
-                                         static_cast<unsigned long long*>(nullptr), n);
-  return (t + 255) & ~size_t(255);
-}
+static size_t scan_bytes(size_t n) { return (avdb::scan::workspace_bytes(n) + 255) & ~size_t(255); }
 
 extern "C" int avdb_format_workspace_size(size_t n, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
@@ -77,7 +72,7 @@ extern "C" int avdb_vcf_format_size(avdb_ctx* ctx, const uint8_t* text, size_t t
   hipLaunchKernelGGL(k_vcf_format<false>, dim3(grid), dim3(kBlock), 0, s, A);
   AVDB_LAUNCH_CHECK("k_vcf_format<size>");
   size_t tb = scan_bytes(n_lines + 1);
-  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, co, co, n_lines + 1, s));
-  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, mo, mo, n_lines + 1, s));
+  if (int e = avdb::scan::exclusive_u64(copy_off, copy_off, n_lines + 1, workspace, tb, s)) return e;
+  if (int e = avdb::scan::exclusive_u64(map_off, map_off, n_lines + 1, workspace, tb, s)) return e;
   return AVDB_OK;
 }

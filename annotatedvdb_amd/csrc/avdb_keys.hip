@@ -2,7 +2,7 @@
 // avdb_primary_keys (primary keys + ltree bin paths of a record batch) (gfx950).
 #include "avdb_fmt.hpp"
 
-#include <hipcub/hipcub.hpp>
+#include "avdb_scan.hpp"
 #include <string.h>
 
 namespace avdb {
@@ -1054,28 +1054,13 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
 
 using namespace avdb;
 
-static size_t scan_bytes(size_t n) {
-  size_t t = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, static_cast<const unsigned long long*>(nullptr),
-                                         static_cast<unsigned long long*>(nullptr), n);
-  return (t + 255) & ~size_t(255);
-}
+static size_t scan_bytes(size_t n) { return (scan::workspace_bytes(n) + 255) & ~size_t(255); }
 
 // K7's size pass writes each record's key and path size as u16 into the
 // workspace and the scans widen them to the u64 offsets: the pass writes 4
 // bytes per record instead of 16 and the scans read 2 instead of 8 per array
 // (C4k: 1.25e8 records, two 1 GB u64 scans at 0.76 ms each).
-struct Widen16 {
-  __host__ __device__ unsigned long long operator()(const uint16_t& x) const { return x; }
-};
-typedef hipcub::TransformInputIterator<unsigned long long, Widen16, const uint16_t*> Wide16It;
-
-static size_t scan16_bytes(size_t n) {
-  size_t t = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, Wide16It(nullptr, Widen16()),
-                                         static_cast<unsigned long long*>(nullptr), n);
-  return (t + 255) & ~size_t(255);
-}
+static size_t scan16_bytes(size_t n) { return scan_bytes(n); }
 
 static size_t size16_slot(size_t n) { return ((2 * (n + 1)) + 255) & ~size_t(255); }
 
@@ -1114,7 +1099,7 @@ extern "C" int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, cons
                        ref_len, alt_len, heap, heap_bytes, n, out_off, nullptr, rec_state);
     AVDB_LAUNCH_CHECK("k_display<size>");
     size_t tb = scan_bytes(n + 1);
-    AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, oo, oo, n + 1, s));
+    if (int e = scan::exclusive_u64(oo, oo, n + 1, workspace, tb, s)) return e;
     return AVDB_OK;
   }
   if (n == 0) return AVDB_OK;
@@ -1191,16 +1176,17 @@ extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint
       A.path_sz = bin_code ? psz : nullptr;
       hipLaunchKernelGGL(k_record_keys<0>, dim3(grid), dim3(kBlock), 0, s, A);
       AVDB_LAUNCH_CHECK("k_record_keys<size>");
-      AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, Wide16It(ksz, Widen16()), ko, n + 1, s));
+      if (int e = scan::exclusive_u64(ksz, ko, n + 1, workspace, tb, s)) return e;
       if (bin_code)
-        AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, Wide16It(psz, Widen16()), po, n + 1, s));
+        if (int e = scan::exclusive_u64(psz, po, n + 1, workspace, tb, s)) return e;
       return AVDB_OK;
     }
     hipLaunchKernelGGL(k_record_keys<0>, dim3(grid), dim3(kBlock), 0, s, A);
     AVDB_LAUNCH_CHECK("k_record_keys<size>");
     size_t tb = scan_bytes(n + 1);
-    AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, ko, ko, n + 1, s));
-    if (bin_code) AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, po, po, n + 1, s));
+    if (int e = scan::exclusive_u64(ko, ko, n + 1, workspace, tb, s)) return e;
+    if (bin_code)
+      if (int e = scan::exclusive_u64(po, po, n + 1, workspace, tb, s)) return e;
     return AVDB_OK;
   }
   if (n == 0) return AVDB_OK;

@@ -13,7 +13,7 @@
 //   avdb_vcf_select_copy   the selected lines (+ '\n') gathered into one text
 #include "avdb_internal.hpp"
 
-#include <hipcub/hipcub.hpp>
+#include "avdb_scan.hpp"
 #include <string.h>
 
 namespace avdb {
@@ -84,10 +84,7 @@ using namespace avdb;
 
 extern "C" int avdb_shard_workspace_size(size_t n_lines, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
-  size_t t = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, static_cast<const unsigned long long*>(nullptr),
-                                         static_cast<unsigned long long*>(nullptr), n_lines + 1);
-  *bytes = (t + 255) & ~size_t(255);
+  *bytes = (scan::workspace_bytes(n_lines + 1) + 255) & ~size_t(255);
   return AVDB_OK;
 }
 
@@ -132,7 +129,7 @@ extern "C" int avdb_vcf_select_lines(avdb_ctx* ctx, size_t n_lines, const avdb_v
                      so);
   AVDB_LAUNCH_CHECK("k_vcf_select");
   size_t tb = need;
-  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(workspace, tb, so, so, n_lines + 1, s));
+  if (int e = scan::exclusive_u64(sel_off, sel_off, n_lines + 1, workspace, tb, s)) return e;
   return AVDB_OK;
 }
 

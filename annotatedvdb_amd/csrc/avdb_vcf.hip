@@ -13,7 +13,7 @@
 //                  LDS: rstrip, tab fields, CHROM -> contig code, POS, ID / INFO RS ->
 //                  refSNP key, ALT count, heap bytes (spans over kStage bytes parse
 //                  straight from global memory)
-//   (hipCUB exclusive scans: record and heap offsets per line)
+//   (exclusive scans, avdb_scan.hpp: record and heap offsets per line)
 //   k_vcf_emit     same staging; one lane per line: one record per ALT != '.',
 //                  REF+ALT copied to the allele heap
 // Only canonical text is resolved here; the rest is flagged (AVDB_VCF_*_HOST) for
@@ -21,7 +21,7 @@
 #include "avdb_fmt.hpp"
 #include "avdb_vcfline.hpp"
 
-#include <hipcub/hipcub.hpp>
+#include "avdb_scan.hpp"
 
 namespace avdb {
 
@@ -327,12 +327,7 @@ static int count_pass(const uint8_t* text, size_t text_bytes, void* ws, unsigned
   return AVDB_OK;
 }
 
-static size_t scan_temp_bytes(size_t n) {
-  size_t t = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, static_cast<const unsigned long long*>(nullptr),
-                                         static_cast<unsigned long long*>(nullptr), n);
-  return (t + 255) & ~size_t(255);
-}
+static size_t scan_temp_bytes(size_t n) { return (scan::workspace_bytes(n) + 255) & ~size_t(255); }
 
 extern "C" int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes) {
   (void)text_bytes;
@@ -411,8 +406,8 @@ extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
   hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, starts,
                      lines, rc, hc, cm, min_fields);
   AVDB_LAUNCH_CHECK("k_vcf_parse");
-  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, rc, rc, n_lines + 1, s));
-  AVDB_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, hc, hc, n_lines + 1, s));
+  if (int e = scan::exclusive_u64(rec_off, rec_off, n_lines + 1, tmp, tmp_bytes, s)) return e;
+  if (int e = scan::exclusive_u64(heap_off, heap_off, n_lines + 1, tmp, tmp_bytes, s)) return e;
   return AVDB_OK;
 }
 
