@@ -28,7 +28,7 @@
 #include "avdb_scan.hpp"
 
 
-static size_t scan_bytes(size_t n) { return (avdb::scan::workspace_bytes(n) + 255) & ~size_t(255); }
+static size_t scan_bytes(size_t n) { return (avdb::scan::workspace_bytes(n, 2) + 255) & ~size_t(255); }
 
 extern "C" int avdb_format_workspace_size(size_t n, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
@@ -72,7 +72,7 @@ extern "C" int avdb_vcf_format_size(avdb_ctx* ctx, const uint8_t* text, size_t t
   hipLaunchKernelGGL(k_vcf_format<false>, dim3(grid), dim3(kBlock), 0, s, A);
   AVDB_LAUNCH_CHECK("k_vcf_format<size>");
   size_t tb = scan_bytes(n_lines + 1);
-  if (int e = avdb::scan::exclusive_u64(copy_off, copy_off, n_lines + 1, workspace, tb, s)) return e;
-  if (int e = avdb::scan::exclusive_u64(map_off, map_off, n_lines + 1, workspace, tb, s)) return e;
+  if (int e = avdb::scan::exclusive_u64_pair(copy_off, copy_off, map_off, map_off, n_lines + 1, workspace, tb, s))
+    return e;
   return AVDB_OK;
 }

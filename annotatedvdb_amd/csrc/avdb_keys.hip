@@ -747,6 +747,14 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
 // its bytes: the span is reserved from the SoA either way, and a key's text is
 // read only when its state is AVDB_KEY_OK.
 // ---------------------------------------------------------------------------
+// AVDB_K7V2_EXP: attribution knobs for tools/k7_attr.sh (each drops one part of
+// the pass and produces wrong text; 0 in every shipped build): 1 no key render,
+// 2 no path render, 4 no ':' / ASCII check, 8 no allele ranges, 16 no ':rs'
+// suffix, 32 no "label:pos:" prefix, 64 no flushes, 128 no window loads
+#ifndef AVDB_K7V2_EXP
+#define AVDB_K7V2_EXP 0
+#endif
+#define K7X(b) ((AVDB_K7V2_EXP & (b)) != 0)
 constexpr uint32_t kWinWords = 7;  // a range of <= 49 bytes at byte offset <= 7
 
 // inclusive wave64 prefix sum through DPP row shifts and row broadcasts: six
@@ -826,12 +834,12 @@ __device__ __forceinline__ void append_win(O& o, const uint64_t (&W)[kWinWords],
       uint64_t x = W[j] >> (8 * m);
       if (j + 1 < kWinWords) x |= (W[j + 1] << (63 - 8 * m)) << 1;  // (m == 0: nothing)
       if (n - 8 * j >= 8) {
-        bad |= key_bad(x);
+        if (!K7X(4)) bad |= key_bad(x);
         o.append(x, 8);
       } else {
         const uint32_t t = n - 8 * j;
         x &= low_bytes_mask(t);
-        bad |= key_bad(x);
+        if (!K7X(4)) bad |= key_bad(x);
         o.append(x, t);
       }
     }
@@ -862,6 +870,81 @@ __device__ __forceinline__ void append2(O& o, uint64_t w0, uint64_t w1, uint32_t
     if (n > 8) o.append(w1 & low_bytes_mask(n - 8), n - 8);
   } else {
     o.append(w0 & low_bytes_mask(n), n);
+  }
+}
+
+#ifndef AVDB_K7_POS
+#define AVDB_K7_POS 0  // 1: keys rendered piece-at-position (A/B; 0: the append sink)
+#endif
+#ifndef AVDB_K7_POS_UNALIGNED
+#define AVDB_K7_POS_UNALIGNED 1  // body windows by unaligned loads (0: aligned loads + a funnel shift)
+#endif
+#ifndef AVDB_K7_PUT_COND
+#define AVDB_K7_PUT_COND 0  // lds_put's second word only when the piece is unaligned
+#endif
+__device__ __forceinline__ void lds_or(lds_u64* w, uint64_t v) {
+  __hip_atomic_fetch_or(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// OR up to 8 bytes x (bytes past them zero) into the image at byte D: two words
+// (the second gets 0 when D is aligned: (x >> 1) >> 63 is 0)
+__device__ __forceinline__ void lds_put(lds_u64* img, uint32_t D, uint64_t x) {
+  const uint32_t k = 8 * (D & 7u), q = D >> 3;
+  lds_or(img + q, x << k);
+  if (!AVDB_K7_PUT_COND || k) lds_or(img + q + 1, (x >> 1) >> (63 - k));
+}
+
+// bytes [a, a + need) as kWinWords unaligned words from address a (need <= 56);
+// bytes outside h read as 0 (then word by word from aligned loads)
+__device__ __forceinline__ void load_win_at(uint64_t (&W)[kWinWords], uintptr_t a, uint32_t need, const Heap& h) {
+  if (AVDB_K7_POS_UNALIGNED && a >= h.lo && a + 8 * kWinWords <= h.hi) {
+#pragma unroll
+    for (uint32_t k = 0; k < kWinWords; ++k) W[k] = reinterpret_cast<g_u64u>(a + 8 * k)->v;
+  } else if (!AVDB_K7_POS_UNALIGNED && (a & ~uintptr_t(7)) >= h.lo && (a & ~uintptr_t(7)) + 8 * kWinWords + 8 <= h.hi) {
+    // aligned words, one funnel shift per word
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~uintptr_t(7));
+    const uint32_t sh = 8 * uint32_t(a & 7);
+    uint64_t prev = w[0];
+#pragma unroll
+    for (uint32_t k = 0; k < kWinWords; ++k) {
+      const uint64_t nx = w[k + 1];
+      W[k] = (prev >> sh) | ((nx << 1) << (63 - sh));
+      prev = nx;
+    }
+  } else {
+    const uintptr_t a0 = a & ~uintptr_t(7);
+    const uint32_t sh = 8 * uint32_t(a & 7), lim = need ? need + uint32_t(a & 7) : 0u;
+    uint64_t prev = lim ? heap_word(a0, h) : 0ull;
+#pragma unroll
+    for (uint32_t k = 0; k < kWinWords; ++k) {
+      const uint64_t nx = 8 * (k + 1) < lim ? heap_word(a0 + 8 * (k + 1), h) : 0ull;
+      W[k] = sh ? (prev >> sh) | (nx << (64 - sh)) : prev;
+      prev = nx;
+    }
+  }
+}
+
+// window words 0.. of a range of n bytes placed at image byte D (word 0 holds
+// D & 7 bytes that are not the range's): masked at both ends, ORed in place;
+// bad collects key_bad's pre-mask terms (the caller masks with kHiBits once).
+// The loop ends when no lane has words left (wave-uniform).
+__device__ __forceinline__ void put_range(lds_u64* img, const uint64_t (&W)[kWinWords], uint32_t D, uint32_t n,
+                                          uint64_t& bad) {
+  const uint32_t k = D & 7u, end = k + n;
+  lds_u64* q = img + (D >> 3);
+#pragma unroll
+  for (uint32_t j = 0; j < kWinWords; ++j) {
+    if (!__any(end > 8 * j)) break;
+    if (end > 8 * j) {
+      uint64_t x = W[j];
+      if (j == 0) x &= ~low_bytes_mask(k);
+      if (end < 8 * j + 8) x &= low_bytes_mask(end - 8 * j);
+      if (!K7X(4)) {
+        const uint64_t v = x ^ 0x3A3A3A3A3A3A3A3Aull;
+        bad |= ((v - 0x0101010101010101ull) & ~v) | x;
+      }
+      lds_or(q + j, x);
+    }
   }
 }
 
@@ -959,6 +1042,82 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
       else if (!lng && cur.off + r + a > A.heap_bytes) st = AVDB_KEY_HOST;
       if (st == AVDB_KEY_OK && ko1 > A.key_cap) st = AVDB_KEY_OVERFLOW;
     }
+#if AVDB_K7_POS
+    // stream 0: keys, each piece ORed into the image at its own byte position
+    // (primary_key_generator.py:106-122): "label:pos:" at D0, the body range (32
+    // digest characters, or ref) at D1, ':' and alt at D2 / D3, ":rs<id>" at D4.
+    // The body ranges are read through unaligned 8-byte loads that start (D & 7)
+    // bytes before the range, so every loaded word is already an image word: no
+    // source shift, no destination shift, no pending word carried between pieces.
+    const bool kok = st == AVDB_KEY_OK;
+    const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap;
+    uint64_t bad = 0;
+    uint64_t q0, q1;
+    const uint32_t lp = key_prefix(c, dp, &q0, &q1);
+    const uint32_t D0 = uint32_t(ko - (gk0 & ~uint64_t(15)));
+    const uint32_t D1 = D0 + lp;
+    const uint32_t n1 = lng ? uint32_t(AVDB_DIGEST_CHARS) : r, n2 = lng ? 0u : a;
+    const uint32_t D3 = D1 + n1 + (lng ? 0u : 1u);
+    const uint32_t k1 = D1 & 7u, k3 = D3 & 7u;
+    // the positional form: an LDS-image span and both ranges within a window
+    const bool fast = kok && kst && k1 + n1 <= 8 * kWinWords && k3 + n2 <= 8 * kWinWords;
+    if (kok && !K7X(1)) {
+      if (fast) {
+        uint64_t W1[kWinWords], W2[kWinWords];
+        const uintptr_t s1 = lng ? reinterpret_cast<uintptr_t>(A.digest) + 32 * i
+                                 : reinterpret_cast<uintptr_t>(A.heap) + cur.off;
+        const Heap h1 = lng ? make_heap(reinterpret_cast<const uint8_t*>(A.digest), 32 * A.n) : hheap;
+        load_win_at(W1, s1 - k1, k1 + n1, h1);
+        load_win_at(W2, s1 + r - k3, lng ? 0u : k3 + n2, hheap);
+        lds_put(kimg, D0, q0);
+        if (lp > 8) lds_put(kimg, D0 + 8, q1);
+        put_range(kimg, W1, D1, n1, bad);
+        if (!lng) {
+          lds_or(kimg + ((D1 + n1) >> 3), 0x3Aull << (8 * ((D1 + n1) & 7u)));
+          put_range(kimg, W2, D3, n2, bad);
+        }
+        if (e) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
+          const uint32_t D4 = D3 + n2;
+          if (e32) {
+            lds_put(kimg, D4, 0x73723Aull | (de.lo << 24));
+            if (de.n > 5) lds_put(kimg, D4 + 8, (de.lo >> 40) | (de.hi << 24));
+          } else {
+            Out<true, true> o(LdsImage{}, kimg, D4);
+            o.lit(":rs");
+            o.u64v(e);
+            o.finish();
+          }
+        }
+        bad &= kHiBits;
+      } else {  // a range past the window, or a span outside the image: piece by piece
+        auto render_key = [&](auto o) {
+          append2(o, q0, q1, lp);
+          if (lng) {
+            o.bytes((glb_cp)(A.digest + 32 * i), AVDB_DIGEST_CHARS);
+          } else {
+            const uint64_t off = cur.off;
+            if (!key_allele_ok((glb_cp)(A.heap + off), r + a)) bad = kHiBits;
+            o.bytes((glb_cp)(A.heap + off), r);
+            o.put(':');
+            o.bytes((glb_cp)(A.heap + off + r), a);
+          }
+          if (e) {
+            o.lit(":rs");
+            o.u64v(e);
+          }
+          return o;
+        };
+        if (kst) {
+          Out<true, true> o(LdsImage{}, kimg, D0);
+          render_key(o).finish();
+        } else {
+          Out<true> o(A.key_out, ko);
+          render_key(o).finish();
+        }
+      }
+      if (bad) st = AVDB_KEY_HOST;
+    }
+#else
     // the body's two ranges: a long record's 32 digest characters, or ref then alt
     // (windows loaded up front, independent of each other)
     const bool kok = st == AVDB_KEY_OK;
@@ -981,8 +1140,13 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
       m2 = uint32_t(s2 & 7);
       wide = m1 + n1 > 8 * kWinWords || m2 + n2 > 8 * kWinWords;
       const Heap h1 = lng ? Heap{s1, s1 + AVDB_DIGEST_CHARS} : hheap;
-      load_win(W1, s1, wide ? 0u : n1, h1);
-      load_win(W2, s2, wide ? 0u : n2, hheap);
+      if (!K7X(128)) {
+        load_win(W1, s1, wide ? 0u : n1, h1);
+        load_win(W2, s2, wide ? 0u : n2, hheap);
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < kWinWords; ++k) W1[k] = W2[k] = uint64_t(s1 ^ s2) * (k + 1);
+      }
     } else {
 #pragma unroll
       for (uint32_t k = 0; k < kWinWords; ++k) W1[k] = W2[k] = 0;
@@ -992,9 +1156,12 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
     uint64_t bad = 0;
     auto render_key = [&](auto o) {  // primary_key_generator.py:106-122
       uint64_t q0, q1;
-      const uint32_t lp = key_prefix(c, dp, &q0, &q1);
-      append2(o, q0, q1, lp);
-      if (!wide) {
+      if (!K7X(32)) {
+        const uint32_t lp = key_prefix(c, dp, &q0, &q1);
+        append2(o, q0, q1, lp);
+      }
+      if (K7X(8)) {
+      } else if (!wide) {
         append_win(o, W1, m1, n1, bad);
         if (!lng) o.put(':');
         append_win(o, W2, m2, n2, bad);
@@ -1005,7 +1172,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
         o.put(':');
         o.bytes((glb_cp)(A.heap + off + r), a);
       }
-      if (e) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
+      if (e && !K7X(16)) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
         if (e32) {
           append2(o, 0x73723Aull | (de.lo << 24), (de.lo >> 40) | (de.hi << 24), 3 + de.n);
         } else {
@@ -1015,7 +1182,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
       }
       return o;
     };
-    if (kok) {
+    if (kok && !K7X(1)) {
       if (kst) {
         Out<true, true> o(LdsImage{}, kimg, ko - (gk0 & ~uint64_t(15)));
         render_key(o).finish();
@@ -1025,6 +1192,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
       }
       if (bad) st = AVDB_KEY_HOST;
     }
+#endif
     // stream 1: ltree paths
     bool pst = false, path_over = false;
     if (A.code) {
@@ -1032,7 +1200,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
       const uint32_t cd = live ? cur.cd : AVDB_BIN_NONE;
       const bool has_path = live && cd != AVDB_BIN_NONE && c < n_chrom;
       path_over = has_path && po1 > A.path_cap;
-      if (has_path && !path_over) {
+      if (has_path && !path_over && !K7X(2)) {
         if (pst) {
           Out<true, true> o(LdsImage{}, pimg, po - (gp0 & ~uint64_t(15)));
           bin_path(o, c, cd).finish();
@@ -1044,8 +1212,8 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
     }
     if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
     wave_lds_sync();
-    if (kst) flush_span32(kimg, A.key_out, gk0, gk1, lane);
-    if (pst) flush_span32(pimg, A.path_out, gp0, gp1, lane);
+    if (kst && !K7X(64)) flush_span32(kimg, A.key_out, gk0, gk1, lane);
+    if (pst && !K7X(64)) flush_span32(pimg, A.path_out, gp0, gp1, lane);
     wave_lds_sync();
   }
 }

@@ -327,7 +327,7 @@ static int count_pass(const uint8_t* text, size_t text_bytes, void* ws, unsigned
   return AVDB_OK;
 }
 
-static size_t scan_temp_bytes(size_t n) { return (scan::workspace_bytes(n) + 255) & ~size_t(255); }
+static size_t scan_temp_bytes(size_t n) { return (scan::workspace_bytes(n, 2) + 255) & ~size_t(255); }
 
 extern "C" int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes) {
   (void)text_bytes;
@@ -406,8 +406,7 @@ extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
   hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, starts,
                      lines, rc, hc, cm, min_fields);
   AVDB_LAUNCH_CHECK("k_vcf_parse");
-  if (int e = scan::exclusive_u64(rec_off, rec_off, n_lines + 1, tmp, tmp_bytes, s)) return e;
-  if (int e = scan::exclusive_u64(heap_off, heap_off, n_lines + 1, tmp, tmp_bytes, s)) return e;
+  if (int e = scan::exclusive_u64_pair(rec_off, rec_off, heap_off, heap_off, n_lines + 1, tmp, tmp_bytes, s)) return e;
   return AVDB_OK;
 }
 
