@@ -74,12 +74,26 @@ AVDB_HD Heap make_heap(const uint8_t* p, size_t bytes) {
   return Heap{reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + bytes};
 }
 
+// A device load from an integer address goes through a global-address-space
+// pointer: a generic pointer made from an integer is a FLAT access, which counts on
+// both vmcnt and lgkmcnt and retires out of order, so every use of its result
+// waits vmcnt(0) + lgkmcnt(0) — behind every older store and LDS operation.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define AVDB_GLOBAL __attribute__((address_space(1)))
+#else
+#define AVDB_GLOBAL
+#endif
+template <class T>
+AVDB_HD const AVDB_GLOBAL T* gptr(uintptr_t a) {
+  return reinterpret_cast<const AVDB_GLOBAL T*>(a);
+}
+
 AVDB_HD uint64_t heap_word(uintptr_t a, const Heap& h) {  // a 8-aligned
-  if (a >= h.lo && a + 8 <= h.hi) return *reinterpret_cast<const uint64_t*>(a);
+  if (a >= h.lo && a + 8 <= h.hi) return *gptr<uint64_t>(a);
   uint64_t v = 0;
   for (int k = 0; k < 8; ++k) {
     const uintptr_t b = a + k;
-    if (b >= h.lo && b < h.hi) v |= uint64_t(*reinterpret_cast<const uint8_t*>(b)) << (8 * k);
+    if (b >= h.lo && b < h.hi) v |= uint64_t(*gptr<uint8_t>(b)) << (8 * k);
   }
   return v;
 }

@@ -592,7 +592,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
               // the whole window inside: plain loads, one bounds check per record instead of per word
 #pragma unroll
               for (uint32_t k = 0; k < kKeyWords; ++k)
-                if (k < nw) w[k] = *reinterpret_cast<const uint64_t*>(aw + 8 * k);
+                if (k < nw) w[k] = *gptr<uint64_t>(aw + 8 * k);
             } else {
 #pragma unroll
               for (uint32_t k = 0; k < kKeyWords; ++k)
@@ -815,7 +815,7 @@ __device__ __forceinline__ void load_win(uint64_t (&W)[kWinWords], uintptr_t src
     // the whole window inside the allocation: all seven words, no per-word select
     // (words past the range are only ever read under a byte mask)
 #pragma unroll
-    for (uint32_t k = 0; k < kWinWords; ++k) W[k] = reinterpret_cast<const uint64_t*>(aw)[k];
+    for (uint32_t k = 0; k < kWinWords; ++k) W[k] = gptr<uint64_t>(aw)[k];
   } else {
 #pragma unroll
     for (uint32_t k = 0; k < kWinWords; ++k) W[k] = k < nw ? heap_word(aw + 8 * k, h) : 0ull;
@@ -870,81 +870,6 @@ __device__ __forceinline__ void append2(O& o, uint64_t w0, uint64_t w1, uint32_t
     if (n > 8) o.append(w1 & low_bytes_mask(n - 8), n - 8);
   } else {
     o.append(w0 & low_bytes_mask(n), n);
-  }
-}
-
-#ifndef AVDB_K7_POS
-#define AVDB_K7_POS 0  // 1: keys rendered piece-at-position (A/B; 0: the append sink)
-#endif
-#ifndef AVDB_K7_POS_UNALIGNED
-#define AVDB_K7_POS_UNALIGNED 1  // body windows by unaligned loads (0: aligned loads + a funnel shift)
-#endif
-#ifndef AVDB_K7_PUT_COND
-#define AVDB_K7_PUT_COND 0  // lds_put's second word only when the piece is unaligned
-#endif
-__device__ __forceinline__ void lds_or(lds_u64* w, uint64_t v) {
-  __hip_atomic_fetch_or(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// OR up to 8 bytes x (bytes past them zero) into the image at byte D: two words
-// (the second gets 0 when D is aligned: (x >> 1) >> 63 is 0)
-__device__ __forceinline__ void lds_put(lds_u64* img, uint32_t D, uint64_t x) {
-  const uint32_t k = 8 * (D & 7u), q = D >> 3;
-  lds_or(img + q, x << k);
-  if (!AVDB_K7_PUT_COND || k) lds_or(img + q + 1, (x >> 1) >> (63 - k));
-}
-
-// bytes [a, a + need) as kWinWords unaligned words from address a (need <= 56);
-// bytes outside h read as 0 (then word by word from aligned loads)
-__device__ __forceinline__ void load_win_at(uint64_t (&W)[kWinWords], uintptr_t a, uint32_t need, const Heap& h) {
-  if (AVDB_K7_POS_UNALIGNED && a >= h.lo && a + 8 * kWinWords <= h.hi) {
-#pragma unroll
-    for (uint32_t k = 0; k < kWinWords; ++k) W[k] = reinterpret_cast<g_u64u>(a + 8 * k)->v;
-  } else if (!AVDB_K7_POS_UNALIGNED && (a & ~uintptr_t(7)) >= h.lo && (a & ~uintptr_t(7)) + 8 * kWinWords + 8 <= h.hi) {
-    // aligned words, one funnel shift per word
-    const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~uintptr_t(7));
-    const uint32_t sh = 8 * uint32_t(a & 7);
-    uint64_t prev = w[0];
-#pragma unroll
-    for (uint32_t k = 0; k < kWinWords; ++k) {
-      const uint64_t nx = w[k + 1];
-      W[k] = (prev >> sh) | ((nx << 1) << (63 - sh));
-      prev = nx;
-    }
-  } else {
-    const uintptr_t a0 = a & ~uintptr_t(7);
-    const uint32_t sh = 8 * uint32_t(a & 7), lim = need ? need + uint32_t(a & 7) : 0u;
-    uint64_t prev = lim ? heap_word(a0, h) : 0ull;
-#pragma unroll
-    for (uint32_t k = 0; k < kWinWords; ++k) {
-      const uint64_t nx = 8 * (k + 1) < lim ? heap_word(a0 + 8 * (k + 1), h) : 0ull;
-      W[k] = sh ? (prev >> sh) | (nx << (64 - sh)) : prev;
-      prev = nx;
-    }
-  }
-}
-
-// window words 0.. of a range of n bytes placed at image byte D (word 0 holds
-// D & 7 bytes that are not the range's): masked at both ends, ORed in place;
-// bad collects key_bad's pre-mask terms (the caller masks with kHiBits once).
-// The loop ends when no lane has words left (wave-uniform).
-__device__ __forceinline__ void put_range(lds_u64* img, const uint64_t (&W)[kWinWords], uint32_t D, uint32_t n,
-                                          uint64_t& bad) {
-  const uint32_t k = D & 7u, end = k + n;
-  lds_u64* q = img + (D >> 3);
-#pragma unroll
-  for (uint32_t j = 0; j < kWinWords; ++j) {
-    if (!__any(end > 8 * j)) break;
-    if (end > 8 * j) {
-      uint64_t x = W[j];
-      if (j == 0) x &= ~low_bytes_mask(k);
-      if (end < 8 * j + 8) x &= low_bytes_mask(end - 8 * j);
-      if (!K7X(4)) {
-        const uint64_t v = x ^ 0x3A3A3A3A3A3A3A3Aull;
-        bad |= ((v - 0x0101010101010101ull) & ~v) | x;
-      }
-      lds_or(q + j, x);
-    }
   }
 }
 
@@ -1042,82 +967,6 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
       else if (!lng && cur.off + r + a > A.heap_bytes) st = AVDB_KEY_HOST;
       if (st == AVDB_KEY_OK && ko1 > A.key_cap) st = AVDB_KEY_OVERFLOW;
     }
-#if AVDB_K7_POS
-    // stream 0: keys, each piece ORed into the image at its own byte position
-    // (primary_key_generator.py:106-122): "label:pos:" at D0, the body range (32
-    // digest characters, or ref) at D1, ':' and alt at D2 / D3, ":rs<id>" at D4.
-    // The body ranges are read through unaligned 8-byte loads that start (D & 7)
-    // bytes before the range, so every loaded word is already an image word: no
-    // source shift, no destination shift, no pending word carried between pieces.
-    const bool kok = st == AVDB_KEY_OK;
-    const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap;
-    uint64_t bad = 0;
-    uint64_t q0, q1;
-    const uint32_t lp = key_prefix(c, dp, &q0, &q1);
-    const uint32_t D0 = uint32_t(ko - (gk0 & ~uint64_t(15)));
-    const uint32_t D1 = D0 + lp;
-    const uint32_t n1 = lng ? uint32_t(AVDB_DIGEST_CHARS) : r, n2 = lng ? 0u : a;
-    const uint32_t D3 = D1 + n1 + (lng ? 0u : 1u);
-    const uint32_t k1 = D1 & 7u, k3 = D3 & 7u;
-    // the positional form: an LDS-image span and both ranges within a window
-    const bool fast = kok && kst && k1 + n1 <= 8 * kWinWords && k3 + n2 <= 8 * kWinWords;
-    if (kok && !K7X(1)) {
-      if (fast) {
-        uint64_t W1[kWinWords], W2[kWinWords];
-        const uintptr_t s1 = lng ? reinterpret_cast<uintptr_t>(A.digest) + 32 * i
-                                 : reinterpret_cast<uintptr_t>(A.heap) + cur.off;
-        const Heap h1 = lng ? make_heap(reinterpret_cast<const uint8_t*>(A.digest), 32 * A.n) : hheap;
-        load_win_at(W1, s1 - k1, k1 + n1, h1);
-        load_win_at(W2, s1 + r - k3, lng ? 0u : k3 + n2, hheap);
-        lds_put(kimg, D0, q0);
-        if (lp > 8) lds_put(kimg, D0 + 8, q1);
-        put_range(kimg, W1, D1, n1, bad);
-        if (!lng) {
-          lds_or(kimg + ((D1 + n1) >> 3), 0x3Aull << (8 * ((D1 + n1) & 7u)));
-          put_range(kimg, W2, D3, n2, bad);
-        }
-        if (e) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
-          const uint32_t D4 = D3 + n2;
-          if (e32) {
-            lds_put(kimg, D4, 0x73723Aull | (de.lo << 24));
-            if (de.n > 5) lds_put(kimg, D4 + 8, (de.lo >> 40) | (de.hi << 24));
-          } else {
-            Out<true, true> o(LdsImage{}, kimg, D4);
-            o.lit(":rs");
-            o.u64v(e);
-            o.finish();
-          }
-        }
-        bad &= kHiBits;
-      } else {  // a range past the window, or a span outside the image: piece by piece
-        auto render_key = [&](auto o) {
-          append2(o, q0, q1, lp);
-          if (lng) {
-            o.bytes((glb_cp)(A.digest + 32 * i), AVDB_DIGEST_CHARS);
-          } else {
-            const uint64_t off = cur.off;
-            if (!key_allele_ok((glb_cp)(A.heap + off), r + a)) bad = kHiBits;
-            o.bytes((glb_cp)(A.heap + off), r);
-            o.put(':');
-            o.bytes((glb_cp)(A.heap + off + r), a);
-          }
-          if (e) {
-            o.lit(":rs");
-            o.u64v(e);
-          }
-          return o;
-        };
-        if (kst) {
-          Out<true, true> o(LdsImage{}, kimg, D0);
-          render_key(o).finish();
-        } else {
-          Out<true> o(A.key_out, ko);
-          render_key(o).finish();
-        }
-      }
-      if (bad) st = AVDB_KEY_HOST;
-    }
-#else
     // the body's two ranges: a long record's 32 digest characters, or ref then alt
     // (windows loaded up front, independent of each other)
     const bool kok = st == AVDB_KEY_OK;
@@ -1192,7 +1041,6 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
       }
       if (bad) st = AVDB_KEY_HOST;
     }
-#endif
     // stream 1: ltree paths
     bool pst = false, path_over = false;
     if (A.code) {

@@ -90,7 +90,7 @@ __device__ __forceinline__ Window stage_window(const Heap& h, size_t s0, size_t 
       const uintptr_t a = w.a0 + 16 * i;
       u32x4 v;
       if (a >= h.lo && a + 16 <= h.hi) {
-        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a));
+        v = __builtin_nontemporal_load(gptr<u32x4>(a));
       } else {
         const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
         v = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};

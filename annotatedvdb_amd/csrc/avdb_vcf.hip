@@ -63,7 +63,7 @@ __device__ __forceinline__ Mask16 nl_mask16(uintptr_t a, const Heap& h, uintptr_
   if (a >= end) return Mask16{0, 0, 0};
   uint64_t x, y;
   if (a >= h.lo && a + 16 <= h.hi) {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a));
+    const u32x4 v = __builtin_nontemporal_load(gptr<u32x4>(a));
     x = uint64_t(v[0]) | uint64_t(v[1]) << 32;
     y = uint64_t(v[2]) | uint64_t(v[3]) << 32;
   } else {

@@ -49,7 +49,7 @@ def main():
             if k in c:
                 row[k.replace("SQ_INSTS_", "").lower() + "_per_tile"] = round(c[k] / TILES, 1)
         out.append(row)
-    base = next((r for r in out if r["variant"] == "x0"), None)
+    base = next((r for r in out if r["variant"] in ("x0", "xbase")), None)
     if base:
         for r in out:
             if r is not base and r.get("keys_paths_ms") and base.get("keys_paths_ms"):
