@@ -827,15 +827,20 @@ class Engine:
             last_nl = host.endswith(b"\n") if host else True
         else:
             text_t = self._dev(text)
-            last_nl = bool(text_t.numel() == 0 or int(text_t[-1].item()) == 10)
+            last_nl = None  # (read with the newline count: one host sync, not two)
         nb = int(text_t.numel())
         tp = N.ptr(text_t) if nb else None
         s = self._stream()
         ws0 = self.empty(N.VCF_COUNT_WORKSPACE_BYTES, torch.uint8)
-        nl = torch.zeros(1, dtype=torch.int64, device=self.device)
+        nl = torch.zeros(2, dtype=torch.int64, device=self.device)  # newlines, last byte
         N.check("avdb_vcf_count_lines", self.lib.avdb_vcf_count_lines(
             self.ctx, tp, nb, N.ptr(ws0), ws0.numel(), N.ptr(nl), s))
-        n_nl = int(nl.item())
+        if last_nl is None and nb:
+            nl[1:2].copy_(text_t[-1:])
+        got = nl.cpu()
+        n_nl = int(got[0])
+        if last_nl is None:
+            last_nl = nb == 0 or int(got[1]) == 10
         n_lines = n_nl + (0 if (last_nl or nb == 0) else 1)
         sz = ctypes.c_size_t()
         self.lib.avdb_vcf_workspace_size(nb, n_lines, ctypes.byref(sz))
