@@ -26,6 +26,9 @@
 namespace avdb {
 
 constexpr int kVcfGrid = 1024;
+#ifndef AVDB_VCF_WINDOW_PARSE
+#define AVDB_VCF_WINDOW_PARSE 1  // parse windows with their own line starts (0: the k_vcf_starts pass, A/B)
+#endif
 
 __device__ __forceinline__ uint32_t count_byte(uint64_t x, uint64_t pattern) {
   return uint32_t(__popcll(zero_bytes_mask(x ^ pattern)));
@@ -55,12 +58,11 @@ __device__ __forceinline__ void wave_range(size_t text_bytes, size_t gw, size_t*
 // restricted to [lo, end)
 struct Mask16 {
   uint64_t m0, m1;
-  uint32_t commas;  // ',' bytes in the same range (k_vcf_count; dead code elsewhere)
 };
 
 __device__ __forceinline__ Mask16 nl_mask16(uintptr_t a, const Heap& h, uintptr_t lo, uintptr_t end) {
   uint64_t m0 = 0, m1 = 0;
-  if (a >= end) return Mask16{0, 0, 0};
+  if (a >= end) return Mask16{0, 0};
   uint64_t x, y;
   if (a >= h.lo && a + 16 <= h.hi) {
     const u32x4 v = __builtin_nontemporal_load(gptr<u32x4>(a));
@@ -72,49 +74,67 @@ __device__ __forceinline__ Mask16 nl_mask16(uintptr_t a, const Heap& h, uintptr_
   }
   m0 = zero_bytes_mask(x ^ kNL) & 0x8080808080808080ull;
   m1 = zero_bytes_mask(y ^ kNL) & 0x8080808080808080ull;
-  uint64_t k0 = bytes_eq_mask(x, ','), k1 = bytes_eq_mask(y, ',');
   if (a < lo) {
     const uint32_t sh = uint32_t(lo - a);  // 1..15 bytes before the range
-    if (sh >= 8) { m0 = 0; m1 &= ~low_bytes_mask(sh - 8); k0 = 0; k1 &= ~low_bytes_mask(sh - 8); }
-    else { m0 &= ~low_bytes_mask(sh); k0 &= ~low_bytes_mask(sh); }
+    if (sh >= 8) { m0 = 0; m1 &= ~low_bytes_mask(sh - 8); }
+    else m0 &= ~low_bytes_mask(sh);
   }
   if (a + 16 > end) {
     const uint32_t keep = uint32_t(end - a);  // 1..15 bytes inside the range
-    if (keep <= 8) { m1 = 0; m0 &= low_bytes_mask(keep); k1 = 0; k0 &= low_bytes_mask(keep); }
-    else { m1 &= low_bytes_mask(keep - 8); k1 &= low_bytes_mask(keep - 8); }
+    if (keep <= 8) { m1 = 0; m0 &= low_bytes_mask(keep); }
+    else m1 &= low_bytes_mask(keep - 8);
   }
-  return Mask16{m0, m1, uint32_t(__popcll(k0) + __popcll(k1))};
+  return Mask16{m0, m1};
 }
 
 constexpr int kNlUnroll = 4;                           // 16-byte lane loads in flight
 constexpr uintptr_t kNlStep = 16 * kWave;              // bytes per wave load
 
+// The parse pass's windows: each wave sub-chunk [t0, t1) is cut into windows of
+// kParseWin bytes from t0; with a count workspace of avdb_vcf_count_workspace_size
+// bytes the count pass also writes every window's newline count, and the parse
+// pass then takes one workgroup per window and finds its line starts itself.
+#ifndef AVDB_VCF_PARSE_WIN_KB
+#define AVDB_VCF_PARSE_WIN_KB 28  // window size (A/B knob; a multiple of 4)
+#endif
+// (8.4 M dbSNP lines: 16 / 20 / 24 / 28 KB windows 2.14 / 2.02 / 1.90 / 1.88 ms per
+// tokenize: the per-window costs — the staged overhang, the bitmaps, the search for
+// the last line's end — favour the largest window the stage holds)
+constexpr uint32_t kParseWin = AVDB_VCF_PARSE_WIN_KB * 1024;   // (a multiple of kNlUnroll * kNlStep)
+constexpr uint32_t kParseOver = kStage - kParseWin - 64 < 4096u ? kStage - kParseWin - 64 : 4096u;  // staged past a window
+static_assert(kParseWin % (kNlUnroll * kNlStep) == 0, "window / count step");
+
 __global__ __launch_bounds__(kBlock) void k_vcf_count(const uint8_t* __restrict__ text,
                                                       size_t text_bytes,
                                                       uint32_t* __restrict__ wave_cnt,
-                                                      unsigned long long* __restrict__ commas) {
+                                                      uint32_t* __restrict__ win_cnt, uint32_t wps) {
   const Heap h = make_heap(text, text_bytes);
   const size_t gw = size_t(blockIdx.x) * kVcfWaves + threadIdx.x / kWave;
   size_t t0, t1;
   wave_range(text_bytes, gw, &t0, &t1);
-  const uintptr_t lo = h.lo + t0, end = h.lo + t1;
-  uint32_t c = 0, k = 0;
-  for (uintptr_t a = (lo & ~uintptr_t(15)) + 16 * __lane_id(); a < end; a += kNlUnroll * kNlStep) {
-    Mask16 m[kNlUnroll];
+  uint32_t c = 0;
+  uint32_t wk = 0;
+  for (size_t w0 = t0; w0 < t1; w0 += kParseWin, ++wk) {  // (one trip without windows: kParseWin is
+    const size_t w1 = win_cnt && w0 + kParseWin < t1 ? w0 + kParseWin : t1;  //  then the whole sub-chunk)
+    const uintptr_t lo = h.lo + w0, end = h.lo + w1;
+    uint32_t cw = 0;
+    for (uintptr_t a = (lo & ~uintptr_t(15)) + 16 * __lane_id(); a < end; a += kNlUnroll * kNlStep) {
+      Mask16 m[kNlUnroll];
 #pragma unroll
-    for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask16(a + u * kNlStep, h, lo, end);
+      for (int u = 0; u < kNlUnroll; ++u) m[u] = nl_mask16(a + u * kNlStep, h, lo, end);
 #pragma unroll
-    for (int u = 0; u < kNlUnroll; ++u) {
-      c += uint32_t(__popcll(m[u].m0) + __popcll(m[u].m1));
-      k += m[u].commas;
+      for (int u = 0; u < kNlUnroll; ++u) cw += uint32_t(__popcll(m[u].m0) + __popcll(m[u].m1));
     }
+    if (win_cnt) {
+      uint32_t x = cw;
+      for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, kWave);
+      if (__lane_id() == 0 && wk < wps) win_cnt[gw * wps + wk] = x;
+    }
+    c += cw;
+    if (!win_cnt) break;
   }
   for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
   if (__lane_id() == 0) wave_cnt[gw] = c;
-  if (commas) {  // (a bound on the records: every record is a line or follows a comma)
-    for (int d = 32; d > 0; d >>= 1) k += __shfl_xor(k, d, kWave);
-    if (__lane_id() == 0 && k) atomicAdd(commas, (unsigned long long)k);
-  }
 }
 
 // per-workgroup newline totals -> exclusive offsets (one workgroup of kVcfGrid threads)
@@ -233,6 +253,195 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
   }
 }
 
+// ---- k_vcf_parse_windows: the parse pass without the line-starts pass ---------
+// One workgroup per window (kParseWin bytes of a count-pass sub-chunk, whose
+// newline count the count pass wrote).  The window is staged in LDS with the byte
+// before it and kParseOver bytes after it; newline bitmaps (64 bytes per bitmap
+// word, two adjacent words per thread, so the block scan numbers lines in text
+// order) give the starts of the lines that begin in it; the end of its last line is
+// the first '\n' at or after its last byte; then one lane per line parses it
+// (parse_line, as k_vcf_parse), 256 lines a round.  Lines start at byte 0 and
+// after every '\n' except a final one.
+static_assert(kParseWin % 64 == 0 && kParseWin / 64 + 2 <= 2 * kBlock, "window bitmap words");
+static_assert(kParseWin + kParseOver + 32 <= kStage, "window stage");
+
+__device__ __forceinline__ uint32_t nl_bits8(uint64_t w) {  // bit k: byte k of w is '\n'
+  const uint64_t m = zero_bytes_mask(w ^ kNL) & kHiBits;
+  return uint32_t(((m >> 7) * 0x0102040810204080ull) >> 56);
+}
+
+// exclusive block scan of one u32 per thread (kBlock threads); *total = sum
+__device__ __forceinline__ uint32_t block_excl32(uint32_t v, uint32_t* s_w, uint32_t* total) {
+  const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t u = __shfl_up(x, d, kWave);
+    if (lane >= uint32_t(d)) x += u;
+  }
+  if (lane == kWave - 1) s_w[wv] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kVcfWaves; ++w) {
+    const uint32_t t = s_w[w];
+    if (w < wv) base += t;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
+                                                              size_t n_lines,
+                                                              const unsigned long long* __restrict__ blk_off,
+                                                              const uint32_t* __restrict__ wave_cnt,
+                                                              const uint32_t* __restrict__ win_cnt, uint32_t wps,
+                                                              avdb_vcf_line* __restrict__ lines,
+                                                              unsigned long long* __restrict__ rec_cnt,
+                                                              unsigned long long* __restrict__ heap_cnt,
+                                                              ChromMapView cm, uint32_t min_fields) {
+  __shared__ u32x4 s_text[kStage / 16];
+  __shared__ uint32_t s_start[kBlock + 1];  // line starts of the round, relative to the window start
+  __shared__ uint32_t s_w[kVcfWaves];
+  __shared__ uint32_t s_tail;               // (first '\n' at or after w1 - 1) + 1 - w0
+  const Heap h = make_heap(text, text_bytes);
+  const size_t nb = text_bytes;
+  const uint32_t tid = threadIdx.x, lane = __lane_id(), wv = tid / kWave;
+  const size_t gw = blockIdx.x / wps;
+  const uint32_t wk = blockIdx.x % wps;
+  size_t t0, t1;
+  wave_range(nb, gw, &t0, &t1);
+  const size_t w0 = t0 + size_t(wk) * kParseWin;
+  if (w0 >= t1) return;  // (uniform)
+  const size_t w1 = w0 + kParseWin < t1 ? w0 + kParseWin : t1;
+  // lines starting before w0: 1 + the newlines in [0, w0 - 1)
+  size_t li0 = 0;
+  if (w0) {
+    unsigned long long k = blk_off[gw / kVcfWaves];
+    for (size_t w = (gw / kVcfWaves) * kVcfWaves; w < gw; ++w) k += wave_cnt[w];
+    for (uint32_t j = 0; j < wk; ++j) k += win_cnt[gw * wps + j];
+    li0 = 1 + k - (text[w0 - 1] == '\n' ? 1u : 0u);
+  }
+  const lds_cp64 lw = (lds_cp64)(reinterpret_cast<const uint64_t*>(s_text));
+  const size_t q0 = w0 ? w0 - 1 : 0;  // newline positions [q0, w1 - 1) start this window's lines
+  // ---- stage [q0, w1 + kParseOver) ----
+  const uintptr_t a0 = (h.lo + q0) & ~uintptr_t(15);
+  const uintptr_t wend = h.lo + (w1 + kParseOver < nb ? w1 + kParseOver : nb);
+  const uint32_t n16 = uint32_t((wend - a0 + 15) / 16);
+  for (uint32_t i = tid; i < n16; i += kBlock) {
+    const uintptr_t a = a0 + 16 * size_t(i);
+    u32x4 v;
+    if (a >= h.lo && a + 16 <= h.hi) {
+      v = __builtin_nontemporal_load(gptr<u32x4>(a));
+    } else {
+      const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
+      v = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};
+    }
+    s_text[i] = v;
+  }
+  __syncthreads();
+  // ---- newline bitmaps of [q0, w1 - 1) ----
+  const uint32_t o_lo = uint32_t(h.lo + q0 - a0), o_hi = uint32_t(h.lo + w1 - 1 - a0);
+  const uint32_t nblk = w1 - 1 > q0 ? (o_hi + 63) / 64 : 0u;
+  uint64_t bm[2] = {0, 0};
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t b = 2 * tid + k;
+    if (b < nblk) {
+      uint64_t m = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) m |= uint64_t(nl_bits8(lw[8 * b + q])) << (8 * q);
+      const uint32_t blo = 64 * b;
+      if (o_lo > blo) m &= o_lo - blo >= 64 ? 0ull : ~0ull << (o_lo - blo);
+      if (o_hi < blo + 64) m &= o_hi <= blo ? 0ull : ~0ull >> (64 - (o_hi - blo));
+      bm[k] = m;
+      cnt += uint32_t(__popcll(m));
+    }
+  }
+  uint32_t T;
+  const uint32_t pref = block_excl32(cnt, s_w, &T);
+  const uint32_t first = w0 == 0 ? 1u : 0u;  // line 0 starts at byte 0
+  T += first;
+  if (!T) return;  // (uniform; no line starts here)
+  // ---- the end of the window's last line: first '\n' at or after w1 - 1 ----
+  if (wv == 0) {
+    size_t q = w1 - 1;
+    uint32_t found = 0;
+    const uint32_t ob = uint32_t(h.lo + q - a0), oe = uint32_t(wend - a0);
+    for (uint32_t o = ob & ~7u; o < oe && !found; o += 8 * kWave) {  // in the staged overhang
+      const uint32_t wo = o + 8 * lane;
+      uint32_t m = wo < oe ? nl_bits8(lw[wo / 8]) : 0u;
+      if (wo < ob) m &= ob - wo >= 8 ? 0u : ~0u << (ob - wo);
+      if (wo + 8 > oe) m &= oe <= wo ? 0u : 0xFFu >> (8 - (oe - wo));
+      const uint64_t bal = __ballot(m != 0);
+      if (bal) {
+        const uint32_t l = uint32_t(__ffsll((unsigned long long)bal)) - 1;
+        const uint32_t ml = __shfl(m, l, kWave);
+        q = (a0 - h.lo) + o + 8 * l + uint32_t(__builtin_ctz(ml));
+        found = 1;
+      }
+    }
+    for (uintptr_t ga = wend & ~uintptr_t(7); !found && ga < h.hi; ga += 8 * kWave) {  // past it
+      const uintptr_t wa = ga + 8 * lane;
+      uint32_t m = wa < h.hi ? nl_bits8(text_word(wa, h)) : 0u;
+      if (wa < wend) m &= wend - wa >= 8 ? 0u : ~0u << (wend - wa);
+      const uint64_t bal = __ballot(m != 0);
+      if (bal) {
+        const uint32_t l = uint32_t(__ffsll((unsigned long long)bal)) - 1;
+        const uint32_t ml = __shfl(m, l, kWave);
+        q = (ga - h.lo) + 8 * l + uint32_t(__builtin_ctz(ml));
+        found = 1;
+      }
+    }
+    if (lane == 0) s_tail = uint32_t((found ? q + 1 : nb + 1) - w0);
+  }
+  // ---- parse: rounds of kBlock lines ----
+  const uint32_t rounds = (T + kBlock - 1) / kBlock;
+  for (uint32_t r = 0; r < rounds; ++r) {
+    const uint32_t lo = kBlock * r, hi = lo + kBlock;
+    if (r == 0 && first && tid == 0) s_start[0] = 0;
+    uint32_t idx = first + pref;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint64_t m = bm[k];
+      while (m && idx <= hi) {
+        const uint32_t bit = uint32_t(__builtin_ctzll(m));
+        m &= m - 1;
+        if (idx >= lo) s_start[idx - lo] = uint32_t(a0 - h.lo - w0) + 64 * (2 * tid + k) + bit + 1;
+        ++idx;
+      }
+    }
+    if (tid == 0 && T <= hi) s_start[T - lo] = s_tail;
+    __syncthreads();
+    const size_t li = li0 + lo + tid;
+    if (lo + tid < T && li < n_lines) {
+      avdb_vcf_line L;
+      L.start = w0 + s_start[tid];
+      size_t nl = w0 + s_start[tid + 1] - 1;  // its newline, or the text end
+      if (nl < L.start || nl > nb) nl = L.start;  // (never expected: starts increase)
+      const uint32_t raw = uint32_t(nl - L.start);
+      const uint32_t mis = uint32_t((h.lo + L.start) & 7);
+      uint64_t recs, hbytes;
+      if (h.lo + nl <= wend) {
+        const uint8_t* ls = reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - a0);
+        const lds_cp64 lw2 = (lds_cp64)(reinterpret_cast<const uint64_t*>(ls - mis));
+        parse_line((lds_cp)ls, [lw2](uint32_t k) { return lw2[k]; }, mis, raw, L, recs, hbytes, cm, min_fields);
+      } else {
+        const uintptr_t la = h.lo + L.start - mis;
+        parse_line((glb_cp)(text + L.start), [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); }, mis,
+                   raw, L, recs, hbytes, cm, min_fields);
+      }
+      lines[li] = L;
+      rec_cnt[li] = recs;
+      heap_cnt[li] = hbytes;
+    }
+    __syncthreads();  // s_start is refilled by the next round
+  }
+}
+
 // (Rendering the allele heap through an LDS image of the tile's heap span with a
 // coalesced flush, as K7 does for its text, measured slower: 0.66 vs 0.60 ms for
 // 8.4 M lines — the pass is bound by re-staging the text, not by these stores.)
@@ -314,13 +523,37 @@ __global__ __launch_bounds__(kBlock) void k_vcf_emit(
 using namespace avdb;
 
 // k_vcf_count + k_vcf_scan_blocks into a count workspace (layout: kCountWs*)
-static int count_pass(const uint8_t* text, size_t text_bytes, void* ws, unsigned long long* total,
-                      hipStream_t s, unsigned long long* commas = nullptr) {
+// the count pass's cut (wave_range) and the parse windows inside it, host side
+static size_t sub_chunk_bytes(size_t text_bytes) {
+  const size_t nw = size_t(kVcfGrid) * kVcfWaves;
+  const size_t per = (text_bytes + nw - 1) / nw;
+  return (per + 63) & ~size_t(63);
+}
+static uint32_t windows_per_chunk(size_t text_bytes) {
+  const size_t per = sub_chunk_bytes(text_bytes);
+  return per ? uint32_t((per + kParseWin - 1) / kParseWin) : 1u;
+}
+static size_t count_ws_full(size_t text_bytes) {  // header part + one u32 per window
+  return AVDB_VCF_COUNT_WORKSPACE_BYTES +
+         ((4 * size_t(kVcfGrid) * kVcfWaves * windows_per_chunk(text_bytes) + 255) & ~size_t(255));
+}
+
+extern "C" int avdb_vcf_count_workspace_size(size_t text_bytes, size_t* bytes) {
+  if (!bytes) return AVDB_EINVAL;
+  *bytes = count_ws_full(text_bytes);
+  return AVDB_OK;
+}
+
+// k_vcf_count + k_vcf_scan_blocks into a count workspace (layout: kCountWs*, then
+// the window counts when `windows`)
+static int count_pass(const uint8_t* text, size_t text_bytes, void* ws, unsigned long long* total, hipStream_t s,
+                      bool windows) {
   char* w = static_cast<char*>(ws);
   auto* wave = reinterpret_cast<uint32_t*>(w + kCountWsWave);
   auto* blk = reinterpret_cast<unsigned long long*>(w + kCountWsBlkOff);
-  if (commas) AVDB_HIP_TRY(hipMemsetAsync(commas, 0, 8, s));
-  hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, wave, commas);
+  auto* win = windows ? reinterpret_cast<uint32_t*>(w + AVDB_VCF_COUNT_WORKSPACE_BYTES) : nullptr;
+  hipLaunchKernelGGL(k_vcf_count, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, wave, win,
+                     windows_per_chunk(text_bytes));
   AVDB_LAUNCH_CHECK("k_vcf_count");
   hipLaunchKernelGGL(k_vcf_scan_blocks, dim3(1), dim3(kVcfGrid), 0, s, wave, blk, total);
   AVDB_LAUNCH_CHECK("k_vcf_scan_blocks");
@@ -330,11 +563,9 @@ static int count_pass(const uint8_t* text, size_t text_bytes, void* ws, unsigned
 static size_t scan_temp_bytes(size_t n) { return (scan::workspace_bytes(n, 2) + 255) & ~size_t(255); }
 
 extern "C" int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes) {
-  (void)text_bytes;
   if (!bytes) return AVDB_EINVAL;
-  // count workspace | line starts | scan temp
-  *bytes = AVDB_VCF_COUNT_WORKSPACE_BYTES + ((8 * n_lines + 255) & ~size_t(255)) +
-           scan_temp_bytes(n_lines + 1) + 256;
+  // count workspace (for a recount) | line starts | scan temp
+  *bytes = count_ws_full(text_bytes) + ((8 * n_lines + 255) & ~size_t(255)) + scan_temp_bytes(n_lines + 1) + 256;
   return AVDB_OK;
 }
 
@@ -349,14 +580,14 @@ extern "C" int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (text_bytes == 0) return hipMemsetAsync(n_newlines, 0, 8, s) == hipSuccess ? AVDB_OK : AVDB_EHIP;
-  return count_pass(text, text_bytes, workspace, reinterpret_cast<unsigned long long*>(n_newlines), s);
+  return count_pass(text, text_bytes, workspace, reinterpret_cast<unsigned long long*>(n_newlines), s,
+                    workspace_bytes >= count_ws_full(text_bytes));
 }
 
-extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes,
-                                    size_t n_lines, const void* line_counts, void* workspace,
-                                    size_t workspace_bytes,
-                                    avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off,
-                                    const avdb_vcf_opts* opts, void* stream) {
+static int parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                       const void* line_counts, size_t line_counts_bytes, void* workspace, size_t workspace_bytes,
+                       avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off, const avdb_vcf_opts* opts,
+                       void* stream) {
   if (!ctx || !lines || !rec_off || !heap_off) {
     avdb_set_error("avdb_vcf_parse_lines: null argument");
     return AVDB_EINVAL;
@@ -385,29 +616,59 @@ extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t t
     AVDB_HIP_TRY(hipMemsetAsync(heap_off, 0, 8, s));
     return AVDB_OK;
   }
-  auto* starts = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + AVDB_VCF_COUNT_WORKSPACE_BYTES);
+  const size_t cw_full = count_ws_full(text_bytes);
+  auto* starts = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + cw_full);
   void* tmp = reinterpret_cast<char*>(starts) + ((8 * n_lines + 255) & ~size_t(255));
   size_t tmp_bytes = scan_temp_bytes(n_lines + 1);
   const char* cw = static_cast<const char*>(line_counts);
-  if (!cw) {  // recount into the front of this workspace (same cut as k_vcf_starts)
-    const int rc = count_pass(text, text_bytes, workspace, nullptr, s);
+  bool windows = cw && line_counts_bytes >= cw_full;
+  if (!cw) {  // recount into the front of this workspace (same cut, window counts included)
+    const int rc = count_pass(text, text_bytes, workspace, nullptr, s, true);
     if (rc != AVDB_OK) return rc;
     cw = static_cast<const char*>(workspace);
+    windows = true;
   }
-  hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes,
-                     reinterpret_cast<const unsigned long long*>(cw + kCountWsBlkOff),
-                     reinterpret_cast<const uint32_t*>(cw + kCountWsWave), n_lines, starts);
-  AVDB_LAUNCH_CHECK("k_vcf_starts");
+  if (!AVDB_VCF_WINDOW_PARSE) windows = false;
   auto* rc = reinterpret_cast<unsigned long long*>(rec_off);
   auto* hc = reinterpret_cast<unsigned long long*>(heap_off);
   AVDB_HIP_TRY(hipMemsetAsync(rc + n_lines, 0, 8, s));
   AVDB_HIP_TRY(hipMemsetAsync(hc + n_lines, 0, 8, s));
-  const unsigned grid = stream_grid(n_lines, kBlock, 4096);
-  hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, starts,
-                     lines, rc, hc, cm, min_fields);
-  AVDB_LAUNCH_CHECK("k_vcf_parse");
+  const auto* blk = reinterpret_cast<const unsigned long long*>(cw + kCountWsBlkOff);
+  const auto* wave = reinterpret_cast<const uint32_t*>(cw + kCountWsWave);
+  if (windows) {  // one workgroup per parse window, line starts found in it
+    const uint32_t wps = windows_per_chunk(text_bytes);
+    hipLaunchKernelGGL(k_vcf_parse_windows, dim3(unsigned(size_t(kVcfGrid) * kVcfWaves * wps)), dim3(kBlock), 0, s,
+                       text, text_bytes, n_lines, blk, wave,
+                       reinterpret_cast<const uint32_t*>(cw + AVDB_VCF_COUNT_WORKSPACE_BYTES), wps, lines, rc, hc,
+                       cm, min_fields);
+    AVDB_LAUNCH_CHECK("k_vcf_parse_windows");
+  } else {  // the line-starts pass, then 256 lines per workgroup
+    hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk, wave, n_lines, starts);
+    AVDB_LAUNCH_CHECK("k_vcf_starts");
+    const unsigned grid = stream_grid(n_lines, kBlock, 4096);
+    hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, starts,
+                       lines, rc, hc, cm, min_fields);
+    AVDB_LAUNCH_CHECK("k_vcf_parse");
+  }
   if (int e = scan::exclusive_u64_pair(rec_off, rec_off, heap_off, heap_off, n_lines + 1, tmp, tmp_bytes, s)) return e;
   return AVDB_OK;
+}
+
+extern "C" int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes,
+                                    size_t n_lines, const void* line_counts, void* workspace,
+                                    size_t workspace_bytes,
+                                    avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off,
+                                    const avdb_vcf_opts* opts, void* stream) {
+  return parse_lines(ctx, text, text_bytes, n_lines, line_counts, AVDB_VCF_COUNT_WORKSPACE_BYTES, workspace,
+                     workspace_bytes, lines, rec_off, heap_off, opts, stream);
+}
+
+extern "C" int avdb_vcf_parse_lines2(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                                     const void* line_counts, size_t line_counts_bytes, void* workspace,
+                                     size_t workspace_bytes, avdb_vcf_line* lines, uint64_t* rec_off,
+                                     uint64_t* heap_off, const avdb_vcf_opts* opts, void* stream) {
+  return parse_lines(ctx, text, text_bytes, n_lines, line_counts, line_counts_bytes, workspace, workspace_bytes,
+                     lines, rec_off, heap_off, opts, stream);
 }
 
 extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,

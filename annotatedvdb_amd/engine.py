@@ -831,7 +831,9 @@ class Engine:
         nb = int(text_t.numel())
         tp = N.ptr(text_t) if nb else None
         s = self._stream()
-        ws0 = self.empty(N.VCF_COUNT_WORKSPACE_BYTES, torch.uint8)
+        csz = ctypes.c_size_t()
+        self.lib.avdb_vcf_count_workspace_size(nb, ctypes.byref(csz))  # (with the parse windows' counts)
+        ws0 = self.empty(int(csz.value), torch.uint8)
         nl = torch.zeros(2, dtype=torch.int64, device=self.device)  # newlines, last byte
         N.check("avdb_vcf_count_lines", self.lib.avdb_vcf_count_lines(
             self.ctx, tp, nb, N.ptr(ws0), ws0.numel(), N.ptr(nl), s))
@@ -848,8 +850,8 @@ class Engine:
         lines = self.empty(max(1, n_lines) * VCF_LINE_DTYPE.itemsize, torch.uint8)
         rec_off = self.empty(n_lines + 1, torch.int64)
         heap_off = self.empty(n_lines + 1, torch.int64)
-        N.check("avdb_vcf_parse_lines", self.lib.avdb_vcf_parse_lines(
-            self.ctx, tp, nb, n_lines, N.ptr(ws0), N.ptr(ws), ws.numel(), N.ptr(lines), N.ptr(rec_off),
+        N.check("avdb_vcf_parse_lines2", self.lib.avdb_vcf_parse_lines2(
+            self.ctx, tp, nb, n_lines, N.ptr(ws0), ws0.numel(), N.ptr(ws), ws.numel(), N.ptr(lines), N.ptr(rec_off),
             N.ptr(heap_off), ctypes.byref(vcf_opts) if vcf_opts is not None else None, s))
         if n_lines:
             tot = torch.stack([rec_off[n_lines], heap_off[n_lines]]).cpu().tolist()

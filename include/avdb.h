@@ -225,8 +225,14 @@ typedef struct avdb_vcf_line {
   uint8_t pad[3];
 } avdb_vcf_line;
 
-#define AVDB_VCF_COUNT_WORKSPACE_BYTES 32768u /* workspace of avdb_vcf_count_lines */
+#define AVDB_VCF_COUNT_WORKSPACE_BYTES 32768u /* minimum workspace of avdb_vcf_count_lines */
 int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes);
+/* Workspace of avdb_vcf_count_lines that also holds the newline count of every
+ * parse window (28 KB pieces of the count pass's cut): given that much, the count
+ * pass writes them and avdb_vcf_parse_lines2 parses one window per workgroup,
+ * finding the line starts itself, with no separate line-starts pass.  With only
+ * AVDB_VCF_COUNT_WORKSPACE_BYTES the starts pass runs (same outputs). */
+int avdb_vcf_count_workspace_size(size_t text_bytes, size_t* bytes);
 int avdb_vcf_count_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
                          size_t workspace_bytes, uint64_t* n_newlines, void* stream);
 /* Parse options (nullable = the default 8-field header, no chromosome map):
@@ -254,6 +260,12 @@ int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, 
                          const void* line_counts, void* workspace, size_t workspace_bytes,
                          avdb_vcf_line* lines,
                          uint64_t* rec_off, uint64_t* heap_off, const avdb_vcf_opts* opts, void* stream);
+/* avdb_vcf_parse_lines with the size of `line_counts`: a count workspace of at
+ * least avdb_vcf_count_workspace_size(text_bytes) bytes takes the window path. */
+int avdb_vcf_parse_lines2(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                          const void* line_counts, size_t line_counts_bytes, void* workspace,
+                          size_t workspace_bytes, avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off,
+                          const avdb_vcf_opts* opts, void* stream);
 int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
                   const avdb_vcf_line* lines, const uint64_t* rec_off, const uint64_t* heap_off,
                   uint8_t* chrom, uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len,

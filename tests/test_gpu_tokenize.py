@@ -137,3 +137,57 @@ def test_k0_chrom_map_and_header(engine):
     opts = engine.vcf_opts(chrom_map=cm, min_fields=8)
     n, nr, checked = _check(engine, text.encode(), opts, chrom_of=lambda c: back.get(c, c))
     assert checked > 0.8 * n
+
+
+def _starts_path(engine, text: bytes):
+    """K0 through the line-starts pass: a count workspace of the minimum size and
+    the original avdb_vcf_parse_lines entry (no window counts)."""
+    import ctypes
+    from annotatedvdb_amd import _native as N
+    from annotatedvdb_amd.engine import VCF_LINE_DTYPE
+    lib = engine.lib
+    t = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(engine.device)
+    nb = t.numel()
+    s = N.stream_handle(engine.device)
+    ws0 = torch.empty(N.VCF_COUNT_WORKSPACE_BYTES, dtype=torch.uint8, device=engine.device)
+    nl = torch.zeros(1, dtype=torch.int64, device=engine.device)
+    N.check("count", lib.avdb_vcf_count_lines(engine.ctx, N.ptr(t), nb, N.ptr(ws0), ws0.numel(), N.ptr(nl), s))
+    n_lines = int(nl.item()) + (0 if text.endswith(b"\n") else 1)
+    sz = ctypes.c_size_t()
+    lib.avdb_vcf_workspace_size(nb, n_lines, ctypes.byref(sz))
+    ws = torch.empty(int(sz.value), dtype=torch.uint8, device=engine.device)
+    lines = torch.empty(max(1, n_lines) * VCF_LINE_DTYPE.itemsize, dtype=torch.uint8, device=engine.device)
+    ro = torch.empty(n_lines + 1, dtype=torch.int64, device=engine.device)
+    ho = torch.empty(n_lines + 1, dtype=torch.int64, device=engine.device)
+    N.check("parse", lib.avdb_vcf_parse_lines(engine.ctx, N.ptr(t), nb, n_lines, N.ptr(ws0), N.ptr(ws), ws.numel(),
+                                              N.ptr(lines), N.ptr(ro), N.ptr(ho), None, s))
+    torch.cuda.synchronize()
+    return n_lines, lines[: n_lines * 80].cpu().numpy(), ro.cpu().numpy(), ho.cpu().numpy()
+
+
+@pytest.mark.parametrize("which", ["golden", "dbsnp", "short", "empty_lines", "long", "crlf_tail"])
+def test_k0_window_parse_equals_starts_pass(engine, which):
+    """The window parse (line starts found in 28 KB windows from the count pass's
+    per-window newline counts) gives the same line table and offsets as the
+    line-starts pass, byte for byte, including lines across window edges and lines
+    longer than a window."""
+    if which == "golden":
+        text = _golden_text()
+    elif which == "dbsnp":
+        text = _synth(60000, 53)
+    elif which == "short":
+        text = b"\n".join(b"%d\t%d\t.\tA\tG\t.\t.\t." % (1 + i % 22, 1000 + i) for i in range(50000)) + b"\n"
+    elif which == "empty_lines":
+        text = b"\n" * 90001 + b"1\t5\t.\tA\tG\t.\t.\t."
+    elif which == "long":
+        base = _synth(4000, 59).split(b"\n")[:-1]
+        huge = b"2\t888\t.\tC\tG,T\t.\t.\tZ=" + b"Q" * 70000
+        text = b"\n".join(base[:2000] + [huge] + base[2000:] + [huge]) + b"\n"
+    else:
+        text = _synth(20000, 61).replace(b"\n", b"\r\n")[:-3]
+    n0, lines0, ro0, ho0 = _starts_path(engine, text)
+    vb = engine.vcf_tokenize(text)
+    assert vb.n_lines == n0
+    assert (vb.lines[: n0 * 80].cpu().numpy() == lines0).all()
+    assert (vb.rec_off[: n0 + 1].cpu().numpy() == ro0).all()
+    assert (vb.heap_off[: n0 + 1].cpu().numpy() == ho0).all()
