@@ -148,6 +148,10 @@ static PyObject* py_display(PyObject* self, PyObject* const* args, Py_ssize_t na
     d = Py_BuildValue("(OiI)", Py_None, out.end_rel, out.lcp);
     goto done;
   }
+  if (out.variant_class > AVDB_VC_DELETION) {
+    PyErr_Format(PyExc_RuntimeError, "avdb_annotate_host: variant class %u", out.variant_class);
+    goto done;
+  }
   {
     PyObject* dict = PyDict_New();
     if (!dict) goto done;
