@@ -881,9 +881,10 @@ def run_workload(a, name, ri, dev, cpu):
         out["data"] = "synthetic dbSNP-shaped VCF text (numpy PCG64 lines tiled on the device)"
         out["config"].update(lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
                              records_processed=None)
-        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (count pass, line starts + "
-                                   "parse, two scans, emit, and its two host reads); the line table and line "
-                                   "offsets it also writes (96 B per line) are not counted")
+        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (count pass with per-window "
+                                   "newline counts, window parse, one paired offset scan, emit, and its two host "
+                                   "reads); the line table and line offsets it also writes (96 B per line) are not "
+                                   "counted")
     return out
 
 
