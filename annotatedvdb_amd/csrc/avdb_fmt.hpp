@@ -107,15 +107,33 @@ struct Dec {
   uint32_t n;
 };
 
+#ifndef AVDB_DEC_TEXT_SWAR
+#define AVDB_DEC_TEXT_SWAR 1  // digit count from the SWAR digits (0: a compare chain, A/B)
+#endif
 AVDB_HD Dec dec_text(uint32_t v) {
-  const uint32_t n = ndigits(v);
-  if (n <= 8) return Dec{ascii8(v) >> (8 * (8 - n)), 0ull, n};
-  const uint32_t hi = v / 100000000u;  // 1..42
+  if (!AVDB_DEC_TEXT_SWAR) {
+    const uint32_t n = ndigits(v);
+    if (n <= 8) return Dec{ascii8(v) >> (8 * (8 - n)), 0ull, n};
+    const uint32_t hi = v / 100000000u;  // 1..42
+    const uint64_t b = ascii8(v - hi * 100000000u);
+    const uint32_t nh = n - 8;           // 1 or 2 leading digits
+    const uint64_t a = hi < 10u ? uint64_t('0' + hi)
+                                : (uint64_t('0' + hi / 10u) | (uint64_t('0' + hi % 10u) << 8));
+    return Dec{a | (b << (8 * nh)), b >> (64 - 8 * nh), n};
+  }
+  // branch-free: the low 8 digits are converted either way, and the count of the
+  // number's digits comes from them (the lowest nonzero digit byte is its first
+  // digit: (d + 0x7F) sets bit 7 of each byte d >= 1, no carries for d <= 9)
+  // instead of a chain of ten compares
+  const uint32_t hi = v / 100000000u;  // 0..42
   const uint64_t b = ascii8(v - hi * 100000000u);
-  const uint32_t nh = n - 8;           // 1 or 2 leading digits
+  const uint64_t nz = ((b - 0x3030303030303030ull) + 0x7F7F7F7F7F7F7F7Full) & kHiBits;
+  const uint32_t nlo = nz ? 8u - (uint32_t(__builtin_ctzll(nz)) >> 3) : 1u;  // digits of v < 10^8
+  const uint32_t nh = hi >= 10u ? 2u : 1u;
   const uint64_t a = hi < 10u ? uint64_t('0' + hi)
                               : (uint64_t('0' + hi / 10u) | (uint64_t('0' + hi % 10u) << 8));
-  return Dec{a | (b << (8 * nh)), b >> (64 - 8 * nh), n};
+  const uint64_t lo8 = b >> (8 * (8 - nlo));
+  return hi ? Dec{a | (b << (8 * nh)), b >> (64 - 8 * nh), 8u + nh} : Dec{lo8, 0ull, nlo};
 }
 
 typedef __attribute__((address_space(3))) uint64_t lds_u64;

@@ -750,7 +750,9 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
 // AVDB_K7V2_EXP: attribution knobs for tools/k7_attr.sh (each drops one part of
 // the pass and produces wrong text; 0 in every shipped build): 1 no key render,
 // 2 no path render, 4 no ':' / ASCII check, 8 no allele ranges, 16 no ':rs'
-// suffix, 32 no "label:pos:" prefix, 64 no flushes, 128 no window loads
+// suffix, 32 no "label:pos:" prefix, 64 no flushes, 128 no window loads, 256 no
+// offset / state stores, 512 no SoA loads (values from the index), 1024 no
+// group-base loads
 #ifndef AVDB_K7V2_EXP
 #define AVDB_K7V2_EXP 0
 #endif
@@ -913,8 +915,12 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
     const size_t i = t0 + lane;
     const bool live = i < A.n;
     const KeyTileIn cur = nx;
-    if (tn < A.n) nx = load_in(tn);
-    if (((t0 / kWave) & (tpg - 1)) == 0) {  // a new group: its scanned base
+    if (K7X(512)) {  // (attribution: no SoA loads, values from the index)
+      nx.c = uint32_t(tn + lane) % 22u; nx.p = uint32_t(tn + lane) * 7u + 1u; nx.r = 1; nx.a = 1;
+      nx.e = tn + lane + 1; nx.off = 2 * (tn + lane); nx.cd = (13u << 28) | (uint32_t(tn + lane) & 0xFFFu);
+    } else if (tn < A.n) nx = load_in(tn);
+    if (K7X(1024)) {  // (attribution: no group-base loads)
+    } else if (((t0 / kWave) & (tpg - 1)) == 0) {  // a new group: its scanned base
       const size_t g = (t0 / kWave) >> A.group_log2;
       const size_t b = g / kGroupsPerBlock;
       const uint2 gp = A.grp_pre[g];
@@ -955,8 +961,8 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
     const bool lng = uint64_t(r) + a > A.max_seq_len;
     uint8_t st = AVDB_KEY_HOST;
     if (live) {
-      A.key_off[i] = ko;
-      if (A.code) A.path_off[i] = po;
+      if (!K7X(256)) A.key_off[i] = ko;
+      if (A.code && !K7X(256)) A.path_off[i] = po;
       if (i + 1 == A.n) {
         A.key_off[A.n] = ko1;
         if (A.code) A.path_off[A.n] = po1;
@@ -1058,7 +1064,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
         }
       }
     }
-    if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
+    if (live && !K7X(256)) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
     wave_lds_sync();
     if (kst && !K7X(64)) flush_span32(kimg, A.key_out, gk0, gk1, lane);
     if (pst && !K7X(64)) flush_span32(pimg, A.path_out, gp0, gp1, lane);
