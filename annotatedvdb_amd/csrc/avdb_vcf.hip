@@ -95,13 +95,22 @@ constexpr uintptr_t kNlStep = 16 * kWave;              // bytes per wave load
 // bytes the count pass also writes every window's newline count, and the parse
 // pass then takes one workgroup per window and finds its line starts itself.
 #ifndef AVDB_VCF_PARSE_WIN_KB
-#define AVDB_VCF_PARSE_WIN_KB 28  // window size (A/B knob; a multiple of 4)
+#define AVDB_VCF_PARSE_WIN_KB 24  // window size (A/B knob; a multiple of 4)
 #endif
-// (8.4 M dbSNP lines: 16 / 20 / 24 / 28 KB windows 2.14 / 2.02 / 1.90 / 1.88 ms per
-// tokenize: the per-window costs — the staged overhang, the bitmaps, the search for
-// the last line's end — favour the largest window the stage holds)
+#ifndef AVDB_VCF_PARSE_OVER
+#define AVDB_VCF_PARSE_OVER 1024  // bytes staged past a window (A/B knob; a multiple of 64)
+#endif
+#ifndef AVDB_VCF_PARSE_WAVES
+#define AVDB_VCF_PARSE_WAVES 6    // launch-bounds minimum waves per SIMD of the window parse (A/B knob)
+#endif
+// (8.4 M dbSNP lines, the stage sized to the window: 20 / 24 / 28 KB windows with
+// 4 KB of overhang 1.86 / 1.78 / 1.89 ms per tokenize — 24 KB is the largest that
+// leaves five workgroups' LDS on a CU, against four at 28 KB; then a 1 KB overhang
+// (26.7 KB of LDS) and 80 VGPRs (6 waves per SIMD, 20 B of spills) put six on a
+// CU: 1.71 ms.  A line that runs more than 1 KB past its window parses from
+// global memory.)
 constexpr uint32_t kParseWin = AVDB_VCF_PARSE_WIN_KB * 1024;   // (a multiple of kNlUnroll * kNlStep)
-constexpr uint32_t kParseOver = kStage - kParseWin - 64 < 4096u ? kStage - kParseWin - 64 : 4096u;  // staged past a window
+constexpr uint32_t kParseOver = AVDB_VCF_PARSE_OVER;           // staged past a window (its last line)
 static_assert(kParseWin % (kNlUnroll * kNlStep) == 0, "window / count step");
 
 __global__ __launch_bounds__(kBlock) void k_vcf_count(const uint8_t* __restrict__ text,
@@ -263,7 +272,10 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
 // (parse_line, as k_vcf_parse), 256 lines a round.  Lines start at byte 0 and
 // after every '\n' except a final one.
 static_assert(kParseWin % 64 == 0 && kParseWin / 64 + 2 <= 2 * kBlock, "window bitmap words");
-static_assert(kParseWin + kParseOver + 32 <= kStage, "window stage");
+// the window kernel's own stage: the window, its overhang and the 16-byte
+// alignment slack on both sides (LDS per workgroup decides how many fit a CU)
+constexpr uint32_t kParseStage = kParseWin + kParseOver + 48;
+static_assert(kParseStage <= kStage, "window stage");
 
 __device__ __forceinline__ uint32_t nl_bits8(uint64_t w) {  // bit k: byte k of w is '\n'
   const uint64_t m = zero_bytes_mask(w ^ kNL) & kHiBits;
@@ -293,7 +305,7 @@ __device__ __forceinline__ uint32_t block_excl32(uint32_t v, uint32_t* s_w, uint
   return base + x - v;
 }
 
-__global__ __launch_bounds__(kBlock) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
+__global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
                                                               size_t n_lines,
                                                               const unsigned long long* __restrict__ blk_off,
                                                               const uint32_t* __restrict__ wave_cnt,
@@ -302,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse_windows(const uint8_t* __r
                                                               unsigned long long* __restrict__ rec_cnt,
                                                               unsigned long long* __restrict__ heap_cnt,
                                                               ChromMapView cm, uint32_t min_fields) {
-  __shared__ u32x4 s_text[kStage / 16];
+  __shared__ u32x4 s_text[kParseStage / 16];
   __shared__ uint32_t s_start[kBlock + 1];  // line starts of the round, relative to the window start
   __shared__ uint32_t s_w[kVcfWaves];
   __shared__ uint32_t s_tail;               // (first '\n' at or after w1 - 1) + 1 - w0
