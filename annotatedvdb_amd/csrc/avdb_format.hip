@@ -68,7 +68,7 @@ extern "C" int avdb_vcf_format_size(avdb_ctx* ctx, const uint8_t* text, size_t t
   A.copy_off = copy_off;
   A.map_off = map_off;
   A.line_state = line_state;
-  const unsigned grid = stream_grid(n_lines, kBlock, 4096);
+  const unsigned grid = stream_grid(n_lines, kBlock, AVDB_K5_SIZE_GRID);
   hipLaunchKernelGGL(k_vcf_format<false>, dim3(grid), dim3(kBlock), 0, s, A);
   AVDB_LAUNCH_CHECK("k_vcf_format<size>");
   size_t tb = scan_bytes(n_lines + 1);

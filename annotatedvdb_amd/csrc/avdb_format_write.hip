@@ -29,7 +29,7 @@ extern "C" int avdb_vcf_format_write(avdb_ctx* ctx, const uint8_t* text, size_t 
   A.copy_out = copy_out;
   A.map_out = map_out;
   A.counters = reinterpret_cast<unsigned long long*>(counters);
-  const unsigned grid = stream_grid(n_lines, kBlock, 4096);
+  const unsigned grid = stream_grid(n_lines, kBlock, AVDB_K5_WRITE_GRID);
   hipLaunchKernelGGL(k_vcf_format<true>, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), A);
   AVDB_LAUNCH_CHECK("k_vcf_format<write>");
   return AVDB_OK;

@@ -375,6 +375,15 @@ __device__ __forceinline__ uint32_t tile_order(const FormatArgs& A, size_t base,
   return s_key[t];
 }
 
+// K5 workgroups over 256-line tiles (A/B on 8.4 M lines, load workload): the size
+// pass with one workgroup per tile 1.73 -> 1.56 ms (against a 4,096-workgroup
+// grid-stride), the write pass best at 8,192 (4.48 -> 4.39 ms; one per tile 4.43)
+#ifndef AVDB_K5_SIZE_GRID
+#define AVDB_K5_SIZE_GRID (1u << 30)
+#endif
+#ifndef AVDB_K5_WRITE_GRID
+#define AVDB_K5_WRITE_GRID 8192
+#endif
 template <bool WRITE>
 __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs A) {
   __shared__ u32x4 s_text[kStage / 16];

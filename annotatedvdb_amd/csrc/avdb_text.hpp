@@ -79,12 +79,13 @@ struct Window {
   bool staged;
 };
 
-__device__ __forceinline__ Window stage_window(const Heap& h, size_t s0, size_t s1, u32x4* lds) {
+__device__ __forceinline__ Window stage_window(const Heap& h, size_t s0, size_t s1, u32x4* lds,
+                                               uint32_t stage_bytes = kStage) {
   Window w;
   w.a0 = (h.lo + s0) & ~uintptr_t(15);
   const uintptr_t end = h.lo + s1;
   const size_t n16 = (end - w.a0 + 15) / 16;
-  w.staged = n16 * 16 <= kStage;
+  w.staged = n16 * 16 <= stage_bytes;
   if (w.staged) {
     for (size_t i = threadIdx.x; i < n16; i += blockDim.x) {
       const uintptr_t a = w.a0 + 16 * i;

@@ -497,22 +497,38 @@ __device__ __forceinline__ void emit_line(CP s, const avdb_vcf_line& L, size_t l
     hs.finish();
 }
 
-__global__ __launch_bounds__(kBlock) void k_vcf_emit(
+// EMIT_LINES lines per workgroup (one thread each), their text staged in an LDS
+// window of EMIT_STAGE bytes: smaller tiles with a right-sized stage put more
+// workgroups on a CU (as the window parse)
+#ifndef AVDB_VCF_EMIT_LINES
+#define AVDB_VCF_EMIT_LINES 256
+#endif
+#ifndef AVDB_VCF_EMIT_STAGE_KB
+#define AVDB_VCF_EMIT_STAGE_KB 36
+#endif
+#ifndef AVDB_VCF_EMIT_GRID
+#define AVDB_VCF_EMIT_GRID (1u << 30)  // emit workgroups (one per tile; a cap grid-strides: 4096 was 0.5 % slower)
+#endif
+constexpr uint32_t kEmitLines = AVDB_VCF_EMIT_LINES;
+constexpr uint32_t kEmitStage = AVDB_VCF_EMIT_STAGE_KB * 1024;
+static_assert(kEmitStage <= kStage && kEmitLines <= 1024, "emit tile");
+
+__global__ __launch_bounds__(kEmitLines) void k_vcf_emit(
     const uint8_t* __restrict__ text, size_t text_bytes, size_t n_lines,
     const avdb_vcf_line* __restrict__ lines, const uint64_t* __restrict__ rec_off,
     const uint64_t* __restrict__ heap_off, uint8_t* __restrict__ chrom, uint32_t* __restrict__ pos,
     uint64_t* __restrict__ allele_off, uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
     uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap, uint32_t* __restrict__ rec_line,
     uint32_t* __restrict__ rec_alt) {
-  __shared__ u32x4 s_text[kStage / 16];
+  __shared__ u32x4 s_text[kEmitStage / 16];
   const Heap h = make_heap(text, text_bytes);
-  for (size_t base = size_t(blockIdx.x) * kBlock; base < n_lines; base += size_t(gridDim.x) * kBlock) {
-    const size_t last = base + kBlock < n_lines ? base + kBlock : n_lines;
+  for (size_t base = size_t(blockIdx.x) * kEmitLines; base < n_lines; base += size_t(gridDim.x) * kEmitLines) {
+    const size_t last = base + kEmitLines < n_lines ? base + kEmitLines : n_lines;
     // the window only has to reach the end of the last line's ALT field
     const size_t s0 = lines[base].start;
     const avdb_vcf_line& Z = lines[last - 1];
     const size_t s1 = Z.start + Z.len;
-    const Window w = stage_window(h, s0, s1, s_text);
+    const Window w = stage_window(h, s0, s1, s_text, kEmitStage);
     const size_t li = base + threadIdx.x;
     if (li < n_lines) {
       const avdb_vcf_line L = lines[li];
@@ -696,8 +712,8 @@ extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_byt
   }
   if (n_lines == 0) return AVDB_OK;
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
-  const unsigned grid = stream_grid(n_lines, kBlock, 4096);
-  hipLaunchKernelGGL(k_vcf_emit, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+  const unsigned grid = stream_grid(n_lines, kEmitLines, AVDB_VCF_EMIT_GRID);
+  hipLaunchKernelGGL(k_vcf_emit, dim3(grid), dim3(kEmitLines), 0, static_cast<hipStream_t>(stream),
                      text, text_bytes, n_lines, lines, rec_off, heap_off, chrom, pos, allele_off, ref_len,
                      alt_len, ext_id, heap, rec_line, rec_alt);
   AVDB_LAUNCH_CHECK("k_vcf_emit");

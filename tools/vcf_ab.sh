@@ -1,9 +1,10 @@
 #!/bin/bash
-# K0 A/B: the vcf bench line for the in-tree library and every variant under
-# annotatedvdb_amd/_lib/var/ (two passes), after the tokenizer GPU tests.
-#   tools/vcf_ab.sh TAG
+# K0 / K5 A/B: the vcf (or WORKLOAD) bench line for the in-tree library and every
+# variant under annotatedvdb_amd/_lib/var/ (two passes), after the tokenizer GPU tests.
+#   tools/vcf_ab.sh TAG [WORKLOAD]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-vcfab}
+W=${2:-vcf}
 OUT=gpurun_out/$T
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -14,9 +15,9 @@ LIBS="annotatedvdb_amd/_lib/libavdb_hip.so $(ls annotatedvdb_amd/_lib/var/libavd
 for rep in 1 2; do
   for lib in $LIBS; do
     v=$(basename "$lib" .so)
-    AVDB_LIB=$lib timeout -k 10 300 python bench.py --workload vcf --steps 10 --warmup 3 --cpu-baseline off \
-      > "$OUT/vcf_${v}_$rep.log" 2>&1 || exit 1
-    python3 - "$OUT/vcf_${v}_$rep.log" "$v" <<'PY'
+    AVDB_LIB=$lib timeout -k 10 300 python bench.py --workload "$W" --steps 10 --warmup 3 --cpu-baseline off \
+      > "$OUT/${W}_${v}_$rep.log" 2>&1 || exit 1
+    python3 - "$OUT/${W}_${v}_$rep.log" "$v" <<'PY'
 import json, sys
 d = json.loads([x for x in open(sys.argv[1]) if x.startswith("{")][-1])
 print(sys.argv[2], round(d["ms_per_step"], 4), d["config"]["stage_ms"])
