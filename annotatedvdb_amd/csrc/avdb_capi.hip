@@ -120,12 +120,6 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     const int v = atoi(s);
     if (v >= 1 && v <= 3) c->k4_blocks_per_cu = v;
   }
-  // K0 one-pass tokenizer: resident workgroups per CU (each stages a 20 KB window)
-  c->k0_blocks_per_cu = 6;
-  if (const char* s = getenv("AVDB_K0_BLOCKS_PER_CU")) {
-    const int v = atoi(s);
-    if (v >= 1 && v <= 7) c->k0_blocks_per_cu = v;
-  }
   // (the one-kernel run scan for C1's 1.1 M records measured 22.2 us against 5.7 + 7.6 us
   // for the list form: the list form is the default at every size)
   c->k7_raw_blocks = 256;

@@ -272,7 +272,6 @@ struct avdb_ctx {
   int k2_blocks_per_cu;  // K2 grid = n_cu * this (env AVDB_K2_BLOCKS_PER_CU)
   int k2_keyed_unroll;   // keyed K2 (K7 group totals) groups per lane per trip (env AVDB_K2_KEYED_UNROLL)
   int k4_blocks_per_cu;  // K4 digest grid = n_cu * this (env AVDB_K4_BLOCKS_PER_CU; default: its occupancy, 3)
-  int k0_blocks_per_cu;  // K0 one-pass grid = n_cu * this (env AVDB_K0_BLOCKS_PER_CU)
   size_t k7_raw_blocks;  // K7 one-pass: write pass sums up to this many block totals itself (env AVDB_K7_RAW_BLOCKS)
   int k7_v2;             // K7 one-pass write pass: 1 the split-range key renderer (default), 0 the round-3 one (env AVDB_K7_V2)
   size_t k3_list_min;    // K3 grouped: two-phase list form from this many records on (env AVDB_K3_LIST_MIN)
