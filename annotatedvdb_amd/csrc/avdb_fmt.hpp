@@ -453,43 +453,83 @@ struct LeafPath {
   }
 };
 
-template <uint32_t L, uint32_t J>
+#ifndef AVDB_LEAF_WORD32
+#define AVDB_LEAF_WORD32 1  // 0: K7 too uses the 64-bit template constants (A/B knob)
+#endif
+// W32: the caller's choice (K7: 32-bit halves; K5's write pass keeps the 64-bit
+// form: the 32-bit one moved its spills from SGPRs to scratch, 172 -> 288 B/lane)
+template <uint32_t L, uint32_t J, bool W32 = false>
 AVDB_HD uint64_t leaf_word(uint64_t label, uint32_t g) {  // word J of the path
   using P = LeafPath<L>;
-  uint64_t w = P::word(J);
-  if constexpr (J == 0) w |= label << 24;
-  if constexpr (P::digit_pos(1) / 8 == J) w += uint64_t(g >> 12) << (8 * (P::digit_pos(1) % 8));
+  if constexpr (W32) {
+    // Each half is its template literal plus the label / digit bytes (a digit
+    // byte is '1' + 0..8: no carry between bytes, so two 32-bit adds).  A 32-bit
+    // literal is an operand of the add itself; 64-bit template constants were
+    // hoisted out of K7's tile loop into SGPR pairs, which ran out and spilled
+    // to VGPR lanes (a v_readlane / v_writelane pair per word and tile).
+    constexpr uint64_t T = P::word(J);
+    uint32_t lo = 0, hi = 0;
+    if constexpr (J == 0) {
+      lo |= uint32_t(label << 24);
+      hi |= uint32_t(label >> 8);
+    }
+    if constexpr (P::digit_pos(1) / 8 == J) {
+      constexpr uint32_t p = P::digit_pos(1) % 8;
+      if constexpr (p < 4) lo |= (g >> 12) << (8 * p); else hi |= (g >> 12) << (8 * (p - 4));
+    }
 #pragma unroll
-  for (uint32_t l = 2; l <= 13; ++l)
-    if (P::digit_pos(l) / 8 == J) w += uint64_t((g >> (13 - l)) & 1u) << (8 * (P::digit_pos(l) % 8));
-  return w;
+    for (uint32_t l = 2; l <= 13; ++l)
+      if (P::digit_pos(l) / 8 == J) {
+        const uint32_t p = P::digit_pos(l) % 8, b = (g >> (13 - l)) & 1u;
+        if (p < 4) lo |= b << (8 * p); else hi |= b << (8 * (p - 4));
+      }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the literals are materialised where they are used (SALU moves, issued beside
+    // the VALU): loop-invariant constants are otherwise hoisted out of the tile loop
+    // into registers the loop does not have
+    uint32_t tlo, thi;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(tlo) : "n"(uint32_t(T)));
+    asm volatile("s_mov_b32 %0, %1" : "=s"(thi) : "n"(uint32_t(T >> 32)));
+    return (uint64_t(thi + hi) << 32) | uint32_t(tlo + lo);
+#else
+    return (uint64_t(uint32_t(T >> 32) + hi) << 32) | uint32_t(uint32_t(T) + lo);
+#endif
+  } else {
+    uint64_t w = P::word(J);
+    if constexpr (J == 0) w |= label << 24;
+    if constexpr (P::digit_pos(1) / 8 == J) w += uint64_t(g >> 12) << (8 * (P::digit_pos(1) % 8));
+#pragma unroll
+    for (uint32_t l = 2; l <= 13; ++l)
+      if (P::digit_pos(l) / 8 == J) w += uint64_t((g >> (13 - l)) & 1u) << (8 * (P::digit_pos(l) % 8));
+    return w;
+  }
 }
 
 // each word is built just before it is appended (one live word: the K5 write
 // pass runs at its register limit)
-template <uint32_t L, class O>
+template <uint32_t L, bool W32 = false, class O>
 AVDB_HD O leaf_path(O o, uint64_t label, uint32_t g) {
-  o.append(leaf_word<L, 0>(label, g), 8);
-  o.append(leaf_word<L, 1>(label, g), 8);
-  o.append(leaf_word<L, 2>(label, g), 8);
-  o.append(leaf_word<L, 3>(label, g), 8);
-  o.append(leaf_word<L, 4>(label, g), 8);
-  o.append(leaf_word<L, 5>(label, g), 8);
-  o.append(leaf_word<L, 6>(label, g), 8);
-  o.append(leaf_word<L, 7>(label, g), 8);
-  o.append(leaf_word<L, 8>(label, g), 8);
-  o.append(leaf_word<L, 9>(label, g), 8);
-  o.append(leaf_word<L, 10>(label, g), LeafPath<L>::kLen - 80);
+  o.append(leaf_word<L, 0, W32>(label, g), 8);
+  o.append(leaf_word<L, 1, W32>(label, g), 8);
+  o.append(leaf_word<L, 2, W32>(label, g), 8);
+  o.append(leaf_word<L, 3, W32>(label, g), 8);
+  o.append(leaf_word<L, 4, W32>(label, g), 8);
+  o.append(leaf_word<L, 5, W32>(label, g), 8);
+  o.append(leaf_word<L, 6, W32>(label, g), 8);
+  o.append(leaf_word<L, 7, W32>(label, g), 8);
+  o.append(leaf_word<L, 8, W32>(label, g), 8);
+  o.append(leaf_word<L, 9, W32>(label, g), 8);
+  o.append(leaf_word<L, 10, W32>(label, g), LeafPath<L>::kLen - 80);
   return o;
 }
 
-template <class O>
+template <bool W32 = false, class O>
 AVDB_HD O bin_path(O o, uint32_t c, uint32_t code) {
   const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
   if (AVDB_LEAF_PATH && level == 13 && c < 25 && (g >> 12) < 9) {
-    if (c < 9) return leaf_path<1>(o, uint64_t('1' + c), g);
-    if (c < 22) return leaf_path<2>(o, uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8), g);
-    return leaf_path<1>(o, c == 22 ? uint64_t('X') : (c == 23 ? uint64_t('Y') : uint64_t('M')), g);
+    if (c < 9) return leaf_path<1, W32>(o, uint64_t('1' + c), g);
+    if (c < 22) return leaf_path<2, W32>(o, uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8), g);
+    return leaf_path<1, W32>(o, c == 22 ? uint64_t('X') : (c == 23 ? uint64_t('Y') : uint64_t('M')), g);
   }
   o.lit("chr");
   chrom_name(o, c);

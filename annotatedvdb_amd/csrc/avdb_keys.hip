@@ -1057,10 +1057,10 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
       if (has_path && !path_over && !K7X(2)) {
         if (pst) {
           Out<true, true> o(LdsImage{}, pimg, po - (gp0 & ~uint64_t(15)));
-          bin_path(o, c, cd).finish();
+          bin_path<AVDB_LEAF_WORD32>(o, c, cd).finish();
         } else {
           Out<true> o(A.path_out, po);
-          bin_path(o, c, cd).finish();
+          bin_path<AVDB_LEAF_WORD32>(o, c, cd).finish();
         }
       }
     }
