@@ -688,7 +688,9 @@ def run_workload(a, name, ri, dev, cpu):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        if graph is not None:
+        if graph is not None and name in ("c2", "c3", "c4"):
+            timed("bin_assign", True, graph.replay)  # one kernel: the replay is its launch
+        elif graph is not None:
             graph.replay()
         else:
             step(True)
