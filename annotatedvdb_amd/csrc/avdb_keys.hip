@@ -875,12 +875,16 @@ __device__ __forceinline__ void append2(O& o, uint64_t w0, uint64_t w1, uint32_t
   }
 }
 
+#ifndef AVDB_K7_V2_BLOCK
+#define AVDB_K7_V2_BLOCK 256  // write-pass workgroup size (A/B knob; waves are independent, no barriers)
+#endif
+constexpr uint32_t kV2Block = AVDB_K7_V2_BLOCK, kV2Waves = kV2Block / kWave;
 #ifndef AVDB_K7_V2_WAVES
 #define AVDB_K7_V2_WAVES 4
 #endif
-__global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(KeyArgs A) {
-  __shared__ uint64_t s_kimg[kWavesPerBlock * kKeyWave / 8];
-  __shared__ uint64_t s_pimg[kWavesPerBlock * kPathWave / 8];
+__global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(KeyArgs A) {
+  __shared__ uint64_t s_kimg[kV2Waves * kKeyWave / 8];
+  __shared__ uint64_t s_pimg[kV2Waves * kPathWave / 8];
   const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
   lds_u64* kimg = (lds_u64*)s_kimg + wv * (kKeyWave / 8);
   lds_u64* pimg = (lds_u64*)s_pimg + wv * (kPathWave / 8);
@@ -903,7 +907,7 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_V2_WAVES) void k_record_keys_v2(Key
     }
     return v;
   };
-  const size_t gwave = size_t(blockIdx.x) * kWavesPerBlock + wv, n_gw = size_t(gridDim.x) * kWavesPerBlock;
+  const size_t gwave = size_t(blockIdx.x) * kV2Waves + wv, n_gw = size_t(gridDim.x) * kV2Waves;
   const uint32_t tpg = 1u << A.group_log2;
   size_t t0 = gwave * (size_t(kWave) << A.group_log2);
   KeyTileIn nx{};
@@ -1350,7 +1354,9 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   const unsigned grid = unsigned((ng + kWavesPerBlock - 1) / kWavesPerBlock < AVDB_K7_GRID
                                      ? (ng + kWavesPerBlock - 1) / kWavesPerBlock : AVDB_K7_GRID);
   if (ctx->k7_v2) {
-    hipLaunchKernelGGL(k_record_keys_v2, dim3(grid), dim3(kBlock), 0, s, A);
+    // (the same cap on waves whatever the workgroup size)
+    const size_t wmax = size_t(AVDB_K7_GRID) * kWavesPerBlock / kV2Waves, wneed = (ng + kV2Waves - 1) / kV2Waves;
+    hipLaunchKernelGGL(k_record_keys_v2, dim3(unsigned(wneed < wmax ? wneed : wmax)), dim3(kV2Block), 0, s, A);
     AVDB_LAUNCH_CHECK("k_record_keys_v2");
   } else {
     hipLaunchKernelGGL(k_record_keys<2>, dim3(grid), dim3(kBlock), 0, s, A);
