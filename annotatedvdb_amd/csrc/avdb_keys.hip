@@ -876,7 +876,7 @@ __device__ __forceinline__ void append2(O& o, uint64_t w0, uint64_t w1, uint32_t
 }
 
 #ifndef AVDB_K7_V2_BLOCK
-#define AVDB_K7_V2_BLOCK 256  // write-pass workgroup size (A/B knob; waves are independent, no barriers)
+#define AVDB_K7_V2_BLOCK 64  // write-pass workgroup size: one wave (waves share nothing; against 256 threads K7 -0.5 to -0.9 %, A/B knob)
 #endif
 constexpr uint32_t kV2Block = AVDB_K7_V2_BLOCK, kV2Waves = kV2Block / kWave;
 #ifndef AVDB_K7_V2_WAVES
