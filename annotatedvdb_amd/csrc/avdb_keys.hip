@@ -100,7 +100,7 @@ struct KeyArgs {
 #define AVDB_K7_SIZE16 1  // A/B knob: 0 writes u64 sizes and scans them in place
 #endif
 #ifndef AVDB_K7_GRID
-#define AVDB_K7_GRID 16384u  // write-pass workgroups (A/B knob; C4k K7 5.14 -> 5.00 ms against 4,096)
+#define AVDB_K7_GRID 16384u  // write-pass waves / 4 (A/B knob; C4k K7 5.14 -> 5.00 ms against 4,096; with one-wave workgroups the v2 grid is 4x this)
 #endif
 // (A periodic-span flush for tiles whose 64 records share one bin — the path
 // rendered once, each chunk read from it at its phase — measured no faster:
