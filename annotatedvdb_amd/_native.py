@@ -55,7 +55,7 @@ CTR_ADSP_UPDATES = 29
 FORMAT_ADSP = 1
 MATCH_NONE, MATCH_EXACT, MATCH_SWITCHED, MATCH_HOST = 0, 1, 2, 255
 LINE_GPU, LINE_HOST, LINE_SKIP = 0, 1, 2
-KEY_OK, KEY_HOST, KEY_NEED_DIGEST, KEY_OVERFLOW = 0, 1, 2, 3
+KEY_OK, KEY_HOST, KEY_NEED_DIGEST, KEY_OVERFLOW, KEY_DIGEST_PENDING = 0, 1, 2, 3, 4
 PATH_OVERFLOW = 0x10
 MAX_ALG_ID = 64
 
@@ -85,7 +85,7 @@ class LineResult(ctypes.Structure):
 # every symbol include/avdb.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED_SYMBOLS = [
     "avdb_abi_version", "avdb_last_error", "avdb_device_count",
-    "avdb_ctx_create", "avdb_ctx_destroy", "avdb_ctx_n_chrom",
+    "avdb_ctx_create", "avdb_ctx_destroy", "avdb_ctx_n_chrom", "avdb_ctx_set_option",
     "avdb_ctx_set_sequence_digests", "avdb_l8_bin_count",
     "avdb_bin_assign", "avdb_record_prep",
     "avdb_pk_dedup_workspace_size", "avdb_pk_dedup", "avdb_pk_dedup_ex",
@@ -99,6 +99,7 @@ EXPORTED_SYMBOLS = [
     "avdb_keyset_workspace_size", "avdb_keyset_build", "avdb_keyset_probe",
     "avdb_primary_keys", "avdb_keyset_probe_text", "avdb_primary_keys_bound",
     "avdb_primary_keys_onepass_workspace_size", "avdb_primary_keys_onepass", "avdb_primary_keys_onepass_ex",
+    "avdb_primary_keys_fill_digests",
     "avdb_record_prep_keyed",
     "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
     "avdb_small_prep", "avdb_small_prep_host", "avdb_bin_path_host", "avdb_annotate_host", "avdb_host_alloc", "avdb_host_free",
@@ -109,6 +110,8 @@ EXPORTED_SYMBOLS = [
 
 SMALL_PATH, SMALL_KEY, SMALL_DISPLAY = 1, 2, 4
 KEYS_TOTALS_READY = 1  # AVDB_KEYS_TOTALS_READY
+KEYS_DIGEST_DEFERRED = 2  # AVDB_KEYS_DIGEST_DEFERRED
+OPT_K4_GRID = 1  # avdb_ctx_set_option
 KEYED_TOTALS, KEYED_LONG_CODES, KEYED_DEDUP_MARKS = 1, 2, 4  # avdb_record_prep_keyed's *totals_written bits
 DEDUP_MARKED = 1  # AVDB_DEDUP_MARKED
 DIGEST_CODES_READY = 1  # AVDB_DIGEST_CODES_READY
@@ -155,6 +158,7 @@ def _sig(lib):
     f.avdb_ctx_create.argtypes = [I32, ctypes.POINTER(U32), I32, ctypes.POINTER(P)]
     f.avdb_ctx_destroy.argtypes = [P]
     f.avdb_ctx_n_chrom.argtypes = [P]
+    f.avdb_ctx_set_option.argtypes = [P, I32, ctypes.c_int64]
     f.avdb_ctx_set_sequence_digests.argtypes = [P, ctypes.c_char_p, I32]
     f.avdb_l8_bin_count.argtypes = [P, ctypes.POINTER(U32)]
     f.avdb_bin_assign.argtypes = [P, P, P, P, SZ, P, P, P, P, P]
@@ -192,6 +196,7 @@ def _sig(lib):
     f.avdb_primary_keys_onepass_ex.argtypes = list(f.avdb_primary_keys.argtypes)[:-1] + [U32, P]
     f.avdb_record_prep_keyed.argtypes = list(f.avdb_record_prep.argtypes)[:-1] + [P, U32, I32, I32, P, SZ, P, SZ,
                                                                                  P, SZ, P, ctypes.POINTER(I32), P]
+    f.avdb_primary_keys_fill_digests.argtypes = [P, P, P, SZ, P, P, P, P, P]
     f.avdb_primary_keys_bound.argtypes = [SZ, SZ, ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
     f.avdb_primary_keys_onepass_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]

@@ -68,6 +68,8 @@ __device__ __forceinline__ void st_(T v, T* p) {
 }
 
 constexpr int kK1Block = 512;  // 8 waves: one LDS histogram per 8 waves
+constexpr int kK2Unroll = 2;       // plain K2: groups of 4 records per lane per trip
+constexpr int kK2KeyedUnroll = 1;  // the keyed K2 (144 VGPRs at 2)
 
 // chrom codes of one lane-group: V u32 words (4 codes each)
 template <int V> struct ChromVec;
@@ -365,7 +367,6 @@ __global__ __launch_bounds__(kBlock) void k_record_prep(
 // end / code leave as u32x4 stores, status as one u32.  Consecutive lanes hold
 // consecutive records, so a wave's heap peeks fall in one contiguous stretch of
 // the heap.  Grid-stride over a resident grid, as K1.
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // The keyed form (KEYS, avdb_record_prep_keyed) also gives K7 its group totals:
 // a wave's 64 lanes x 4 records per step are exactly one of K7's 256-record scan
@@ -655,49 +656,30 @@ extern "C" int avdb_bin_assign(avdb_ctx* ctx, const uint8_t* chrom, const uint32
   const int lds_hist = hist && ctx->tab.n_l8 <= uint32_t(kMaxLdsHistBins);
   const size_t shm = lds_hist ? size_t(ctx->tab.n_l8) * 4 : 0;
   auto* ctr = reinterpret_cast<unsigned long long*>(counters);
-  // K1 variants (records per lane-group 4V, groups in flight U, memory flags F);
-  // the default was chosen by on-device A/B (tools/k1_geom.py)
-  struct K1Var { int V, U, F; };
-  static const K1Var kVars[] = {{1, 2, 6}, {2, 1, 6}, {2, 2, 6}, {4, 1, 6}, {1, 2, 2}, {1, 4, 6},
-                                 {1, 2, 7}, {1, 2, 4}, {1, 4, 4}, {2, 1, 4}, {1, 1, 4}};
-  const K1Var kv = kVars[(ctx->k1_variant >= 0 && ctx->k1_variant < 11) ? ctx->k1_variant : 0];
-  const int R = 4 * kv.V;
+  // K1's shape: 4 records per lane-group (chrom as one u32, start / end / code as
+  // u32x4), 2 groups in flight, nontemporal loads and stores, grid-stride — chosen among
+  // eleven shapes and memory policies by on-device A/B (tools/k1_geom.py,
+  // profiles/r01_k1_*.log; the others were removed in round 5)
+  constexpr int kV = 1, kU = 2, kF = 4, R = 4 * kV;
   const bool vec = aligned(chrom, size_t(R)) && aligned(start, 16) && (!end || aligned(end, 16)) &&
                    aligned(bin_code, 16) && (!status || aligned(status, size_t(R))) && n >= size_t(R);
   if (vec) {
     const size_t ngroups = n / R;
     // One resident wave of workgroups (n_cu x blocks_per_cu); each step of a
-    // workgroup covers bdim*U*R consecutive records.
-    const unsigned bdim = unsigned(ctx->k1_block);
+    // workgroup covers kK1Block*U*R consecutive records.
+    const unsigned bdim = unsigned(kK1Block);
     const unsigned grid =
-        stream_grid(ngroups, bdim * kv.U, unsigned(ctx->n_cu * ctx->k1_blocks_per_cu));
+        stream_grid(ngroups, bdim * kU, unsigned(ctx->n_cu * ctx->k1_blocks_per_cu));
     const size_t tail = ngroups * R;
-#define K1V(HE, HI, V_, U_, F_)                                                                 \
-  hipLaunchKernelGGL((k_bin_assign4<HE, HI, V_, U_, F_>), dim3(grid), dim3(bdim), shm, s,       \
-                     reinterpret_cast<const typename ChromVec<V_>::T*>(chrom),                   \
+#define K1V(HE, HI)                                                                             \
+  hipLaunchKernelGGL((k_bin_assign4<HE, HI, kV, kU, kF>), dim3(grid), dim3(bdim), shm, s,      \
+                     reinterpret_cast<const typename ChromVec<kV>::T*>(chrom),                   \
                      reinterpret_cast<const u32x4*>(start), reinterpret_cast<const u32x4*>(end), \
                      ngroups, reinterpret_cast<u32x4*>(bin_code),                               \
-                     reinterpret_cast<typename ChromVec<V_>::T*>(status), ctx->tab, hist_l8, ctr, \
+                     reinterpret_cast<typename ChromVec<kV>::T*>(status), ctx->tab, hist_l8, ctr, \
                      lds_hist, chrom, start, end, tail, n, bin_code, status)
-#define K1ALL(HE, HI)                                                        \
-  do {                                                                       \
-    switch (ctx->k1_variant) {                                               \
-      case 1: K1V(HE, HI, 2, 1, 6); break;                                   \
-      case 2: K1V(HE, HI, 2, 2, 6); break;                                   \
-      case 3: K1V(HE, HI, 4, 1, 6); break;                                   \
-      case 4: K1V(HE, HI, 1, 2, 2); break;                                   \
-      case 5: K1V(HE, HI, 1, 4, 6); break;                                   \
-      case 6: K1V(HE, HI, 1, 2, 7); break;                                   \
-      case 7: K1V(HE, HI, 1, 2, 4); break;                                   \
-      case 8: K1V(HE, HI, 1, 4, 4); break;                                   \
-      case 9: K1V(HE, HI, 2, 1, 4); break;                                   \
-      case 10: K1V(HE, HI, 1, 1, 4); break;                                  \
-      default: K1V(HE, HI, 1, 2, 6); break;                                  \
-    }                                                                        \
-  } while (0)
-    if (end) { if (hist) K1ALL(true, true); else K1ALL(true, false); }
-    else { if (hist) K1ALL(false, true); else K1ALL(false, false); }
-#undef K1ALL
+    if (end) { if (hist) K1V(true, true); else K1V(true, false); }
+    else { if (hist) K1V(false, true); else K1V(false, false); }
 #undef K1V
     AVDB_LAUNCH_CHECK("k_bin_assign4");
   } else {
@@ -723,7 +705,7 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
 // grid-stride trips of bdim * U groups of 4, plus the < 4 records of block 0's
 // scalar tail): one K3 list slice each
 static unsigned keyed_grid(const avdb_ctx* ctx, size_t n) {
-  return stream_grid(n / 4, unsigned(kK1Block) * unsigned(ctx->k2_keyed_unroll),
+  return stream_grid(n / 4, unsigned(kK1Block) * unsigned(kK2KeyedUnroll),
                      unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
 }
 namespace avdb {
@@ -732,10 +714,10 @@ void keyed_prep_layout(const avdb_ctx* ctx, size_t n, unsigned* grid, size_t* sl
   *slice = 0;
   if (!ctx || n < 4) return;
   const unsigned g = keyed_grid(ctx, n);
-  const size_t per_trip = size_t(kK1Block) * size_t(ctx->k2_keyed_unroll) * g;  // groups of 4 per grid trip
+  const size_t per_trip = size_t(kK1Block) * size_t(kK2KeyedUnroll) * g;  // groups of 4 per grid trip
   const size_t trips = (n / 4 + per_trip - 1) / per_trip;
   *grid = g;
-  *slice = 4 * size_t(kK1Block) * size_t(ctx->k2_keyed_unroll) * trips + 4;
+  *slice = 4 * size_t(kK1Block) * size_t(kK2KeyedUnroll) * trips + 4;
 }
 }  // namespace avdb
 
@@ -825,7 +807,7 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
   const int lds_hist = hist && ctx->tab.n_l8 <= uint32_t(kMaxLdsHistBins);
   const size_t shm = lds_hist ? size_t(ctx->tab.n_l8) * 4 : 0;
   auto* ctr = reinterpret_cast<unsigned long long*>(counters);
-  const bool vec = ctx->k2_vector && n >= 4 && aligned(chrom, 4) && aligned(pos, 16) && aligned(allele_off, 16) &&
+  const bool vec = n >= 4 && aligned(chrom, 4) && aligned(pos, 16) && aligned(allele_off, 16) &&
                    aligned(ref_len, 16) && aligned(alt_len, 16) && aligned(end_out, 16) && aligned(bin_code, 16) &&
                    (!status || aligned(status, 4)) && (!lcp || aligned(lcp, 16));
   // keyed: the vector form with 16-byte aligned refSNP keys
@@ -834,10 +816,14 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
   if (vec) {
     const size_t ngroups = n / 4;
     const unsigned bdim = unsigned(kK1Block);
-    const int U = keys ? ctx->k2_keyed_unroll : ctx->k2_unroll;  // (the keyed form's registers: 144 VGPRs at U=2)
-    const unsigned grid = keys ? keyed_grid(ctx, n) : stream_grid(ngroups, bdim * U, unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
-#define K2V(HI, UU)                                                                                       \
-  if (keys && kt.group_log2 < 2) K2VK(HI, UU, 2); else if (keys) K2VK(HI, UU, 1); else K2VK(HI, UU, 0)
+    // groups of 4 records per lane per trip: 2 for plain K2, 1 for the keyed form
+    // (its registers: 144 VGPRs at 2); 1 / 2 / 4 measured on the box
+    // (tools/k2_probe.py: U=2 0.234-0.247 ms, U=1 0.26-0.31, U=4 0.44-0.47 with spills)
+    const unsigned grid = keys ? keyed_grid(ctx, n)
+                               : stream_grid(ngroups, bdim * kK2Unroll, unsigned(ctx->n_cu * ctx->k2_blocks_per_cu));
+#define K2V(HI)                                                                                           \
+  if (keys && kt.group_log2 < 2) K2VK(HI, kK2KeyedUnroll, 2); else if (keys) K2VK(HI, kK2KeyedUnroll, 1); \
+  else K2VK(HI, kK2Unroll, 0)
 #define K2VK(HI, UU, KK)                                                                                  \
   hipLaunchKernelGGL((k_record_prep4<HI, UU, KK>), dim3(grid), dim3(bdim), shm, s,                       \
                      reinterpret_cast<const uint32_t*>(chrom), reinterpret_cast<const u32x4*>(pos),      \
@@ -847,16 +833,8 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
                      reinterpret_cast<uint32_t*>(status), reinterpret_cast<u32x4*>(lcp), ctx->tab, hist_l8, \
                      ctr, lds_hist, kt, chrom, pos, allele_off, ref_len, alt_len, ngroups * 4, n, end_out,  \
                      bin_code, status, lcp)
-    if (U == 1) {
-      if (hist) K2V(true, 1);
-      else K2V(false, 1);
-    } else if (U == 4) {
-      if (hist) K2V(true, 4);
-      else K2V(false, 4);
-    } else {
-      if (hist) K2V(true, 2);
-      else K2V(false, 2);
-    }
+    if (hist) K2V(true);
+    else K2V(false);
 #undef K2V
 #undef K2VK
     AVDB_LAUNCH_CHECK("k_record_prep4");

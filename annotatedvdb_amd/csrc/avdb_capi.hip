@@ -71,47 +71,24 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
         cus > 0)
       c->n_cu = cus;
   }
+  // Grid knobs (the same kernels on other grids; tests/test_gpu_parity.py::
+  // test_grid_knobs_parity runs each at a non-default value against the oracle).
   // K1 defaults from the on-device A/B (tools/k1_sweep.py, tools/k1_geom.py;
   // profiles/r01_k1_*.log): 512-thread workgroups x 4 per CU (32 waves, one
   // 24.7 KB LDS histogram per 8 waves), 2 lane-groups in flight, nontemporal
   // loads AND stores, grid-stride sweep (each workgroup step covers 4096
-  // consecutive records, so a sorted batch still hits ~1 histogram bin per step).
-  // Variant 7 was chosen in back-to-back launches (the bench's steady state, where
-  // every launch also pays for its predecessor's 0.4 GB write-back): 5.75 TB/s on
-  // C2 and 5.76 TB/s on C3 vs 5.45 / 5.33 for plain stores (variant 0).
+  // consecutive records, so a sorted batch still hits ~1 histogram bin per step):
+  // 5.75 TB/s on C2 and 5.76 TB/s on C3 in back-to-back launches vs 5.45 / 5.33
+  // for plain stores.
   c->k1_blocks_per_cu = 4;
   if (const char* s = getenv("AVDB_K1_BLOCKS_PER_CU")) {
     const int v = atoi(s);
     if (v >= 1 && v <= 64) c->k1_blocks_per_cu = v;
   }
-  c->k1_variant = 7;
-  if (const char* s = getenv("AVDB_K1_VARIANT")) {
-    const int v = atoi(s);
-    if (v >= 0 && v <= 10) c->k1_variant = v;
-  }
-  c->k1_block = 512;
-  if (const char* s = getenv("AVDB_K1_BLOCK")) {
-    const int v = atoi(s);
-    if (v == 256 || v == 512) c->k1_block = v;
-  }
-  // K2 vector form (4 records per lane from 16-byte loads) when the arrays are
-  // aligned; AVDB_K2_VECTOR=0 keeps the one-record-per-lane form (A/B)
-  c->k2_vector = true;
-  if (const char* s = getenv("AVDB_K2_VECTOR")) c->k2_vector = atoi(s) != 0;
-  c->k2_unroll = 2;
-  if (const char* s = getenv("AVDB_K2_UNROLL")) {
-    const int v = atoi(s);
-    if (v == 1 || v == 2 || v == 4) c->k2_unroll = v;
-  }
   c->k2_blocks_per_cu = 4;
   if (const char* s = getenv("AVDB_K2_BLOCKS_PER_CU")) {
     const int v = atoi(s);
     if (v >= 1 && v <= 64) c->k2_blocks_per_cu = v;
-  }
-  c->k2_keyed_unroll = 1;
-  if (const char* s = getenv("AVDB_K2_KEYED_UNROLL")) {
-    const int v = atoi(s);
-    if (v == 1 || v == 2 || v == 4) c->k2_keyed_unroll = v;
   }
   // K4 (SHA-512, VALU-bound) persistent grid: its occupancy by default; fewer
   // workgroups leave CUs to a kernel running beside it on another stream
@@ -120,16 +97,27 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     const int v = atoi(s);
     if (v >= 1 && v <= 3) c->k4_blocks_per_cu = v;
   }
-  // (the one-kernel run scan for C1's 1.1 M records measured 22.2 us against 5.7 + 7.6 us
-  // for the list form: the list form is the default at every size)
+  c->k4_grid = 0;  // avdb_ctx_set_option(AVDB_OPT_K4_GRID): workgroups, 0 = n_cu * k4_blocks_per_cu
   c->k7_raw_blocks = 256;
   if (const char* s = getenv("AVDB_K7_RAW_BLOCKS")) c->k7_raw_blocks = size_t(strtoull(s, nullptr, 10));
-  c->k7_v2 = 1;
-  if (const char* s = getenv("AVDB_K7_V2")) c->k7_v2 = atoi(s);
-  c->k3_list_min = 0;
-  if (const char* s = getenv("AVDB_K3_LIST_MIN")) c->k3_list_min = size_t(strtoull(s, nullptr, 10));
   *out = c;
   return AVDB_OK;
+}
+
+extern "C" int avdb_ctx_set_option(avdb_ctx* ctx, int option, int64_t value) {
+  if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
+  switch (option) {
+    case AVDB_OPT_K4_GRID:
+      if (value < 0 || value > 65536) {
+        avdb_set_error("avdb_ctx_set_option: K4 grid of %lld workgroups out of range", (long long)value);
+        return AVDB_EINVAL;
+      }
+      ctx->k4_grid = int(value);
+      return AVDB_OK;
+    default:
+      avdb_set_error("avdb_ctx_set_option: unknown option %d", option);
+      return AVDB_EINVAL;
+  }
 }
 
 extern "C" int avdb_ctx_destroy(avdb_ctx* ctx) {

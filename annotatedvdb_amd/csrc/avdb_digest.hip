@@ -929,8 +929,10 @@ extern "C" int avdb_vrs_digest_ex(avdb_ctx* ctx, const uint8_t* chrom, const uin
                        max_seq_len, counts, list);
   AVDB_LAUNCH_CHECK("k_long_scatter");
   // persistent grid over the grouped list
+  // (a smaller grid leaves CUs to K7 running beside it: avdb_ctx_set_option)
   const int per_cu = ctx->k4_blocks_per_cu < kDigestWavesPerSimd ? ctx->k4_blocks_per_cu : kDigestWavesPerSimd;
-  hipLaunchKernelGGL(k_vrs_digest, dim3(ctx->n_cu * per_cu), dim3(kBlock), 0, s, chrom, pos,
+  const unsigned grid = ctx->k4_grid > 0 ? unsigned(ctx->k4_grid) : unsigned(ctx->n_cu * per_cu);
+  hipLaunchKernelGGL(k_vrs_digest, dim3(grid), dim3(kBlock), 0, s, chrom, pos,
                      allele_off,
                      ref_len, alt_len, heap, heap_bytes, list, total, ctx->d_seq_digest, ctx->d_loc_tail,
                      ctx->tab.n, digest_out);

@@ -15,6 +15,7 @@ namespace avdb {
 #define AVDB_HD __host__ __device__ __forceinline__
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;               // 4 waves per workgroup
@@ -265,16 +266,10 @@ struct avdb_ctx {
   int device;
   int n_cu;            // compute units on the device (256 on MI355X)
   int k1_blocks_per_cu;  // K1 grid = n_cu * k1_blocks_per_cu workgroups (env AVDB_K1_BLOCKS_PER_CU)
-  int k1_variant;        // K1 lane-group shape / memory policy (env AVDB_K1_VARIANT, bins.hip)
-  int k1_block;          // K1 workgroup size: 256 or 512 (env AVDB_K1_BLOCK)
-  bool k2_vector;        // K2 4-records-per-lane form (env AVDB_K2_VECTOR, default on)
-  int k2_unroll;         // K2 groups of 4 records per lane per trip (env AVDB_K2_UNROLL: 1, 2, 4)
   int k2_blocks_per_cu;  // K2 grid = n_cu * this (env AVDB_K2_BLOCKS_PER_CU)
-  int k2_keyed_unroll;   // keyed K2 (K7 group totals) groups per lane per trip (env AVDB_K2_KEYED_UNROLL)
   int k4_blocks_per_cu;  // K4 digest grid = n_cu * this (env AVDB_K4_BLOCKS_PER_CU; default: its occupancy, 3)
+  int k4_grid;           // K4 digest grid in workgroups when > 0 (avdb_ctx_set_option AVDB_OPT_K4_GRID)
   size_t k7_raw_blocks;  // K7 one-pass: write pass sums up to this many block totals itself (env AVDB_K7_RAW_BLOCKS)
-  int k7_v2;             // K7 one-pass write pass: 1 the split-range key renderer (default), 0 the round-3 one (env AVDB_K7_V2)
-  size_t k3_list_min;    // K3 grouped: two-phase list form from this many records on (env AVDB_K3_LIST_MIN)
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null
   uint64_t* d_loc_tail;  // K4: block 1 of each contig's SequenceLocation message per digit count (avdb_digest.hip)

@@ -43,10 +43,21 @@ __global__ __launch_bounds__(kBlock) void k_display(const uint8_t* __restrict__ 
   }
 }
 
+
 // ---------------------------------------------------------------------------
-// K7: primary keys (+ ltree bin paths) of a record batch; one lane per record.
-// SIZE needs only the SoA (lengths, pos, ext): it never reads the heap, so it
-// is a cheap streaming pass; WRITE renders the text and checks the allele bytes.
+// K7: primary keys (+ ltree bin paths) of a record batch as text.
+//   key  = label ':' pos ':' ref ':' alt [':rs' id]     (primary_key_generator.py:106-122)
+//          label ':' pos ':' <32 digest chars> [':rs' id]  (ref_len + alt_len > max_seq_len)
+//   path = generate_bin_index_references.py's ltree label of the record's bin
+// The batch is cut into scan groups of 64 or 256 records.  Each group's (keys,
+// paths) byte total comes from the keyed K2 (avdb_record_prep_keyed) or from
+// k_key_group_totals; k_key_group_scan scans them per block of 4,096 groups; the
+// write pass (k_record_keys_v2) recomputes each record's sizes from the SoA it
+// reads anyway, scans them over the wave, writes the u64 offsets itself and
+// renders the text.  A device-wide decoupled look-back over 64-record tiles was
+// built first: the agent-scope status loads of each look-back window cost more
+// than the tile (168 ms for C4k's 1.25e8 records), so the scan runs over group
+// totals instead.
 // ---------------------------------------------------------------------------
 struct KeyArgs {
   const uint8_t* chrom;
@@ -57,109 +68,34 @@ struct KeyArgs {
   const uint8_t* heap;
   const uint64_t* ext;
   const uint32_t* code;   // nullable: no paths
-  const char* digest;     // nullable: long records get state NEED_DIGEST
+  const char* digest;     // nullable: long records get state NEED_DIGEST (or DIGEST_PENDING)
   size_t heap_bytes, n, key_cap, path_cap;
   uint32_t max_seq_len;
   int32_t n_chrom;
+  uint32_t defer;         // AVDB_KEYS_DIGEST_DEFERRED: long keys laid out, their 32 chars left for the fill pass
   uint64_t* key_off;
   uint64_t* path_off;
   uint8_t* key_out;
   uint8_t* path_out;
   uint8_t* state;
-  uint16_t* key_sz;   // SIZE: sizes as u16 in the workspace (scanned into key_off), or NULL
-  uint16_t* path_sz;
-  // MODE 2: per 256-record group the (keys, paths) offset of its first record =
+  // per group the (keys, paths) offset of its first record =
   // blk_pre[2*(g / kGroupsPerBlock) + {0,1}] + grp_pre[g].{x,y}
   const uint2* grp_pre;
   const uint64_t* blk_pre;
-  uint32_t group_log2;  // MODE 2: records per scan group = 64 << group_log2 (tiles per group = 1 << group_log2)
-  uint32_t blk_raw;     // MODE 2: blk_pre holds each block's totals, not their exclusive scan
+  uint32_t group_log2;  // records per scan group = 64 << group_log2 (tiles per group = 1 << group_log2)
+  uint32_t blk_raw;     // blk_pre holds each block's totals, not their exclusive scan
 };
 
-// WRITE renders each wave's 64 records as a tile: each stream's span (the
-// records' texts are adjacent) is staged in the wave's own LDS image when it fits
-// (keys <= 40 B and ltree paths <= 87 B on average; else the lanes write global
-// memory directly), then flushed by the same wave with coalesced 16-byte stores
-// (a wave of per-lane 8-byte stores would touch 64 partly written lines per
-// instruction).  Tiles are per wave, with no s_barrier (the workgroup-tile form
-// with two barriers per tile measured the same: 13.46 vs 13.40 ms on C4k).  The
-// flush zeroes what it read, which keeps the images zero between tiles (the sink
-// ORs the words lanes share).  2.5 + 5.5 KB per wave, 32 KB per workgroup.
-// What the key stream waited on was its loads inside per-lane branches (the
-// digest, short-allele and long-indel pieces each a dependent global load in
-// turn): the register window below took keys + paths from 13.40 to 10.19 ms.
-// Then each tile's SoA and offsets are loaded one tile ahead (a record's end
-// offset is the next lane's start, by shuffle): 9.89 -> 8.20 ms at 4 waves/SIMD
-// (104 VGPRs; forcing 5 waves measured the same).  Loading the next tile's key
-// window ahead as well (AVDB_K7_PREFETCH=2, 121 VGPRs) was slower: 8.30 vs 8.16.
-// AVDB_K7_EXP: on-device A/B knobs for the write pass (tools/k7_ab.sh; some
-// produce wrong text and exist only to time a part): 1 no heap bytes, 2 no rsid
-// digits, 4 no allele check, 8 no POS digits, 16 keys to global (no LDS image),
-// 32 paths to global, 64 key bytes read per piece (no register window).
-#ifndef AVDB_K7_SIZE16
-#define AVDB_K7_SIZE16 1  // A/B knob: 0 writes u64 sizes and scans them in place
-#endif
 #ifndef AVDB_K7_GRID
-#define AVDB_K7_GRID 16384u  // write-pass waves / 4 (A/B knob; C4k K7 5.14 -> 5.00 ms against 4,096; with one-wave workgroups the v2 grid is 4x this)
+#define AVDB_K7_GRID 16384u  // write-pass waves / 4 (C4k K7 5.14 -> 5.00 ms against 4,096; with one-wave workgroups the grid is 4x this)
 #endif
 // (A periodic-span flush for tiles whose 64 records share one bin — the path
 // rendered once, each chunk read from it at its phase — measured no faster:
 // 10.21 vs 10.19 ms on C4k keys + paths; not kept.)
-#ifndef AVDB_K7_EXP
-#define AVDB_K7_EXP 0
-#endif
-#ifndef AVDB_K7_WINCHECK
-#define AVDB_K7_WINCHECK 1  // key window: one bounds check per record (0: per word, A/B)
-#endif
 constexpr uint32_t kKeyWave = 2560;
 constexpr uint32_t kPathWave = 5632;
+
 constexpr uint32_t kWavesPerBlock = kBlock / kWave;
-
-// bytes [s, s+n) of the 7-word register window w (s + n <= 56)
-constexpr uint32_t kKeyWords = 7;
-template <class O>
-__device__ __forceinline__ void append_range(O& o, const uint64_t (&w)[kKeyWords], uint32_t s, uint32_t n) {
-  const uint32_t e = s + n;
-#pragma unroll
-  for (uint32_t k = 0; k < kKeyWords; ++k) {
-    const uint32_t lo = s > 8 * k ? s : 8 * k;
-    const uint32_t hi = e < 8 * k + 8 ? e : 8 * k + 8;
-    if (hi > lo) o.append((w[k] >> (8 * (lo - 8 * k))) & low_bytes_mask(hi - lo), hi - lo);
-  }
-}
-
-// "ref:alt" from the window: the bytes [s, s+r+a) shifted to byte 0, a ':'
-// inserted at byte r (the words past it move up one byte), then appended as up
-// to seven words — one append per 8 output bytes instead of one per piece of
-// each allele
-#ifndef AVDB_K7_KEYJOIN
-#define AVDB_K7_KEYJOIN 1  // A/B knob: 0 appends ref, ':' and alt as separate ranges
-#endif
-template <class O>
-__device__ __forceinline__ void append_joined(O& o, const uint64_t (&w)[kKeyWords], uint32_t s, uint32_t r,
-                                              uint32_t a) {
-  uint64_t y[kKeyWords];
-#pragma unroll
-  for (uint32_t k = 0; k < kKeyWords; ++k) {
-    const uint64_t nx = k + 1 < kKeyWords ? w[k + 1] : 0ull;
-    y[k] = s ? (w[k] >> (8 * s)) | (nx << (64 - 8 * s)) : w[k];
-  }
-  const uint32_t len = r + 1 + a;
-  uint64_t prev = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < kKeyWords; ++j) {
-    const int32_t rel = int32_t(r) - int32_t(8 * j);  // ':' position in word j
-    const uint64_t mlo = rel <= 0 ? 0ull : (rel >= 8 ? ~0ull : low_bytes_mask(uint32_t(rel)));
-    const uint64_t mhi = rel >= 7 ? 0ull : (rel < 0 ? ~0ull : ~low_bytes_mask(uint32_t(rel + 1)));
-    const uint64_t colon = (rel >= 0 && rel < 8) ? (0x3Aull << (8 * rel)) : 0ull;
-    const uint64_t z = (y[j] & mlo) | (((y[j] << 8) | (prev >> 56)) & mhi) | colon;
-    prev = y[j];
-    if (8 * j < len) {
-      const uint32_t t = len - 8 * j < 8u ? len - 8 * j : 8u;
-      o.append(z & low_bytes_mask(t), t);
-    }
-  }
-}
 
 // the wave's LDS writes (lanes OR into words their neighbours share) are complete
 // and visible to all its lanes before it reads them back: DS instructions of one
@@ -171,16 +107,6 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ---------------------------------------------------------------------------
-// K7 with group offsets (MODE 2): the size pass writes one (keys, paths) total
-// per 256-record group, two small kernels scan them (per block of 4,096 groups,
-// then the block totals), and the write pass recomputes each record's sizes
-// from the SoA it reads anyway, scans them over the wave, and writes the u64
-// offsets itself.  A device-wide decoupled look-back over 64-record tiles was
-// built first (one launch, tiles in launch order): the agent-scope status loads
-// of each look-back window cost more than the tile (168 ms for C4k's 1.25e8
-// records), so the scan runs over group totals instead.
-// ---------------------------------------------------------------------------
 // Records per scan group: 256 (4 tiles of 64, one wave renders them in turn)
 // for large batches; 64 (one tile) below kSmallGroupN records, where a wave per
 // tile gives the launch 4x the waves (C1, 1.1 M records: one generation of waves).
@@ -195,11 +121,11 @@ constexpr uint32_t kScanThreads = 1024;       // 4 groups per thread
 // totals before its group itself (<= 4 loads per lane at a group's start) instead
 // of a separate one-workgroup scan launch
 
-// the sizes the size pass gives record j (SoA-decidable key state only)
+// the sizes the write pass gives record j (SoA-decidable key state only)
 __device__ __forceinline__ void record_sizes(const KeyArgs& A, uint32_t c, uint32_t p, uint32_t r, uint32_t a,
                                              uint64_t e, uint32_t cd, uint32_t* ks, uint32_t* ps) {
-  key_path_sizes(c, p, r, a, e, cd, A.max_seq_len, uint32_t(A.n_chrom), A.digest != nullptr, A.code != nullptr, ks,
-                 ps);
+  key_path_sizes(c, p, r, a, e, cd, A.max_seq_len, uint32_t(A.n_chrom), A.digest != nullptr || A.defer,
+                 A.code != nullptr, ks, ps);
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -359,380 +285,29 @@ __global__ __launch_bounds__(kScanThreads) void k_key_block_scan(uint64_t* __res
   }
 }
 
-// a tile's key / path sizes (what the size pass writes) and their wave scans
-struct TileScan {
-  uint32_t ksz, psz, xk, xp, K, P;
-};
-
-#ifndef AVDB_K7_PREFETCH
-#define AVDB_K7_PREFETCH 1  // the next tile's SoA and offsets are loaded before this one renders (0: A/B)
-#endif
-// a tile's per-record inputs (WRITE with AVDB_K7_PREFETCH)
-struct KeyTileIn {
-  uint32_t c, p, r, a, cd;
-  uint64_t e, off, ko, po;
-  // AVDB_K7_PREFETCH >= 2: the key window too, loaded once `off` has arrived
-  uint64_t w[kKeyWords];
-  uint32_t wmis;
-  bool in_regs;
-};
-
-// MODE 0: size pass; 1: write pass (offsets given); 2: one pass (sizes, look-back
-// scan, offsets written, text)
-template <int MODE>
-#ifndef AVDB_K7_WAVES
-#define AVDB_K7_WAVES (AVDB_K7_PREFETCH ? 4 : 5)
-#endif
-__global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A) {
-  constexpr bool WRITE = MODE != 0;
-  constexpr bool ONEP = MODE == 2;
-  static_assert(!ONEP || AVDB_K7_PREFETCH, "the group-offset form reads each tile's SoA ahead");
-  __shared__ uint64_t s_kimg[WRITE ? kWavesPerBlock * kKeyWave / 8 : 1];
-  __shared__ uint64_t s_pimg[WRITE ? kWavesPerBlock * kPathWave / 8 : 1];
-  const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
-  lds_u64* kimg = (lds_u64*)s_kimg + (WRITE ? wv * (kKeyWave / 8) : 0);
-  lds_u64* pimg = (lds_u64*)s_pimg + (WRITE ? wv * (kPathWave / 8) : 0);
-  if constexpr (WRITE) {
-    for (uint32_t q = lane; q < kKeyWave / 8; q += kWave) kimg[q] = 0;
-    for (uint32_t q = lane; q < kPathWave / 8; q += kWave) pimg[q] = 0;
-    wave_lds_sync();
-  }
-  // WRITE: one 64-record tile per wave; SIZE: one record per lane (same indexing).
-  const uint32_t bid = blockIdx.x;
-  const size_t stride = size_t(gridDim.x) * blockDim.x;
-  constexpr bool PF = WRITE && AVDB_K7_PREFETCH;
-  auto load_in = [&](size_t t) {
-    KeyTileIn v{};
-    const size_t j = t + lane;
-    if (j < A.n) {
-      v.c = A.chrom[j];
-      v.p = A.pos[j];
-      v.r = A.rl[j];
-      v.a = A.al[j];
-      v.e = A.ext ? A.ext[j] : 0ull;
-      v.off = A.off[j];
-      if constexpr (!ONEP) v.ko = A.key_off[j];
-      if (A.code) {
-        v.cd = A.code[j];
-        if constexpr (!ONEP) v.po = A.path_off[j];
-      }
-    }
-    return v;
-  };
-  constexpr bool PFW = WRITE && AVDB_K7_PREFETCH >= 2;
-  // the key bytes of record j (a short record's ref+alt, a long one's digest row)
-  // as the register window, for a tile loaded ahead
-  auto load_window = [&](KeyTileIn& v, size_t j) {
-    v.in_regs = false;
-    v.wmis = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kKeyWords; ++k) v.w[k] = 0;
-    if (j >= A.n || (AVDB_K7_EXP & 64)) return;
-    const bool lngj = uint64_t(v.r) + v.a > A.max_seq_len;
-    const uint32_t ra = v.r + v.a;
-    if (v.c >= uint32_t(A.n_chrom) || (v.e >> 63) || (lngj && !A.digest) || (!lngj && v.off + ra > A.heap_bytes))
-      return;
-    const uintptr_t src = lngj ? reinterpret_cast<uintptr_t>(A.digest) + 32 * j
-                               : reinterpret_cast<uintptr_t>(A.heap) + v.off;
-    const uintptr_t aw = src & ~uintptr_t(7);
-    v.wmis = uint32_t(src & 7);
-    const uint32_t nb = lngj ? AVDB_DIGEST_CHARS : ra;
-    v.in_regs = v.wmis + nb <= 8 * kKeyWords;
-    if (v.in_regs) {
-      const uint32_t nw = (v.wmis + nb + 7) >> 3;
-      const Heap h = lngj ? Heap{src, src + AVDB_DIGEST_CHARS} : make_heap(A.heap, A.heap_bytes);
-#pragma unroll
-      for (uint32_t k = 0; k < kKeyWords; ++k)
-        if (k < nw) v.w[k] = heap_word(aw + 8 * k, h);
-    }
-  };
-  // ONEP: a wave takes 256-record groups (grid-stride) and their four 64-record
-  // tiles in order, carrying the running offsets from the group's scanned base
-  const size_t gwave = size_t(bid) * kWavesPerBlock + wv, n_gw = size_t(gridDim.x) * kWavesPerBlock;
-  auto next_tile = [&](size_t t) -> size_t {
-    const uint32_t tpg = 1u << A.group_log2;
-    return ((t / kWave) & (tpg - 1)) != tpg - 1 ? t + kWave
-                                                : t - size_t(tpg - 1) * kWave + n_gw * (size_t(kWave) << A.group_log2);
-  };
-  // ONEP: sizes of the tile whose SoA is in v (first record t), scanned over the wave
-  auto tile_sizes = [&](const KeyTileIn& v, size_t t) {
-    TileScan q{};
-    if (t + lane < A.n) record_sizes(A, v.c, v.p, v.r, v.a, v.e, v.cd, &q.ksz, &q.psz);
-    q.xk = q.ksz;
-    q.xp = q.psz;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t uk = __shfl_up(q.xk, d, kWave), up = __shfl_up(q.xp, d, kWave);
-      if (lane >= uint32_t(d)) {
-        q.xk += uk;
-        q.xp += up;
-      }
-    }
-    q.K = __shfl(q.xk, kWave - 1, kWave);
-    q.P = __shfl(q.xp, kWave - 1, kWave);
-    return q;
-  };
-  size_t t0 = ONEP ? gwave * (size_t(kWave) << A.group_log2) : size_t(bid) * blockDim.x + size_t(wv) * kWave;
-  KeyTileIn nx{};
-  uint64_t run_k = 0, run_p = 0;  // ONEP: offsets of the current tile's first record
-  if (PF && t0 < A.n) {
-    nx = load_in(t0);
-    if (PFW) load_window(nx, t0 + lane);
-  }
-  for (size_t tn = 0; t0 < A.n; t0 = tn) {
-    tn = ONEP ? next_tile(t0) : t0 + stride;
-    const size_t i = t0 + lane;
-    const bool live = i < A.n;
-    const KeyTileIn cur = nx;
-    if (PF && tn < A.n) nx = load_in(tn);
-    TileScan sc{};
-    if constexpr (ONEP) {
-      if (((t0 / kWave) & ((1u << A.group_log2) - 1)) == 0) {  // a new group: its scanned base
-        const size_t g = (t0 / kWave) >> A.group_log2;
-        const size_t b = g / kGroupsPerBlock;
-        const uint2 gp = A.grp_pre[g];
-        if (A.blk_raw) {  // the totals of the blocks before b, summed over the wave
-          uint64_t bk = 0, bp = 0;
-          for (size_t q = lane; q < b; q += kWave) {
-            bk += A.blk_pre[2 * q];
-            bp += A.blk_pre[2 * q + 1];
-          }
-          run_k = wave_sum64(bk) + gp.x;
-          run_p = wave_sum64(bp) + gp.y;
-        } else {
-          run_k = A.blk_pre[2 * b] + gp.x;
-          run_p = A.blk_pre[2 * b + 1] + gp.y;
-        }
-      }
-      sc = tile_sizes(cur, t0);
-    }
-    uint32_t c = 0, p = 0, r = 0, a = 0;
-    uint64_t e = 0;
-    bool lng = false;
-    uint8_t st = AVDB_KEY_HOST;
-    if (live) {
-      c = PF ? cur.c : A.chrom[i];
-      p = PF ? cur.p : A.pos[i];
-      r = PF ? cur.r : A.rl[i];
-      a = PF ? cur.a : A.al[i];
-      e = PF ? cur.e : (A.ext ? A.ext[i] : 0ull);
-      lng = uint64_t(r) + a > A.max_seq_len;
-      // SoA-decidable states; the WRITE pass adds the allele-byte checks
-      st = AVDB_KEY_OK;
-      if (c >= uint32_t(A.n_chrom) || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
-      else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
-    }
-
-    // WRITE: the bytes a key copies — a short record's ref+alt, or a long record's
-    // 32 digest characters — are loaded into a 7-word register window up front,
-    // all loads independent and outside any branch.  Loads inside the per-lane
-    // branches (digest / short / long-indel paths) each cost the wave a full
-    // memory latency in turn, since nearly every wave has lanes on several paths.
-    uint64_t w[kKeyWords];
-#pragma unroll
-    for (uint32_t k = 0; k < kKeyWords; ++k) w[k] = 0;
-    uint32_t wmis = 0;     // byte offset of the first key byte in w
-    bool in_regs = false;  // the window holds them (else: the per-piece global path)
-    auto key = [&](auto o) {  // primary_key_generator.py:106-122
-      chrom_name(o, c);
-      if constexpr (!(WRITE && (AVDB_K7_EXP & 8))) {
-        o.put(':');
-        o.u32v(p);
-      } else {
-        o.put(':');
-      }
-      o.put(':');
-      if (WRITE && (AVDB_K7_EXP & 1)) {
-        o.append(0x473A41ull, 3);
-      } else if (WRITE && in_regs && lng) {
-        append_range(o, w, 0, AVDB_DIGEST_CHARS);
-      } else if (WRITE && in_regs && AVDB_K7_KEYJOIN) {
-        append_joined(o, w, wmis, r, a);
-      } else if (WRITE && in_regs) {
-        append_range(o, w, wmis, r);
-        o.put(':');
-        append_range(o, w, wmis + r, a);
-      } else if (lng) {  // only reached with a digest array (st == OK)
-        o.bytes((glb_cp)(A.digest + 32 * i), AVDB_DIGEST_CHARS);
-      } else {
-        const uint64_t off = A.off[i];
-        o.bytes((glb_cp)(A.heap + off), r);
-        o.put(':');
-        o.bytes((glb_cp)(A.heap + off + r), a);
-      }
-      if (e && !(e >> 63)) {
-        o.lit(":rs");
-        if constexpr (!(WRITE && (AVDB_K7_EXP & 2))) o.u64v(e);
-      }
-      return o;
-    };
-    if constexpr (WRITE) {
-      if (live && st == AVDB_KEY_OK) {
-        const uint64_t off = lng ? 0 : (PF ? cur.off : A.off[i]);
-        const uint32_t ra = r + a;
-        if (!lng && off + ra > A.heap_bytes) {
-          st = AVDB_KEY_HOST;
-        } else if (PFW) {
-#pragma unroll
-          for (uint32_t k = 0; k < kKeyWords; ++k) w[k] = cur.w[k];
-          wmis = cur.wmis;
-          in_regs = cur.in_regs;
-        } else if (!(AVDB_K7_EXP & 64)) {
-          const uintptr_t src = lng ? reinterpret_cast<uintptr_t>(A.digest) + 32 * i
-                                    : reinterpret_cast<uintptr_t>(A.heap) + off;
-          const uintptr_t aw = src & ~uintptr_t(7);
-          wmis = uint32_t(src & 7);
-          const uint32_t nb = lng ? AVDB_DIGEST_CHARS : ra;
-          in_regs = wmis + nb <= 8 * kKeyWords;
-          if (in_regs) {
-            const uint32_t nw = (wmis + nb + 7) >> 3;
-            // (bytes outside the digest row / the heap allocation read as 0)
-            const Heap h = lng ? Heap{src, src + AVDB_DIGEST_CHARS} : make_heap(A.heap, A.heap_bytes);
-            if (AVDB_K7_WINCHECK && aw >= h.lo && aw + 8 * nw <= h.hi) {
-              // the whole window inside: plain loads, one bounds check per record instead of per word
-#pragma unroll
-              for (uint32_t k = 0; k < kKeyWords; ++k)
-                if (k < nw) w[k] = *gptr<uint64_t>(aw + 8 * k);
-            } else {
-#pragma unroll
-              for (uint32_t k = 0; k < kKeyWords; ++k)
-                if (k < nw) w[k] = heap_word(aw + 8 * k, h);
-            }
-          }
-        }
-        if (!lng && st == AVDB_KEY_OK && !(AVDB_K7_EXP & 4)) {
-          if (in_regs) {  // no ':' (metaseqId.split) and ASCII only, on the window
-            uint64_t bad = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < kKeyWords; ++k) {
-              const uint32_t lo = wmis > 8 * k ? wmis : 8 * k, e2 = wmis + ra;
-              const uint32_t hi = e2 < 8 * k + 8 ? e2 : 8 * k + 8;
-              if (hi > lo) {
-                const uint64_t m = low_bytes_mask(hi - 8 * k) & ~low_bytes_mask(lo - 8 * k);
-                bad |= ((w[k] & kHiBits) | bytes_eq_mask(w[k], ':')) & m & kHiBits;
-              }
-            }
-            if (bad) st = AVDB_KEY_HOST;
-          } else if (!key_allele_ok((glb_cp)(A.heap + off), ra)) {
-            st = AVDB_KEY_HOST;
-          }
-        }
-      }
-      const size_t last = t0 + kWave < A.n ? t0 + kWave : A.n;
-      // the tile's spans [gk0, gk1) / [gp0, gp1) and each record's [ko, ko1) / [po, po1)
-      uint64_t gk0, gk1, ko = 0, ko1 = 0, gp0 = 0, gp1 = 0, po = 0, po1 = 0;
-      if constexpr (ONEP) {
-        const uint64_t EK = run_k, EP = run_p;
-        run_k += sc.K;
-        run_p += sc.P;
-        gk0 = EK;
-        gk1 = EK + sc.K;
-        ko = EK + sc.xk - sc.ksz;
-        ko1 = EK + sc.xk;
-        gp0 = EP;
-        gp1 = EP + sc.P;
-        po = EP + sc.xp - sc.psz;
-        po1 = EP + sc.xp;
-        if (live) {
-          A.key_off[i] = ko;
-          if (A.code) A.path_off[i] = po;
-          if (i + 1 == A.n) {  // the totals (also from k_key_block_scan when it runs)
-            A.key_off[A.n] = ko1;
-            if (A.code) A.path_off[A.n] = po1;
-          }
-        }
-      } else {
-        gk0 = A.key_off[t0];
-        gk1 = A.key_off[last];
-        // (PF: a record's end offset is the next lane's start; the tile's last live
-        // record ends at gk1 / gp1)
-        auto next_of = [&](uint64_t v, uint64_t g1) -> uint64_t {
-          const uint64_t nv = (uint64_t(uint32_t(__shfl_down(uint32_t(v >> 32), 1, kWave))) << 32) |
-                              uint32_t(__shfl_down(uint32_t(v), 1, kWave));
-          return i + 1 == last ? g1 : nv;
-        };
-        if (PF) {
-          ko = cur.ko;
-          ko1 = next_of(cur.ko, gk1);
-        } else if (live) {
-          ko = A.key_off[i];
-          ko1 = A.key_off[i + 1];
-        }
-        if (A.code) {
-          gp0 = A.path_off[t0];
-          gp1 = A.path_off[last];
-          if (PF) {
-            po = cur.po;
-            po1 = next_of(cur.po, gp1);
-          } else if (live) {
-            po = A.path_off[i];
-            po1 = A.path_off[i + 1];
-          }
-        }
-      }
-      // stream 0: keys
-      const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap && !(AVDB_K7_EXP & 16);
-      if (live && st == AVDB_KEY_OK && ko1 > A.key_cap)
-        st = AVDB_KEY_OVERFLOW;  // never write past the buffer; say so in the state
-      if (live && st == AVDB_KEY_OK) {
-        const uint64_t at = ko;
-        if (kst) {
-          Out<true, true> o(LdsImage{}, kimg, at - (gk0 & ~uint64_t(15)));
-          key(o).finish();
-        } else {
-          Out<true> o(A.key_out, at);
-          key(o).finish();
-        }
-      }
-      // stream 1: ltree paths
-      bool pst = false, path_over = false;
-      if (A.code) {
-        pst = gp1 - (gp0 & ~uint64_t(15)) + 16 <= kPathWave && gp1 <= A.path_cap && !(AVDB_K7_EXP & 32);
-        const uint32_t cd = live ? (PF ? cur.cd : A.code[i]) : AVDB_BIN_NONE;
-        const bool has_path = live && cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom);
-        path_over = has_path && po1 > A.path_cap;
-        if (has_path && !path_over) {
-          const uint64_t at = po;
-          if (pst) {
-            Out<true, true> o(LdsImage{}, pimg, at - (gp0 & ~uint64_t(15)));
-            bin_path(o, c, cd).finish();
-          } else {
-            Out<true> o(A.path_out, at);
-            bin_path(o, c, cd).finish();
-          }
-        }
-      }
-      if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
-      wave_lds_sync();
-      if (kst) flush_span(kimg, A.key_out, gk0, gk1, lane, kWave);
-      if (pst) flush_span(pimg, A.path_out, gp0, gp1, lane, kWave);
-      // the next tile's key window: its offsets have arrived by now
-      if (PFW && tn < A.n) load_window(nx, tn + lane);
-      wave_lds_sync();
-    } else if (live) {
-      const uint32_t ks = st == AVDB_KEY_OK ? key(Out<false>(nullptr, 0)).size() : 0;
-      if (A.key_sz) A.key_sz[i] = uint16_t(ks);
-      else A.key_off[i] = ks;
-      if (A.code) {
-        const uint32_t cd = A.code[i];
-        const uint32_t ps = (cd != AVDB_BIN_NONE && c < uint32_t(A.n_chrom))
-                                ? bin_path(Out<false>(nullptr, 0), c, cd).size() : 0;
-        if (A.path_sz) A.path_sz[i] = uint16_t(ps);
-        else A.path_off[i] = ps;
-      }
-    }
+// the two-call form's size pass (avdb_primary_keys with key_out == NULL): each
+// record's key and path size in place in key_off / path_off, scanned afterwards
+__global__ __launch_bounds__(kBlock) void k_key_sizes(KeyArgs A) {
+  for (size_t j = size_t(blockIdx.x) * blockDim.x + threadIdx.x; j < A.n; j += size_t(gridDim.x) * blockDim.x) {
+    uint32_t ks, ps;
+    record_sizes(A, A.chrom[j], A.pos[j], A.rl[j], A.al[j], A.ext ? A.ext[j] : 0ull,
+                 A.code ? A.code[j] : AVDB_BIN_NONE, &ks, &ps);
+    A.key_off[j] = ks;
+    if (A.code) A.path_off[j] = ps;
   }
 }
 
-
 // ---------------------------------------------------------------------------
-// K7 write pass, round 4 (k_record_keys_v2; the group-offset one-pass form).
-// Round 3's pass issued ~1,280 VALU wave-instructions per 64-record tile
-// (profiles/pmc_k7.json), most of them in the key stream: a seven-word join of
-// ref ':' alt with the ':' shifted in word by word, a separate seven-word ':' /
-// ASCII check, and a separate 32-character digest path — all of it executed by
-// the whole wave whenever one lane needs it (2 % long records put one in 73 % of
-// tiles).  Here:
+// The write pass (k_record_keys_v2).  Each wave takes 256-record groups
+// (grid-stride) and renders their four 64-record tiles in turn; each stream's
+// span of a tile (the records' texts are adjacent) is staged in the wave's own
+// LDS image when it fits (keys <= 40 B and ltree paths <= 87 B on average; else
+// the lanes write global memory directly), then flushed by the same wave with
+// coalesced 16-byte stores (a wave of per-lane 8-byte stores would touch 64
+// partly written lines per instruction).  The flush zeroes what it read, which
+// keeps the images zero between tiles (the sink ORs the words lanes share).
+// Round 4 (the round-3 pass issued ~1,280 VALU wave-instructions per tile,
+// profiles/pmc_k7.json, most of them in the key stream):
 //  * a long record's digest row and a short record's ref are the same kind of
 //    piece, a byte range of a register window, so one code path renders both;
 //  * ref and alt come from two windows (each aligned at its own range), appended
@@ -746,18 +321,18 @@ __global__ __launch_bounds__(kBlock, AVDB_K7_WAVES) void k_record_keys(KeyArgs A
 // A key that turns out HOST (':' or a non-ASCII byte) has its span written with
 // its bytes: the span is reserved from the SoA either way, and a key's text is
 // read only when its state is AVDB_KEY_OK.
+// Deferred digests (A.defer, digest == NULL): a long record's key is laid out
+// with its 32 digest characters as zero bytes and state AVDB_KEY_DIGEST_PENDING;
+// avdb_primary_keys_fill_digests writes them once K4 is done.  K7 then does not
+// wait for K4 (SHA-512, VALU-bound), so the two can share the chip.
 // ---------------------------------------------------------------------------
-// AVDB_K7V2_EXP: attribution knobs for tools/k7_attr.sh (each drops one part of
-// the pass and produces wrong text; 0 in every shipped build): 1 no key render,
-// 2 no path render, 4 no ':' / ASCII check, 8 no allele ranges, 16 no ':rs'
-// suffix, 32 no "label:pos:" prefix, 64 no flushes, 128 no window loads, 256 no
-// offset / state stores, 512 no SoA loads (values from the index), 1024 no
-// group-base loads
-#ifndef AVDB_K7V2_EXP
-#define AVDB_K7V2_EXP 0
-#endif
-#define K7X(b) ((AVDB_K7V2_EXP & (b)) != 0)
 constexpr uint32_t kWinWords = 7;  // a range of <= 49 bytes at byte offset <= 7
+
+// a tile's per-record inputs, loaded one tile ahead
+struct KeyTileIn {
+  uint32_t c, p, r, a, cd;
+  uint64_t e, off;
+};
 
 // inclusive wave64 prefix sum through DPP row shifts and row broadcasts: six
 // VALU adds with no LDS round trip (__shfl_up lowers to ds_bpermute: six
@@ -836,19 +411,19 @@ __device__ __forceinline__ void append_win(O& o, const uint64_t (&W)[kWinWords],
       uint64_t x = W[j] >> (8 * m);
       if (j + 1 < kWinWords) x |= (W[j + 1] << (63 - 8 * m)) << 1;  // (m == 0: nothing)
       if (n - 8 * j >= 8) {
-        if (!K7X(4)) bad |= key_bad(x);
+        bad |= key_bad(x);
         o.append(x, 8);
       } else {
         const uint32_t t = n - 8 * j;
         x &= low_bytes_mask(t);
-        if (!K7X(4)) bad |= key_bad(x);
+        bad |= key_bad(x);
         o.append(x, t);
       }
     }
   }
 }
 
-// "label:pos:" (contigs 0..24) as up to 14 bytes in two words
+// "label:pos:" (contigs 0..24) as up to 14 bytes in two words; returns its length
 __device__ __forceinline__ uint32_t key_prefix(uint32_t c, const Dec& d, uint64_t* p0, uint64_t* p1) {
   const uint32_t L = (c >= 9 && c < 22) ? 2u : 1u;
   const uint64_t lab = c < 9 ? uint64_t('1' + c)
@@ -893,6 +468,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
   wave_lds_sync();
   const Heap hheap = make_heap(A.heap, A.heap_bytes);
   const uint32_t n_chrom = uint32_t(A.n_chrom);
+  const bool has_digest = A.digest != nullptr || A.defer;  // long keys are laid out
   auto load_in = [&](size_t t) {
     KeyTileIn v{};
     const size_t j = t + lane;
@@ -919,12 +495,8 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
     const size_t i = t0 + lane;
     const bool live = i < A.n;
     const KeyTileIn cur = nx;
-    if (K7X(512)) {  // (attribution: no SoA loads, values from the index)
-      nx.c = uint32_t(tn + lane) % 22u; nx.p = uint32_t(tn + lane) * 7u + 1u; nx.r = 1; nx.a = 1;
-      nx.e = tn + lane + 1; nx.off = 2 * (tn + lane); nx.cd = (13u << 28) | (uint32_t(tn + lane) & 0xFFFu);
-    } else if (tn < A.n) nx = load_in(tn);
-    if (K7X(1024)) {  // (attribution: no group-base loads)
-    } else if (((t0 / kWave) & (tpg - 1)) == 0) {  // a new group: its scanned base
+    if (tn < A.n) nx = load_in(tn);
+    if (((t0 / kWave) & (tpg - 1)) == 0) {  // a new group: its scanned base
       const size_t g = (t0 / kWave) >> A.group_log2;
       const size_t b = g / kGroupsPerBlock;
       const uint2 gp = A.grp_pre[g];
@@ -949,7 +521,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
     uint32_t ksz = 0, psz = 0;
     if (live) {
       const bool lg = uint64_t(cur.r) + cur.a > A.max_seq_len;
-      if (cur.c < uint32_t(A.n_chrom) && !(cur.e >> 63) && !(lg && !A.digest))
+      if (cur.c < uint32_t(A.n_chrom) && !(cur.e >> 63) && !(lg && !has_digest))
         ksz = ((cur.c >= 9 && cur.c < 22) ? 2u : 1u) + 2u + dp.n + (lg ? uint32_t(AVDB_DIGEST_CHARS) : cur.r + 1u + cur.a) +
               (cur.e ? 3u + (e32 ? de.n : ndigits64(cur.e)) : 0u);
       if (A.code && cur.cd != AVDB_BIN_NONE && cur.c < uint32_t(A.n_chrom)) psz = bin_path_size(cur.c, cur.cd);
@@ -960,67 +532,61 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
     const uint64_t ko = gk0 + xk - ksz, ko1 = gk0 + xk, po = gp0 + xp - psz, po1 = gp0 + xp;
     run_k = gk1;
     run_p = gp1;
-    const uint32_t c = cur.c, p = cur.p, r = cur.r, a = cur.a;
+    const uint32_t c = cur.c, r = cur.r, a = cur.a;
     const uint64_t e = cur.e;
     const bool lng = uint64_t(r) + a > A.max_seq_len;
     uint8_t st = AVDB_KEY_HOST;
     if (live) {
-      if (!K7X(256)) A.key_off[i] = ko;
-      if (A.code && !K7X(256)) A.path_off[i] = po;
+      A.key_off[i] = ko;
+      if (A.code) A.path_off[i] = po;
       if (i + 1 == A.n) {
         A.key_off[A.n] = ko1;
         if (A.code) A.path_off[A.n] = po1;
       }
       st = AVDB_KEY_OK;
       if (c >= n_chrom || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
-      else if (lng && !A.digest) st = AVDB_KEY_NEED_DIGEST;
+      else if (lng && !A.digest) st = A.defer ? AVDB_KEY_DIGEST_PENDING : AVDB_KEY_NEED_DIGEST;
       else if (!lng && cur.off + r + a > A.heap_bytes) st = AVDB_KEY_HOST;
-      if (st == AVDB_KEY_OK && ko1 > A.key_cap) st = AVDB_KEY_OVERFLOW;
+      if ((st == AVDB_KEY_OK || st == AVDB_KEY_DIGEST_PENDING) && ko1 > A.key_cap) st = AVDB_KEY_OVERFLOW;
     }
     // the body's two ranges: a long record's 32 digest characters, or ref then alt
-    // (windows loaded up front, independent of each other)
-    const bool kok = st == AVDB_KEY_OK;
+    // (windows loaded up front, independent of each other); a pending digest is 32
+    // zero bytes here
+    const bool kok = st == AVDB_KEY_OK || st == AVDB_KEY_DIGEST_PENDING;
     uint64_t W1[kWinWords], W2[kWinWords];
     uint32_t m1 = 0, n1 = 0, m2 = 0, n2 = 0;
     bool wide = false;  // a range past the window (max_seq_len > 50): the per-piece path
+#pragma unroll
+    for (uint32_t k = 0; k < kWinWords; ++k) W1[k] = W2[k] = 0;
     if (kok) {
-      uintptr_t s1, s2;
       if (lng) {
-        s1 = reinterpret_cast<uintptr_t>(A.digest) + 32 * i;
         n1 = AVDB_DIGEST_CHARS;
-        s2 = s1;
+        if (A.digest) {
+          const uintptr_t s1 = reinterpret_cast<uintptr_t>(A.digest) + 32 * i;
+          m1 = uint32_t(s1 & 7);
+          load_win(W1, s1, n1, Heap{s1, s1 + AVDB_DIGEST_CHARS});
+        }
       } else {
-        s1 = reinterpret_cast<uintptr_t>(A.heap) + cur.off;
+        const uintptr_t s1 = reinterpret_cast<uintptr_t>(A.heap) + cur.off, s2 = s1 + r;
         n1 = r;
-        s2 = s1 + r;
         n2 = a;
+        m1 = uint32_t(s1 & 7);
+        m2 = uint32_t(s2 & 7);
+        wide = m1 + n1 > 8 * kWinWords || m2 + n2 > 8 * kWinWords;
+        if (!wide) {
+          load_win(W1, s1, n1, hheap);
+          load_win(W2, s2, n2, hheap);
+        }
       }
-      m1 = uint32_t(s1 & 7);
-      m2 = uint32_t(s2 & 7);
-      wide = m1 + n1 > 8 * kWinWords || m2 + n2 > 8 * kWinWords;
-      const Heap h1 = lng ? Heap{s1, s1 + AVDB_DIGEST_CHARS} : hheap;
-      if (!K7X(128)) {
-        load_win(W1, s1, wide ? 0u : n1, h1);
-        load_win(W2, s2, wide ? 0u : n2, hheap);
-      } else {
-#pragma unroll
-        for (uint32_t k = 0; k < kWinWords; ++k) W1[k] = W2[k] = uint64_t(s1 ^ s2) * (k + 1);
-      }
-    } else {
-#pragma unroll
-      for (uint32_t k = 0; k < kWinWords; ++k) W1[k] = W2[k] = 0;
     }
     // stream 0: keys
     const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap;
     uint64_t bad = 0;
     auto render_key = [&](auto o) {  // primary_key_generator.py:106-122
       uint64_t q0, q1;
-      if (!K7X(32)) {
-        const uint32_t lp = key_prefix(c, dp, &q0, &q1);
-        append2(o, q0, q1, lp);
-      }
-      if (K7X(8)) {
-      } else if (!wide) {
+      const uint32_t lp = key_prefix(c, dp, &q0, &q1);
+      append2(o, q0, q1, lp);
+      if (!wide) {
         append_win(o, W1, m1, n1, bad);
         if (!lng) o.put(':');
         append_win(o, W2, m2, n2, bad);
@@ -1031,7 +597,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
         o.put(':');
         o.bytes((glb_cp)(A.heap + off + r), a);
       }
-      if (e && !K7X(16)) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
+      if (e) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
         if (e32) {
           append2(o, 0x73723Aull | (de.lo << 24), (de.lo >> 40) | (de.hi << 24), 3 + de.n);
         } else {
@@ -1041,7 +607,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
       }
       return o;
     };
-    if (kok && !K7X(1)) {
+    if (kok) {
       if (kst) {
         Out<true, true> o(LdsImage{}, kimg, ko - (gk0 & ~uint64_t(15)));
         render_key(o).finish();
@@ -1058,7 +624,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
       const uint32_t cd = live ? cur.cd : AVDB_BIN_NONE;
       const bool has_path = live && cd != AVDB_BIN_NONE && c < n_chrom;
       path_over = has_path && po1 > A.path_cap;
-      if (has_path && !path_over && !K7X(2)) {
+      if (has_path && !path_over) {
         if (pst) {
           Out<true, true> o(LdsImage{}, pimg, po - (gp0 & ~uint64_t(15)));
           bin_path<AVDB_LEAF_WORD32>(o, c, cd).finish();
@@ -1068,11 +634,50 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
         }
       }
     }
-    if (live && !K7X(256)) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
+    if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
     wave_lds_sync();
-    if (kst && !K7X(64)) flush_span32(kimg, A.key_out, gk0, gk1, lane);
-    if (pst && !K7X(64)) flush_span32(pimg, A.path_out, gp0, gp1, lane);
+    if (kst) flush_span32(kimg, A.key_out, gk0, gk1, lane);
+    if (pst) flush_span32(pimg, A.path_out, gp0, gp1, lane);
     wave_lds_sync();
+  }
+}
+
+// avdb_primary_keys_fill_digests: the 32 digest characters of every key K7 left
+// pending, at key_off[i] + len("label:pos:"), then its state AVDB_KEY_OK.  A wave
+// reads 1,024 states per step (16 per lane); the pending ones (the long records)
+// load their digest row as two 16-byte loads and store it as four 8-byte stores.
+__global__ __launch_bounds__(kBlock) void k_fill_digests(const uint8_t* __restrict__ chrom,
+                                                         const uint32_t* __restrict__ pos, size_t n,
+                                                         const char* __restrict__ digest,
+                                                         const uint64_t* __restrict__ key_off,
+                                                         uint8_t* __restrict__ key_out, uint8_t* __restrict__ state) {
+  const size_t stride = size_t(gridDim.x) * blockDim.x * 16;
+  for (size_t j0 = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * 16; j0 < n; j0 += stride) {
+    uint8_t st[16];
+    if (j0 + 16 <= n) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(state + j0);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) st[k] = uint8_t(w[k >> 2] >> (8 * (k & 3)));
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) st[k] = j0 + k < n ? state[j0 + k] : uint8_t(0);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if ((st[k] & 0x0F) != AVDB_KEY_DIGEST_PENDING) continue;
+      const size_t i = j0 + k;
+      const uint32_t c = chrom[i];
+      const uint64_t at = key_off[i] + ((c >= 9 && c < 22) ? 2u : 1u) + 2u + ndigits(pos[i]);
+      const u32x4* d = reinterpret_cast<const u32x4*>(digest + 32 * i);
+      const u32x4 d0 = d[0], d1 = d[1];
+      gw_u64u q = reinterpret_cast<gw_u64u>((gbyte*)key_out + at);
+      q[0].v = uint64_t(d0.x) | (uint64_t(d0.y) << 32);
+      q[1].v = uint64_t(d0.z) | (uint64_t(d0.w) << 32);
+      q[2].v = uint64_t(d1.x) | (uint64_t(d1.y) << 32);
+      q[3].v = uint64_t(d1.z) | (uint64_t(d1.w) << 32);
+      state[i] = uint8_t((st[k] & 0xF0) | AVDB_KEY_OK);
+    }
   }
 }
 
@@ -1080,19 +685,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
 
 using namespace avdb;
 
-static size_t scan_bytes(size_t n) { return (scan::workspace_bytes(n) + 255) & ~size_t(255); }
-
-// K7's size pass writes each record's key and path size as u16 into the
-// workspace and the scans widen them to the u64 offsets: the pass writes 4
-// bytes per record instead of 16 and the scans read 2 instead of 8 per array
-// (C4k: 1.25e8 records, two 1 GB u64 scans at 0.76 ms each).
-static size_t scan16_bytes(size_t n) { return scan_bytes(n); }
-
-static size_t size16_slot(size_t n) { return ((2 * (n + 1)) + 255) & ~size_t(255); }
-
-namespace avdb {
-size_t key_size_workspace(size_t n) { return scan16_bytes(n + 1) + 2 * size16_slot(n); }
-}  // namespace avdb
+static size_t scan_bytes(size_t n) { return (scan::workspace_bytes(n, 2) + 255) & ~size_t(255); }
 
 extern "C" int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                        const uint32_t* end, const uint64_t* allele_off,
@@ -1140,98 +733,6 @@ extern "C" int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, cons
   return AVDB_OK;
 }
 
-extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
-                                 const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
-                                 const uint8_t* heap, size_t heap_bytes, const uint64_t* ext_id,
-                                 const uint32_t* bin_code, const char* digest, size_t n, uint32_t max_seq_len,
-                                 void* workspace, size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off,
-                                 uint8_t* key_out, size_t key_cap, uint8_t* path_out, size_t path_cap,
-                                 uint8_t* key_state, void* stream) {
-  if (!ctx || !key_off || (bin_code && !path_off)) {
-    avdb_set_error("avdb_primary_keys: null argument");
-    return AVDB_EINVAL;
-  }
-  AVDB_HIP_TRY(hipSetDevice(ctx->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  KeyArgs A;
-  memset(&A, 0, sizeof(A));
-  A.chrom = chrom;
-  A.pos = pos;
-  A.off = allele_off;
-  A.rl = ref_len;
-  A.al = alt_len;
-  A.heap = heap;
-  A.ext = ext_id;
-  A.code = bin_code;
-  A.digest = digest;
-  A.heap_bytes = heap_bytes;
-  A.n = n;
-  A.max_seq_len = max_seq_len;
-  A.n_chrom = ctx->tab.n < 25 ? ctx->tab.n : 25;  // labelled contigs (chromosomes.py:9-38)
-  A.key_off = key_off;
-  A.path_off = path_off;
-  A.key_cap = key_cap;
-  A.path_cap = path_cap;
-  A.key_out = key_out;
-  A.path_out = path_out;
-  A.state = key_state;
-  auto* ko = reinterpret_cast<unsigned long long*>(key_off);
-  auto* po = reinterpret_cast<unsigned long long*>(path_off);
-  if (!key_out) {  // size pass + scans
-    AVDB_HIP_TRY(hipMemsetAsync(ko + n, 0, 8, s));
-    if (bin_code) AVDB_HIP_TRY(hipMemsetAsync(po + n, 0, 8, s));
-    if (n == 0) return AVDB_OK;
-    if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap) {
-      avdb_set_error("avdb_primary_keys: null array");
-      return AVDB_EINVAL;
-    }
-    size_t need = 0;
-    avdb_format_workspace_size(n, &need);
-    if (!workspace || workspace_bytes < need) {
-      avdb_set_error("avdb_primary_keys: workspace of %zu bytes required", need);
-      return AVDB_ERANGE;
-    }
-    const unsigned grid = stream_grid(n, kBlock, 4096);
-    if (max_seq_len <= 60000 && AVDB_K7_SIZE16) {  // every key and path fits in u16
-      size_t tb = scan16_bytes(n + 1);
-      auto* ksz = reinterpret_cast<uint16_t*>(static_cast<char*>(workspace) + tb);
-      auto* psz = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(ksz) + size16_slot(n));
-      AVDB_HIP_TRY(hipMemsetAsync(ksz + n, 0, 2, s));
-      AVDB_HIP_TRY(hipMemsetAsync(psz + n, 0, 2, s));
-      A.key_sz = ksz;
-      A.path_sz = bin_code ? psz : nullptr;
-      hipLaunchKernelGGL(k_record_keys<0>, dim3(grid), dim3(kBlock), 0, s, A);
-      AVDB_LAUNCH_CHECK("k_record_keys<size>");
-      if (int e = scan::exclusive_u64(ksz, ko, n + 1, workspace, tb, s)) return e;
-      if (bin_code)
-        if (int e = scan::exclusive_u64(psz, po, n + 1, workspace, tb, s)) return e;
-      return AVDB_OK;
-    }
-    hipLaunchKernelGGL(k_record_keys<0>, dim3(grid), dim3(kBlock), 0, s, A);
-    AVDB_LAUNCH_CHECK("k_record_keys<size>");
-    size_t tb = scan_bytes(n + 1);
-    if (int e = scan::exclusive_u64(ko, ko, n + 1, workspace, tb, s)) return e;
-    if (bin_code)
-      if (int e = scan::exclusive_u64(po, po, n + 1, workspace, tb, s)) return e;
-    return AVDB_OK;
-  }
-  if (n == 0) return AVDB_OK;
-  if (!key_state || (bin_code && !path_out)) {
-    avdb_set_error("avdb_primary_keys: null output");
-    return AVDB_EINVAL;
-  }
-  if (reinterpret_cast<uintptr_t>(key_out) % 8 || (path_out && reinterpret_cast<uintptr_t>(path_out) % 8)) {
-    avdb_set_error("avdb_primary_keys: outputs must be 8-byte aligned");
-    return AVDB_EINVAL;
-  }
-  // (one resident generation, 5 workgroups per CU, ran 12.3 vs 10.2 ms on C4k,
-  // with or without XCD-aware renumbering: the finer grid balances better)
-  const unsigned grid = stream_grid(n, kBlock, AVDB_K7_GRID);
-  hipLaunchKernelGGL(k_record_keys<1>, dim3(grid), dim3(kBlock), 0, s, A);
-  AVDB_LAUNCH_CHECK("k_record_keys<write>");
-  return AVDB_OK;
-}
-
 // ---- K7 with group offsets --------------------------------------------------------
 #ifndef AVDB_K7_SMALL_LOG2
 #define AVDB_K7_SMALL_LOG2 0u  // group size below kSmallGroupN records (A/B knob: 64 << this)
@@ -1256,6 +757,17 @@ extern "C" int avdb_primary_keys_onepass_workspace_size(size_t n, size_t* bytes)
   return AVDB_OK;
 }
 
+namespace avdb {
+// the two-call form (avdb_format_workspace_size): the size call's paired scan,
+// and the write call's one-pass layout (group totals and their scans)
+size_t key_size_workspace(size_t n) {
+  size_t one = 0;
+  avdb_primary_keys_onepass_workspace_size(n, &one);
+  const size_t sc = scan_bytes(n + 1);
+  return sc > one ? sc : one;
+}
+}  // namespace avdb
+
 extern "C" int avdb_primary_keys_bound(size_t n, size_t heap_bytes, size_t* key_cap, size_t* path_cap) {
   if (!key_cap || !path_cap) return AVDB_EINVAL;
   // key: label (2) ':' pos (10) ':' ref ':' alt | digest (32), ':rs' + 19 digits
@@ -1263,6 +775,36 @@ extern "C" int avdb_primary_keys_bound(size_t n, size_t heap_bytes, size_t* key_
   // path: "chr" + label (2) + 13 levels of <= 7 bytes, B up to 3 digits at L1
   *path_cap = 98 * n + 8;
   return AVDB_OK;
+}
+
+static KeyArgs key_args(const avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                        const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                        const uint64_t* ext_id, const uint32_t* bin_code, const char* digest, size_t n,
+                        uint32_t max_seq_len, uint64_t* key_off, uint64_t* path_off, uint8_t* key_out, size_t key_cap,
+                        uint8_t* path_out, size_t path_cap, uint8_t* key_state) {
+  KeyArgs A;
+  memset(&A, 0, sizeof(A));
+  A.chrom = chrom;
+  A.pos = pos;
+  A.off = allele_off;
+  A.rl = ref_len;
+  A.al = alt_len;
+  A.heap = heap;
+  A.ext = ext_id;
+  A.code = bin_code;
+  A.digest = digest;
+  A.heap_bytes = heap_bytes;
+  A.n = n;
+  A.max_seq_len = max_seq_len;
+  A.n_chrom = ctx->tab.n < 25 ? ctx->tab.n : 25;  // labelled contigs (chromosomes.py:9-38)
+  A.key_off = key_off;
+  A.path_off = path_off;
+  A.key_cap = key_cap;
+  A.path_cap = path_cap;
+  A.key_out = key_out;
+  A.path_out = path_out;
+  A.state = key_state;
+  return A;
 }
 
 extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
@@ -1275,6 +817,14 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
                                             void* stream) {
   if (!ctx || !key_off || (bin_code && !path_off) || !key_state || !key_out || (bin_code && !path_out)) {
     avdb_set_error("avdb_primary_keys_onepass: null argument");
+    return AVDB_EINVAL;
+  }
+  if (flags & ~(AVDB_KEYS_TOTALS_READY | AVDB_KEYS_DIGEST_DEFERRED)) {
+    avdb_set_error("avdb_primary_keys_onepass_ex: unknown flags 0x%x", flags);
+    return AVDB_EINVAL;
+  }
+  if ((flags & AVDB_KEYS_DIGEST_DEFERRED) && digest) {
+    avdb_set_error("avdb_primary_keys_onepass_ex: AVDB_KEYS_DIGEST_DEFERRED takes digest == NULL");
     return AVDB_EINVAL;
   }
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
@@ -1307,31 +857,13 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   auto* tot = reinterpret_cast<uint2*>(ws);
   auto* gpre = tot + ((ng + 1) & ~size_t(1));
   auto* bpre = reinterpret_cast<uint64_t*>(gpre + ((ng + 1) & ~size_t(1)));
-  KeyArgs A;
-  memset(&A, 0, sizeof(A));
-  A.chrom = chrom;
-  A.pos = pos;
-  A.off = allele_off;
-  A.rl = ref_len;
-  A.al = alt_len;
-  A.heap = heap;
-  A.ext = ext_id;
-  A.code = bin_code;
-  A.digest = digest;
-  A.heap_bytes = heap_bytes;
-  A.n = n;
-  A.max_seq_len = max_seq_len;
-  A.n_chrom = ctx->tab.n < 25 ? ctx->tab.n : 25;
-  A.key_off = key_off;
-  A.path_off = path_off;
-  A.key_cap = key_cap;
-  A.path_cap = path_cap;
-  A.key_out = key_out;
-  A.path_out = path_out;
-  A.state = key_state;
+  KeyArgs A = key_args(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id, bin_code, digest, n,
+                       max_seq_len, key_off, path_off, key_out, key_cap, path_out, path_cap, key_state);
+  A.defer = (flags & AVDB_KEYS_DIGEST_DEFERRED) ? 1u : 0u;
   A.grp_pre = gpre;
   A.blk_pre = bpre;
   A.group_log2 = key_group_log2(n);
+  const size_t wmax = size_t(AVDB_K7_GRID) * kWavesPerBlock / kV2Waves, wneed = (ng + kV2Waves - 1) / kV2Waves;
   A.blk_raw = nb <= ctx->k7_raw_blocks ? 1u : 0u;
   // the keyed K2 wrote every group's totals but the last one's, which may hold the
   // < 4 records its vector form leaves to a scalar tail: the scan sums that one again
@@ -1350,18 +882,11 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   }
   // (one workgroup doing both scans for C1's 17 K groups measured 11.9 us against
   // 5.2 + 4.9 us for the two launches: not kept; up to k7_raw_blocks blocks the
-  // write pass sums the block totals itself)
-  const unsigned grid = unsigned((ng + kWavesPerBlock - 1) / kWavesPerBlock < AVDB_K7_GRID
-                                     ? (ng + kWavesPerBlock - 1) / kWavesPerBlock : AVDB_K7_GRID);
-  if (ctx->k7_v2) {
-    // (the same cap on waves whatever the workgroup size)
-    const size_t wmax = size_t(AVDB_K7_GRID) * kWavesPerBlock / kV2Waves, wneed = (ng + kV2Waves - 1) / kV2Waves;
-    hipLaunchKernelGGL(k_record_keys_v2, dim3(unsigned(wneed < wmax ? wneed : wmax)), dim3(kV2Block), 0, s, A);
-    AVDB_LAUNCH_CHECK("k_record_keys_v2");
-  } else {
-    hipLaunchKernelGGL(k_record_keys<2>, dim3(grid), dim3(kBlock), 0, s, A);
-    AVDB_LAUNCH_CHECK("k_record_keys<groups>");
-  }
+  // write pass sums the block totals itself.  One resident generation, 5
+  // workgroups per CU, ran 12.3 vs 10.2 ms on C4k, with or without XCD-aware
+  // renumbering: the finer grid balances better.)
+  hipLaunchKernelGGL(k_record_keys_v2, dim3(unsigned(wneed < wmax ? wneed : wmax)), dim3(kV2Block), 0, s, A);
+  AVDB_LAUNCH_CHECK("k_record_keys_v2");
   return AVDB_OK;
 }
 
@@ -1375,4 +900,80 @@ extern "C" int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, co
   return avdb_primary_keys_onepass_ex(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id,
                                       bin_code, digest, n, max_seq_len, workspace, workspace_bytes, key_off, path_off,
                                       key_out, key_cap, path_out, path_cap, key_state, 0u, stream);
+}
+
+// The two-call form.  Size call (key_out == NULL): each record's sizes in place,
+// then one paired exclusive scan into key_off / path_off.  Write call: the one
+// write pass above, with its own group totals in `workspace` (the format
+// workspace holds the one-pass layout); it writes the same offsets again.
+extern "C" int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                 const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                                 const uint8_t* heap, size_t heap_bytes, const uint64_t* ext_id,
+                                 const uint32_t* bin_code, const char* digest, size_t n, uint32_t max_seq_len,
+                                 void* workspace, size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off,
+                                 uint8_t* key_out, size_t key_cap, uint8_t* path_out, size_t path_cap,
+                                 uint8_t* key_state, void* stream) {
+  if (!ctx || !key_off || (bin_code && !path_off)) {
+    avdb_set_error("avdb_primary_keys: null argument");
+    return AVDB_EINVAL;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  size_t need = 0;
+  avdb_format_workspace_size(n, &need);
+  if (!key_out) {  // size pass + scans
+    auto* ko = reinterpret_cast<unsigned long long*>(key_off);
+    auto* po = reinterpret_cast<unsigned long long*>(path_off);
+    AVDB_HIP_TRY(hipMemsetAsync(ko + n, 0, 8, s));
+    if (bin_code) AVDB_HIP_TRY(hipMemsetAsync(po + n, 0, 8, s));
+    if (n == 0) return AVDB_OK;
+    if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap) {
+      avdb_set_error("avdb_primary_keys: null array");
+      return AVDB_EINVAL;
+    }
+    if (!workspace || workspace_bytes < need) {
+      avdb_set_error("avdb_primary_keys: workspace of %zu bytes required", need);
+      return AVDB_ERANGE;
+    }
+    KeyArgs A = key_args(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id, bin_code, digest,
+                         n, max_seq_len, key_off, path_off, nullptr, 0, nullptr, 0, nullptr);
+    hipLaunchKernelGGL(k_key_sizes, dim3(stream_grid(n, kBlock, 4096)), dim3(kBlock), 0, s, A);
+    AVDB_LAUNCH_CHECK("k_key_sizes");
+    const size_t tb = scan_bytes(n + 1);
+    if (bin_code) return scan::exclusive_u64_pair(ko, ko, po, po, n + 1, workspace, tb, s);
+    return scan::exclusive_u64(ko, ko, n + 1, workspace, tb, s);
+  }
+  if (n == 0) return AVDB_OK;
+  if (!key_state || (bin_code && !path_out)) {
+    avdb_set_error("avdb_primary_keys: null output");
+    return AVDB_EINVAL;
+  }
+  if (!workspace || workspace_bytes < need) {
+    avdb_set_error("avdb_primary_keys: workspace of %zu bytes required", need);
+    return AVDB_ERANGE;
+  }
+  return avdb_primary_keys_onepass_ex(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id,
+                                      bin_code, digest, n, max_seq_len, workspace, workspace_bytes, key_off, path_off,
+                                      key_out, key_cap, path_out, path_cap, key_state, 0u, stream);
+}
+
+extern "C" int avdb_primary_keys_fill_digests(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, size_t n,
+                                              const char* digest, const uint64_t* key_off, uint8_t* key_out,
+                                              uint8_t* key_state, void* stream) {
+  if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
+  if (n == 0) return AVDB_OK;
+  if (!chrom || !pos || !digest || !key_off || !key_out || !key_state) {
+    avdb_set_error("avdb_primary_keys_fill_digests: null array");
+    return AVDB_EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(digest) % 16 || reinterpret_cast<uintptr_t>(key_state) % 16) {
+    avdb_set_error("avdb_primary_keys_fill_digests: digest and key_state must be 16-byte aligned");
+    return AVDB_EINVAL;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_fill_digests, dim3(stream_grid((n + 15) / 16, kBlock, 2048)), dim3(kBlock), 0, s, chrom, pos,
+                     n, digest, key_off, key_out, key_state);
+  AVDB_LAUNCH_CHECK("k_fill_digests");
+  return AVDB_OK;
 }

@@ -575,6 +575,10 @@ class Engine:
         # first phase in a dedup workspace + keep).  Every record_prep call drops
         # all of them first.
         self._pending: Dict[str, tuple] = {}
+        # test hook: every output / workspace tensor the engine allocates is filled
+        # with this byte first (None: torch.empty), so a check sees only what the
+        # kernels wrote, never what an earlier pass left in a recycled block
+        self.poison: Optional[int] = None
         if sequence_digests is not None:
             self.set_sequence_digests(sequence_digests)
 
@@ -641,7 +645,14 @@ class Engine:
 
     # -- buffers -----------------------------------------------------------
     def empty(self, n, dtype):
-        return torch.empty(n, dtype=dtype, device=self.device)
+        t = torch.empty(n, dtype=dtype, device=self.device)
+        if self.poison is not None:
+            t.view(torch.uint8).fill_(self.poison)
+        return t
+
+    def set_option(self, option: int, value: int):
+        """``avdb_ctx_set_option`` (launch shape only: ``N.OPT_K4_GRID``)."""
+        N.check("avdb_ctx_set_option", self.lib.avdb_ctx_set_option(self.ctx, int(option), int(value)))
 
     def new_histogram(self) -> torch.Tensor:
         return torch.zeros(self.n_l8, dtype=torch.int32, device=self.device)
@@ -780,7 +791,7 @@ class Engine:
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
-        dig = torch.empty((n, N.DIGEST_CHARS), dtype=torch.uint8, device=self.device)
+        dig = self.empty(max(1, n) * N.DIGEST_CHARS, torch.uint8).view(-1, N.DIGEST_CHARS)[:n]
         is_long = self.empty(n, torch.uint8)
         sz = ctypes.c_size_t()
         self.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
@@ -969,22 +980,28 @@ class Engine:
     # -- K7: primary keys + bin paths as text ------------------------------------
     def primary_keys(self, b: RecordBatch, code: Optional[torch.Tensor] = None,
                      digest: Optional[torch.Tensor] = None, max_seq_len: int = 50, *,
-                     out: Optional["KeyText"] = None, onepass: bool = True) -> "KeyText":
+                     out: Optional["KeyText"] = None, onepass: bool = True,
+                     defer_digest: bool = False) -> "KeyText":
         """``generate_primary_key`` (and, with ``code``, the ltree bin path) for
         every record of ``b`` as text on the device.  Without ``out`` the size
         pass is followed by one host read of the totals; passing a ``KeyText``
         from an earlier call on a same-shaped batch reuses its buffers (no host
         sync: a text that would end past a buffer is not written and its record's
         state says so — ``KEY_OVERFLOW`` for the key, ``PATH_OVERFLOW`` ORed in
-        for the path; ``KeyText.host`` raises on either)."""
+        for the path; ``KeyText.host`` raises on either).  ``defer_digest`` (no
+        ``digest``): long records' keys are laid out with their 32 digest
+        characters left for :meth:`fill_digests` (state ``KEY_DIGEST_PENDING``),
+        so this launch need not wait for K4."""
         b = b if b.device == self.device else b.to(self.device)
         self._check_alleles(b)
         n = b.n
         s = self._stream()
         code = self._dev(code)
         digest = self._dev(digest)
+        if defer_digest and (digest is not None or not onepass):
+            raise ValueError("primary_keys: defer_digest takes no digest (one-pass form)")
         if onepass:
-            return self._primary_keys_onepass(b, code, digest, max_seq_len, out)
+            return self._primary_keys_onepass(b, code, digest, max_seq_len, out, defer_digest)
         if out is None:
             sz = ctypes.c_size_t()
             self.lib.avdb_format_workspace_size(n, ctypes.byref(sz))
@@ -1008,7 +1025,31 @@ class Engine:
                 out.paths.numel() if out.paths is not None else 0, N.ptr(out.state), s))
         return out
 
-    def _primary_keys_onepass(self, b: RecordBatch, code, digest, max_seq_len: int, out) -> "KeyText":
+    def new_key_text(self, n: int, heap_bytes: int, paths: bool = True) -> "KeyText":
+        """Buffers for one-pass K7 output over ``n`` records with ``heap_bytes`` of
+        alleles (texts sized by ``avdb_primary_keys_bound``): what a keyed K2 writes
+        its group totals into before the first ``primary_keys(..., out=...)``."""
+        sz = ctypes.c_size_t()
+        self.lib.avdb_primary_keys_onepass_workspace_size(n, ctypes.byref(sz))
+        kc, pc = ctypes.c_size_t(), ctypes.c_size_t()
+        self.lib.avdb_primary_keys_bound(n, heap_bytes, ctypes.byref(kc), ctypes.byref(pc))
+        return KeyText(ws=self.empty(int(sz.value), torch.uint8), key_off=self.empty(n + 1, torch.int64),
+                       path_off=self.empty(n + 1, torch.int64) if paths else None,
+                       state=self.empty(max(16, n), torch.uint8), keys=self.empty(int(kc.value), torch.uint8),
+                       paths=self.empty(int(pc.value), torch.uint8) if paths else None)
+
+    def fill_digests(self, b: RecordBatch, digest: torch.Tensor, kt: "KeyText"):
+        """``avdb_primary_keys_fill_digests``: the digest characters of every key a
+        ``primary_keys(..., defer_digest=True)`` left pending (``digest`` = this
+        batch's ``vrs_digest`` output)."""
+        b = b if b.device == self.device else b.to(self.device)
+        N.check("avdb_primary_keys_fill_digests", self.lib.avdb_primary_keys_fill_digests(
+            self.ctx, N.ptr(b.chrom), N.ptr(b.pos), b.n, N.ptr(digest), N.ptr(kt.key_off), N.ptr(kt.keys),
+            N.ptr(kt.state), self._stream()))
+        return kt
+
+    def _primary_keys_onepass(self, b: RecordBatch, code, digest, max_seq_len: int, out,
+                              defer: bool = False) -> "KeyText":
         """K7 without a host round trip (``avdb_primary_keys_onepass``): per-group
         size totals, two small scans, then the write pass that recomputes each
         record's sizes, writes its offsets and the text; the text buffers are sized
@@ -1016,13 +1057,8 @@ class Engine:
         n = b.n
         sz = ctypes.c_size_t()
         self.lib.avdb_primary_keys_onepass_workspace_size(n, ctypes.byref(sz))
-        kc, pc = ctypes.c_size_t(), ctypes.c_size_t()
-        self.lib.avdb_primary_keys_bound(n, b.heap.numel(), ctypes.byref(kc), ctypes.byref(pc))
         if out is None:
-            out = KeyText(ws=self.empty(int(sz.value), torch.uint8), key_off=self.empty(n + 1, torch.int64),
-                          path_off=self.empty(n + 1, torch.int64) if code is not None else None,
-                          state=self.empty(max(1, n), torch.uint8), keys=self.empty(int(kc.value), torch.uint8),
-                          paths=self.empty(int(pc.value), torch.uint8) if code is not None else None)
+            out = self.new_key_text(n, b.heap.numel(), paths=code is not None)
         if out.key_off.numel() < n + 1 or out.state.numel() < max(1, n) or \
                 (code is not None and (out.path_off is None or out.path_off.numel() < n + 1 or out.paths is None)):
             raise ValueError("primary_keys: the reused KeyText holds fewer records (or no paths)")
@@ -1031,14 +1067,15 @@ class Engine:
         # the keyed K2 wrote this batch's group totals into this KeyText's workspace
         # (sizes from these length / id arrays and, for the paths, these bin codes)
         tot = self._pending.pop("totals", None)
-        ready = (tot is not None and tot[1] is out and tot[2:] == (n, int(max_seq_len), digest is not None)
+        ready = (tot is not None and tot[1] is out and tot[2:] == (n, int(max_seq_len), digest is not None or defer)
                  and _stamp_ok(tot[0], out.ws, b.chrom, b.pos, b.ref_len, b.alt_len, b.ext_id, code))
+        flags = (N.KEYS_TOTALS_READY if ready else 0) | (N.KEYS_DIGEST_DEFERRED if defer else 0)
         N.check("avdb_primary_keys_onepass_ex", self.lib.avdb_primary_keys_onepass_ex(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
             N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), N.ptr(code), N.ptr(digest), n, int(max_seq_len),
             N.ptr(out.ws), out.ws.numel(), N.ptr(out.key_off), N.ptr(out.path_off), N.ptr(out.keys), out.keys.numel(),
             N.ptr(out.paths), out.paths.numel() if out.paths is not None else 0, N.ptr(out.state),
-            N.KEYS_TOTALS_READY if ready else 0, self._stream()))
+            flags, self._stream()))
         return out
 
     # -- K6: existing-variant key set ----------------------------------------

@@ -78,17 +78,47 @@ def set_algorithm_invocation_provider(provider):
     _ALG_INVOCATION_PROVIDER = provider
 
 
+def _split_sql(sql):
+    """psycopg2.extras._split_sql's rule: the text before and after the one ``%s``
+    placeholder, with ``%%`` turned back into ``%``; any other ``%`` escape, a
+    second ``%s`` or none at all raise ``ValueError``.  ``sql`` is str or bytes
+    and the parts keep its type."""
+    b = isinstance(sql, bytes)
+    pct, ess = (b"%", b"s") if b else ("%", "s")
+    pre, post = [], []
+    cur = pre
+    for tok in re.split(rb"(%.)" if b else r"(%.)", sql):
+        if len(tok) != 2 or tok[:1] != pct:
+            cur.append(tok)
+        elif tok[1:] == ess:
+            if cur is not pre:
+                raise ValueError("the query contains more than one '%s' placeholder")
+            cur = post
+        elif tok[1:] == pct:
+            cur.append(pct)
+        else:
+            raise ValueError("unsupported format character: %r" % (tok[1:],))
+    if cur is pre:
+        raise ValueError("the query doesn't contain any '%s' placeholder")
+    j = b"" if b else ""
+    return j.join(pre), j.join(post)
+
+
 def _execute_values(cur, sql, argslist, template=None, page_size=100):
     """psycopg2.extras.execute_values (what variant_loader.py:471 calls): the
     ``VALUES %s`` placeholder expanded to one page of mogrified rows per
-    ``execute``.  Uses psycopg2's own when it is importable."""
+    ``execute``.  Uses psycopg2's own when it is importable; otherwise the same
+    rule (``_split_sql``), every part in the type of ``sql`` (psycopg2 encodes a
+    str query with the connection's encoding first; a cursor without a
+    connection gets the text as it came)."""
     try:
         from psycopg2.extras import execute_values
     except ImportError:
         execute_values = None
     if execute_values is not None:
         return execute_values(cur, sql, argslist, template=template, page_size=page_size)
-    pre, post = sql.split("%s", 1) if isinstance(sql, str) else sql.split(b"%s", 1)
+    b = isinstance(sql, bytes)
+    pre, post = _split_sql(sql)
     rows = list(argslist)
     for lo in range(0, len(rows), page_size):
         page = rows[lo:lo + page_size]
@@ -96,8 +126,12 @@ def _execute_values(cur, sql, argslist, template=None, page_size=100):
         for row in page:
             t = template or "(" + ",".join(["%s"] * len(row)) + ")"
             v = cur.mogrify(t, row)
-            parts.append(v.decode() if isinstance(v, bytes) else v)
-        cur.execute(pre + ",".join(parts) + post)
+            if b and not isinstance(v, bytes):
+                v = v.encode()
+            elif not b and isinstance(v, bytes):
+                v = v.decode()
+            parts.append(v)
+        cur.execute(pre + (b"," if b else ",").join(parts) + post)
 
 
 _SLOW = object()  # parse_variant: the line needs the general path

@@ -1,0 +1,135 @@
+"""The keyed record-prep step over one resident batch, as one object: what
+``bench.py`` times for C1 and C4k (BASELINE configs[0] and the per-GPU shard of
+configs[3]) and what ``tests/test_gpu_c4k.py`` / ``tests/test_gpu_c1.py`` check
+against the C oracle — the same calls, buffers and stream layout, so the benched
+form is the checked form.
+
+One step (north_star's "bin path plus primary-key generation and dedup before the
+DB write"; Load/lib ``VCFVariantLoader.__parse_alt_alleles``,
+vcf_variant_loader.py:259-348, batched):
+
+  K2  avdb_record_prep_keyed       end, bin code, status (variant_annotator.py:36-79,
+                                   bin_index.py:59-75); it also writes K7's group totals,
+                                   K4's long-record codes and K3's first phase
+  K3  avdb_pk_dedup_ex (MARKED)    keep-first per primary key (removeDuplicates.sql:2-24)
+  K4  avdb_vrs_digest_ex           VRS digests of the long records (primary_key_generator.py:125-165)
+  K7  avdb_primary_keys_onepass_ex keys + ltree paths as text (primary_key_generator.py:99-122)
+
+Layouts (``layout``):
+  ``serial``   K2, K3, K4, K7 in the launch stream;
+  ``fork``     K3 on a second stream beside K4 / K7 (it reads only K2's outputs and
+               nothing reads keep until the step ends), joined at the end;
+  ``overlap``  K7 does not wait for K4: it lays out the long keys with their digest
+               characters pending (AVDB_KEYS_DIGEST_DEFERRED) while K4 (SHA-512,
+               VALU-bound) runs on a second stream beside the store-bound K7, then
+               K3 follows K4 there, and the step joins and fills the digests
+               (avdb_primary_keys_fill_digests).
+
+All buffers the kernels hand each other (the K7 workspace and text buffers, the
+K3 and K4 workspaces) are allocated once, in ``__init__``; the per-step outputs
+(end / code / status, keep, digests) come from the engine per call, as in any
+caller's loop.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import torch
+
+from . import _native as N
+
+LAYOUTS = ("serial", "fork", "overlap")
+# what bench.py times for C4k (AVDB_BENCH_LAYOUT overrides there) and what
+# tests/test_gpu_c4k.py checks over the whole 1e9-record job
+C4K_LAYOUT = "serial"
+
+
+class KeyedStep:
+    def __init__(self, engine, batch, *, digests: bool, layout: str = "serial", max_seq_len: int = 50,
+                 hist: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None,
+                 k4_grid: int = 0):
+        if layout not in LAYOUTS:
+            raise ValueError("layout must be one of %s" % (LAYOUTS,))
+        if layout == "overlap" and not digests:
+            raise ValueError("the overlap layout runs K4 beside K7: it needs digests")
+        self.eng, self.b = engine, batch
+        self.digests, self.layout, self.max_seq_len = bool(digests), layout, int(max_seq_len)
+        self.hist, self.counters = hist, counters
+        n = batch.n
+        dev = engine.device
+        self.kt = engine.new_key_text(n, int(batch.heap.numel()), paths=True)
+        # K3 list workspace (+ 2^22 entries: the keyed K2's per-workgroup suspect slices round up)
+        self.ws3 = engine.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), torch.uint8)
+        self.ws4 = None
+        if self.digests:
+            sz = ctypes.c_size_t()
+            engine.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
+            self.ws4 = engine.empty(int(sz.value), torch.uint8)
+        if k4_grid:
+            engine.set_option(N.OPT_K4_GRID, int(k4_grid))
+        self.side = torch.cuda.Stream(dev) if layout != "serial" else None
+        self.out: Dict[str, object] = {}
+
+    # ---- one step ----------------------------------------------------------
+    def _timed(self, events, name, stream, fn):
+        if events is None:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r = fn()
+        e1.record(stream)
+        events.setdefault(name, []).append((e0, e1))
+        return r
+
+    def run(self, events: Optional[dict] = None) -> Dict[str, object]:
+        """One step on the current stream; returns (and keeps in ``self.out``)
+        ``end, code, status, keep, digest, is_long, kt``.  ``events``: per-stage
+        HIP event pairs (on the stream each stage ran on) and ``step_span`` on the
+        launch stream."""
+        eng, b, kt, msl = self.eng, self.b, self.kt, self.max_seq_len
+        main = torch.cuda.current_stream(eng.device)
+        side = self.side
+        t = lambda name, s, fn: self._timed(events, name, s, fn)  # noqa: E731
+        span0 = None
+        if events is not None:
+            span0 = torch.cuda.Event(enable_timing=True)
+            span0.record(main)
+        end, code, status, _ = t("record_prep", main, lambda: eng.record_prep(
+            b, want_lcp=False, hist=self.hist, counters=self.counters, keys=kt, key_digest=self.digests,
+            max_seq_len=msl, digest_workspace=self.ws4, dedup_workspace=self.ws3))
+        dedup = lambda: eng.pk_dedup(b, grouped=True, counters=self.counters, workspace=self.ws3)  # noqa: E731
+        digest = lambda: eng.vrs_digest(b, msl, workspace=self.ws4)  # noqa: E731
+        dig = is_long = keep = None
+        if self.layout == "serial":
+            keep = t("pk_dedup", main, dedup)
+            if self.digests:
+                dig, is_long = t("vrs_digest", main, digest)
+            t("primary_keys", main, lambda: eng.primary_keys(b, code=code, digest=dig, max_seq_len=msl, out=kt))
+        elif self.layout == "fork":
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                keep = t("pk_dedup", side, dedup)
+            if self.digests:
+                dig, is_long = t("vrs_digest", main, digest)
+            t("primary_keys", main, lambda: eng.primary_keys(b, code=code, digest=dig, max_seq_len=msl, out=kt))
+            main.wait_stream(side)
+            keep.record_stream(main)
+        else:  # overlap
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                dig, is_long = t("vrs_digest", side, digest)
+                keep = t("pk_dedup", side, dedup)
+            t("primary_keys", main, lambda: eng.primary_keys(b, code=code, max_seq_len=msl, out=kt,
+                                                             defer_digest=True))
+            main.wait_stream(side)
+            for x in (dig, is_long, keep):
+                x.record_stream(main)
+            t("fill_digests", main, lambda: eng.fill_digests(b, dig, kt))
+        if events is not None:
+            span1 = torch.cuda.Event(enable_timing=True)
+            span1.record(main)
+            events.setdefault("step_span", []).append((span0, span1))
+        self.out = dict(end=end, code=code, status=status, keep=keep, digest=dig, is_long=is_long, kt=kt)
+        return self.out

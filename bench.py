@@ -175,22 +175,123 @@ def _cpu_worker(k):
     return len(pos), time.perf_counter() - t0
 
 
+def host_cpu_share():
+    """``(cores, source)``: the host CPUs this process may use for the CPU baseline.
+    A cgroup CPU quota (v2 ``cpu.max``, v1 ``cfs_quota_us``) is the share when one
+    is set; else ``OMP_NUM_THREADS`` when it is below the affinity mask (the GPU
+    box sets it to one GPU's CPU share while its affinity mask shows the whole
+    machine); else ``len(os.sched_getaffinity(0))`` (BASELINE.md / SURVEY.md 8d)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max" and int(q) > 0:
+            return max(1, min(aff, int(q) // int(per))), f"cgroup v2 cpu.max {q} {per} (affinity {aff})"
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, min(aff, q // per)), f"cgroup v1 cfs_quota_us {q} / cfs_period_us {per} (affinity {aff})"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < aff:
+        return int(omp), f"OMP_NUM_THREADS={omp}, no cgroup quota (affinity {aff})"
+    return aff, "sched_getaffinity (no cgroup quota, no OMP_NUM_THREADS below it)"
+
+
+def cpu_openmp(workload: str, threads: int, reps: int = 3):
+    """the C oracle's per-record closed forms at -O3 with OpenMP on
+    ``threads`` host threads (oracle/cpu_baseline.c) — a stronger comparator than the
+    reference-structured port, on the same synthetic workload."""
+    import ctypes
+    import oracle
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.chromosomes import length_table
+    lib = oracle.cpubase()
+    lens = np.asarray(length_table(), dtype=np.uint32)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    if workload in ("c2", "c3", "c4"):
+        n = 20_000_000  # (a bounded sample: generating and sorting the whole set takes ~45 s)
+        if workload == "c2":
+            chrom, start = synth.np_point_snvs(n, seed=2)
+            end = None
+        else:
+            chrom, start, end = synth.np_spans(n, seed=3 if workload == "c3" else 4, mix=workload)
+        start = np.ascontiguousarray(start, dtype=np.uint32)
+        end = None if end is None else np.ascontiguousarray(end, dtype=np.uint32)
+        code = np.empty(n, np.uint32)
+        st = np.empty(n, np.uint8)
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            lib.avdb_cpubase_bin_assign(P(chrom), P(start), None if end is None else P(end), n, P(lens), len(lens),
+                                        P(code), P(st), threads)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return {"value": n / best, "unit": "variants/s", "cores": threads, "kind": "port-openmp",
+                "sample": f"{n:,} records of the {workload.upper()} workload (numpy PCG64, sorted), the C oracle's closed "
+                          f"form (oracle/cpu_baseline.c, gcc -O3 -fopenmp) on {threads} threads, best of {reps}: "
+                          f"{best * 1e3:.1f} ms"}
+    if workload in ("c4k", "c5"):
+        n = 8_000_000 if workload == "c4k" else 4_000_000
+        b = synth.dbsnp_alleles(n, seed=4, device="cpu") if workload == "c4k" else \
+            synth.alleles(n, seed=5, device="cpu")
+        h = {k: np.ascontiguousarray(getattr(b, k).numpy()) for k in ("chrom", "pos", "allele_off", "ref_len",
+                                                                        "alt_len", "heap", "ext_id")}
+        seqd = "".join("%032d" % i for i in range(25)).encode()
+        end, code = np.empty(n, np.uint32), np.empty(n, np.uint32)
+        st, keep = np.empty(n, np.uint8), np.empty(n, np.uint8)
+        dig = np.empty(32 * n, np.uint8)
+        mx = int(max(h["ref_len"].max(), h["alt_len"].max())) + 8
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            tb = lib.avdb_cpubase_keyed(P(h["chrom"]), P(h["pos"]), P(h["allele_off"]), P(h["ref_len"]),
+                                        P(h["alt_len"]), P(h["heap"]), P(h["ext_id"]), n, P(lens), len(lens), 50,
+                                        seqd, P(end), P(code), P(st), P(keep), P(dig), 65536, 2 * mx, threads)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return {"value": n / best, "unit": "variants/s", "cores": threads, "kind": "port-openmp",
+                "sample": f"{n:,} {'dbSNP-mix' if workload == 'c4k' else 'ADSP-style'} records "
+                          f"({workload.upper()} generator on the CPU); the C oracle's record prep + VRS digests + "
+                          f"keys + ltree paths ({tb / n:.0f} B of text per record) + grouped dedup "
+                          f"(oracle/cpu_baseline.c, gcc -O3 -fopenmp, chunks of 65,536 records) on {threads} "
+                          f"threads, best of {reps}: {best * 1e3:.1f} ms"}
+    return None
+
+
 def cpu_baseline(workload: str, seconds_per_worker: float):
     """Reference-structured Python port (one-bin L13 cache + BinIndexRef table
     search on a miss, bin_index.py:59-75) over a bounded sample of the same
-    workload, one process per host core like load_vcf_file.py:307-313."""
+    workload, one process per host core like load_vcf_file.py:307-313; for the
+    record workloads also the OpenMP comparator (``openmp``)."""
+    try:
+        host_cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        host_cores = os.cpu_count() or 1
+    # one process per core of this process's CPU share (host_cpu_share: the cgroup
+    # quota, else OMP_NUM_THREADS below the affinity mask, else the affinity mask)
+    workers, core_source = host_cpu_share()
+    res = _cpu_port(workload, seconds_per_worker, workers, host_cores)
+    res["core_source"] = core_source
+    if workload in ("c2", "c3", "c4", "c4k", "c5"):
+        res["openmp"] = cpu_openmp(workload, workers)
+        res["openmp"]["core_source"] = core_source
+    return res
+
+
+def _cpu_port(workload: str, seconds_per_worker: float, workers: int, host_cores: int):
+    """The reference-structured Python port, ``workers`` processes."""
     global _SAMPLE, _TABLE
     import multiprocessing as mp
     from annotatedvdb_amd import synth
     from annotatedvdb_amd.chromosomes import CHROM_NAMES, GRCH38_LENGTHS
     from oracle import avdb_oracle as O
-    try:
-        host_cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        host_cores = os.cpu_count() or 1
-    # one process per core, at most 16: the GPU box gives one GPU's job a 16-CPU share
-    # (its affinity mask shows the whole machine)
-    workers = max(1, min(16, host_cores))
     if workload == "c1":
         # the reference parallelises one process per chromosome file
         # (load_vcf_file.py:307-313): C1 is one file (chr22), so one process
@@ -569,72 +670,24 @@ def run_workload(a, name, ri, dev, cpu):
         e1.record(s_)
         evs.setdefault(stage, []).append((e0, e1))
 
-    # K3 (dedup) shares no data with K4 / K7 (both read K2's outputs only), so on C1 it runs
-    # on a second stream beside K7 and the step joins it at the end: inside the HIP graph a
-    # parallel branch (0.098 -> 0.092 ms per step).  On C4k the branch gains nothing (K4's
-    # grid fills the chip and K3 only slows it: 9.27 vs 9.27 ms), so C4k stays in one stream.
-    # AVDB_BENCH_FORK=1 / 0 forces the branch on / off for either (A/B).
-    fork_env = os.environ.get("AVDB_BENCH_FORK")
-    fork = (fork_env != "0") if fork_env is not None else name == "c1"
-    side = torch.cuda.Stream(dev) if fork else None
-
-    def dedup_branch(record, box, k3_fn):
-        if side is None:
-            timed("pk_dedup", record, lambda: box.setdefault("keep", k3_fn()))
-            return
-        side.wait_stream(stream)
-        with torch.cuda.stream(side):
-            timed("pk_dedup", record, lambda: box.setdefault("keep", k3_fn()), on=side)
-
-    def join(box):
-        if side is not None:
-            stream.wait_stream(side)
-            box["keep"].record_stream(stream)
-
-    def c1_step(record: bool):
-        box = {}
-        # (K2 also writes K7's group totals into the reused KeyText's workspace)
-        timed("record_prep", record, lambda: box.setdefault(
-            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr, keys=last.get("kt"),
-                                    dedup_workspace=last.get("ws3") if k3_marks else None)))
-        dedup_branch(record, box, lambda: eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3")))
-        code_ = box["prep"][1]
-        timed("primary_keys", record, lambda: box.setdefault(
-            "kt", eng.primary_keys(batch, code=code_, out=last.get("kt"))))
-        join(box)
-        last.setdefault("kt", box["kt"])
-        last["prep"], last["keep"] = box["prep"], box["keep"]
-
-    # (AVDB_BENCH_K4_CODES=0: K4 classifies the records itself; A/B of the keyed K2's long-record codes)
-    k4_codes = os.environ.get("AVDB_BENCH_K4_CODES", "1") != "0"
-    # (AVDB_BENCH_K3_MARKS=0: K3 runs its own mark pass; A/B of the keyed K2's K3 first phase)
-    k3_marks = os.environ.get("AVDB_BENCH_K3_MARKS", "1") != "0"
-
-    def c4k_step(record: bool):
-        box = {}
-        # (K2 also writes K7's group totals into the reused KeyText's workspace:
-        # avdb_record_prep_keyed; the first step allocates the KeyText)
-        timed("record_prep", record, lambda: box.setdefault(
-            "prep", eng.record_prep(batch, want_lcp=False, hist=hist, counters=ctr, keys=last.get("kt"),
-                                    key_digest=True, digest_workspace=last.get("ws4") if k4_codes else None,
-                                    dedup_workspace=last.get("ws3") if k3_marks else None)))
-        dedup_branch(record, box, lambda: eng.pk_dedup(batch, grouped=True, counters=ctr, workspace=last.get("ws3")))
-        timed("vrs_digest", record, lambda: box.setdefault(
-            "dig", eng.vrs_digest(batch, 50, workspace=last.get("ws4"))))
-        code_, dig_ = box["prep"][1], box["dig"][0]
-        timed("primary_keys", record, lambda: box.setdefault(
-            "kt", eng.primary_keys(batch, code=code_, digest=dig_, out=last.get("kt"))))
-        join(box)
-        last.setdefault("kt", box["kt"])
-        last["prep"], last["keep"], last["dig"] = box["prep"], box["keep"], box["dig"]
+    # C1 / C4k: the keyed record-prep step (annotatedvdb_amd.pipeline.KeyedStep, the
+    # object the parity tests run).  C1 (K2, K3, K7; no long records) takes the "fork"
+    # layout: K3 on a second stream beside K7, which inside the HIP graph is a parallel
+    # branch (0.098 -> 0.092 ms per step).  C4k takes AVDB_BENCH_LAYOUT (serial | fork |
+    # overlap: K7 beside K4 with the digests filled afterwards), default below.
+    ks = None
+    if name in ("c1", "c4k"):
+        from annotatedvdb_amd.pipeline import C4K_LAYOUT, KeyedStep
+        layout = "fork" if name == "c1" else os.environ.get("AVDB_BENCH_LAYOUT", C4K_LAYOUT)
+        ks = KeyedStep(eng, batch, digests=name == "c4k", layout=layout, hist=hist, counters=ctr,
+                       k4_grid=int(os.environ.get("AVDB_BENCH_K4_GRID", "0")))
 
     def step(record: bool):
-        if name == "c1":
-            c1_step(record)
-        elif name == "c4k":
-            # (the whole step on the launch stream: with K3 on the side stream the
-            # stages overlap, so their sum is not the step's kernel time)
-            timed("step_span", record, lambda: c4k_step(record))
+        if ks is not None:
+            # (stage events on the stream each stage ran on, and the whole step on the
+            # launch stream: with a second stream the stages overlap, so their sum is
+            # not the step's kernel time)
+            ks.run(evs if record else None)
         elif name in ("c2", "c3", "c4"):
             timed("bin_assign", record, lambda: eng.bin_assign(
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
@@ -656,14 +709,6 @@ def run_workload(a, name, ri, dev, cpu):
             timed("vrs_digest", record, lambda: eng.vrs_digest(batch, 50))
 
     last = {}
-    if name in ("c1", "c4k"):  # dedup workspace, allocated once
-        # (+ 2^22 entries: the keyed K2's per-workgroup suspect slices round up)
-        last["ws3"] = torch.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), dtype=torch.uint8, device=dev)
-    if name == "c4k":  # K4 compaction workspace, allocated once
-        import ctypes
-        sz = ctypes.c_size_t()
-        eng.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
-        last["ws4"] = torch.empty(int(sz.value), dtype=torch.uint8, device=dev)
     for _ in range(a.warmup):
         step(False)
     use_graph = a.graph == "on" or (a.graph == "auto" and name == "c1")
@@ -708,8 +753,7 @@ def run_workload(a, name, ri, dev, cpu):
     if name == "c1":
         kern_ms = elapsed * 1e3 / a.steps  # the whole step (launch-bound at 1.1 M records)
     if name == "c4k":
-        kern_ms = (stage_ms["step_span"] if fork else
-                   sum(stage_ms[k] for k in ("record_prep", "pk_dedup", "vrs_digest", "primary_keys")))
+        kern_ms = stage_ms["step_span"]
     if name in ("vcf", "load"):
         n_lines, n = n, n_rec  # the unit is emitted variant records (per-ALT rows)
     total_records = n * ri.world * a.steps
@@ -718,7 +762,7 @@ def run_workload(a, name, ri, dev, cpu):
     if name == "c4k":
         # SURVEY.md §8d per-record bytes of the keyed record path (34 + rlen + alen + 24 per
         # long record) plus the key and ltree-path text K7 writes, over the four kernels' time
-        kt = last["kt"]
+        kt = ks.kt
         rl, al = batch.ref_len.long(), batch.alt_len.long()
         n_long = int(((rl + al) > 50).sum().item())
         text = int(kt.key_off[n].item()) + int(kt.path_off[n].item())
@@ -733,7 +777,7 @@ def run_workload(a, name, ri, dev, cpu):
         # SURVEY.md §8d per-record bytes of the C5-style record path (in chrom 1 + pos 4 +
         # heap_off 8 + rlen 4 + alen 4 + rs 4, the allele bytes, out bin 4 + end 4 +
         # keep 1) plus the text K7 writes (keys + ltree paths)
-        kt = last["kt"]
+        kt = ks.kt
         rl, al = batch.ref_len.long(), batch.alt_len.long()
         text = int(kt.key_off[n].item()) + int(kt.path_off[n].item())
         bytes_per_launch = 34 * n + int((rl + al).sum().item()) + text
@@ -841,13 +885,14 @@ def run_workload(a, name, ri, dev, cpu):
                                     "sha512_compressions_per_launch": pk.get("sha512_compressions_per_launch"),
                                     "note": pk.get("note")}
     if name == "c4k":
-        kt = last["kt"]
+        kt = ks.kt
         out["dtype"] = "u8"
         out["data"] = "synthetic dbSNP-mix records (synth.dbsnp_alleles, torch PCG on device), resident in HBM"
         out["config"].update(key_bytes=int(kt.key_off[n].item()), path_bytes=int(kt.path_off[n].item()),
                              long_records=n_long, heap_bytes=heap_bytes,
                              duplicates=int(node_ctr[21].item()) // max(1, a.steps))
         k7_ms = stage_ms["primary_keys"]
+        out["config"]["layout"] = ks.layout
         out["k7_roofline"] = {"kernel": "avdb_primary_keys_onepass_ex (group scan + LDS-staged write pass; "
                                         "group totals from the keyed K2)",
                               "bound": "hbm", "achieved": k7_bytes / (k7_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
@@ -855,18 +900,23 @@ def run_workload(a, name, ri, dev, cpu):
                               "algorithmic_bytes_per_launch": k7_bytes, "stage_ms": k7_ms}
         out["roofline"]["note"] = ("achieved = SURVEY 8d keyed-record bytes (34 + rlen + alen + 24 if long) + "
                                    "key/path text written, over the HIP-event time of " +
-                                   ("the whole step on the launch stream (K2, then K4 + K7 with K3 beside them "
-                                    "on a second stream, joined)" if fork else "K2 + K3 + K4 + K7 in one stream") +
+                                   {"serial": "K2 + K3 + K4 + K7 in one stream",
+                                    "fork": "the whole step on the launch stream (K2, then K4 + K7 with K3 beside "
+                                            "them on a second stream, joined)",
+                                    "overlap": "the whole step on the launch stream (K2, then K7 with the long keys' "
+                                               "digests pending beside K4 + K3 on a second stream, joined, then the "
+                                               "digest fill)"}[ks.layout] +
                                    "; K4 (SHA-512) is VALU-bound, the others HBM-bound")
     if name == "c1":
-        kt = last["kt"]
+        kt = ks.kt
         out["dtype"] = "u8"
         out["data"] = "synthetic C1 records (numpy PCG64 seed 1, synth.np_c1), resident in HBM"
         out["config"].update(key_bytes=int(kt.key_off[n].item()), path_bytes=int(kt.path_off[n].item()),
                              duplicates=int(node_ctr[21].item()) // max(1, a.steps))
         out["roofline"]["note"] = ("achieved = SURVEY 8d record bytes + key/path text written / whole step "
                                    "time; at 1.1 M records the step is launch-bound (4 kernels in one HIP graph" +
-                                   (", K3 on a parallel branch beside K7" if fork else "") + "), not HBM-bound")
+                                   (", K3 on a parallel branch beside K7" if ks.layout == "fork" else "") +
+                                   "), not HBM-bound")
         if cpu:
             out["cpu_baseline"]["reference_survey_per_core"] = "285-306 K variants/s (SURVEY.md 6, build container)"
     if name == "load":

@@ -104,6 +104,12 @@ int avdb_device_count(int* n);
  * Not thread-safe per context; calls are ordered on the caller's stream.  */
 int avdb_ctx_create(int device, const uint32_t* chrom_len_host, int n_chrom, avdb_ctx** out);
 int avdb_ctx_destroy(avdb_ctx* ctx);
+/* Launch-shape options of a context (same results, another grid):
+ *   AVDB_OPT_K4_GRID  workgroups of K4's persistent digest grid, 0 = its occupancy on
+ *                     every CU (the default); fewer leave CUs to K7 running beside K4
+ *                     on another stream (AVDB_KEYS_DIGEST_DEFERRED). */
+#define AVDB_OPT_K4_GRID 1
+int avdb_ctx_set_option(avdb_ctx* ctx, int option, int64_t value);
 int avdb_ctx_n_chrom(const avdb_ctx* ctx);
 /* GA4GH refget digests (32 chars each, no "ga4gh:SQ." prefix) of every contig,
  * host array n_chrom*32 bytes; required only by avdb_vrs_digest. */
@@ -228,7 +234,8 @@ typedef struct avdb_vcf_line {
 #define AVDB_VCF_COUNT_WORKSPACE_BYTES 32768u /* minimum workspace of avdb_vcf_count_lines */
 int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes);
 /* Workspace of avdb_vcf_count_lines that also holds the newline count of every
- * parse window (28 KB pieces of the count pass's cut): given that much, the count
+ * parse window (AVDB_VCF_PARSE_WIN_KB pieces of the count pass's cut, 24 KB by
+ * default): given that much, the count
  * pass writes them and avdb_vcf_parse_lines2 parses one window per workgroup,
  * finding the line starts itself, with no separate line-starts pass.  With only
  * AVDB_VCF_COUNT_WORKSPACE_BYTES the starts pass runs (same outputs). */
@@ -383,13 +390,19 @@ int avdb_display_attributes(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
  * path_off[n+1]) from the SoA alone; then with key_out (and path_out), 8-byte
  * aligned, of key_cap (path_cap) bytes >= the totals, which writes the text and
  * key_state[n] (a text that would end past its cap is not written, and its record's
- * state says so: AVDB_KEY_OVERFLOW / AVDB_PATH_OVERFLOW): */
+ * state says so: AVDB_KEY_OVERFLOW / AVDB_PATH_OVERFLOW).  The write call runs the
+ * one-pass write pass below (workspace: avdb_format_workspace_size(n) bytes, 16-byte
+ * aligned) and writes the same key_off / path_off again: */
 #define AVDB_KEY_OK 0
 #define AVDB_KEY_HOST 1          /* ':' in an allele (the reference raises ValueError),
                                   * non-ASCII bytes, a contig without label or an
                                   * interned (non-rs) external id: caller renders */
 #define AVDB_KEY_NEED_DIGEST 2   /* long record and digest == NULL */
 #define AVDB_KEY_OVERFLOW 3      /* the key would end past key_cap: not written */
+#define AVDB_KEY_DIGEST_PENDING 4 /* long record under AVDB_KEYS_DIGEST_DEFERRED: the key is
+                                  * written except its 32 digest characters (zero bytes)
+                                  * until avdb_primary_keys_fill_digests sets them and the
+                                  * state to AVDB_KEY_OK */
 #define AVDB_PATH_OVERFLOW 0x10u /* ORed in: the path would end past path_cap: not written */
 int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
                       const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap,
@@ -399,9 +412,10 @@ int avdb_primary_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, 
                       size_t key_cap, uint8_t* path_out, size_t path_cap, uint8_t* key_state,
                       void* stream);
 
-/* K7 in ONE pass: each record's key and path sizes, their offsets (a decoupled
- * look-back scan over 64-record tiles taken in launch order) and the text, in
- * one launch that reads the SoA once.  Same inputs and outputs as
+/* K7 without a host round trip: per group of 64 / 256 records the key and path
+ * byte totals (or the keyed K2's), one scan over the group totals, then the write
+ * pass, which recomputes each record's sizes from the SoA it reads anyway, writes
+ * the offsets and renders the text.  Same inputs and outputs as
  * avdb_primary_keys, except that key_off[n+1] / path_off[n+1] are OUTPUTS and the
  * text buffers are sized in advance: avdb_primary_keys_bound gives capacities no
  * batch of n records with heap_bytes of alleles can exceed.  workspace:
@@ -420,6 +434,12 @@ int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, const uint32_
  * digest presence and paths), so the totals pass over the SoA is skipped (only
  * the last group is summed again, inside the scan). */
 #define AVDB_KEYS_TOTALS_READY 1u
+/* AVDB_KEYS_DIGEST_DEFERRED (digest == NULL): long records' keys are laid out with
+ * their 32 digest characters still to come (state AVDB_KEY_DIGEST_PENDING), so K7
+ * need not wait for K4: run avdb_vrs_digest beside it (another stream) and then
+ * avdb_primary_keys_fill_digests.  The keyed K2 totals for this are the ones made
+ * with has_digest != 0. */
+#define AVDB_KEYS_DIGEST_DEFERRED 2u
 int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                  const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
                                  const uint8_t* heap, size_t heap_bytes, const uint64_t* ext_id,
@@ -427,6 +447,13 @@ int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint
                                  void* workspace, size_t workspace_bytes, uint64_t* key_off, uint64_t* path_off,
                                  uint8_t* key_out, size_t key_cap, uint8_t* path_out, size_t path_cap,
                                  uint8_t* key_state, uint32_t flags, void* stream);
+/* The digest characters of every AVDB_KEY_DIGEST_PENDING key: digest = the
+ * avdb_vrs_digest output for the same batch (32 chars per record, 16-byte
+ * aligned), key_off / key_out / key_state = the deferred K7 call's (key_state
+ * 16-byte aligned).  Each pending key's state becomes AVDB_KEY_OK. */
+int avdb_primary_keys_fill_digests(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, size_t n,
+                                   const char* digest, const uint64_t* key_off, uint8_t* key_out,
+                                   uint8_t* key_state, void* stream);
 /* K2 that also writes K7's group totals (key / path bytes per group of 64 or 256
  * records) into a one-pass K7 workspace, from the SoA it reads anyway plus the
  * refSNP ids: the record-prep half of the keyed pipeline (C4k, C1).  With a K4

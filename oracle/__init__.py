@@ -12,7 +12,9 @@ import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 C_LIB = os.path.join(_HERE, "_build", "libavdb_oracle.so")
+CPUBASE_LIB = os.path.join(_HERE, "_build", "libavdb_cpubase.so")
 _c = None
+_cb = None
 
 
 def build_c_oracle() -> str:
@@ -40,3 +42,21 @@ def c_oracle():
         lib.avdb_oracle_bin_paths.restype = SZ
         _c = lib
     return _c
+
+
+def cpubase():
+    """ctypes handle of the OpenMP comparator (``cpu_baseline.c``: the C oracle's
+    per-record functions at -O3 over all host cores) — bench.py's second
+    ``cpu_baseline`` leg only."""
+    global _cb
+    if _cb is None:
+        if not os.path.exists(CPUBASE_LIB):
+            build_c_oracle()
+        lib = ctypes.CDLL(CPUBASE_LIB)
+        P, SZ, I, U32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32
+        lib.avdb_cpubase_bin_assign.argtypes = [P, P, P, SZ, P, I, P, P, I]
+        lib.avdb_cpubase_keyed.argtypes = [P, P, P, P, P, P, P, SZ, P, I, U32, ctypes.c_char_p, P, P, P, P, P, SZ,
+                                           SZ, I]
+        lib.avdb_cpubase_keyed.restype = ctypes.c_uint64
+        _cb = lib
+    return _cb

@@ -284,7 +284,8 @@ def test_keyed_record_prep_feeds_k7(engine, n):
     pipelines) then K7 without its totals pass == plain K2 + K7: end / bin / status
     and every key, path, offset and state — 256-record groups from 4 Mi records on,
     64-record groups (four per K2 wave step) below; under 4 records the keyed call
-    is plain K2 and K7 sums the totals itself."""
+    is plain K2 and K7 sums the totals itself.  The keyed pair writes into a fresh
+    KeyText whose workspace, offsets, states and text are all sentinel bytes."""
     from annotatedvdb_amd import synth
     digs = ["%032d" % (5 * i) for i in range(25)]
     engine.set_sequence_digests(digs)
@@ -292,9 +293,9 @@ def test_keyed_record_prep_feeds_k7(engine, n):
     end, code, status, _ = engine.record_prep(b, want_lcp=False)
     dig, _ = engine.vrs_digest(b, 50)
     ref = engine.primary_keys(b, code=code, digest=dig)
-    kt = engine.primary_keys(b, code=code, digest=dig)  # the reused buffers
-    kt.state.fill_(77)
-    kt.key_off.fill_(0)
+    kt = engine.new_key_text(n, b.heap.numel())  # fresh buffers, every byte a sentinel
+    for t in (kt.ws, kt.key_off, kt.path_off, kt.state, kt.keys, kt.paths):
+        t.view(torch.uint8).fill_(0xA5)
     end2, code2, status2, _ = engine.record_prep(b, want_lcp=False, keys=kt, key_digest=True)
     assert ("totals" in engine._pending) == (n >= 4)
     assert torch.equal(end, end2) and torch.equal(code, code2) and torch.equal(status, status2)
@@ -470,3 +471,82 @@ def test_keyed_record_prep_marks_for_k3(engine, n, dup):
     c = synth.alleles(n, seed=99 + n % 5, long_frac=0.02, dup_frac=dup, device="cuda")
     engine.record_prep(b, want_lcp=False, keys=kt, dedup_workspace=ws)
     assert torch.equal(engine.pk_dedup(c, grouped=True, workspace=ws)[:n], engine.pk_dedup(c, grouped=True)[:n])
+
+
+def test_c1_graph_replay_vs_c_oracle(engine):
+    """The step bench.py times for C1, as it times it: ``pipeline.KeyedStep`` in
+    the "fork" layout (K3 on a second stream beside K7) captured once as a HIP
+    graph and replayed.  Every buffer is a sentinel before the capture, and the
+    text buffers and outputs are poisoned again between replays; after each
+    replay end / bin / status / keep and every key, path, offset and state are
+    bit-exact vs the C oracle."""
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.pipeline import KeyedStep
+    b = synth.c1_batch(device="cuda")
+    n = b.n
+    h = host(b)
+    re_, rc, rs, rk = oracle_prep(h)
+    kb, ko = oracle_keys(h)
+    exp_paths = paths_of(h["chrom"], rc)
+    engine.poison = 0xA5
+    try:
+        ks = KeyedStep(engine, b, digests=False, layout="fork", hist=engine.new_histogram(),
+                       counters=engine.new_counters())
+        ks.run()  # warm-up step (the bench's warmup)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ks.run()
+    finally:
+        engine.poison = None
+    for rep in range(2):
+        out = ks.out
+        for t in (out["end"], out["code"], out["status"], out["keep"], ks.kt.keys, ks.kt.paths, ks.kt.key_off,
+                  ks.kt.path_off, ks.kt.state):
+            t.view(torch.uint8).fill_(0x5A + rep)
+        g.replay()
+        torch.cuda.synchronize()
+        kt = out["kt"]
+        assert np.array_equal(u32(out["end"]), re_)
+        assert np.array_equal(u32(out["code"]), rc)
+        assert np.array_equal(out["status"].cpu().numpy(), rs)
+        assert np.array_equal(out["keep"][:n].cpu().numpy(), rk)
+        assert not kt.state[:n].cpu().numpy().any()
+        assert np.array_equal(kt.key_off[: n + 1].cpu().numpy().astype(np.uint64), ko)
+        assert np.array_equal(kt.keys[: len(kb)].cpu().numpy(), np.frombuffer(kb, dtype=np.uint8))
+        po = kt.path_off[: n + 1].cpu().numpy()
+        pb = kt.paths[: int(po[n])].cpu().numpy().tobytes().decode()
+        assert all(pb[po[i]:po[i + 1]] == exp_paths[i] for i in range(n))
+
+
+@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 4097, 300001, (4 << 20) + 4099])
+def test_k7_deferred_digests_then_fill(engine, n):
+    """K7 with AVDB_KEYS_DIGEST_DEFERRED (no digests yet: long keys laid out with
+    their digest characters pending, state KEY_DIGEST_PENDING) then
+    avdb_primary_keys_fill_digests == K7 given the digests: offsets, states,
+    key and path text; and the pending states before the fill are exactly the
+    long records with a labelled contig.  Keyed (K2 totals) and plain forms."""
+    from annotatedvdb_amd import _native as N
+    from annotatedvdb_amd import synth
+    digs = ["%032d" % (17 * i) for i in range(25)]
+    engine.set_sequence_digests(digs)
+    b = synth.alleles(n, seed=41 + n % 9, long_frac=0.2, device="cuda")
+    end, code, status, _ = engine.record_prep(b, want_lcp=False)
+    dig, is_long = engine.vrs_digest(b, 50)
+    ref = engine.primary_keys(b, code=code, digest=dig)
+    for keyed in (False, True):
+        kt = engine.new_key_text(n, b.heap.numel())
+        for t in (kt.ws, kt.key_off, kt.path_off, kt.state, kt.keys, kt.paths):
+            t.view(torch.uint8).fill_(0xA5)
+        if keyed:
+            engine.record_prep(b, want_lcp=False, keys=kt, key_digest=True)
+        out = engine.primary_keys(b, code=code, out=kt, defer_digest=True)
+        st = out.state[:n].cpu().numpy()
+        chrom = b.chrom.cpu().numpy()
+        assert np.array_equal(st == N.KEY_DIGEST_PENDING, is_long[:n].cpu().numpy().astype(bool) & (chrom < 25))
+        engine.fill_digests(b, dig, out)
+        assert torch.equal(out.key_off[: n + 1], ref.key_off[: n + 1])
+        assert torch.equal(out.path_off[: n + 1], ref.path_off[: n + 1])
+        assert torch.equal(out.state[:n], ref.state[:n])
+        kn, pn = int(ref.key_off[n]), int(ref.path_off[n])
+        assert torch.equal(out.keys[:kn], ref.keys[:kn]) and torch.equal(out.paths[:pn], ref.paths[:pn])

@@ -1,18 +1,21 @@
 """north_star's target on BASELINE config C4: "bit-exact bin paths and primary
 keys for 1B synthetic variants".  The keyed C4 job (``synth.dbsnp_alleles``,
 the bench's own generator and seeds: 8 ranks' length-balanced pieces x 1.25e8
-records = 1e9) runs shard by shard on one GPU through K2 (end, bin), K3
+records = 1e9) runs shard by shard on one GPU through the step bench.py times —
+``pipeline.KeyedStep`` in the bench's layout (``pipeline.C4K_LAYOUT``): K2 (end,
+bin, and K7's group totals, K4's long-record codes, K3's first phase), K3
 (keep-first dedup), K4 (VRS digests of the long records) and K7 (primary-key and
-ltree-path text), in the keyed form bench.py times (K2 also writing K7's group
-totals, K4's long-record codes and K3's first phase); every output of every
-record is compared with the C oracle.
-The oracle runs in chunks on a thread pool (ctypes releases the GIL).
+ltree-path text).  Nothing runs before it on the shard: every buffer the engine
+and the step allocate — text buffers, offsets, states, workspaces, every output
+— is filled with a sentinel byte first (``Engine.poison``), so what is compared
+is only what the benched kernels wrote.  Every output of every record is
+compared with the C oracle, which runs in chunks on a thread pool (ctypes
+releases the GIL).
 
 The long-record digests are checked against the oracle's restatement of the
 VRS 1.x serialisation; that restatement itself is unpinned against vrs-python
 (absent here)."""
 
-import ctypes
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -28,53 +31,46 @@ LENGTHS = np.asarray(length_table(), dtype=np.uint32)
 N_PER_RANK = 125_000_000
 CHUNK = 4_000_000
 DIGS = ["%032d" % i for i in range(25)]  # the bench's synthetic refget ids
+POISON = 0xA5
 
 
 def _p(a, k=0):
     return a.ctypes.data + k * a.itemsize
 
 
-def _check_shard(engine, n, seed, pieces):
+def _check_shard(engine, n, seed, pieces, layout=None, steps=1):
     import oracle
     from annotatedvdb_amd import synth
+    from annotatedvdb_amd.pipeline import C4K_LAYOUT, KeyedStep
     lib = oracle.c_oracle()
     b = synth.dbsnp_alleles(n, seed=seed, device="cuda", pieces=pieces)
-    sz = ctypes.c_size_t()
-    engine.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
-    ws4 = torch.empty(int(sz.value), dtype=torch.uint8, device="cuda")
-    ws3 = torch.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), dtype=torch.uint8, device="cuda")
-    end, code, status, _ = engine.record_prep(b, want_lcp=False)
-    keep = engine.pk_dedup(b, grouped=True)
-    dig, is_long = engine.vrs_digest(b, 50, workspace=ws4)
-    kt = engine.primary_keys(b, code=code, digest=dig)
-    del end, code, status, keep, dig, is_long
-    # then the bench's keyed step on the same batch, reusing the key text buffers:
-    # K2 writes K7's group totals, K4's long-record codes and K3's first phase, and
-    # K7, K4 and K3 skip their own passes over the SoA (what bench.py --workload c4k times)
-    end, code, status, _ = engine.record_prep(b, want_lcp=False, keys=kt, key_digest=True, digest_workspace=ws4,
-                                              dedup_workspace=ws3)
-    assert set(engine._pending) == {"totals", "codes", "marks"}
-    keep = engine.pk_dedup(b, grouped=True, workspace=ws3)
-    dig, is_long = engine.vrs_digest(b, 50, workspace=ws4)
-    kt = engine.primary_keys(b, code=code, digest=dig, out=kt)
+    engine.poison = POISON
+    try:
+        ks = KeyedStep(engine, b, digests=True, layout=layout or C4K_LAYOUT)
+        for k in range(steps):
+            if k:  # the text buffers the previous step wrote: poisoned again
+                for t in (ks.kt.keys, ks.kt.paths, ks.kt.key_off, ks.kt.path_off, ks.kt.state):
+                    t.view(torch.uint8).fill_(POISON)
+            out = ks.run()
+    finally:
+        engine.poison = None
     torch.cuda.synchronize()
-    del ws4, ws3
+    kt = out["kt"]
     assert not kt.state[:n].cpu().numpy().any()
     h = {k: getattr(b, k).cpu().numpy() for k in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "heap",
                                                   "ext_id")}
     chrom, pos = h["chrom"], h["pos"].view(np.uint32)
     off, rl, al = h["allele_off"].view(np.uint64), h["ref_len"].view(np.uint32), h["alt_len"].view(np.uint32)
     heap, ext = h["heap"], h["ext_id"].view(np.uint64)
-    g_end, g_code = end.cpu().numpy().view(np.uint32), code.cpu().numpy().view(np.uint32)
-    g_status, g_keep = status.cpu().numpy(), keep.cpu().numpy()
-    g_long = is_long.cpu().numpy().astype(bool)
-    g_dig = dig.cpu().numpy()
-    del end, code, status, keep, dig, is_long
+    g_end, g_code = out["end"].cpu().numpy().view(np.uint32), out["code"].cpu().numpy().view(np.uint32)
+    g_status, g_keep = out["status"].cpu().numpy(), out["keep"][:n].cpu().numpy()
+    g_long = out["is_long"].cpu().numpy().astype(bool)
+    g_dig = out["digest"].cpu().numpy()
     g_ko = kt.key_off[: n + 1].cpu().numpy().view(np.uint64)
     g_po = kt.path_off[: n + 1].cpu().numpy().view(np.uint64)
     g_keys = kt.keys[: int(g_ko[n])].cpu().numpy()
     g_paths = kt.paths[: int(g_po[n])].cpu().numpy()
-    del kt, b
+    del out, kt, ks, b
     torch.cuda.empty_cache()
     seqd = "".join(DIGS).encode()
     long_ = (rl.astype(np.int64) + al) > 50
@@ -129,9 +125,10 @@ def _check_shard(engine, n, seed, pieces):
 
 @pytest.mark.parametrize("rank", range(8))
 def test_c4k_shard_vs_c_oracle(engine, rank):
-    """Rank ``rank``'s whole shard of the keyed C4 job (1.25e8 records): end,
-    bin code, status, keep, long-record digests, primary-key text and ltree-path
-    text (with their offsets) bit-exact vs the C oracle."""
+    """Rank ``rank``'s whole shard of the keyed C4 job (1.25e8 records), the
+    bench's step on sentinel-filled buffers: end, bin code, status, keep,
+    long-record digests, primary-key text and ltree-path text (with their
+    offsets) bit-exact vs the C oracle."""
     from annotatedvdb_amd import shard
     eng = type(engine)(0, sequence_digests=DIGS)
     plan = shard.plan(8)
@@ -139,8 +136,11 @@ def test_c4k_shard_vs_c_oracle(engine, rank):
     assert n_long > 0.015 * N_PER_RANK and kbytes > 20 * N_PER_RANK and pbytes > 50 * N_PER_RANK
 
 
-def test_c4k_small_vs_c_oracle(engine):
-    """The same check at a size the oracle finishes instantly (every code path,
-    one chunk boundary)."""
+@pytest.mark.parametrize("layout", ["serial", "fork", "overlap"])
+def test_c4k_small_vs_c_oracle(engine, layout):
+    """Every stream layout of the step at a size the oracle finishes instantly
+    (every code path, one chunk boundary), twice over the same buffers (the
+    bench's steady state: the second step's K2 hands over into the workspaces the
+    first step used; its text buffers are poisoned again in between)."""
     eng = type(engine)(0, sequence_digests=DIGS)
-    _check_shard(eng, CHUNK + 12345, 77, None)
+    _check_shard(eng, CHUNK + 12345, 77, None, layout=layout, steps=2)

@@ -430,3 +430,53 @@ def test_c5_full_size_vs_c_oracle(engine):
         e = O.vrs_allele_digest(digs[h["chrom"][i]], int(h["pos"][i]), h["heap"][o:o + r].tobytes(),
                                 h["heap"][o + r:o + r + a].tobytes())
         assert got[i].tobytes().decode() == e
+
+
+# ---------------------------------------------------------------------------
+# launch-shape knobs: the same kernels on other grids give the same results
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("knob,value", [("AVDB_K1_BLOCKS_PER_CU", "1"), ("AVDB_K2_BLOCKS_PER_CU", "16"),
+                                        ("AVDB_K4_BLOCKS_PER_CU", "1"), ("AVDB_K7_RAW_BLOCKS", "0")])
+def test_grid_knobs_parity(engine, knob, value):
+    """Every environment knob the library reads (``grep getenv csrc/``) at a
+    non-default value: K1 spans + histogram, the keyed step (K2, K3, K4, K7) and
+    its outputs equal the default context's; and ``AVDB_OPT_K4_GRID`` (K4's
+    persistent grid, what the overlap layout shrinks) the same way."""
+    from annotatedvdb_amd import _native as N
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.engine import Engine
+    from annotatedvdb_amd.pipeline import KeyedStep
+    digs = ["%032d" % (13 * i) for i in range(25)]
+    os.environ[knob] = value
+    try:
+        alt = Engine(0, sequence_digests=digs)
+    finally:
+        del os.environ[knob]
+    ref = Engine(0, sequence_digests=digs)
+    chrom, start, end = synth.np_spans(1 << 20, seed=4)
+    outs = []
+    for e in (ref, alt):
+        h = e.new_histogram()
+        code, status = e.bin_assign(torch.from_numpy(chrom), torch.from_numpy(start), torch.from_numpy(end), hist=h)
+        outs.append((code, status, h))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    n = 3 * 4096 * 64 + 77  # several K7 scan blocks
+    b = synth.alleles(n, seed=6, long_frac=0.04, dup_frac=0.05, device="cuda")
+    res = []
+    for e, grid in ((ref, 0), (alt, 0), (alt, 37)):
+        if grid:
+            e.set_option(N.OPT_K4_GRID, grid)
+        o = KeyedStep(e, b, digests=True).run()
+        kt = o["kt"]
+        sel = o["is_long"].bool()
+        res.append((o["end"], o["code"], o["status"], o["keep"][:n], o["is_long"], o["digest"][sel],
+                    kt.key_off[: n + 1], kt.path_off[: n + 1], kt.state[:n], kt.keys[: int(kt.key_off[n])],
+                    kt.paths[: int(kt.path_off[n])]))
+    for r in res[1:]:
+        for x, y in zip(res[0], r):
+            assert torch.equal(x, y)
+    with pytest.raises(N.NativeError):
+        alt.set_option(N.OPT_K4_GRID, -1)
+    with pytest.raises(N.NativeError):
+        alt.set_option(99, 1)

@@ -165,12 +165,15 @@ def _starts_path(engine, text: bytes):
     return n_lines, lines[: n_lines * 80].cpu().numpy(), ro.cpu().numpy(), ho.cpu().numpy()
 
 
-@pytest.mark.parametrize("which", ["golden", "dbsnp", "short", "empty_lines", "long", "crlf_tail"])
+@pytest.mark.parametrize("which", ["golden", "dbsnp", "short", "empty_lines", "long", "crlf_tail", "big"])
 def test_k0_window_parse_equals_starts_pass(engine, which):
-    """The window parse (line starts found in 28 KB windows from the count pass's
-    per-window newline counts) gives the same line table and offsets as the
-    line-starts pass, byte for byte, including lines across window edges and lines
-    longer than a window."""
+    """The window parse (line starts found in 24 KB windows, AVDB_VCF_PARSE_WIN_KB,
+    from the count pass's per-window newline counts) gives the same line table and
+    offsets as the line-starts pass, byte for byte, including lines across window
+    edges and lines longer than a window.  "big" (~200 MB) makes each count
+    sub-chunk (text / 4,096) hold several parse windows, so a window's first line
+    index sums the windows before it in its sub-chunk, with 70 kB lines laid
+    across window edges throughout."""
     if which == "golden":
         text = _golden_text()
     elif which == "dbsnp":
@@ -183,6 +186,14 @@ def test_k0_window_parse_equals_starts_pass(engine, which):
         base = _synth(4000, 59).split(b"\n")[:-1]
         huge = b"2\t888\t.\tC\tG,T\t.\t.\tZ=" + b"Q" * 70000
         text = b"\n".join(base[:2000] + [huge] + base[2000:] + [huge]) + b"\n"
+    elif which == "big":
+        tile = _synth(60000, 67).split(b"\n")[:-1]
+        huge = b"3\t4242\trs7\tG\tA,C\t.\t.\tZ=" + b"Q" * 70000
+        parts = []
+        for k in range(30):
+            parts += tile[: 7000 + 997 * k] + [huge] + tile[7000 + 997 * k:]
+        text = b"\n".join(parts) + b"\n"
+        assert len(text) > 4096 * 25 * 1024  # sub-chunk (text / 4,096) > one 24 KB window
     else:
         text = _synth(20000, 61).replace(b"\n", b"\r\n")[:-3]
     n0, lines0, ro0, ho0 = _starts_path(engine, text)

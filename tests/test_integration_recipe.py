@@ -175,6 +175,17 @@ def test_loader_cursor_surface(host_engine):
                              "('1:100:A:G','chr1'),('2:5:C:T:rs9','chr2')) AS d(record_primary_key, chromosome) "
                              "WHERE v.chromosome = d.chromosome", None)]
     assert ld.update_buffer(sizeOnly=True) == 0
+    # psycopg2's _split_sql rule: '%%' is a literal '%', every part keeps
+    # the query's type (bytes here), and a second placeholder is refused
+    ld.set_update_sql(b"UPDATE v SET note = 'x%%' FROM (VALUES %s) AS d(k, c)")
+    ld.update_buffer().extend([("1:100:A:G", "chr1")])
+    ld.update_variants()
+    assert cur.executed[-1] == (b"UPDATE v SET note = 'x%' FROM (VALUES ('1:100:A:G','chr1')) AS d(k, c)", None)
+    ld.set_update_sql("UPDATE v SET a = %s FROM (VALUES %s) AS d")
+    ld.update_buffer().extend([("1:100:A:G", "chr1")])
+    with pytest.raises(ValueError, match="more than one"):
+        ld.update_variants()
+    ld.update_buffer().clear()
     ld.set_batch_update()
     ld.update_buffer().write("UPDATE x;")
     ld.update_variants()
