@@ -111,7 +111,7 @@ EXPORTED_SYMBOLS = [
 SMALL_PATH, SMALL_KEY, SMALL_DISPLAY = 1, 2, 4
 KEYS_TOTALS_READY = 1  # AVDB_KEYS_TOTALS_READY
 KEYS_DIGEST_DEFERRED = 2  # AVDB_KEYS_DIGEST_DEFERRED
-OPT_K4_GRID = 1  # avdb_ctx_set_option
+OPT_K4_GRID, OPT_K7_GRID = 1, 2  # avdb_ctx_set_option
 KEYED_TOTALS, KEYED_LONG_CODES, KEYED_DEDUP_MARKS = 1, 2, 4  # avdb_record_prep_keyed's *totals_written bits
 DEDUP_MARKED = 1  # AVDB_DEDUP_MARKED
 DIGEST_CODES_READY = 1  # AVDB_DIGEST_CODES_READY

@@ -98,6 +98,7 @@ extern "C" int avdb_ctx_create(int device, const uint32_t* chrom_len, int n_chro
     if (v >= 1 && v <= 3) c->k4_blocks_per_cu = v;
   }
   c->k4_grid = 0;  // avdb_ctx_set_option(AVDB_OPT_K4_GRID): workgroups, 0 = n_cu * k4_blocks_per_cu
+  c->k7_grid = 0;  // avdb_ctx_set_option(AVDB_OPT_K7_GRID): workgroups, 0 = the compiled grid
   c->k7_raw_blocks = 256;
   if (const char* s = getenv("AVDB_K7_RAW_BLOCKS")) c->k7_raw_blocks = size_t(strtoull(s, nullptr, 10));
   *out = c;
@@ -113,6 +114,13 @@ extern "C" int avdb_ctx_set_option(avdb_ctx* ctx, int option, int64_t value) {
         return AVDB_EINVAL;
       }
       ctx->k4_grid = int(value);
+      return AVDB_OK;
+    case AVDB_OPT_K7_GRID:
+      if (value < 0 || value > (int64_t(1) << 24)) {
+        avdb_set_error("avdb_ctx_set_option: K7 grid of %lld workgroups out of range", (long long)value);
+        return AVDB_EINVAL;
+      }
+      ctx->k7_grid = int(value);
       return AVDB_OK;
     default:
       avdb_set_error("avdb_ctx_set_option: unknown option %d", option);

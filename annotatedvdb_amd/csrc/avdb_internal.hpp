@@ -269,6 +269,7 @@ struct avdb_ctx {
   int k2_blocks_per_cu;  // K2 grid = n_cu * this (env AVDB_K2_BLOCKS_PER_CU)
   int k4_blocks_per_cu;  // K4 digest grid = n_cu * this (env AVDB_K4_BLOCKS_PER_CU; default: its occupancy, 3)
   int k4_grid;           // K4 digest grid in workgroups when > 0 (avdb_ctx_set_option AVDB_OPT_K4_GRID)
+  int k7_grid;           // K7 write-pass workgroups when > 0 (avdb_ctx_set_option AVDB_OPT_K7_GRID)
   size_t k7_raw_blocks;  // K7 one-pass: write pass sums up to this many block totals itself (env AVDB_K7_RAW_BLOCKS)
   avdb::ChromTable tab;
   char* d_seq_digest;  // device copy of the refget digests (n * 32 chars), or null

@@ -145,8 +145,7 @@ AVDB_HD O freq_json(O o, CP s, uint32_t v0, uint32_t v1, uint32_t k) {
   return o;
 }
 
-// oc / om: the COPY and .mapping sinks (a counting sink for a stream a pass does
-// not write: the split write pass renders each stream in a launch of its own)
+// oc / om: the COPY and .mapping sinks
 template <bool WRITE, class OC, class OM, class CP>
 AVDB_HD uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, CP s, size_t li,
                                OC& oc, OM& om, uint32_t* n_rows, uint32_t* n_skip,
@@ -386,12 +385,7 @@ __device__ __forceinline__ uint32_t tile_order(const FormatArgs& A, size_t base,
 #ifndef AVDB_K5_WRITE_GRID
 #define AVDB_K5_WRITE_GRID 8192
 #endif
-#ifndef AVDB_K5_SPLIT
-#define AVDB_K5_SPLIT 0  // A/B knob: 1 = the write pass as two launches, COPY rows then .mapping lines
-#endif
-// STREAMS (WRITE): 3 renders both texts in one pass; 1 / 2 only the COPY rows /
-// only the .mapping lines (the split form, AVDB_K5_SPLIT: two launches)
-template <bool WRITE, int STREAMS = 3>
+template <bool WRITE>
 __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs A) {
   __shared__ u32x4 s_text[kStage / 16];
   __shared__ uint32_t s_key[kBlock + 8];
@@ -410,8 +404,7 @@ __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs 
         if constexpr (WRITE) {
           const uint8_t st = A.line_state[li];
           if (st == kLineGpu) {
-            Out<(STREAMS & 1) != 0> oc(A.copy_out, (STREAMS & 1) ? A.copy_off[li] : 0);
-            Out<(STREAMS & 2) != 0> om(A.map_out, (STREAMS & 2) ? A.map_off[li] : 0);
+            Out<true> oc(A.copy_out, A.copy_off[li]), om(A.map_out, A.map_off[li]);
             format_line<true>(A, L, s, li, oc, om, &rows, &skip, &dups, &upds);
             oc.finish();
             om.finish();
@@ -433,7 +426,7 @@ __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs 
     }
     __syncthreads();  // the window is reused by the next trip
   }
-  if (WRITE && (STREAMS & 1) && A.counters) {  // (the COPY pass counts for both)
+  if (WRITE && A.counters) {
     for (int d = 32; d > 0; d >>= 1) {
       rows += __shfl_down(rows, d, kWave);
       skip += __shfl_down(skip, d, kWave);

@@ -863,7 +863,10 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   A.grp_pre = gpre;
   A.blk_pre = bpre;
   A.group_log2 = key_group_log2(n);
-  const size_t wmax = size_t(AVDB_K7_GRID) * kWavesPerBlock / kV2Waves, wneed = (ng + kV2Waves - 1) / kV2Waves;
+  // (avdb_ctx_set_option AVDB_OPT_K7_GRID caps the write pass's workgroups: fewer
+  // leave registers to K4 running beside it, AVDB_KEYS_DIGEST_DEFERRED)
+  const size_t wmax = ctx->k7_grid > 0 ? size_t(ctx->k7_grid) : size_t(AVDB_K7_GRID) * kWavesPerBlock / kV2Waves;
+  const size_t wneed = (ng + kV2Waves - 1) / kV2Waves;
   A.blk_raw = nb <= ctx->k7_raw_blocks ? 1u : 0u;
   // the keyed K2 wrote every group's totals but the last one's, which may hold the
   // < 4 records its vector form leaves to a scalar tail: the scan sums that one again

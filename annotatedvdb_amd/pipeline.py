@@ -49,7 +49,7 @@ C4K_LAYOUT = "serial"
 class KeyedStep:
     def __init__(self, engine, batch, *, digests: bool, layout: str = "serial", max_seq_len: int = 50,
                  hist: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None,
-                 k4_grid: int = 0):
+                 k4_grid: int = 0, k7_grid: int = 0):
         if layout not in LAYOUTS:
             raise ValueError("layout must be one of %s" % (LAYOUTS,))
         if layout == "overlap" and not digests:
@@ -69,6 +69,8 @@ class KeyedStep:
             self.ws4 = engine.empty(int(sz.value), torch.uint8)
         if k4_grid:
             engine.set_option(N.OPT_K4_GRID, int(k4_grid))
+        if k7_grid:
+            engine.set_option(N.OPT_K7_GRID, int(k7_grid))
         self.side = torch.cuda.Stream(dev) if layout != "serial" else None
         self.out: Dict[str, object] = {}
 

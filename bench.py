@@ -680,7 +680,8 @@ def run_workload(a, name, ri, dev, cpu):
         from annotatedvdb_amd.pipeline import C4K_LAYOUT, KeyedStep
         layout = "fork" if name == "c1" else os.environ.get("AVDB_BENCH_LAYOUT", C4K_LAYOUT)
         ks = KeyedStep(eng, batch, digests=name == "c4k", layout=layout, hist=hist, counters=ctr,
-                       k4_grid=int(os.environ.get("AVDB_BENCH_K4_GRID", "0")))
+                       k4_grid=int(os.environ.get("AVDB_BENCH_K4_GRID", "0")),
+                       k7_grid=int(os.environ.get("AVDB_BENCH_K7_GRID", "0")))
 
     def step(record: bool):
         if ks is not None:

@@ -107,8 +107,12 @@ int avdb_ctx_destroy(avdb_ctx* ctx);
 /* Launch-shape options of a context (same results, another grid):
  *   AVDB_OPT_K4_GRID  workgroups of K4's persistent digest grid, 0 = its occupancy on
  *                     every CU (the default); fewer leave CUs to K7 running beside K4
- *                     on another stream (AVDB_KEYS_DIGEST_DEFERRED). */
+ *                     on another stream (AVDB_KEYS_DIGEST_DEFERRED).
+ */
 #define AVDB_OPT_K4_GRID 1
+/*   AVDB_OPT_K7_GRID  workgroups (one wave each) of K7's write pass, 0 = the default; a
+ *                     persistent grid below the chip's occupancy leaves registers to K4 */
+#define AVDB_OPT_K7_GRID 2
 int avdb_ctx_set_option(avdb_ctx* ctx, int option, int64_t value);
 int avdb_ctx_n_chrom(const avdb_ctx* ctx);
 /* GA4GH refget digests (32 chars each, no "ga4gh:SQ." prefix) of every contig,

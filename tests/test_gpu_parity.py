@@ -440,8 +440,9 @@ def test_c5_full_size_vs_c_oracle(engine):
 def test_grid_knobs_parity(engine, knob, value):
     """Every environment knob the library reads (``grep getenv csrc/``) at a
     non-default value: K1 spans + histogram, the keyed step (K2, K3, K4, K7) and
-    its outputs equal the default context's; and ``AVDB_OPT_K4_GRID`` (K4's
-    persistent grid, what the overlap layout shrinks) the same way."""
+    its outputs equal the default context's; and ``AVDB_OPT_K4_GRID`` /
+    ``AVDB_OPT_K7_GRID`` (K4's persistent grid and K7's write-pass grid, what the
+    overlap layout shrinks) the same way, in the serial and the overlap layout."""
     from annotatedvdb_amd import _native as N
     from annotatedvdb_amd import synth
     from annotatedvdb_amd.engine import Engine
@@ -464,10 +465,8 @@ def test_grid_knobs_parity(engine, knob, value):
     n = 3 * 4096 * 64 + 77  # several K7 scan blocks
     b = synth.alleles(n, seed=6, long_frac=0.04, dup_frac=0.05, device="cuda")
     res = []
-    for e, grid in ((ref, 0), (alt, 0), (alt, 37)):
-        if grid:
-            e.set_option(N.OPT_K4_GRID, grid)
-        o = KeyedStep(e, b, digests=True).run()
+    for e, grid, layout in ((ref, 0, "serial"), (alt, 0, "serial"), (alt, 37, "serial"), (alt, 37, "overlap")):
+        o = KeyedStep(e, b, digests=True, layout=layout, k4_grid=grid, k7_grid=grid).run()
         kt = o["kt"]
         sel = o["is_long"].bool()
         res.append((o["end"], o["code"], o["status"], o["keep"][:n], o["is_long"], o["digest"][sel],
@@ -478,5 +477,7 @@ def test_grid_knobs_parity(engine, knob, value):
             assert torch.equal(x, y)
     with pytest.raises(N.NativeError):
         alt.set_option(N.OPT_K4_GRID, -1)
+    with pytest.raises(N.NativeError):
+        alt.set_option(N.OPT_K7_GRID, -1)
     with pytest.raises(N.NativeError):
         alt.set_option(99, 1)
