@@ -113,6 +113,29 @@ constexpr uint32_t kParseWin = AVDB_VCF_PARSE_WIN_KB * 1024;   // (a multiple of
 constexpr uint32_t kParseOver = AVDB_VCF_PARSE_OVER;           // staged past a window (its last line)
 static_assert(kParseWin % (kNlUnroll * kNlStep) == 0, "window / count step");
 
+// What k_vcf_emit needs of a line, when no caller asked for the public 80-byte
+// avdb_vcf_line table (avdb_vcf_parse_lines2 with lines == NULL): 32 bytes in the
+// parse workspace instead of 80 written and read back (the tokenize-only path;
+// the load path keeps the public table, which K5 reads).
+struct VcfEmitRec {
+  uint64_t start_chrom;  // line start | contig code << 56
+  uint64_t ext_id;
+  uint32_t pos, ref0, alt0, aend;  // REF field [ref0, alt0 - 1), ALT field [alt0, aend), relative to start
+};
+static_assert(sizeof(VcfEmitRec) == 32, "emit record");
+
+__device__ __forceinline__ VcfEmitRec emit_rec(const avdb_vcf_line& L) {
+  const uint32_t nfields = L.n_fields < 8 ? L.n_fields : 8;
+  return VcfEmitRec{L.start | (uint64_t(L.chrom) << 56), L.ext_id, L.pos, L.field[3], L.field[4],
+                    5 < nfields ? L.field[5] - 1 : L.len};
+}
+
+// the line's public record or its emit record, one of them (the other NULL)
+__device__ __forceinline__ void put_line(avdb_vcf_line* lines, VcfEmitRec* erec, size_t li, const avdb_vcf_line& L) {
+  if (lines) lines[li] = L;
+  else erec[li] = emit_rec(L);
+}
+
 __global__ __launch_bounds__(kBlock) void k_vcf_count(const uint8_t* __restrict__ text,
                                                       size_t text_bytes,
                                                       uint32_t* __restrict__ wave_cnt,
@@ -227,6 +250,7 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
                                                       size_t text_bytes, size_t n_lines,
                                                       const uint64_t* __restrict__ starts,
                                                       avdb_vcf_line* __restrict__ lines,
+                                                      VcfEmitRec* __restrict__ erec,
                                                       unsigned long long* __restrict__ rec_cnt,
                                                       unsigned long long* __restrict__ heap_cnt,
                                                       ChromMapView cm, uint32_t min_fields) {
@@ -254,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
         parse_line((glb_cp)(text + L.start), [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); },
                    mis, raw, L, recs, hbytes, cm, min_fields);
       }
-      lines[li] = L;
+      put_line(lines, erec, li, L);
       rec_cnt[li] = recs;
       heap_cnt[li] = hbytes;
     }
@@ -311,6 +335,7 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
                                                               const uint32_t* __restrict__ wave_cnt,
                                                               const uint32_t* __restrict__ win_cnt, uint32_t wps,
                                                               avdb_vcf_line* __restrict__ lines,
+                                                              VcfEmitRec* __restrict__ erec,
                                                               unsigned long long* __restrict__ rec_cnt,
                                                               unsigned long long* __restrict__ heap_cnt,
                                                               ChromMapView cm, uint32_t min_fields) {
@@ -446,7 +471,7 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
         parse_line((glb_cp)(text + L.start), [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); }, mis,
                    raw, L, recs, hbytes, cm, min_fields);
       }
-      lines[li] = L;
+      put_line(lines, erec, li, L);
       rec_cnt[li] = recs;
       heap_cnt[li] = hbytes;
     }
@@ -458,19 +483,19 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
 // coalesced flush, as K7 does for its text, measured slower: 0.66 vs 0.60 ms for
 // 8.4 M lines — the pass is bound by re-staging the text, not by these stores.)
 template <class CP>
-__device__ __forceinline__ void emit_line(CP s, const avdb_vcf_line& L, size_t li,
+__device__ __forceinline__ void emit_line(CP s, const VcfEmitRec& E, size_t li,
                                           uint64_t r, uint64_t h, uint8_t* __restrict__ chrom,
                                           uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
                                           uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
                                           uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap,
                                           uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
-    const uint32_t nfields = L.n_fields < 8 ? L.n_fields : 8;
-    const uint32_t rend = L.field[4] - 1;
-    const uint32_t aend = 5 < nfields ? L.field[5] - 1 : L.len;
-    const CP ref = s + L.field[3];
-    const uint32_t rlen = rend - L.field[3];
-    const CP alt = s + L.field[4];
-    const uint32_t an = aend - L.field[4];
+    const uint32_t rend = E.alt0 - 1;
+    const uint32_t aend = E.aend;
+    const CP ref = s + E.ref0;
+    const uint32_t rlen = rend - E.ref0;
+    const CP alt = s + E.alt0;
+    const uint32_t an = aend - E.alt0;
+    const uint8_t cc = uint8_t(E.start_chrom >> 56);
     // ALTs found with SWAR comma scans; the heap bytes leave through the 8-byte
     // register sink (this lane's records are contiguous in the heap)
     Out<true> hs(heap, h);
@@ -479,12 +504,12 @@ __device__ __forceinline__ void emit_line(CP s, const avdb_vcf_line& L, size_t l
       const uint32_t a1 = a0 + swar_find(alt + a0, an - a0, [](uint64_t x) { return bytes_eq_mask(x, ','); });
       const uint32_t al = a1 - a0;
       if (!(al == 1 && alt[a0] == '.')) {
-        chrom[r] = L.chrom;
-        pos[r] = L.pos;
+        chrom[r] = cc;
+        pos[r] = E.pos;
         allele_off[r] = h;
         ref_len[r] = rlen;
         alt_len[r] = al;
-        ext_id[r] = L.ext_id;
+        ext_id[r] = E.ext_id;
         rec_line[r] = uint32_t(li);
         rec_alt[r] = ai;
         hs.bytes(ref, rlen);
@@ -513,33 +538,45 @@ constexpr uint32_t kEmitLines = AVDB_VCF_EMIT_LINES;
 constexpr uint32_t kEmitStage = AVDB_VCF_EMIT_STAGE_KB * 1024;
 static_assert(kEmitStage <= kStage && kEmitLines <= 1024, "emit tile");
 
+// COMPACT: the lines come as emit records (lines == NULL at parse), else as the
+// public table
+template <bool COMPACT>
 __global__ __launch_bounds__(kEmitLines) void k_vcf_emit(
     const uint8_t* __restrict__ text, size_t text_bytes, size_t n_lines,
-    const avdb_vcf_line* __restrict__ lines, const uint64_t* __restrict__ rec_off,
+    const avdb_vcf_line* __restrict__ lines, const VcfEmitRec* __restrict__ erec, const uint64_t* __restrict__ rec_off,
     const uint64_t* __restrict__ heap_off, uint8_t* __restrict__ chrom, uint32_t* __restrict__ pos,
     uint64_t* __restrict__ allele_off, uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
     uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap, uint32_t* __restrict__ rec_line,
     uint32_t* __restrict__ rec_alt) {
   __shared__ u32x4 s_text[kEmitStage / 16];
   const Heap h = make_heap(text, text_bytes);
+  constexpr uint64_t kStartMask = (uint64_t(1) << 56) - 1;
   for (size_t base = size_t(blockIdx.x) * kEmitLines; base < n_lines; base += size_t(gridDim.x) * kEmitLines) {
     const size_t last = base + kEmitLines < n_lines ? base + kEmitLines : n_lines;
     // the window only has to reach the end of the last line's ALT field
-    const size_t s0 = lines[base].start;
-    const avdb_vcf_line& Z = lines[last - 1];
-    const size_t s1 = Z.start + Z.len;
+    size_t s0, s1;
+    if constexpr (COMPACT) {
+      s0 = erec[base].start_chrom & kStartMask;
+      const VcfEmitRec& Z = erec[last - 1];
+      s1 = (Z.start_chrom & kStartMask) + Z.aend;
+    } else {
+      s0 = lines[base].start;
+      const avdb_vcf_line& Z = lines[last - 1];
+      s1 = Z.start + Z.len;
+    }
     const Window w = stage_window(h, s0, s1, s_text, kEmitStage);
     const size_t li = base + threadIdx.x;
     if (li < n_lines) {
-      const avdb_vcf_line L = lines[li];
-      if (L.n_rec) {
+      const uint64_t r0 = rec_off[li], r1 = rec_off[li + 1];
+      if (r1 > r0) {
+        const VcfEmitRec E = COMPACT ? erec[li] : emit_rec(lines[li]);
+        const size_t st = E.start_chrom & kStartMask;
         if (w.staged)
-          emit_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - w.a0)), L, li,
-                    rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id, heap,
-                    rec_line, rec_alt);
+          emit_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + st - w.a0)), E, li, r0,
+                    heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id, heap, rec_line, rec_alt);
         else
-          emit_line((glb_cp)(text + L.start), L, li, rec_off[li], heap_off[li], chrom, pos, allele_off, ref_len,
-                    alt_len, ext_id, heap, rec_line, rec_alt);
+          emit_line((glb_cp)(text + st), E, li, r0, heap_off[li], chrom, pos, allele_off, ref_len, alt_len, ext_id,
+                    heap, rec_line, rec_alt);
       }
     }
     __syncthreads();
@@ -590,10 +627,16 @@ static int count_pass(const uint8_t* text, size_t text_bytes, void* ws, unsigned
 
 static size_t scan_temp_bytes(size_t n) { return (scan::workspace_bytes(n, 2) + 255) & ~size_t(255); }
 
+static VcfEmitRec* emit_recs_of(void* workspace, size_t text_bytes, size_t n_lines) {
+  return reinterpret_cast<VcfEmitRec*>(static_cast<char*>(workspace) + count_ws_full(text_bytes) +
+                                       ((8 * n_lines + 255) & ~size_t(255)) + scan_temp_bytes(n_lines + 1));
+}
+
 extern "C" int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
-  // count workspace (for a recount) | line starts | scan temp
-  *bytes = count_ws_full(text_bytes) + ((8 * n_lines + 255) & ~size_t(255)) + scan_temp_bytes(n_lines + 1) + 256;
+  // count workspace (for a recount) | line starts | scan temp | emit records
+  *bytes = count_ws_full(text_bytes) + ((8 * n_lines + 255) & ~size_t(255)) + scan_temp_bytes(n_lines + 1) +
+           sizeof(VcfEmitRec) * n_lines + 256;
   return AVDB_OK;
 }
 
@@ -616,7 +659,7 @@ static int parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, si
                        const void* line_counts, size_t line_counts_bytes, void* workspace, size_t workspace_bytes,
                        avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off, const avdb_vcf_opts* opts,
                        void* stream) {
-  if (!ctx || !lines || !rec_off || !heap_off) {
+  if (!ctx || !rec_off || !heap_off) {
     avdb_set_error("avdb_vcf_parse_lines: null argument");
     return AVDB_EINVAL;
   }
@@ -648,6 +691,8 @@ static int parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, si
   auto* starts = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + cw_full);
   void* tmp = reinterpret_cast<char*>(starts) + ((8 * n_lines + 255) & ~size_t(255));
   size_t tmp_bytes = scan_temp_bytes(n_lines + 1);
+  // lines == NULL: no public table; the emit records go to the workspace instead
+  VcfEmitRec* erec = lines ? nullptr : emit_recs_of(workspace, text_bytes, n_lines);
   const char* cw = static_cast<const char*>(line_counts);
   bool windows = cw && line_counts_bytes >= cw_full;
   if (!cw) {  // recount into the front of this workspace (same cut, window counts included)
@@ -667,15 +712,15 @@ static int parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, si
     const uint32_t wps = windows_per_chunk(text_bytes);
     hipLaunchKernelGGL(k_vcf_parse_windows, dim3(unsigned(size_t(kVcfGrid) * kVcfWaves * wps)), dim3(kBlock), 0, s,
                        text, text_bytes, n_lines, blk, wave,
-                       reinterpret_cast<const uint32_t*>(cw + AVDB_VCF_COUNT_WORKSPACE_BYTES), wps, lines, rc, hc,
-                       cm, min_fields);
+                       reinterpret_cast<const uint32_t*>(cw + AVDB_VCF_COUNT_WORKSPACE_BYTES), wps, lines, erec, rc,
+                       hc, cm, min_fields);
     AVDB_LAUNCH_CHECK("k_vcf_parse_windows");
   } else {  // the line-starts pass, then 256 lines per workgroup
     hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk, wave, n_lines, starts);
     AVDB_LAUNCH_CHECK("k_vcf_starts");
     const unsigned grid = stream_grid(n_lines, kBlock, 4096);
     hipLaunchKernelGGL(k_vcf_parse, dim3(grid), dim3(kBlock), 0, s, text, text_bytes, n_lines, starts,
-                       lines, rc, hc, cm, min_fields);
+                       lines, erec, rc, hc, cm, min_fields);
     AVDB_LAUNCH_CHECK("k_vcf_parse");
   }
   if (int e = scan::exclusive_u64_pair(rec_off, rec_off, heap_off, heap_off, n_lines + 1, tmp, tmp_bytes, s)) return e;
@@ -699,13 +744,11 @@ extern "C" int avdb_vcf_parse_lines2(avdb_ctx* ctx, const uint8_t* text, size_t 
                      lines, rec_off, heap_off, opts, stream);
 }
 
-extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
-                             const avdb_vcf_line* lines, const uint64_t* rec_off,
-                             const uint64_t* heap_off, uint8_t* chrom, uint32_t* pos,
-                             uint64_t* allele_off, uint32_t* ref_len, uint32_t* alt_len,
-                             uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line, uint32_t* rec_alt,
-                             void* stream) {
-  if (!ctx || !lines || !rec_off || !heap_off || !chrom || !pos || !allele_off || !ref_len ||
+static int emit_impl(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines, const avdb_vcf_line* lines,
+                     const VcfEmitRec* erec, const uint64_t* rec_off, const uint64_t* heap_off, uint8_t* chrom,
+                     uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id,
+                     uint8_t* heap, uint32_t* rec_line, uint32_t* rec_alt, void* stream) {
+  if (!ctx || !(lines || erec) || !rec_off || !heap_off || !chrom || !pos || !allele_off || !ref_len ||
       !alt_len || !ext_id || !heap || !rec_line || !rec_alt) {
     avdb_set_error("avdb_vcf_emit: null argument");
     return AVDB_EINVAL;
@@ -713,11 +756,46 @@ extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_byt
   if (n_lines == 0) return AVDB_OK;
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   const unsigned grid = stream_grid(n_lines, kEmitLines, AVDB_VCF_EMIT_GRID);
-  hipLaunchKernelGGL(k_vcf_emit, dim3(grid), dim3(kEmitLines), 0, static_cast<hipStream_t>(stream),
-                     text, text_bytes, n_lines, lines, rec_off, heap_off, chrom, pos, allele_off, ref_len,
-                     alt_len, ext_id, heap, rec_line, rec_alt);
+  if (lines)
+    hipLaunchKernelGGL(k_vcf_emit<false>, dim3(grid), dim3(kEmitLines), 0, static_cast<hipStream_t>(stream), text,
+                       text_bytes, n_lines, lines, nullptr, rec_off, heap_off, chrom, pos, allele_off, ref_len, alt_len,
+                       ext_id, heap, rec_line, rec_alt);
+  else
+    hipLaunchKernelGGL(k_vcf_emit<true>, dim3(grid), dim3(kEmitLines), 0, static_cast<hipStream_t>(stream), text,
+                       text_bytes, n_lines, nullptr, erec, rec_off, heap_off, chrom, pos, allele_off, ref_len, alt_len,
+                       ext_id, heap, rec_line, rec_alt);
   AVDB_LAUNCH_CHECK("k_vcf_emit");
   return AVDB_OK;
+}
+
+extern "C" int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                             const avdb_vcf_line* lines, const uint64_t* rec_off,
+                             const uint64_t* heap_off, uint8_t* chrom, uint32_t* pos,
+                             uint64_t* allele_off, uint32_t* ref_len, uint32_t* alt_len,
+                             uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line, uint32_t* rec_alt,
+                             void* stream) {
+  if (!lines) {
+    avdb_set_error("avdb_vcf_emit: null line table (use avdb_vcf_emit_ws after a parse without one)");
+    return AVDB_EINVAL;
+  }
+  return emit_impl(ctx, text, text_bytes, n_lines, lines, nullptr, rec_off, heap_off, chrom, pos, allele_off,
+                   ref_len, alt_len, ext_id, heap, rec_line, rec_alt, stream);
+}
+
+extern "C" int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                                const void* parse_workspace, size_t parse_workspace_bytes, const uint64_t* rec_off,
+                                const uint64_t* heap_off, uint8_t* chrom, uint32_t* pos, uint64_t* allele_off,
+                                uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap,
+                                uint32_t* rec_line, uint32_t* rec_alt, void* stream) {
+  size_t need = 0;
+  avdb_vcf_workspace_size(text_bytes, n_lines, &need);
+  if (!parse_workspace || parse_workspace_bytes < need) {
+    avdb_set_error("avdb_vcf_emit_ws: the parse workspace (%zu bytes) required", need);
+    return AVDB_ERANGE;
+  }
+  return emit_impl(ctx, text, text_bytes, n_lines, nullptr,
+                   emit_recs_of(const_cast<void*>(parse_workspace), text_bytes, n_lines), rec_off, heap_off, chrom,
+                   pos, allele_off, ref_len, alt_len, ext_id, heap, rec_line, rec_alt, stream);
 }
 
 // ---- chromosome map (ChromosomeMap.get, chromosome_map_parser.py:84-91) ----------

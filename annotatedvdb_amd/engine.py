@@ -176,7 +176,7 @@ class VcfBatch:
     """Output of ``Engine.vcf_tokenize``: device text, per-line table, records."""
     text: torch.Tensor
     n_lines: int
-    lines: torch.Tensor          # uint8[n_lines * 80] (VCF_LINE_DTYPE)
+    lines: Optional[torch.Tensor]  # uint8[n_lines * 80] (VCF_LINE_DTYPE); None: vcf_tokenize(want_lines=False)
     rec_off: torch.Tensor        # int64[n_lines + 1]
     heap_off: torch.Tensor
     records: RecordBatch
@@ -184,6 +184,8 @@ class VcfBatch:
     rec_alt: torch.Tensor
 
     def lines_host(self) -> np.ndarray:
+        if self.lines is None:
+            raise ValueError("this batch was tokenized without its line table (want_lines=False)")
         if self.n_lines == 0:
             return np.zeros(0, dtype=VCF_LINE_DTYPE)
         return self.lines.cpu().numpy()[: self.n_lines * 80].view(VCF_LINE_DTYPE)
@@ -825,10 +827,13 @@ class Engine:
         return [raw[i * 32:(i + 1) * 32].decode("ascii") for i in range(n)]
 
     # -- K0: VCF text -> records ---------------------------------------------
-    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None) -> "VcfBatch":
+    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None, want_lines: bool = True) -> "VcfBatch":
         """Parse VCF data lines (bytes or a uint8 tensor) on the GPU into the
         record SoA (one row per ALT != '.') plus the per-line table.
-        ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map."""
+        ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map.
+        ``want_lines=False``: no public line table (``VcfBatch.lines`` is None; the
+        emit reads 32-byte records from the parse workspace instead of the 80-byte
+        table) — for callers that need only the records."""
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
             t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
@@ -858,7 +863,7 @@ class Engine:
         sz = ctypes.c_size_t()
         self.lib.avdb_vcf_workspace_size(nb, n_lines, ctypes.byref(sz))
         ws = self.empty(int(sz.value), torch.uint8)
-        lines = self.empty(max(1, n_lines) * VCF_LINE_DTYPE.itemsize, torch.uint8)
+        lines = self.empty(max(1, n_lines) * VCF_LINE_DTYPE.itemsize, torch.uint8) if want_lines else None
         rec_off = self.empty(n_lines + 1, torch.int64)
         heap_off = self.empty(n_lines + 1, torch.int64)
         N.check("avdb_vcf_parse_lines2", self.lib.avdb_vcf_parse_lines2(
@@ -876,11 +881,14 @@ class Engine:
                         ext_id=self.empty(n_rec, torch.int64))
         rec_line = self.empty(n_rec, torch.int32)
         rec_alt = self.empty(n_rec, torch.int32)
-        if n_rec:
+        outs = (N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
+                N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s)
+        if n_rec and want_lines:
             N.check("avdb_vcf_emit", self.lib.avdb_vcf_emit(
-                self.ctx, tp, nb, n_lines, N.ptr(lines), N.ptr(rec_off), N.ptr(heap_off),
-                N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
-                N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s))
+                self.ctx, tp, nb, n_lines, N.ptr(lines), N.ptr(rec_off), N.ptr(heap_off), *outs))
+        elif n_rec:
+            N.check("avdb_vcf_emit_ws", self.lib.avdb_vcf_emit_ws(
+                self.ctx, tp, nb, n_lines, N.ptr(ws), ws.numel(), N.ptr(rec_off), N.ptr(heap_off), *outs))
         return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
                         records=b, rec_line=rec_line, rec_alt=rec_alt)
 

@@ -693,7 +693,8 @@ def run_workload(a, name, ri, dev, cpu):
             timed("bin_assign", record, lambda: eng.bin_assign(
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
         elif name == "vcf":
-            timed("vcf_tokenize", record, lambda: eng.vcf_tokenize(text))
+            # (records only: the public 80-byte line table is for the load path, K5)
+            timed("vcf_tokenize", record, lambda: eng.vcf_tokenize(text, want_lines=False))
         elif name == "load":
             box = {}
             timed("vcf_tokenize", record, lambda: box.setdefault("vb", eng.vcf_tokenize(text)))
@@ -710,6 +711,8 @@ def run_workload(a, name, ri, dev, cpu):
             timed("vrs_digest", record, lambda: eng.vrs_digest(batch, 50))
 
     last = {}
+    # (AVDB_BENCH_STAGE_EVENTS=0: no stage-breakdown pass after the timed region)
+    stage_events = os.environ.get("AVDB_BENCH_STAGE_EVENTS", "1") != "0"
     for _ in range(a.warmup):
         step(False)
     use_graph = a.graph == "on" or (a.graph == "auto" and name == "c1")
@@ -732,29 +735,40 @@ def run_workload(a, name, ri, dev, cpu):
     torch.cuda.synchronize()
     D.barrier(ri)
     torch.cuda.synchronize()
+    # The timed region carries no per-stage events (an event pair around every launch
+    # cost C2 8 us per 157 us step, profiles/c2_ab/r05_stage_events_ab.log): one pair
+    # around the whole loop on the launch stream gives the average step on the device.
+    loop0, loop1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    loop0.record(stream)
     for _ in range(a.steps):
-        if graph is not None and name in ("c2", "c3", "c4"):
-            timed("bin_assign", True, graph.replay)  # one kernel: the replay is its launch
-        elif graph is not None:
+        if graph is not None:
             graph.replay()
         else:
-            step(True)
+            step(False)
+    loop1.record(stream)
     # job-level exchange: per-rank L8 histograms + counters (RCCL all-gather)
     node_hist, node_ctr = D.allgather_stats(hist, ctr, ri)
     torch.cuda.synchronize()
     D.barrier(ri)
     torch.cuda.synchronize()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, ri, device=dev)
+    loop_ms = loop0.elapsed_time(loop1) / a.steps
+    # the stage breakdown: the same steps again after the timed region, plain launches
+    # with an event pair per stage on the stream it ran on
+    if stage_events:
+        for _ in range(a.steps):
+            step(True)
+        torch.cuda.synchronize()
     stage_ms = {k: float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])) for k, v in evs.items()}
+    stage_ms["timed_step_events"] = loop_ms
     if graph is not None:
         stage_ms["graph_replay"] = True
-    kname = {"c5": "record_prep", "vcf": "vcf_tokenize", "load": "format_write"}.get(name, "bin_assign")
-    kern_ms = stage_ms.get(kname)
-    if name == "c1":
-        kern_ms = elapsed * 1e3 / a.steps  # the whole step (launch-bound at 1.1 M records)
-    if name == "c4k":
-        kern_ms = stage_ms["step_span"]
+    # the roofline's kernel time: the one-kernel steps (C2/C3/C4) and the whole-step
+    # workloads (C1, C4k, vcf) from the timed loop's own events; C5's K2 and the load
+    # workload's K5 write pass from the stage breakdown
+    kname = {"c5": "record_prep", "load": "format_write"}.get(name)
+    kern_ms = stage_ms[kname] if kname else loop_ms
     if name in ("vcf", "load"):
         n_lines, n = n, n_rec  # the unit is emitted variant records (per-ALT rows)
     total_records = n * ri.world * a.steps
@@ -900,14 +914,14 @@ def run_workload(a, name, ri, dev, cpu):
                               "unit": "GB/s", "frac": k7_bytes / (k7_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                               "algorithmic_bytes_per_launch": k7_bytes, "stage_ms": k7_ms}
         out["roofline"]["note"] = ("achieved = SURVEY 8d keyed-record bytes (34 + rlen + alen + 24 if long) + "
-                                   "key/path text written, over the HIP-event time of " +
+                                   "key/path text written, over the timed loop's HIP-event time per step on the "
+                                   "launch stream (" +
                                    {"serial": "K2 + K3 + K4 + K7 in one stream",
-                                    "fork": "the whole step on the launch stream (K2, then K4 + K7 with K3 beside "
-                                            "them on a second stream, joined)",
-                                    "overlap": "the whole step on the launch stream (K2, then K7 with the long keys' "
-                                               "digests pending beside K4 + K3 on a second stream, joined, then the "
-                                               "digest fill)"}[ks.layout] +
-                                   "; K4 (SHA-512) is VALU-bound, the others HBM-bound")
+                                    "fork": "K2, then K4 + K7 with K3 beside them on a second stream, joined",
+                                    "overlap": "K2, then K7 with the long keys' digests pending beside K4 + K3 on a "
+                                               "second stream, joined, then the digest fill"}[ks.layout] +
+                                   "); K4 (SHA-512) is VALU-bound, the others HBM-bound; stage_ms from an untimed "
+                                   "pass with an event pair per stage")
     if name == "c1":
         kt = ks.kt
         out["dtype"] = "u8"
@@ -934,10 +948,10 @@ def run_workload(a, name, ri, dev, cpu):
         out["data"] = "synthetic dbSNP-shaped VCF text (numpy PCG64 lines tiled on the device)"
         out["config"].update(lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
                              records_processed=None)
-        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize stage (count pass with per-window "
+        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize step (count pass with per-window "
                                    "newline counts, window parse, one paired offset scan, emit, and its two host "
-                                   "reads); the line table and line offsets it also writes (96 B per line) are not "
-                                   "counted")
+                                   "reads), records only (vcf_tokenize(want_lines=False): no public line table; the "
+                                   "16 B of line offsets per line it writes are not counted)")
     return out
 
 

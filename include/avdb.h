@@ -273,6 +273,9 @@ int avdb_vcf_parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, 
                          uint64_t* rec_off, uint64_t* heap_off, const avdb_vcf_opts* opts, void* stream);
 /* avdb_vcf_parse_lines with the size of `line_counts`: a count workspace of at
  * least avdb_vcf_count_workspace_size(text_bytes) bytes takes the window path. */
+/* `lines` may be NULL here: no public line table is written (the tokenize-only
+ * path), and what the emit needs of each line (32 bytes) goes into `workspace`
+ * instead, for avdb_vcf_emit_ws with that same workspace. */
 int avdb_vcf_parse_lines2(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
                           const void* line_counts, size_t line_counts_bytes, void* workspace,
                           size_t workspace_bytes, avdb_vcf_line* lines, uint64_t* rec_off, uint64_t* heap_off,
@@ -282,6 +285,13 @@ int avdb_vcf_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t 
                   uint8_t* chrom, uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len,
                   uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line,
                   uint32_t* rec_alt, void* stream);
+/* avdb_vcf_emit after avdb_vcf_parse_lines2(..., lines = NULL, ...): the line data
+ * comes from that call's workspace (same text_bytes and n_lines). */
+int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
+                     const void* parse_workspace, size_t parse_workspace_bytes, const uint64_t* rec_off,
+                     const uint64_t* heap_off, uint8_t* chrom, uint32_t* pos, uint64_t* allele_off,
+                     uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line,
+                     uint32_t* rec_alt, void* stream);
 
 /* ---- K5: the load driver's text outputs ---------------------------------
  * Replaces the per-alt COPY row assembly of VCFVariantLoader.__parse_alt_alleles

@@ -202,3 +202,29 @@ def test_k0_window_parse_equals_starts_pass(engine, which):
     assert (vb.lines[: n0 * 80].cpu().numpy() == lines0).all()
     assert (vb.rec_off[: n0 + 1].cpu().numpy() == ro0).all()
     assert (vb.heap_off[: n0 + 1].cpu().numpy() == ho0).all()
+
+
+@pytest.mark.parametrize("which", ["golden", "dbsnp", "long", "big"])
+def test_k0_records_without_line_table(engine, which):
+    """vcf_tokenize(want_lines=False) — no public line table, the emit reading its
+    32-byte records from the parse workspace (avdb_vcf_emit_ws) — gives the same
+    record SoA, allele heap, offsets and back-references as the tokenizer with the
+    table."""
+    if which == "golden":
+        text = _golden_text()
+    elif which == "dbsnp":
+        text = _synth(60000, 71)
+    elif which == "long":
+        base = _synth(4000, 73).split(b"\n")[:-1]
+        huge = b"2\t888\t.\tC\tG,T\t.\t.\tZ=" + b"Q" * 70000
+        text = b"\n".join(base[:2000] + [huge] + base[2000:] + [huge]) + b"\n"
+    else:
+        tile = _synth(60000, 79).split(b"\n")[:-1]
+        text = b"\n".join(tile * 25) + b"\n"
+    a = engine.vcf_tokenize(text)
+    b = engine.vcf_tokenize(text, want_lines=False)
+    assert b.lines is None and a.n_lines == b.n_lines and a.records.n == b.records.n
+    assert torch.equal(a.rec_off, b.rec_off) and torch.equal(a.heap_off, b.heap_off)
+    for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "ext_id", "heap"):
+        assert torch.equal(getattr(a.records, f), getattr(b.records, f)), f
+    assert torch.equal(a.rec_line, b.rec_line) and torch.equal(a.rec_alt, b.rec_alt)
