@@ -394,6 +394,8 @@ struct KeyTotals {
 // batches whose K7 groups are 64 records (below 4 Mi records), where the launch is
 // one generation of workgroups only if 3 fit per CU (C1: 0.110 -> 0.107 ms); at
 // C4k's size the unconstrained form is faster (record prep 1.19 vs 1.25 ms)
+// (the keyed form's occupancy pinned to 5 / 6 waves: 1.25 / 1.51 ms against 1.25;
+// profiles/c4k_ab/r05_occupancy_ab.log)
 template <bool HIST, int UNROLL, int KEYS = 0>
 __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
     const uint32_t* __restrict__ chromv, const u32x4* __restrict__ pos4, const u64x2* __restrict__ off2,
