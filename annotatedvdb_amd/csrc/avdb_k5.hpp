@@ -394,7 +394,10 @@ __global__ __launch_bounds__(kBlock, kFormatWaves) void k_vcf_format(FormatArgs 
   for (size_t base = size_t(blockIdx.x) * kBlock; base < A.n_lines; base += size_t(gridDim.x) * kBlock) {
     const size_t last = base + kBlock < A.n_lines ? base + kBlock : A.n_lines;
     const avdb_vcf_line& Z = A.lines[last - 1];
-    const Window w = stage_window(h, A.lines[base].start, Z.start + Z.len, s_text);
+    // (the tile's text one load per trip: staging it with every load in flight, as
+    // K0 does, spills this pass's registers — write 4.40 -> 4.77 ms,
+    // profiles/k5_ab/r05_stage_batch_ab.log)
+    const Window w = stage_window<kBlock, kStage, false>(h, A.lines[base].start, Z.start + Z.len, s_text);
     const size_t li = base + tile_order<WRITE>(A, base, last, s_key);
     if (li < A.n_lines) {
       const avdb_vcf_line L = A.lines[li];

@@ -79,24 +79,63 @@ struct Window {
   bool staged;
 };
 
-__device__ __forceinline__ Window stage_window(const Heap& h, size_t s0, size_t s1, u32x4* lds,
-                                               uint32_t stage_bytes = kStage) {
+// n16 16-byte words from a0 (16-aligned) into lds[0, n16), by kThreads threads,
+// n16 <= kIter * kThreads: every thread issues all its loads before its first LDS
+// store, so a workgroup's stage costs one memory round trip, not kIter (a load
+// followed by its store in a loop waits vmcnt(0) every trip).  Words outside the
+// text read as 0 (the bounded per-word path is taken only by a stage that reaches
+// past either end of the text).
+template <uint32_t kIter, uint32_t kThreads>
+__device__ __forceinline__ void stage_copy(u32x4* lds, uintptr_t a0, uint32_t n16, const Heap& h) {
+  const uint32_t tid = threadIdx.x;
+  u32x4 v[kIter];
+  if (a0 >= h.lo && a0 + 16 * uintptr_t(n16) <= h.hi) {
+#pragma unroll
+    for (uint32_t k = 0; k < kIter; ++k) {
+      const uint32_t i = tid + k * kThreads;
+      if (i < n16) v[k] = __builtin_nontemporal_load(gptr<u32x4>(a0 + 16 * uintptr_t(i)));
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kIter; ++k) {
+      const uint32_t i = tid + k * kThreads;
+      if (i < n16) {
+        const uintptr_t a = a0 + 16 * uintptr_t(i);
+        const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
+        v[k] = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kIter; ++k) {
+    const uint32_t i = tid + k * kThreads;
+    if (i < n16) lds[i] = v[k];
+  }
+}
+
+// kBatch false: the one-load-per-trip loop (fewer live registers while staging)
+template <uint32_t kThreads, uint32_t kStageBytes = kStage, bool kBatch = true>
+__device__ __forceinline__ Window stage_window(const Heap& h, size_t s0, size_t s1, u32x4* lds) {
   Window w;
   w.a0 = (h.lo + s0) & ~uintptr_t(15);
   const uintptr_t end = h.lo + s1;
   const size_t n16 = (end - w.a0 + 15) / 16;
-  w.staged = n16 * 16 <= stage_bytes;
+  w.staged = n16 * 16 <= kStageBytes;
   if (w.staged) {
-    for (size_t i = threadIdx.x; i < n16; i += blockDim.x) {
-      const uintptr_t a = w.a0 + 16 * i;
-      u32x4 v;
-      if (a >= h.lo && a + 16 <= h.hi) {
-        v = __builtin_nontemporal_load(gptr<u32x4>(a));
-      } else {
-        const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
-        v = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};
+    if constexpr (kBatch) {
+      stage_copy<(kStageBytes / 16 + kThreads - 1) / kThreads, kThreads>(lds, w.a0, uint32_t(n16), h);
+    } else {
+      for (size_t i = threadIdx.x; i < n16; i += kThreads) {
+        const uintptr_t a = w.a0 + 16 * i;
+        u32x4 v;
+        if (a >= h.lo && a + 16 <= h.hi) {
+          v = __builtin_nontemporal_load(gptr<u32x4>(a));
+        } else {
+          const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
+          v = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};
+        }
+        lds[i] = v;
       }
-      lds[i] = v;
     }
   }
   __syncthreads();

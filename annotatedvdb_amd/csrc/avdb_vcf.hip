@@ -260,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_vcf_parse(const uint8_t* __restrict_
     const size_t last = base + kBlock < n_lines ? base + kBlock : n_lines;
     const size_t s0 = starts[base];
     const size_t s1 = last < n_lines ? starts[last] : text_bytes;
-    const Window w = stage_window(h, s0, s1, s_text);
+    const Window w = stage_window<kBlock>(h, s0, s1, s_text);
     const size_t li = base + threadIdx.x;
     if (li < n_lines) {
       avdb_vcf_line L;
@@ -300,10 +300,145 @@ static_assert(kParseWin % 64 == 0 && kParseWin / 64 + 2 <= 2 * kBlock, "window b
 // alignment slack on both sides (LDS per workgroup decides how many fit a CU)
 constexpr uint32_t kParseStage = kParseWin + kParseOver + 48;
 static_assert(kParseStage <= kStage, "window stage");
+constexpr uint32_t kParseStage64 = (kParseStage + 63) & ~63u;  // whole 64-byte bitmap blocks
+static_assert(kParseStage64 / 64 <= 2 * kBlock, "two bitmap blocks per thread");
 
-__device__ __forceinline__ uint32_t nl_bits8(uint64_t w) {  // bit k: byte k of w is '\n'
-  const uint64_t m = zero_bytes_mask(w ^ kNL) & kHiBits;
+__device__ __forceinline__ uint32_t byte_bits8(uint64_t w, uint64_t pat) {  // bit k: byte k of w is pat's byte
+  const uint64_t m = zero_bytes_mask(w ^ pat) & kHiBits;
   return uint32_t(((m >> 7) * 0x0102040810204080ull) >> 56);
+}
+__device__ __forceinline__ uint32_t nl_bits8(uint64_t w) { return byte_bits8(w, kNL); }
+
+// fields_swar from the window's tab bitmap (bit t of tab[t / 64]: stage byte t is
+// a tab): the line is stage bytes [sp, sp + len).  Each field start is a ctz on a
+// register word; a line of ~100 bytes spans two or three bitmap words, where the
+// SWAR scan reads and tests every 8-byte word of the line.
+__device__ __forceinline__ uint32_t fields_bits(lds_cp64 tab, uint32_t sp, uint32_t len, avdb_vcf_line& L) {
+  const uint32_t e = sp + len;
+  const uint32_t we = (e + 63) >> 6;  // words [sp / 64, we) hold the line
+  uint32_t wi = sp >> 6;
+  auto clip = [e](uint32_t w, uint64_t x) {  // bits of word w at stage bytes < e
+    const uint32_t hi = e - 64 * w;
+    return hi >= 64 ? x : x & ((uint64_t(1) << hi) - 1);
+  };
+  uint64_t m = wi < we ? clip(wi, tab[wi] & (~uint64_t(0) << (sp & 63))) : 0ull;
+  uint32_t nf = 1;
+#pragma unroll
+  for (int f = 1; f <= 8; ++f) {
+    while (!m && wi + 1 < we) {
+      ++wi;
+      m = clip(wi, tab[wi]);
+    }
+    if (m) {
+      const uint32_t t = 64 * wi + uint32_t(__builtin_ctzll(m)) - sp;
+      if (f < 8) L.field[f] = t + 1;
+      else L.field_end8 = t;
+      m &= m - 1;
+      ++nf;
+    }
+  }
+  if (nf > 8) {  // past INFO: only the count matters
+    nf += uint32_t(__popcll(m));
+    while (wi + 1 < we) {
+      ++wi;
+      nf += uint32_t(__popcll(clip(wi, tab[wi])));
+    }
+  }
+  return nf;
+}
+
+// bytes [p, p + 16) of the stage as two registers (bytes at and past `end` read
+// as 0; words past the stage read as 0: LDS reads outside the allocation return 0)
+__device__ __forceinline__ void stage16(lds_cp64 lw, uint32_t p, uint32_t end, uint64_t* y0, uint64_t* y1) {
+  const uint32_t k = p >> 3, sh = 8 * (p & 7);
+  const uint64_t w0 = lw[k], w1 = lw[k + 1], w2 = lw[k + 2];
+  uint64_t a = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  uint64_t b = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  const uint32_t n = end > p ? end - p : 0u;
+  if (n < 16) {
+    b &= n > 8 ? low_bytes_mask(n - 8) : 0ull;
+    a &= low_bytes_mask(n < 8 ? n : 8);
+  }
+  *y0 = a;
+  *y1 = b;
+}
+
+// The INFO refSNP of a staged line, INFO = stage bytes [A, B): the last entry whose
+// key is exactly "RS" (dict(...) keeps the last; vcf_parser.py:155-169), as the
+// SWAR scan of parse_line_with decides it.  Entries after a ';' are 4-byte
+// windows ";RS=" / ";RS;" at every byte of the INFO words, with the bytes outside
+// [A, B) zeroed (so no window reaches past INFO): one v_alignbyte and two compares
+// per byte instead of five byte-equality masks per word.  The entry at the INFO
+// start and a bare ";RS" ending INFO are checked once.  Returns 0 (no "RS"
+// entry), kRsFound | the number, or kRsFound | kRsHost (a value the reference
+// coerces to something other than rs<int>).
+constexpr uint64_t kRsFound = uint64_t(1) << 62, kRsHost = uint64_t(1) << 63;
+__device__ __noinline__ uint64_t info_rs_staged(lds_cp64 lw, lds_cp stage, uint32_t A, uint32_t B) {
+  int32_t at = -1;  // stage offset of the last entry's 'R'
+  bool val = false;
+  if (B >= A + 4) {
+    auto masked = [A, B](uint32_t k, uint64_t w) {
+      const int32_t lo = int32_t(A) - int32_t(8 * k), hi = int32_t(B) - int32_t(8 * k);
+      if (lo > 0) w &= lo >= 8 ? 0ull : ~low_bytes_mask(uint32_t(lo));
+      if (hi < 8) w &= hi > 0 ? low_bytes_mask(uint32_t(hi)) : 0ull;
+      return w;
+    };
+    const uint32_t k0 = A >> 3, k1 = (B - 4) >> 3;  // words holding the ';' of a window [p, p + 4), p + 4 <= B
+    uint64_t x = masked(k0, lw[k0]);
+    for (uint32_t k = k0; k <= k1; ++k) {
+      const uint64_t nx = masked(k + 1, lw[k + 1]);
+      const uint32_t x0 = uint32_t(x), x1 = uint32_t(x >> 32), n0 = uint32_t(nx);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t w = j < 4 ? __builtin_amdgcn_alignbyte(x1, x0, j) : __builtin_amdgcn_alignbyte(n0, x1, j - 4);
+        const bool eq = w == 0x3D53523Bu;  // ";RS="
+        if (eq || w == 0x3B53523Bu) {      // ";RS;"
+          at = int32_t(8 * k) + j + 1;
+          val = eq;
+        }
+      }
+      x = nx;
+    }
+  }
+  uint64_t y0, y1;
+  if (B >= A + 3) {  // a bare "RS" ending INFO is its last entry
+    stage16(lw, B - 3, B, &y0, &y1);
+    if ((y0 & 0xFFFFFFull) == 0x53523Bull) {
+      at = int32_t(B) - 2;
+      val = false;
+    }
+  }
+  if (at < 0 && B >= A + 2) {  // the first entry: "RS=", "RS;" or all of INFO "RS"
+    stage16(lw, A, B, &y0, &y1);
+    const uint64_t t = y0 & 0xFFFFFFull;
+    if (t == 0x3D5352ull || t == 0x3B5352ull || (B == A + 2 && t == 0x5352ull)) {
+      at = int32_t(A);
+      val = t == 0x3D5352ull;
+    }
+  }
+  if (at < 0) return 0;
+  uint64_t v = 0;
+  bool ok = false;
+  if (val) {  // the value [at + 3, next ';' or B): all digits, 1..18 of them
+    const uint32_t vs = uint32_t(at) + 3, vmax = B - vs;
+    stage16(lw, vs, B, &y0, &y1);
+    const uint64_t nd0 = nondigit_mask(y0), nd1 = nondigit_mask(y1);
+    const uint32_t nd = nd0 ? uint32_t(__builtin_ctzll(nd0)) >> 3 : (nd1 ? 8u + (uint32_t(__builtin_ctzll(nd1)) >> 3) : 16u);
+    if (nd < 16 || vmax <= 16) {
+      const uint32_t n = nd < vmax ? nd : vmax;
+      const bool term = n == vmax || (n < 16 && (((n < 8 ? y0 >> (8 * n) : y1 >> (8 * (n - 8))) & 0xFF) == ';'));
+      if (term && n >= 1) v = decimal16(y0, y1, n, &ok);
+    } else {  // 16 digits and more: the byte loop (<= 18 digits)
+      uint32_t n = 0;
+      while (n < vmax && stage[vs + n] != ';') ++n;
+      ok = n <= 18;
+      for (uint32_t q = 0; ok && q < n; ++q) {
+        ok = is_digit(stage[vs + q]);
+        v = v * 10 + (stage[vs + q] - '0');
+      }
+    }
+  }
+  return ok && v >= 1 ? (kRsFound | v) : (kRsFound | kRsHost);
 }
 
 // exclusive block scan of one u32 per thread (kBlock threads); *total = sum
@@ -339,8 +474,10 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
                                                               unsigned long long* __restrict__ rec_cnt,
                                                               unsigned long long* __restrict__ heap_cnt,
                                                               ChromMapView cm, uint32_t min_fields) {
-  __shared__ u32x4 s_text[kParseStage / 16];
+  __shared__ u32x4 s_text[kParseStage64 / 16];
+  __shared__ uint64_t s_tab[kParseStage64 / 64];  // tab bitmap of the staged bytes
   __shared__ uint32_t s_start[kBlock + 1];  // line starts of the round, relative to the window start
+  __shared__ uint64_t s_rs[kBlock];         // the round's INFO refSNP results (info_rs_staged)
   __shared__ uint32_t s_w[kVcfWaves];
   __shared__ uint32_t s_tail;               // (first '\n' at or after w1 - 1) + 1 - w0
   const Heap h = make_heap(text, text_bytes);
@@ -367,30 +504,27 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
   const uintptr_t a0 = (h.lo + q0) & ~uintptr_t(15);
   const uintptr_t wend = h.lo + (w1 + kParseOver < nb ? w1 + kParseOver : nb);
   const uint32_t n16 = uint32_t((wend - a0 + 15) / 16);
-  for (uint32_t i = tid; i < n16; i += kBlock) {
-    const uintptr_t a = a0 + 16 * size_t(i);
-    u32x4 v;
-    if (a >= h.lo && a + 16 <= h.hi) {
-      v = __builtin_nontemporal_load(gptr<u32x4>(a));
-    } else {
-      const uint64_t x = text_word(a, h), y = text_word(a + 8, h);
-      v = u32x4{uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32)};
-    }
-    s_text[i] = v;
-  }
+  stage_copy<(kParseStage64 / 16 + kBlock - 1) / kBlock, kBlock>(s_text, a0, n16, h);
   __syncthreads();
-  // ---- newline bitmaps of [q0, w1 - 1) ----
+  // ---- newline bitmaps of [q0, w1 - 1); the tab bitmap of the whole stage ----
   const uint32_t o_lo = uint32_t(h.lo + q0 - a0), o_hi = uint32_t(h.lo + w1 - 1 - a0);
   const uint32_t nblk = w1 - 1 > q0 ? (o_hi + 63) / 64 : 0u;
+  const uint32_t nstage = (16 * n16 + 63) / 64;
   uint64_t bm[2] = {0, 0};
   uint32_t cnt = 0;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const uint32_t b = 2 * tid + k;
-    if (b < nblk) {
-      uint64_t m = 0;
+    if (b < nstage) {
+      uint64_t m = 0, t = 0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) m |= uint64_t(nl_bits8(lw[8 * b + q])) << (8 * q);
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t w = lw[8 * b + q];
+        m |= uint64_t(nl_bits8(w)) << (8 * q);
+        t |= uint64_t(byte_bits8(w, kTab)) << (8 * q);
+      }
+      s_tab[b] = t;
+      if (b >= nblk) continue;
       const uint32_t blo = 64 * b;
       if (o_lo > blo) m &= o_lo - blo >= 64 ? 0ull : ~0ull << (o_lo - blo);
       if (o_hi < blo + 64) m &= o_hi <= blo ? 0ull : ~0ull >> (64 - (o_hi - blo));
@@ -454,22 +588,63 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
     if (tid == 0 && T <= hi) s_start[T - lo] = s_tail;
     __syncthreads();
     const size_t li = li0 + lo + tid;
-    if (lo + tid < T && li < n_lines) {
-      avdb_vcf_line L;
+    const bool live = lo + tid < T && li < n_lines;
+    avdb_vcf_line L;
+    uint64_t recs = 0, hbytes = 0;
+    uint32_t info_item = 0;  // a pending INFO: stage offset | length << 15
+    if (live) {
       L.start = w0 + s_start[tid];
       size_t nl = w0 + s_start[tid + 1] - 1;  // its newline, or the text end
       if (nl < L.start || nl > nb) nl = L.start;  // (never expected: starts increase)
       const uint32_t raw = uint32_t(nl - L.start);
       const uint32_t mis = uint32_t((h.lo + L.start) & 7);
-      uint64_t recs, hbytes;
       if (h.lo + nl <= wend) {
         const uint8_t* ls = reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - a0);
         const lds_cp64 lw2 = (lds_cp64)(reinterpret_cast<const uint64_t*>(ls - mis));
-        parse_line((lds_cp)ls, [lw2](uint32_t k) { return lw2[k]; }, mis, raw, L, recs, hbytes, cm, min_fields);
+        const uint32_t sp = uint32_t(h.lo + L.start - a0);
+        const lds_cp64 tb = (lds_cp64)(reinterpret_cast<const uint64_t*>(s_tab));
+        parse_line_with<true>([tb, sp](uint32_t n, avdb_vcf_line& l) { return fields_bits(tb, sp, n, l); },
+                              (lds_cp)ls, [lw2](uint32_t k) { return lw2[k]; }, mis, raw, L, recs, hbytes, cm,
+                              min_fields);
+        if (L.pad[0] == kInfoPending)  // INFO = stage bytes [sp + field 7, sp + its end)
+          info_item = (sp + L.field[7]) | ((L.field_end8 - L.field[7]) << 15);
       } else {
         const uintptr_t la = h.lo + L.start - mis;
         parse_line((glb_cp)(text + L.start), [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); }, mis,
                    raw, L, recs, hbytes, cm, min_fields);
+      }
+    }
+    // the round's pending INFO scans, gathered into the first lanes of the workgroup
+    // (a wave scans INFO once for its lanes that need it, instead of every wave for
+    // the ~40 % of its lines without an rs ID)
+    __syncthreads();  // (s_start and s_w are free: this round's starts are read)
+    const uint64_t pend = __ballot(info_item != 0);
+    if (lane == 0) s_w[wv] = uint32_t(__popcll(pend));
+    __syncthreads();
+    uint32_t n_pend = 0, slot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kVcfWaves; ++w) {
+      const uint32_t c = s_w[w];
+      if (w < wv) slot += c;
+      n_pend += c;
+    }
+    slot += uint32_t(__popcll(pend & ((uint64_t(1) << lane) - 1)));
+    if (info_item) s_start[slot] = info_item;
+    __syncthreads();
+    if (tid < n_pend) {
+      const uint32_t it = s_start[tid], A = it & 0x7FFFu;
+      s_rs[tid] = info_rs_staged(lw, (lds_cp)(reinterpret_cast<const uint8_t*>(s_text)), A, A + (it >> 15));
+    }
+    __syncthreads();
+    if (live) {
+      if (info_item) {
+        const uint64_t rs = s_rs[slot];
+        L.pad[0] = 0;
+        if (rs & kRsFound) {
+          L.flags |= AVDB_VCF_INFO_RS;
+          if (rs & kRsHost) L.flags |= AVDB_VCF_EXT_HOST;
+          else L.ext_id = rs & (kRsFound - 1);
+        }
       }
       put_line(lines, erec, li, L);
       rec_cnt[li] = recs;
@@ -564,7 +739,7 @@ __global__ __launch_bounds__(kEmitLines) void k_vcf_emit(
       const avdb_vcf_line& Z = lines[last - 1];
       s1 = Z.start + Z.len;
     }
-    const Window w = stage_window(h, s0, s1, s_text, kEmitStage);
+    const Window w = stage_window<kEmitLines, kEmitStage>(h, s0, s1, s_text);
     const size_t li = base + threadIdx.x;
     if (li < n_lines) {
       const uint64_t r0 = rec_off[li], r1 = rec_off[li + 1];

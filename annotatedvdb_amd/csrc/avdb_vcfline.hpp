@@ -166,13 +166,48 @@ AVDB_HD uint64_t decimal16(uint64_t x0, uint64_t x1, uint32_t n, bool* ok) {
 constexpr uint64_t kTab = 0x0909090909090909ull;
 constexpr uint64_t kSemi = 0x3B3B3B3B3B3B3B3Bull;
 
+// the tab-separated fields of a line of len bytes (first 8 starts; INFO ends at
+// the 8th tab or the end): L.field[1..7] / L.field_end8 for the tabs present
+// (the caller preset the rest), returns the field count.  SWAR over the line's
+// aligned words (word_at/mis).
+template <class WordAt>
+AVDB_HD uint32_t fields_swar(const WordAt& word_at, uint32_t mis, uint32_t len, avdb_vcf_line& L) {
+  uint32_t nf = 1;
+  const uint32_t k1 = (len + mis + 7) >> 3;
+  for (uint32_t k = 0; k < k1; ++k) {
+    uint64_t m = zero_bytes_mask(word_at(k) ^ kTab) & kHiBits;
+    if (k == 0) m &= ~low_bytes_mask(mis);
+    const uint32_t hi = len + mis - 8 * k;
+    if (hi < 8) m &= low_bytes_mask(hi);
+    if (nf > 8) {  // past INFO: only the count matters
+      nf += uint32_t(__builtin_popcountll(m));
+      continue;
+    }
+    while (m) {
+      const uint32_t i = 8 * k + (uint32_t(__builtin_ctzll(m)) >> 3) - mis;
+      m &= m - 1;
+#pragma unroll
+      for (int f = 1; f < 8; ++f)  // register-resident field table (no dynamic index)
+        if (nf == uint32_t(f)) L.field[f] = i + 1;
+      if (nf == 8) L.field_end8 = i;
+      ++nf;
+    }
+  }
+  return nf;
+}
+
 // one line: s points at its first byte (LDS or global), len = bytes up to its
-// newline; word_at/mis give the same bytes as aligned 8-byte words (SWAR scans)
-template <class CP, class WordAt>
-AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
-                                           uint32_t len, avdb_vcf_line& L, uint64_t& recs,
-                                           uint64_t& hbytes, const ChromMapView& cm = ChromMapView{},
-                                           uint32_t min_fields = 8) {
+// newline; word_at/mis give the same bytes as aligned 8-byte words (SWAR scans);
+// find_fields(len, L) fills the field table and returns the field count
+// (fields_swar, or the tab bitmap of a staged window: avdb_vcf.hip).
+// kDeferInfo: a line whose refSNP must come from INFO gets L.pad[0] =
+// kInfoPending instead of the INFO scan (the window parse gathers those lines of a
+// round and scans their INFO fields with the whole workgroup: avdb_vcf.hip)
+constexpr uint8_t kInfoPending = 1;
+template <bool kDeferInfo = false, class CP, class WordAt, class FindFields>
+AVDB_HD void parse_line_with(const FindFields& find_fields, CP s, const WordAt& word_at, uint32_t mis,
+                             uint32_t len, avdb_vcf_line& L, uint64_t& recs, uint64_t& hbytes,
+                             const ChromMapView& cm, uint32_t min_fields) {
     while (len && is_ws(s[len - 1])) --len;  // str.rstrip()
     L.len = len;
     L.flags = 0;
@@ -182,35 +217,12 @@ AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
     L.n_rec = 0;
     L.chrom = 255;
     L.pad[0] = L.pad[1] = L.pad[2] = 0;
-    uint32_t nf = 1;
     L.field[0] = 0;
     for (int k = 1; k < 8; ++k) L.field[k] = len + 1;
     L.field_end8 = len;
     if (len && s[0] == '#') L.flags |= AVDB_VCF_COMMENT;
     if (!len) L.flags |= AVDB_VCF_EMPTY;
-    // tab-separated fields (first 8 starts; INFO ends at the 8th tab or the end)
-    {
-      const uint32_t k1 = (len + mis + 7) >> 3;
-      for (uint32_t k = 0; k < k1; ++k) {
-        uint64_t m = zero_bytes_mask(word_at(k) ^ kTab) & kHiBits;
-        if (k == 0) m &= ~low_bytes_mask(mis);
-        const uint32_t hi = len + mis - 8 * k;
-        if (hi < 8) m &= low_bytes_mask(hi);
-        if (nf > 8) {  // past INFO: only the count matters
-          nf += uint32_t(__builtin_popcountll(m));
-          continue;
-        }
-        while (m) {
-          const uint32_t i = 8 * k + (uint32_t(__builtin_ctzll(m)) >> 3) - mis;
-          m &= m - 1;
-#pragma unroll
-          for (int f = 1; f < 8; ++f)  // register-resident field table (no dynamic index)
-            if (nf == uint32_t(f)) L.field[f] = i + 1;
-          if (nf == 8) L.field_end8 = i;
-          ++nf;
-        }
-      }
-    }
+    const uint32_t nf = find_fields(len, L);
     L.n_fields = nf;
     recs = 0;
     hbytes = 0;
@@ -235,12 +247,19 @@ AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
           const uint64_t v = n <= 10 ? decimal16(x0, x1, n, &ok) : 0ull;
           if (ok && v <= 0xFFFFFFFFull) L.pos = uint32_t(v); else L.flags |= AVDB_VCF_BAD_POS;
         }
-        // ID
+        // ID (its first 16 bytes in two registers: an "rs<digits>" or '.' ID, the
+        // dbSNP shapes, needs no other read)
         const CP id = s + L.field[2];
         const uint32_t idn = fend(2) - L.field[2];
-        // ID, 16 bytes at a time: digits / number-like bytes / an "rs" pair
-        bool has_rs = false;
-        {
+        uint64_t i0, i1;
+        line16(word_at, mis, len, L.field[2], &i0, &i1);
+        const uint32_t c0 = idn > 0 ? uint32_t(i0 & 0xFF) : 0u, c1 = idn > 1 ? uint32_t((i0 >> 8) & 0xFF) : 0u;
+        const bool rs_head = idn >= 2 && c0 == 'r' && c1 == 's';
+        const bool id_dot = idn == 1 && c0 == '.';
+        bool has_rs = rs_head;
+        if (!rs_head && !id_dot) {
+          // 16 bytes at a time: digits / number-like bytes / an "rs" pair ("rs..."
+          // holds a letter and '.' no digit, so neither can be number-like)
           bool numlike = idn > 0, has_digit = false;
           uint64_t carry_r = 0;  // bit 7: the byte before this block is 'r'
           for (uint32_t b = 0; b < idn; b += 16) {
@@ -264,13 +283,17 @@ AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
           }
           if (numlike && has_digit) L.flags |= AVDB_VCF_ID_HOST;  // Python coerces it to a number
         }
-        if ((idn == 1 && id[0] == '.') || (idn >= 2 && id[0] == 'r' && id[1] == 's'))
-          L.flags |= AVDB_VCF_ID_METASEQ;
+        if (id_dot || rs_head) L.flags |= AVDB_VCF_ID_METASEQ;
         if (has_rs) {
           L.flags |= AVDB_VCF_ID_RS;
-          if (idn >= 3 && idn <= 18 && id[0] == 'r' && id[1] == 's' && id[2] != '0') {
+          if (idn >= 3 && idn <= 18 && rs_head && ((i0 >> 16) & 0xFF) != '0') {
             uint64_t y0, y1;  // "rs" + up to 16 digits, SWAR
-            line16(word_at, mis, len, L.field[2] + 2, &y0, &y1);
+            if (idn <= 16) {  // bytes 2.. of the registers already read
+              y0 = (i0 >> 16) | (i1 << 48);
+              y1 = i1 >> 16;
+            } else {
+              line16(word_at, mis, len, L.field[2] + 2, &y0, &y1);
+            }
             bool ok;
             const uint64_t v = decimal16(y0, y1, idn - 2, &ok);
             L.ext_id = ok ? v : 0ull;
@@ -278,47 +301,74 @@ AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
             L.ext_id = rs_number(id, idn);
           }
           if (!L.ext_id) L.flags |= AVDB_VCF_EXT_HOST;
+        } else if (kDeferInfo) {
+          L.pad[0] = kInfoPending;
         } else {
-          // INFO: last entry whose key is exactly "RS" (dict(...) keeps the last)
-          const CP inf = s + L.field[7];
+          // INFO: the last entry whose key is exactly "RS" (dict(...) keeps the last).
+          // One pass over the INFO's words with no data-dependent branch: an entry
+          // "RS" / "RS=..." is an 'R' at an entry start (the INFO start or after a
+          // ';') followed by 'S', then '=', ';' or the INFO end — exact, as INFO
+          // holds no tab.  The last such entry decides: "RS" bare, "RS=<v>" a value.
           const uint32_t f7 = L.field[7], e7 = fend(7);
-          int64_t vs = -1, ve = -1;
-          bool bare = false;
-          // entries are [i, j) between ';' (INFO-relative), scanned 8 bytes at a time
-          uint32_t i = 0;
-          const uint32_t in = e7 >= f7 ? e7 - f7 : 0;
-          for (uint32_t at = 0; at <= in;) {
-            // next ';' at or after `at` (SWAR), or the INFO end
-            uint32_t j = in;
-            {
-              const uint32_t from = f7 + at, to = e7;
-              const uint32_t k1 = (to + mis + 7) >> 3;
-              for (uint32_t k = (from + mis) >> 3; k < k1; ++k) {
-                uint64_t m = zero_bytes_mask(word_at(k) ^ kSemi) & kHiBits;
-                const int32_t lo = int32_t(from + mis) - int32_t(8 * k);
-                if (lo > 0) m &= ~low_bytes_mask(uint32_t(lo));
-                const uint32_t hi = to + mis - 8 * k;
-                if (hi < 8) m &= low_bytes_mask(hi);
-                if (m) {
-                  j = 8 * k + (uint32_t(__builtin_ctzll(m)) >> 3) - mis - f7;
-                  break;
-                }
+          int64_t rs_at = -1;  // line offset of the last entry's 'R'
+          bool rs_val = false;  // ... followed by '='
+          if (e7 >= f7 + 2) {
+            const uint32_t kend = (len + mis + 7) >> 3;
+            const uint32_t ka = (f7 + mis) >> 3, kb = (e7 + mis + 7) >> 3;
+            uint64_t x = word_at(ka), semi_c = 0;  // semi_c bit 7: the byte before word k is ';'
+            for (uint32_t k = ka; k < kb; ++k) {
+              const uint64_t nx = k + 1 < kend ? word_at(k + 1) : 0ull;
+              const int32_t base = int32_t(8 * k) - int32_t(mis);  // line offset of the word's byte 0
+              const uint64_t semi = bytes_eq_mask(x, ';');
+              uint64_t at = (semi << 8) | semi_c;
+              const int32_t js = int32_t(f7) - base, jz = int32_t(e7) - 1 - base;  // 'R' at [js, jz)
+              if (js >= 0 && js < 8) at |= uint64_t(0x80) << (8 * js);
+              uint64_t range = kHiBits;
+              if (js > 0) range &= ~low_bytes_mask(uint32_t(js));
+              if (jz < 8) range &= jz > 0 ? low_bytes_mask(uint32_t(jz)) : 0ull;
+              const uint64_t v1 = (x >> 8) | (nx << 56), v2 = (x >> 16) | (nx << 48);
+              const int32_t je = int32_t(e7) - 2 - base;  // 'R' two bytes before the INFO end
+              const uint64_t eq = bytes_eq_mask(v2, '=');
+              uint64_t tail = eq | bytes_eq_mask(v2, ';');
+              if (je >= 0 && je < 8) tail |= uint64_t(0x80) << (8 * je);
+              const uint64_t cand = bytes_eq_mask(x, 'R') & bytes_eq_mask(v1, 'S') & at & tail & range;
+              if (cand) {
+                const uint32_t j = (63u - uint32_t(__builtin_clzll(cand))) >> 3;
+                rs_at = base + int32_t(j);
+                rs_val = (eq >> (8 * j)) & 0x80;
               }
+              semi_c = semi >> 56;
+              x = nx;
             }
-            if (j - i >= 2 && inf[i] == 'R' && inf[i + 1] == 'S') {
-              if (j - i == 2) { bare = true; vs = ve = -1; }
-              else if (inf[i + 2] == '=') { bare = false; vs = i + 3; ve = j; }
-            }
-            i = j + 1;
-            at = j + 1;
           }
-          if (vs >= 0 || bare) {
+          if (rs_at >= 0) {
             L.flags |= AVDB_VCF_INFO_RS;
             uint64_t v = 0;
-            bool ok = !bare && ve > vs && ve - vs <= 18;
-            for (int64_t i = vs; ok && i < ve; ++i) {
-              ok = is_digit(inf[i]);
-              v = v * 10 + (inf[i] - '0');
+            bool ok = false;
+            if (rs_val) {
+              // the value [rs_at + 3, next ';' or the INFO end): all digits, 1..18 of them
+              const uint32_t vs = uint32_t(rs_at) + 3;
+              uint64_t y0, y1;
+              line16(word_at, mis, len, vs, &y0, &y1);
+              const uint64_t nd0 = nondigit_mask(y0), nd1 = nondigit_mask(y1);
+              const uint32_t nd = nd0 ? uint32_t(__builtin_ctzll(nd0)) >> 3
+                                      : (nd1 ? 8u + (uint32_t(__builtin_ctzll(nd1)) >> 3) : 16u);
+              const uint32_t vmax = e7 - vs;  // bytes to the INFO end
+              if (nd < 16 || vmax <= 16) {
+                const uint32_t n = nd < vmax ? nd : vmax;  // leading digits inside INFO
+                // the value ends at the INFO end or at a ';' right after its digits
+                const bool term = n == vmax || (n < 16 && (((n < 8 ? y0 >> (8 * n) : y1 >> (8 * (n - 8))) & 0xFF) == ';'));
+                if (term && n >= 1) v = decimal16(y0, y1, n, &ok);
+              } else {  // 16 digits and more: the byte loop (<= 18 digits)
+                const CP inf = s + vs;
+                uint32_t n = 0;
+                while (n < vmax && inf[n] != ';') ++n;
+                ok = n <= 18;
+                for (uint32_t q = 0; ok && q < n; ++q) {
+                  ok = is_digit(inf[q]);
+                  v = v * 10 + (inf[q] - '0');
+                }
+              }
             }
             if (ok && v >= 1) L.ext_id = v;  // 'rs' + str(int(value))
             else L.flags |= AVDB_VCF_EXT_HOST;
@@ -361,6 +411,13 @@ AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis,
         recs = L.n_rec;
       }
     }
+}
+
+template <class CP, class WordAt>
+AVDB_HD void parse_line(CP s, const WordAt& word_at, uint32_t mis, uint32_t len, avdb_vcf_line& L, uint64_t& recs,
+                        uint64_t& hbytes, const ChromMapView& cm = ChromMapView{}, uint32_t min_fields = 8) {
+  parse_line_with([&word_at, mis](uint32_t n, avdb_vcf_line& l) { return fields_swar(word_at, mis, n, l); }, s, word_at,
+                  mis, len, L, recs, hbytes, cm, min_fields);
 }
 
 }  // namespace avdb

@@ -228,3 +228,34 @@ def test_k0_records_without_line_table(engine, which):
     for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "ext_id", "heap"):
         assert torch.equal(getattr(a.records, f), getattr(b.records, f)), f
     assert torch.equal(a.rec_line, b.rec_line) and torch.equal(a.rec_alt, b.rec_alt)
+
+
+def test_k0_info_refsnp_edges(engine):
+    """The INFO refSNP scan in K0's staged window parse (the cases of
+    test_percall_host.INFO_RS_CASES at eight INFO alignments, plus sample columns
+    after INFO, repeated so lines sit at every window position): EXT_HOST exactly
+    where the reference would not give rs<int>, else the record's refSNP key."""
+    from annotatedvdb_amd.engine import VCF_EXT_HOST, VCF_INFO_RS
+    from test_percall_host import info_rs_lines
+    cases = info_rs_lines()
+    # a dbSNP-shaped line between cases shifts the following case by one byte per repeat
+    filler = [b"1\t%d\trs1\tA\tG\t.\t.\t%s" % (200 + k, b"Q" * (1 + k % 64)) for k in range(len(cases) * 3)]
+    lines, want = [], []
+    for k in range(len(cases) * 3):
+        line, w = cases[k % len(cases)]
+        lines += [line.encode(), filler[k]]
+        want += [w, 1]
+    text = b"\n".join(lines) + b"\n"
+    vb = engine.vcf_tokenize(text)
+    L = vb.lines_host()
+    ro = vb.rec_off[: vb.n_lines + 1].cpu().numpy()
+    ext = vb.records.ext_id[: int(vb.records.n)].cpu().numpy().view(np.uint64)
+    assert vb.n_lines == len(lines)
+    for li, w in enumerate(want):
+        fl = int(L[li]["flags"])
+        if w is None:
+            assert fl & VCF_EXT_HOST and fl & VCF_INFO_RS, lines[li]
+            continue
+        assert not fl & VCF_EXT_HOST, lines[li]
+        assert int(ro[li + 1]) - int(ro[li]) == 1 and int(ext[ro[li]]) == w, (lines[li], int(ext[ro[li]]))
+        assert bool(fl & VCF_INFO_RS) == (w != 0 and li % 2 == 0), lines[li]

@@ -345,3 +345,50 @@ def test_k8a_variant_annotator_edges(lib):
     assert d["normalized_metaseq_id"] == "chrUn_KI270302v1:100:AG:-"
     assert list(d) == ["location_start", "location_end", "normalized_metaseq_id", "variant_class",
                        "variant_class_abbrev", "display_allele", "sequence_allele"]
+
+
+# INFO refSNP cases (vcf_parser.py:155-169 via parse_info, :38-52): the last entry
+# whose key is exactly "RS" decides; an int value gives rs<value>, anything the
+# reference coerces otherwise (bare key, float, text, 0, > 18 digits) is the host's.
+# value: the refSNP number, 0 = no refSNP (NULL), None = the line goes to the host
+INFO_RS_CASES = [
+    ("RS=5", 5), ("RS=123;RSPOS=7", 123), ("RSPOS=7;RS=123", 123), ("RS=1;RS=2", 2),
+    ("RS=12;RS", None), ("RS", None), ("RS=", None), ("RS=0", None), ("RS=007", 7),
+    ("RS=12a", None), ("RS=5.0", None), ("X=1;RS=99;Y", 99), ("RSX=4", 0), ("xRS=4", 0),
+    ("VC=SNV;FREQ=a:0.1,0.2", 0), ("RS=12345678901234567", 12345678901234567),
+    ("RS=123456789012345678", 123456789012345678), ("RS=1234567890123456789", None),
+    ("RS=1234567890123456;VC=SNV", 1234567890123456), ("RS=123456789012345", 123456789012345),
+    ("RS=55;dbSNPBuildID=151;SSR=0;VC=SNV;FREQ=1000Genomes:0.9876,0.0124", 55), ("RS=5 ", 5),
+    ("RS=5=6", None), ("R=1;S=2", 0), ("RS=8;R", 8), (".", 0),
+]
+
+
+def info_rs_lines():
+    """(line, expected) with every case at eight alignments of the INFO field, and
+    once with sample columns after INFO."""
+    out = []
+    for info, want in INFO_RS_CASES:
+        for s in range(8):
+            pre = ("Z" * s + "=1;") if s else ""
+            out.append(("1\t100\t.\tA\tG\t.\t.\t%s%s" % (pre, info), want))
+        out.append(("1\t100\t.\tA\tG\t.\t.\t%s\tGT\t0/1" % info.rstrip(), want))
+    return out
+
+
+def test_k5h_info_refsnp_edges(lib, ctx):
+    """The INFO refSNP scan (one SWAR pass over the INFO words) on the per-line
+    host entry: rs<value> in the COPY row's ref_snp_id column, NULL without one,
+    and the host for every value the reference would coerce to something else."""
+    for line, want in info_rs_lines():
+        b = line.encode()
+        opts = N.FormatOpts(b"1", 50, 0)
+        res = N.LineResult()
+        cb, mb = ctypes.create_string_buffer(1 << 14), ctypes.create_string_buffer(1 << 14)
+        N.check("k5h", lib.avdb_vcf_line_host(ctx, b, len(b), ctypes.byref(opts), None, cb, 1 << 14, mb, 1 << 14,
+                                              ctypes.byref(res)))
+        if want is None:
+            assert res.state == N.LINE_HOST, line
+            continue
+        assert res.state == N.LINE_GPU, line
+        col = cb.raw[:res.copy_bytes].decode().split("#")[6]
+        assert col == ("rs%d" % want if want else "NULL"), (line, col)
