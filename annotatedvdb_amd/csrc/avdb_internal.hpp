@@ -227,19 +227,6 @@ struct ErrCounters {
   }
 };
 
-// ---- wave sums (butterfly over the 64 lanes; every lane gets the total) ----
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1)
-    v += (uint64_t(uint32_t(__shfl_xor(uint32_t(v >> 32), d, kWave))) << 32) | uint32_t(__shfl_xor(uint32_t(v), d, kWave));
-  return v;
-}
-
 // ---- wave-aggregated histogram add --------------------------------------
 // Adds 1 to hist[key] for every active lane with key != ~0u.  Position-sorted
 // input gives runs of equal keys in consecutive lanes: only the head lane of

@@ -128,6 +128,17 @@ __device__ __forceinline__ void record_sizes(const KeyArgs& A, uint32_t c, uint3
                  A.code != nullptr, ks, ps);
 }
 
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1)
+    v += (uint64_t(uint32_t(__shfl_xor(uint32_t(v >> 32), d, kWave))) << 32) | uint32_t(__shfl_xor(uint32_t(v), d, kWave));
+  return v;
+}
 
 // the (keys, paths) bytes of group g (records (g << group_log2 + k) * 64 + lane),
 // summed over the wave

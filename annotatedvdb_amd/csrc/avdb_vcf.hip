@@ -464,174 +464,7 @@ __device__ __forceinline__ uint32_t block_excl32(uint32_t v, uint32_t* s_w, uint
   return base + x - v;
 }
 
-// (Rendering the allele heap through an LDS image of the tile's heap span with a
-// coalesced flush, as K7 does for its text, measured slower: 0.66 vs 0.60 ms for
-// 8.4 M lines — the pass is bound by re-staging the text, not by these stores.)
-template <class CP>
-__device__ __forceinline__ void emit_line(CP s, const VcfEmitRec& E, size_t li,
-                                          uint64_t r, uint64_t h, uint8_t* __restrict__ chrom,
-                                          uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
-                                          uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
-                                          uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap,
-                                          uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
-    const uint32_t rend = E.alt0 - 1;
-    const uint32_t aend = E.aend;
-    const CP ref = s + E.ref0;
-    const uint32_t rlen = rend - E.ref0;
-    const CP alt = s + E.alt0;
-    const uint32_t an = aend - E.alt0;
-    const uint8_t cc = uint8_t(E.start_chrom >> 56);
-    // ALTs found with SWAR comma scans; the heap bytes leave through the 8-byte
-    // register sink (this lane's records are contiguous in the heap)
-    Out<true> hs(heap, h);
-    uint32_t ai = 0;
-    for (uint32_t a0 = 0; a0 <= an; ++ai) {
-      const uint32_t a1 = a0 + swar_find(alt + a0, an - a0, [](uint64_t x) { return bytes_eq_mask(x, ','); });
-      const uint32_t al = a1 - a0;
-      if (!(al == 1 && alt[a0] == '.')) {
-        chrom[r] = cc;
-        pos[r] = E.pos;
-        allele_off[r] = h;
-        ref_len[r] = rlen;
-        alt_len[r] = al;
-        ext_id[r] = E.ext_id;
-        rec_line[r] = uint32_t(li);
-        rec_alt[r] = ai;
-        hs.bytes(ref, rlen);
-        hs.bytes(alt + a0, al);
-        h += rlen + al;
-        ++r;
-      }
-      a0 = a1 + 1;
-    }
-    hs.finish();
-}
-
-constexpr uint64_t kStartMask = (uint64_t(1) << 56) - 1;  // VcfEmitRec.start_chrom: the line start
-
-// k_vcf_parse_emit's outputs and look-back state (unused by the plain window parse)
-struct VcfFuse {
-  unsigned long long* status;  // two words per window (records, heap bytes): flag << 62 | value
-  uint32_t* ticket;
-  uint32_t n_win;
-  uint64_t rec_cap, heap_cap;
-  VcfEmitRec* spill;  // per line: the emit records of windows of more than kBlock lines
-  uint8_t* chrom;
-  uint32_t* pos;
-  uint64_t* allele_off;
-  uint32_t* ref_len;
-  uint32_t* alt_len;
-  uint64_t* ext_id;
-  uint8_t* heap;
-  uint32_t* rec_line;
-  uint32_t* rec_alt;
-};
-
-// The look-back of k_vcf_parse_emit: window wid publishes its record / heap totals,
-// sums the totals of the windows before it back to the nearest one that has
-// published its inclusive prefix, then publishes its own.  Each status word is an
-// 8-byte {flag, value} granule written whole by one agent-scope store and read by
-// agent-scope loads (sc1: no fence needed for a granule, MI355X_MICROARCH.md); a
-// window's two words are taken only when both carry the same flag.  Windows take
-// their index from a ticket in launch order, so every window waited on has started,
-// and publishes its totals before it waits on anything.  One wave runs it; a poll
-// that never sees its word (not expected) gives up after kLbSpinCap tries with a
-// zero value instead of hanging.
-constexpr uint64_t kLbAgg = uint64_t(1) << 62, kLbInc = uint64_t(2) << 62, kLbVal = kLbAgg - 1;
-constexpr uint32_t kLbSpinCap = 1u << 16;
-__device__ __forceinline__ void lb_store(unsigned long long* p, uint64_t v) {
-  __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t lb_load(unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __noinline__ void window_lookback(unsigned long long* status, uint32_t wid, uint64_t agg_r, uint64_t agg_h,
-                                             uint64_t* excl_r, uint64_t* excl_h) {
-  const uint32_t lane = __lane_id();
-  if (lane == 0) {
-    lb_store(status + 2 * size_t(wid), kLbAgg | agg_r);
-    lb_store(status + 2 * size_t(wid) + 1, kLbAgg | agg_h);
-  }
-  uint64_t er = 0, eh = 0;
-  for (int64_t p = int64_t(wid) - 1; p >= 0; p -= kWave) {
-    const int64_t q = p - int64_t(lane);
-    uint64_t sr = 0, sh = 0;
-    if (q >= 0) {
-      for (uint32_t spin = 0;; ++spin) {
-        sr = lb_load(status + 2 * size_t(q));
-        sh = lb_load(status + 2 * size_t(q) + 1);
-        if ((sr >> 62) && (sr >> 62) == (sh >> 62)) break;
-        if (spin == kLbSpinCap) {
-          sr = sh = kLbInc;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    const uint64_t inc = __ballot(q >= 0 && (sr >> 62) == 2);
-    const uint32_t stop = inc ? uint32_t(__ffsll((unsigned long long)inc)) - 1 : uint32_t(kWave);
-    const bool take = q >= 0 && lane <= stop;
-    er += wave_sum64(take ? (sr & kLbVal) : 0ull);
-    eh += wave_sum64(take ? (sh & kLbVal) : 0ull);
-    if (inc) break;
-  }
-  if (lane == 0) {
-    lb_store(status + 2 * size_t(wid), kLbInc | (er + agg_r));
-    lb_store(status + 2 * size_t(wid) + 1, kLbInc | (eh + agg_h));
-  }
-  *excl_r = er;
-  *excl_h = eh;
-}
-
-__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, uint32_t d) {
-  return (uint64_t(uint32_t(__shfl_up(uint32_t(v >> 32), d, kWave))) << 32) | uint32_t(__shfl_up(uint32_t(v), d, kWave));
-}
-// exclusive block scan of two u64 per thread (kBlock threads): *xa / *xb, totals *ta / *tb
-__device__ __forceinline__ void block_excl64x2(uint64_t a, uint64_t b, uint64_t* s, uint64_t* xa, uint64_t* xb,
-                                               uint64_t* ta, uint64_t* tb) {
-  const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
-  uint64_t ia = a, ib = b;
-#pragma unroll
-  for (uint32_t d = 1; d < uint32_t(kWave); d <<= 1) {
-    const uint64_t ua = shfl_up64(ia, d), ub = shfl_up64(ib, d);
-    if (lane >= d) {
-      ia += ua;
-      ib += ub;
-    }
-  }
-  if (lane == kWave - 1) {
-    s[2 * wv] = ia;
-    s[2 * wv + 1] = ib;
-  }
-  __syncthreads();
-  uint64_t ba = 0, bb = 0, sa = 0, sb = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < kVcfWaves; ++w) {
-    const uint64_t x = s[2 * w], y = s[2 * w + 1];
-    if (w < wv) {
-      ba += x;
-      bb += y;
-    }
-    sa += x;
-    sb += y;
-  }
-  __syncthreads();
-  *xa = ba + ia - a;
-  *xb = bb + ib - b;
-  *ta = sa;
-  *tb = sb;
-}
-
-// FUSED (k_vcf_parse_emit, avdb_vcf_parse_emit): no line table or emit records;
-// after its parse rounds the workgroup publishes its window's record / heap totals,
-// takes its offsets from the windows before it (window_lookback) and emits its
-// lines' records and allele bytes from the text still staged in LDS, writing
-// rec_cnt / heap_cnt as the exclusive offsets.  Windows are taken in ticket order.
-#ifndef AVDB_VCF_FUSED_WAVES
-#define AVDB_VCF_FUSED_WAVES 4  // launch-bounds minimum waves per SIMD of k_vcf_parse_emit (A/B knob)
-#endif
-template <bool FUSED>
-__global__ __launch_bounds__(kBlock, FUSED ? AVDB_VCF_FUSED_WAVES : AVDB_VCF_PARSE_WAVES) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
+__global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
                                                               size_t n_lines,
                                                               const unsigned long long* __restrict__ blk_off,
                                                               const uint32_t* __restrict__ wave_cnt,
@@ -640,37 +473,26 @@ __global__ __launch_bounds__(kBlock, FUSED ? AVDB_VCF_FUSED_WAVES : AVDB_VCF_PAR
                                                               VcfEmitRec* __restrict__ erec,
                                                               unsigned long long* __restrict__ rec_cnt,
                                                               unsigned long long* __restrict__ heap_cnt,
-                                                              ChromMapView cm, uint32_t min_fields, VcfFuse F) {
+                                                              ChromMapView cm, uint32_t min_fields) {
   __shared__ u32x4 s_text[kParseStage64 / 16];
   __shared__ uint64_t s_tab[kParseStage64 / 64];  // tab bitmap of the staged bytes
   __shared__ uint32_t s_start[kBlock + 1];  // line starts of the round, relative to the window start
   __shared__ uint64_t s_rs[kBlock];         // the round's INFO refSNP results (info_rs_staged)
   __shared__ uint32_t s_w[kVcfWaves];
   __shared__ uint32_t s_tail;               // (first '\n' at or after w1 - 1) + 1 - w0
-  __shared__ uint64_t s_sum[2 * kVcfWaves];  // FUSED: per-wave totals / scan sums
-  __shared__ uint64_t s_base[2];             // FUSED: the window's first record / heap offset
-  __shared__ uint32_t s_wid;
   const Heap h = make_heap(text, text_bytes);
   const size_t nb = text_bytes;
   const uint32_t tid = threadIdx.x, lane = __lane_id(), wv = tid / kWave;
-  uint32_t wid = blockIdx.x;
-  if constexpr (FUSED) {  // windows in launch order: every window waited on has started
-    if (tid == 0) s_wid = atomicAdd(F.ticket, 1u);
-    __syncthreads();
-    wid = s_wid;
-  }
-  const size_t gw = wid / wps;
-  const uint32_t wk = wid % wps;
+  const size_t gw = blockIdx.x / wps;
+  const uint32_t wk = blockIdx.x % wps;
   size_t t0, t1;
   wave_range(nb, gw, &t0, &t1);
-  size_t w0 = t0 + size_t(wk) * kParseWin;
-  const bool empty = w0 >= t1;  // (uniform)
-  if (!FUSED && empty) return;
-  if (empty) w0 = t1;
+  const size_t w0 = t0 + size_t(wk) * kParseWin;
+  if (w0 >= t1) return;  // (uniform)
   const size_t w1 = w0 + kParseWin < t1 ? w0 + kParseWin : t1;
   // lines starting before w0: 1 + the newlines in [0, w0 - 1)
   size_t li0 = 0;
-  if (w0 && !empty) {
+  if (w0) {
     unsigned long long k = blk_off[gw / kVcfWaves];
     for (size_t w = (gw / kVcfWaves) * kVcfWaves; w < gw; ++w) k += wave_cnt[w];
     for (uint32_t j = 0; j < wk; ++j) k += win_cnt[gw * wps + j];
@@ -681,12 +503,12 @@ __global__ __launch_bounds__(kBlock, FUSED ? AVDB_VCF_FUSED_WAVES : AVDB_VCF_PAR
   // ---- stage [q0, w1 + kParseOver) ----
   const uintptr_t a0 = (h.lo + q0) & ~uintptr_t(15);
   const uintptr_t wend = h.lo + (w1 + kParseOver < nb ? w1 + kParseOver : nb);
-  const uint32_t n16 = empty ? 0u : uint32_t((wend - a0 + 15) / 16);
+  const uint32_t n16 = uint32_t((wend - a0 + 15) / 16);
   stage_copy<(kParseStage64 / 16 + kBlock - 1) / kBlock, kBlock>(s_text, a0, n16, h);
   __syncthreads();
   // ---- newline bitmaps of [q0, w1 - 1); the tab bitmap of the whole stage ----
   const uint32_t o_lo = uint32_t(h.lo + q0 - a0), o_hi = uint32_t(h.lo + w1 - 1 - a0);
-  const uint32_t nblk = !empty && w1 - 1 > q0 ? (o_hi + 63) / 64 : 0u;
+  const uint32_t nblk = w1 - 1 > q0 ? (o_hi + 63) / 64 : 0u;
   const uint32_t nstage = (16 * n16 + 63) / 64;
   uint64_t bm[2] = {0, 0};
   uint32_t cnt = 0;
@@ -712,11 +534,11 @@ __global__ __launch_bounds__(kBlock, FUSED ? AVDB_VCF_FUSED_WAVES : AVDB_VCF_PAR
   }
   uint32_t T;
   const uint32_t pref = block_excl32(cnt, s_w, &T);
-  const uint32_t first = w0 == 0 && !empty ? 1u : 0u;  // line 0 starts at byte 0
+  const uint32_t first = w0 == 0 ? 1u : 0u;  // line 0 starts at byte 0
   T += first;
-  if (!FUSED && !T) return;  // (uniform; no line starts here)
+  if (!T) return;  // (uniform; no line starts here)
   // ---- the end of the window's last line: first '\n' at or after w1 - 1 ----
-  if (wv == 0 && T) {
+  if (wv == 0) {
     size_t q = w1 - 1;
     uint32_t found = 0;
     const uint32_t ob = uint32_t(h.lo + q - a0), oe = uint32_t(wend - a0);
@@ -749,10 +571,6 @@ __global__ __launch_bounds__(kBlock, FUSED ? AVDB_VCF_FUSED_WAVES : AVDB_VCF_PAR
   }
   // ---- parse: rounds of kBlock lines ----
   const uint32_t rounds = (T + kBlock - 1) / kBlock;
-  // FUSED: a one-round window keeps its lines' emit records in registers; a longer
-  // one spills them (and the counts, in rec_cnt / heap_cnt) per line
-  VcfEmitRec E{};
-  uint64_t my_r = 0, my_h = 0, acc_r = 0, acc_h = 0;
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint32_t lo = kBlock * r, hi = lo + kBlock;
     if (r == 0 && first && tid == 0) s_start[0] = 0;
@@ -828,92 +646,55 @@ __global__ __launch_bounds__(kBlock, FUSED ? AVDB_VCF_FUSED_WAVES : AVDB_VCF_PAR
           else L.ext_id = rs & (kRsFound - 1);
         }
       }
-      if constexpr (FUSED) {
-        acc_r += recs;
-        acc_h += hbytes;
-        if (rounds == 1) {
-          E = emit_rec(L);
-          my_r = recs;
-          my_h = hbytes;
-        } else {
-          F.spill[li] = emit_rec(L);
-          rec_cnt[li] = recs;
-          heap_cnt[li] = hbytes;
-        }
-      } else {
-        put_line(lines, erec, li, L);
-        rec_cnt[li] = recs;
-        heap_cnt[li] = hbytes;
-      }
+      put_line(lines, erec, li, L);
+      rec_cnt[li] = recs;
+      heap_cnt[li] = hbytes;
     }
     __syncthreads();  // s_start is refilled by the next round
   }
-  if constexpr (FUSED) {
-    // ---- the window's offsets: its totals published, its predecessors' summed ----
-    {
-      const uint64_t wr = wave_sum64(acc_r), wh = wave_sum64(acc_h);
-      if (lane == 0) {
-        s_sum[2 * wv] = wr;
-        s_sum[2 * wv + 1] = wh;
+}
+
+// (Rendering the allele heap through an LDS image of the tile's heap span with a
+// coalesced flush, as K7 does for its text, measured slower: 0.66 vs 0.60 ms for
+// 8.4 M lines — the pass is bound by re-staging the text, not by these stores.)
+template <class CP>
+__device__ __forceinline__ void emit_line(CP s, const VcfEmitRec& E, size_t li,
+                                          uint64_t r, uint64_t h, uint8_t* __restrict__ chrom,
+                                          uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off,
+                                          uint32_t* __restrict__ ref_len, uint32_t* __restrict__ alt_len,
+                                          uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap,
+                                          uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
+    const uint32_t rend = E.alt0 - 1;
+    const uint32_t aend = E.aend;
+    const CP ref = s + E.ref0;
+    const uint32_t rlen = rend - E.ref0;
+    const CP alt = s + E.alt0;
+    const uint32_t an = aend - E.alt0;
+    const uint8_t cc = uint8_t(E.start_chrom >> 56);
+    // ALTs found with SWAR comma scans; the heap bytes leave through the 8-byte
+    // register sink (this lane's records are contiguous in the heap)
+    Out<true> hs(heap, h);
+    uint32_t ai = 0;
+    for (uint32_t a0 = 0; a0 <= an; ++ai) {
+      const uint32_t a1 = a0 + swar_find(alt + a0, an - a0, [](uint64_t x) { return bytes_eq_mask(x, ','); });
+      const uint32_t al = a1 - a0;
+      if (!(al == 1 && alt[a0] == '.')) {
+        chrom[r] = cc;
+        pos[r] = E.pos;
+        allele_off[r] = h;
+        ref_len[r] = rlen;
+        alt_len[r] = al;
+        ext_id[r] = E.ext_id;
+        rec_line[r] = uint32_t(li);
+        rec_alt[r] = ai;
+        hs.bytes(ref, rlen);
+        hs.bytes(alt + a0, al);
+        h += rlen + al;
+        ++r;
       }
+      a0 = a1 + 1;
     }
-    __syncthreads();
-    if (wv == 0) {
-      uint64_t ar = 0, ah = 0, er, eh;
-#pragma unroll
-      for (uint32_t w = 0; w < kVcfWaves; ++w) {
-        ar += s_sum[2 * w];
-        ah += s_sum[2 * w + 1];
-      }
-      window_lookback(F.status, wid, ar, ah, &er, &eh);
-      if (lane == 0) {
-        s_base[0] = er;
-        s_base[1] = eh;
-        if (wid == F.n_win - 1) {  // the last window: the totals
-          rec_cnt[n_lines] = er + ar;
-          heap_cnt[n_lines] = eh + ah;
-        }
-      }
-    }
-    __syncthreads();
-    // ---- emit: each line's records and allele bytes from the staged text ----
-    uint64_t rb = s_base[0], hb = s_base[1];
-    for (uint32_t r = 0; r < rounds; ++r) {
-      const uint32_t lo = kBlock * r;
-      const size_t li = li0 + lo + tid;
-      const bool live = lo + tid < T && li < n_lines;
-      uint64_t nr = 0, nh = 0;
-      VcfEmitRec Er = E;
-      if (live) {
-        if (rounds == 1) {
-          nr = my_r;
-          nh = my_h;
-        } else {
-          Er = F.spill[li];
-          nr = rec_cnt[li];
-          nh = heap_cnt[li];
-        }
-      }
-      uint64_t xr, xh, tr, th;
-      block_excl64x2(nr, nh, s_sum, &xr, &xh, &tr, &th);
-      const uint64_t r0 = rb + xr, h0 = hb + xh;
-      if (live) {
-        rec_cnt[li] = r0;
-        heap_cnt[li] = h0;
-        if (nr && r0 + nr <= F.rec_cap && h0 + nh <= F.heap_cap) {
-          const size_t st = Er.start_chrom & kStartMask;
-          if (h.lo + st + Er.aend <= wend)
-            emit_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + st - a0)), Er, li, r0, h0, F.chrom,
-                      F.pos, F.allele_off, F.ref_len, F.alt_len, F.ext_id, F.heap, F.rec_line, F.rec_alt);
-          else
-            emit_line((glb_cp)(text + st), Er, li, r0, h0, F.chrom, F.pos, F.allele_off, F.ref_len, F.alt_len,
-                      F.ext_id, F.heap, F.rec_line, F.rec_alt);
-        }
-      }
-      rb += tr;
-      hb += th;
-    }
-  }
+    hs.finish();
 }
 
 // EMIT_LINES lines per workgroup (one thread each), their text staged in an LDS
@@ -944,6 +725,7 @@ __global__ __launch_bounds__(kEmitLines) void k_vcf_emit(
     uint32_t* __restrict__ rec_alt) {
   __shared__ u32x4 s_text[kEmitStage / 16];
   const Heap h = make_heap(text, text_bytes);
+  constexpr uint64_t kStartMask = (uint64_t(1) << 56) - 1;
   for (size_t base = size_t(blockIdx.x) * kEmitLines; base < n_lines; base += size_t(gridDim.x) * kEmitLines) {
     const size_t last = base + kEmitLines < n_lines ? base + kEmitLines : n_lines;
     // the window only has to reach the end of the last line's ALT field
@@ -1025,19 +807,11 @@ static VcfEmitRec* emit_recs_of(void* workspace, size_t text_bytes, size_t n_lin
                                        ((8 * n_lines + 255) & ~size_t(255)) + scan_temp_bytes(n_lines + 1));
 }
 
-static size_t n_windows(size_t text_bytes) { return size_t(kVcfGrid) * kVcfWaves * windows_per_chunk(text_bytes); }
-
-// avdb_vcf_parse_emit's look-back words (two per window) and ticket, after the emit records
-static unsigned long long* lookback_of(void* workspace, size_t text_bytes, size_t n_lines) {
-  char* e = reinterpret_cast<char*>(emit_recs_of(workspace, text_bytes, n_lines));
-  return reinterpret_cast<unsigned long long*>(e + ((sizeof(VcfEmitRec) * n_lines + 255) & ~size_t(255)));
-}
-
 extern "C" int avdb_vcf_workspace_size(size_t text_bytes, size_t n_lines, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
-  // count workspace (for a recount) | line starts | scan temp | emit records | look-back words + ticket
+  // count workspace (for a recount) | line starts | scan temp | emit records
   *bytes = count_ws_full(text_bytes) + ((8 * n_lines + 255) & ~size_t(255)) + scan_temp_bytes(n_lines + 1) +
-           ((sizeof(VcfEmitRec) * n_lines + 255) & ~size_t(255)) + 16 * n_windows(text_bytes) + 256;
+           sizeof(VcfEmitRec) * n_lines + 256;
   return AVDB_OK;
 }
 
@@ -1111,10 +885,10 @@ static int parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, si
   const auto* wave = reinterpret_cast<const uint32_t*>(cw + kCountWsWave);
   if (windows) {  // one workgroup per parse window, line starts found in it
     const uint32_t wps = windows_per_chunk(text_bytes);
-    hipLaunchKernelGGL(k_vcf_parse_windows<false>, dim3(unsigned(size_t(kVcfGrid) * kVcfWaves * wps)), dim3(kBlock), 0,
-                       s, text, text_bytes, n_lines, blk, wave,
+    hipLaunchKernelGGL(k_vcf_parse_windows, dim3(unsigned(size_t(kVcfGrid) * kVcfWaves * wps)), dim3(kBlock), 0, s,
+                       text, text_bytes, n_lines, blk, wave,
                        reinterpret_cast<const uint32_t*>(cw + AVDB_VCF_COUNT_WORKSPACE_BYTES), wps, lines, erec, rc,
-                       hc, cm, min_fields, VcfFuse{});
+                       hc, cm, min_fields);
     AVDB_LAUNCH_CHECK("k_vcf_parse_windows");
   } else {  // the line-starts pass, then 256 lines per workgroup
     hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk, wave, n_lines, starts);
@@ -1197,64 +971,6 @@ extern "C" int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_
   return emit_impl(ctx, text, text_bytes, n_lines, nullptr,
                    emit_recs_of(const_cast<void*>(parse_workspace), text_bytes, n_lines), rec_off, heap_off, chrom,
                    pos, allele_off, ref_len, alt_len, ext_id, heap, rec_line, rec_alt, stream);
-}
-
-extern "C" int avdb_vcf_parse_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
-                                   const void* line_counts, size_t line_counts_bytes, void* workspace,
-                                   size_t workspace_bytes, uint64_t* rec_off, uint64_t* heap_off, size_t rec_cap,
-                                   size_t heap_cap, uint8_t* chrom, uint32_t* pos, uint64_t* allele_off,
-                                   uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap,
-                                   uint32_t* rec_line, uint32_t* rec_alt, const avdb_vcf_opts* opts, void* stream) {
-  if (!ctx || !rec_off || !heap_off || (rec_cap && (!chrom || !pos || !allele_off || !ref_len || !alt_len || !ext_id ||
-                                                    !rec_line || !rec_alt)) || (heap_cap && !heap)) {
-    avdb_set_error("avdb_vcf_parse_emit: null argument");
-    return AVDB_EINVAL;
-  }
-  if (opts && opts->struct_size != sizeof(avdb_vcf_opts)) {
-    avdb_set_error("avdb_vcf_parse_emit: avdb_vcf_opts.struct_size %u, this library expects %zu", opts->struct_size,
-                   sizeof(avdb_vcf_opts));
-    return AVDB_EINVAL;
-  }
-  if (opts && opts->chrom_map && opts->chrom_map->device != ctx->device) {
-    avdb_set_error("avdb_vcf_parse_emit: chromosome map made for device %d", opts->chrom_map->device);
-    return AVDB_EINVAL;
-  }
-  const ChromMapView cm = opts && opts->chrom_map ? opts->chrom_map->dev : ChromMapView{};
-  const uint32_t min_fields = opts ? opts->min_fields : 0u;
-  size_t need = 0;
-  avdb_vcf_workspace_size(text_bytes, n_lines, &need);
-  if (!workspace || workspace_bytes < need) {
-    avdb_set_error("avdb_vcf_parse_emit: workspace of %zu bytes required", need);
-    return AVDB_ERANGE;
-  }
-  AVDB_HIP_TRY(hipSetDevice(ctx->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (n_lines == 0) {
-    AVDB_HIP_TRY(hipMemsetAsync(rec_off, 0, 8, s));
-    AVDB_HIP_TRY(hipMemsetAsync(heap_off, 0, 8, s));
-    return AVDB_OK;
-  }
-  const size_t cw_full = count_ws_full(text_bytes);
-  const char* cw = static_cast<const char*>(line_counts);
-  if (!cw || line_counts_bytes < cw_full) {  // the windows' newline counts: recount into this workspace
-    const int rc = count_pass(text, text_bytes, workspace, nullptr, s, true);
-    if (rc != AVDB_OK) return rc;
-    cw = static_cast<const char*>(workspace);
-  }
-  const size_t nw = n_windows(text_bytes);
-  unsigned long long* lb = lookback_of(workspace, text_bytes, n_lines);
-  AVDB_HIP_TRY(hipMemsetAsync(lb, 0, 16 * nw + 16, s));  // look-back words + ticket
-  VcfFuse F{lb, reinterpret_cast<uint32_t*>(lb + 2 * nw), uint32_t(nw), rec_cap, heap_cap,
-            emit_recs_of(workspace, text_bytes, n_lines), chrom, pos, allele_off, ref_len, alt_len, ext_id, heap,
-            rec_line, rec_alt};
-  hipLaunchKernelGGL(k_vcf_parse_windows<true>, dim3(unsigned(nw)), dim3(kBlock), 0, s, text, text_bytes, n_lines,
-                     reinterpret_cast<const unsigned long long*>(cw + kCountWsBlkOff),
-                     reinterpret_cast<const uint32_t*>(cw + kCountWsWave),
-                     reinterpret_cast<const uint32_t*>(cw + AVDB_VCF_COUNT_WORKSPACE_BYTES),
-                     windows_per_chunk(text_bytes), nullptr, nullptr, reinterpret_cast<unsigned long long*>(rec_off),
-                     reinterpret_cast<unsigned long long*>(heap_off), cm, min_fields, F);
-  AVDB_LAUNCH_CHECK("k_vcf_parse_emit");
-  return AVDB_OK;
 }
 
 // ---- chromosome map (ChromosomeMap.get, chromosome_map_parser.py:84-91) ----------

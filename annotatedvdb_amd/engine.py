@@ -827,17 +827,13 @@ class Engine:
         return [raw[i * 32:(i + 1) * 32].decode("ascii") for i in range(n)]
 
     # -- K0: VCF text -> records ---------------------------------------------
-    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None, want_lines: bool = True,
-                     caps: Optional[Tuple[int, int]] = None) -> "VcfBatch":
+    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None, want_lines: bool = True) -> "VcfBatch":
         """Parse VCF data lines (bytes or a uint8 tensor) on the GPU into the
         record SoA (one row per ALT != '.') plus the per-line table.
         ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map.
-        ``want_lines=False``: no public line table (``VcfBatch.lines`` is None) —
-        for callers that need only the records: parse and emit run as one launch
-        (``avdb_vcf_parse_emit``) into outputs sized by an estimate (``caps`` =
-        records, heap bytes; default 1.5 records per line and the text size), and
-        only a batch that exceeds it runs the two-launch path (parse, then emit from
-        32-byte records in the parse workspace) with exact sizes."""
+        ``want_lines=False``: no public line table (``VcfBatch.lines`` is None; the
+        emit reads 32-byte records from the parse workspace instead of the 80-byte
+        table) — for callers that need only the records."""
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
             t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
@@ -870,32 +866,21 @@ class Engine:
         lines = self.empty(max(1, n_lines) * VCF_LINE_DTYPE.itemsize, torch.uint8) if want_lines else None
         rec_off = self.empty(n_lines + 1, torch.int64)
         heap_off = self.empty(n_lines + 1, torch.int64)
-        opts_p = ctypes.byref(vcf_opts) if vcf_opts is not None else None
-        if not want_lines and n_lines:
-            rec_cap, heap_cap = caps if caps is not None else (n_lines + n_lines // 2 + 64, nb + 64)
-            b, rec_line, rec_alt = self._record_outputs(rec_cap, heap_cap)
-            N.check("avdb_vcf_parse_emit", self.lib.avdb_vcf_parse_emit(
-                self.ctx, tp, nb, n_lines, N.ptr(ws0), ws0.numel(), N.ptr(ws), ws.numel(), N.ptr(rec_off),
-                N.ptr(heap_off), rec_cap, heap_cap, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off),
-                N.ptr(b.ref_len), N.ptr(b.alt_len), N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt),
-                opts_p, s))
-            n_rec, n_heap = (int(x) for x in torch.stack([rec_off[n_lines], heap_off[n_lines]]).cpu().tolist())
-            if n_rec <= rec_cap and n_heap <= heap_cap:
-                b = RecordBatch(chrom=b.chrom[:n_rec], pos=b.pos[:n_rec], allele_off=b.allele_off[:n_rec],
-                                ref_len=b.ref_len[:n_rec], alt_len=b.alt_len[:n_rec], heap=b.heap[:max(1, n_heap)],
-                                ext_id=b.ext_id[:n_rec])
-                return VcfBatch(text=text_t, n_lines=n_lines, lines=None, rec_off=rec_off, heap_off=heap_off,
-                                records=b, rec_line=rec_line[:n_rec], rec_alt=rec_alt[:n_rec])
-            del b, rec_line, rec_alt  # past the estimate: the two-launch path with exact sizes
         N.check("avdb_vcf_parse_lines2", self.lib.avdb_vcf_parse_lines2(
             self.ctx, tp, nb, n_lines, N.ptr(ws0), ws0.numel(), N.ptr(ws), ws.numel(), N.ptr(lines), N.ptr(rec_off),
-            N.ptr(heap_off), opts_p, s))
+            N.ptr(heap_off), ctypes.byref(vcf_opts) if vcf_opts is not None else None, s))
         if n_lines:
             tot = torch.stack([rec_off[n_lines], heap_off[n_lines]]).cpu().tolist()
         else:
             tot = [0, 0]
         n_rec, n_heap = int(tot[0]), int(tot[1])
-        b, rec_line, rec_alt = self._record_outputs(n_rec, n_heap)
+        b = RecordBatch(chrom=self.empty(n_rec, torch.uint8), pos=self.empty(n_rec, torch.int32),
+                        allele_off=self.empty(n_rec, torch.int64),
+                        ref_len=self.empty(n_rec, torch.int32), alt_len=self.empty(n_rec, torch.int32),
+                        heap=self.empty(max(1, n_heap), torch.uint8),
+                        ext_id=self.empty(n_rec, torch.int64))
+        rec_line = self.empty(n_rec, torch.int32)
+        rec_alt = self.empty(n_rec, torch.int32)
         outs = (N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
                 N.ptr(b.ext_id), N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s)
         if n_rec and want_lines:
@@ -906,15 +891,6 @@ class Engine:
                 self.ctx, tp, nb, n_lines, N.ptr(ws), ws.numel(), N.ptr(rec_off), N.ptr(heap_off), *outs))
         return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
                         records=b, rec_line=rec_line, rec_alt=rec_alt)
-
-    def _record_outputs(self, n_rec: int, n_heap: int):
-        """K0's record SoA, allele heap and back-references for n_rec records."""
-        b = RecordBatch(chrom=self.empty(n_rec, torch.uint8), pos=self.empty(n_rec, torch.int32),
-                        allele_off=self.empty(n_rec, torch.int64),
-                        ref_len=self.empty(n_rec, torch.int32), alt_len=self.empty(n_rec, torch.int32),
-                        heap=self.empty(max(1, n_heap), torch.uint8),
-                        ext_id=self.empty(n_rec, torch.int64))
-        return b, self.empty(n_rec, torch.int32), self.empty(n_rec, torch.int32)
 
     # -- K9: this rank's lines of a VCF text -----------------------------------
     def vcf_select(self, vb: "VcfBatch", assignment, rank: int, cut: int = 64_000_000) -> torch.Tensor:

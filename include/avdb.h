@@ -292,24 +292,6 @@ int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size
                      const uint64_t* heap_off, uint8_t* chrom, uint32_t* pos, uint64_t* allele_off,
                      uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line,
                      uint32_t* rec_alt, void* stream);
-/* K0 in one launch for callers that need only the records (vcf_parser.py:76-169 and
- * the per-ALT explode of vcf_variant_loader.py:273-280, as avdb_vcf_parse_lines2 +
- * avdb_vcf_emit_ws): each parse window's workgroup also emits its lines' records and
- * allele bytes from the text it holds in LDS, its first record / heap offset summed
- * from the windows before it (a look-back over per-window totals kept in
- * `workspace`, windows taken in launch order).  rec_off / heap_off as
- * avdb_vcf_parse_lines2 (exclusive per line, [n_lines] = the totals).  Records
- * past rec_cap and allele bytes past heap_cap are not written: when
- * rec_off[n_lines] > rec_cap or heap_off[n_lines] > heap_cap the caller sizes its
- * outputs from those totals and runs avdb_vcf_parse_lines2 + avdb_vcf_emit_ws.
- * line_counts: a count workspace of avdb_vcf_count_workspace_size bytes (with the
- * window counts), or NULL to recount into `workspace`. */
-int avdb_vcf_parse_emit(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size_t n_lines,
-                        const void* line_counts, size_t line_counts_bytes, void* workspace, size_t workspace_bytes,
-                        uint64_t* rec_off, uint64_t* heap_off, size_t rec_cap, size_t heap_cap, uint8_t* chrom,
-                        uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id,
-                        uint8_t* heap, uint32_t* rec_line, uint32_t* rec_alt, const avdb_vcf_opts* opts,
-                        void* stream);
 
 /* ---- K5: the load driver's text outputs ---------------------------------
  * Replaces the per-alt COPY row assembly of VCFVariantLoader.__parse_alt_alleles

@@ -204,20 +204,13 @@ def test_k0_window_parse_equals_starts_pass(engine, which):
     assert (vb.heap_off[: n0 + 1].cpu().numpy() == ho0).all()
 
 
-@pytest.mark.parametrize("which", ["golden", "dbsnp", "long", "big", "short", "capped"])
+@pytest.mark.parametrize("which", ["golden", "dbsnp", "long", "big", "short"])
 def test_k0_records_without_line_table(engine, which):
-    """vcf_tokenize(want_lines=False) — parse and emit in one launch
-    (avdb_vcf_parse_emit: each window's records emitted from its staged text at
-    offsets from the windows before it) — gives the same record SoA, allele heap,
-    offsets and back-references as the tokenizer with the public line table.
-    "short": 15-byte lines, ~1,600 per window (the multi-round form that spills its
-    emit records); "capped": outputs sized below the totals, so the two-launch
-    path (parse, then avdb_vcf_emit_ws from the parse workspace) runs instead."""
-    caps = None
-    if which == "capped":
-        text = _synth(60000, 83)
-        caps = (1000, 1 << 16)
-    elif which == "short":
+    """vcf_tokenize(want_lines=False) — no public line table, the emit reading its
+    32-byte records from the parse workspace (avdb_vcf_emit_ws) — gives the same
+    record SoA, allele heap, offsets and back-references as the tokenizer with the
+    table.  "short": 15-byte lines, ~1,600 per parse window (several rounds)."""
+    if which == "short":
         text = b"".join(b"%d\t%d\t.\tA\tG\t.\t.\t.\n" % (1 + i % 9, 10 + i % 90) for i in range(300000))
     elif which == "golden":
         text = _golden_text()
@@ -231,7 +224,7 @@ def test_k0_records_without_line_table(engine, which):
         tile = _synth(60000, 79).split(b"\n")[:-1]
         text = b"\n".join(tile * 25) + b"\n"
     a = engine.vcf_tokenize(text)
-    b = engine.vcf_tokenize(text, want_lines=False, caps=caps)
+    b = engine.vcf_tokenize(text, want_lines=False)
     assert b.lines is None and a.n_lines == b.n_lines and a.records.n == b.records.n
     assert torch.equal(a.rec_off, b.rec_off) and torch.equal(a.heap_off, b.heap_off)
     for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "ext_id", "heap"):
