@@ -44,6 +44,11 @@ LAYOUTS = ("serial", "fork", "overlap")
 # what bench.py times for C4k (AVDB_BENCH_LAYOUT overrides there) and what
 # tests/test_gpu_c4k.py checks over the whole 1e9-record job
 C4K_LAYOUT = "serial"
+# what bench.py times for C1 (captured as one HIP graph) and what
+# tests/test_gpu_c1.py replays: on this round's boxes the graph with K3 on a
+# parallel branch replays slower than the one-stream graph (0.112 vs 0.097 ms per
+# step; plain launches of the fork 0.099 ms), profiles/c1_ab/r05_layout_graph_ab.log
+C1_LAYOUT = "serial"
 
 
 class KeyedStep:

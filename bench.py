@@ -671,14 +671,14 @@ def run_workload(a, name, ri, dev, cpu):
         evs.setdefault(stage, []).append((e0, e1))
 
     # C1 / C4k: the keyed record-prep step (annotatedvdb_amd.pipeline.KeyedStep, the
-    # object the parity tests run).  C1 (K2, K3, K7; no long records) takes the "fork"
-    # layout: K3 on a second stream beside K7, which inside the HIP graph is a parallel
-    # branch (0.098 -> 0.092 ms per step).  C4k takes AVDB_BENCH_LAYOUT (serial | fork |
-    # overlap: K7 beside K4 with the digests filled afterwards), default below.
+    # object the parity tests run), in the layouts pipeline.C1_LAYOUT / C4K_LAYOUT name
+    # (C1: K2, K3, K7, no long records, captured as one HIP graph).  AVDB_BENCH_LAYOUT
+    # (serial | fork: K3 on a second stream beside K7 | overlap: K7 beside K4 with the
+    # digests filled afterwards) overrides either for an A/B.
     ks = None
     if name in ("c1", "c4k"):
-        from annotatedvdb_amd.pipeline import C4K_LAYOUT, KeyedStep
-        layout = "fork" if name == "c1" else os.environ.get("AVDB_BENCH_LAYOUT", C4K_LAYOUT)
+        from annotatedvdb_amd.pipeline import C1_LAYOUT, C4K_LAYOUT, KeyedStep
+        layout = os.environ.get("AVDB_BENCH_LAYOUT", C1_LAYOUT if name == "c1" else C4K_LAYOUT)
         ks = KeyedStep(eng, batch, digests=name == "c4k", layout=layout, hist=hist, counters=ctr,
                        k4_grid=int(os.environ.get("AVDB_BENCH_K4_GRID", "0")),
                        k7_grid=int(os.environ.get("AVDB_BENCH_K7_GRID", "0")))

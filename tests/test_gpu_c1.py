@@ -473,10 +473,11 @@ def test_keyed_record_prep_marks_for_k3(engine, n, dup):
     assert torch.equal(engine.pk_dedup(c, grouped=True, workspace=ws)[:n], engine.pk_dedup(c, grouped=True)[:n])
 
 
-def test_c1_graph_replay_vs_c_oracle(engine):
+@pytest.mark.parametrize("layout", ["serial", "fork"])
+def test_c1_graph_replay_vs_c_oracle(engine, layout):
     """The step bench.py times for C1, as it times it: ``pipeline.KeyedStep`` in
-    the "fork" layout (K3 on a second stream beside K7) captured once as a HIP
-    graph and replayed.  Every buffer is a sentinel before the capture, and the
+    the bench's layout (``pipeline.C1_LAYOUT``; and "fork": K3 on a second stream
+    beside K7) captured once as a HIP graph and replayed.  Every buffer is a sentinel before the capture, and the
     text buffers and outputs are poisoned again between replays; after each
     replay end / bin / status / keep and every key, path, offset and state are
     bit-exact vs the C oracle."""
@@ -490,7 +491,7 @@ def test_c1_graph_replay_vs_c_oracle(engine):
     exp_paths = paths_of(h["chrom"], rc)
     engine.poison = 0xA5
     try:
-        ks = KeyedStep(engine, b, digests=False, layout="fork", hist=engine.new_histogram(),
+        ks = KeyedStep(engine, b, digests=False, layout=layout, hist=engine.new_histogram(),
                        counters=engine.new_counters())
         ks.run()  # warm-up step (the bench's warmup)
         torch.cuda.synchronize()
