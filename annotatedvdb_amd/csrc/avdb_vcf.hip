@@ -373,6 +373,31 @@ __device__ __forceinline__ void stage16(lds_cp64 lw, uint32_t p, uint32_t end, u
 // entry), kRsFound | the number, or kRsFound | kRsHost (a value the reference
 // coerces to something other than rs<int>).
 constexpr uint64_t kRsFound = uint64_t(1) << 62, kRsHost = uint64_t(1) << 63;
+// an "RS=" entry's value, stage bytes [vs, next ';' or B): all digits, 1..18 of
+// them, gives kRsFound | the number; anything else kRsFound | kRsHost
+__device__ __forceinline__ uint64_t info_rs_value(lds_cp64 lw, lds_cp stage, uint32_t vs, uint32_t B) {
+  const uint32_t vmax = B - vs;
+  uint64_t y0, y1, v = 0;
+  bool ok = false;
+  stage16(lw, vs, B, &y0, &y1);
+  const uint64_t nd0 = nondigit_mask(y0), nd1 = nondigit_mask(y1);
+  const uint32_t nd = nd0 ? uint32_t(__builtin_ctzll(nd0)) >> 3 : (nd1 ? 8u + (uint32_t(__builtin_ctzll(nd1)) >> 3) : 16u);
+  if (nd < 16 || vmax <= 16) {
+    const uint32_t n = nd < vmax ? nd : vmax;
+    const bool term = n == vmax || (n < 16 && (((n < 8 ? y0 >> (8 * n) : y1 >> (8 * (n - 8))) & 0xFF) == ';'));
+    if (term && n >= 1) v = decimal16(y0, y1, n, &ok);
+  } else {  // 16 digits and more: the byte loop (<= 18 digits)
+    uint32_t n = 0;
+    while (n < vmax && stage[vs + n] != ';') ++n;
+    ok = n <= 18;
+    for (uint32_t q = 0; ok && q < n; ++q) {
+      ok = is_digit(stage[vs + q]);
+      v = v * 10 + (stage[vs + q] - '0');
+    }
+  }
+  return ok && v >= 1 ? (kRsFound | v) : (kRsFound | kRsHost);
+}
+
 __device__ __noinline__ uint64_t info_rs_staged(lds_cp64 lw, lds_cp stage, uint32_t A, uint32_t B) {
   int32_t at = -1;  // stage offset of the last entry's 'R'
   bool val = false;
@@ -417,28 +442,18 @@ __device__ __noinline__ uint64_t info_rs_staged(lds_cp64 lw, lds_cp stage, uint3
     }
   }
   if (at < 0) return 0;
-  uint64_t v = 0;
-  bool ok = false;
-  if (val) {  // the value [at + 3, next ';' or B): all digits, 1..18 of them
-    const uint32_t vs = uint32_t(at) + 3, vmax = B - vs;
-    stage16(lw, vs, B, &y0, &y1);
-    const uint64_t nd0 = nondigit_mask(y0), nd1 = nondigit_mask(y1);
-    const uint32_t nd = nd0 ? uint32_t(__builtin_ctzll(nd0)) >> 3 : (nd1 ? 8u + (uint32_t(__builtin_ctzll(nd1)) >> 3) : 16u);
-    if (nd < 16 || vmax <= 16) {
-      const uint32_t n = nd < vmax ? nd : vmax;
-      const bool term = n == vmax || (n < 16 && (((n < 8 ? y0 >> (8 * n) : y1 >> (8 * (n - 8))) & 0xFF) == ';'));
-      if (term && n >= 1) v = decimal16(y0, y1, n, &ok);
-    } else {  // 16 digits and more: the byte loop (<= 18 digits)
-      uint32_t n = 0;
-      while (n < vmax && stage[vs + n] != ';') ++n;
-      ok = n <= 18;
-      for (uint32_t q = 0; ok && q < n; ++q) {
-        ok = is_digit(stage[vs + q]);
-        v = v * 10 + (stage[vs + q] - '0');
-      }
-    }
-  }
-  return ok && v >= 1 ? (kRsFound | v) : (kRsFound | kRsHost);
+  return val ? info_rs_value(lw, stage, uint32_t(at) + 3, B) : (kRsFound | kRsHost);
+}
+
+// "RS" entry candidates of the stage, found by the whole workgroup in the bitmap
+// pass: bit j set when word x (nx the next word) holds [';' or tab] 'R' 'S' at
+// bytes j .. j + 2 — a possible "RS" / "RS=..." INFO entry starting at byte j + 1;
+// the byte after it decides the kind when the candidate is placed in its line
+__device__ __forceinline__ uint32_t rs_cand_bits8(uint64_t x, uint64_t nx) {
+  const uint64_t v1 = (x >> 8) | (nx << 56), v2 = (x >> 16) | (nx << 48);
+  const uint64_t m = (bytes_eq_mask(x, ';') | bytes_eq_mask(x, '\t')) & bytes_eq_mask(v1, 'R') &
+                     bytes_eq_mask(v2, 'S');
+  return uint32_t((((m & kHiBits) >> 7) * 0x0102040810204080ull) >> 56);
 }
 
 // exclusive block scan of one u32 per thread (kBlock threads); *total = sum
@@ -479,6 +494,7 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
   __shared__ uint32_t s_start[kBlock + 1];  // line starts of the round, relative to the window start
   __shared__ uint64_t s_rs[kBlock];         // the round's INFO refSNP results (info_rs_staged)
   __shared__ uint32_t s_w[kVcfWaves];
+  __shared__ uint32_t s_wp[kVcfWaves];      // the round's pending INFO scans per wave
   __shared__ uint32_t s_tail;               // (first '\n' at or after w1 - 1) + 1 - w0
   const Heap h = make_heap(text, text_bytes);
   const size_t nb = text_bytes;
@@ -510,20 +526,26 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
   const uint32_t o_lo = uint32_t(h.lo + q0 - a0), o_hi = uint32_t(h.lo + w1 - 1 - a0);
   const uint32_t nblk = w1 - 1 > q0 ? (o_hi + 63) / 64 : 0u;
   const uint32_t nstage = (16 * n16 + 63) / 64;
-  uint64_t bm[2] = {0, 0};
+  uint64_t bm[2] = {0, 0}, rsc[2] = {0, 0};
   uint32_t cnt = 0;
+  uint32_t* s_rsc = reinterpret_cast<uint32_t*>(s_rs);  // the window's "RS" candidate per line (one round)
+  s_rsc[tid] = 0;  // (read after the block scans' barriers)
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const uint32_t b = 2 * tid + k;
     if (b < nstage) {
-      uint64_t m = 0, t = 0;
+      uint64_t m = 0, t = 0, c = 0;
+      uint64_t w = lw[8 * b];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const uint64_t w = lw[8 * b + q];
+        const uint64_t nw = lw[8 * b + q + 1];
         m |= uint64_t(nl_bits8(w)) << (8 * q);
         t |= uint64_t(byte_bits8(w, kTab)) << (8 * q);
+        c |= uint64_t(rs_cand_bits8(w, nw)) << (8 * q);
+        w = nw;
       }
       s_tab[b] = t;
+      rsc[k] = c;
       if (b >= nblk) continue;
       const uint32_t blo = 64 * b;
       if (o_lo > blo) m &= o_lo - blo >= 64 ? 0ull : ~0ull << (o_lo - blo);
@@ -571,6 +593,33 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
   }
   // ---- parse: rounds of kBlock lines ----
   const uint32_t rounds = (T + kBlock - 1) / kBlock;
+  // ---- a one-round window: each line's last "RS" entry candidate (stage offset of
+  // its ';' / tab << 2 | kind: 1 "RS=", 2 bare, 3 resolve by scanning) ----
+  if (rounds == 1) {
+    __syncthreads();  // (s_tail)
+    const uint32_t tail = uint32_t(w0 + s_tail - (a0 - h.lo));  // stage end of the window's last line
+    const lds_cp stage = (lds_cp)(reinterpret_cast<const uint8_t*>(s_text));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint64_t m = rsc[k];
+      while (m) {
+        const uint32_t bit = uint32_t(__builtin_ctzll(m));
+        m &= m - 1;
+        const uint32_t p = 64 * (2 * tid + k) + bit;
+        if (p >= tail) break;
+        const uint64_t below = (uint64_t(1) << bit) - 1;
+        const uint32_t nls = pref + (k ? uint32_t(__popcll(bm[0])) : 0u) + uint32_t(__popcll(bm[k] & below));
+        const int32_t line = int32_t(first + nls) - 1;
+        if (line < 0 || line >= int32_t(T)) continue;
+        // the byte after "RS": '=' an entry with a value, ';' / tab / '\n' a bare one; a
+        // byte below '!' (space, '\r', NUL ...: whitespace rstrip may remove) the line's
+        // own scan decides; anything else ("RSPOS", ...) is no "RS" entry
+        const uint8_t e = stage[p + 3];
+        const uint32_t kind = e == '=' ? 1u : ((e == ';' || e == '\t' || e == '\n') ? 2u : (e < 0x21 ? 3u : 0u));
+        if (kind) atomicMax(&s_rsc[line], (p << 2) | kind);
+      }
+    }
+  }
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint32_t lo = kBlock * r, hi = lo + kBlock;
     if (r == 0 && first && tid == 0) s_start[0] = 0;
@@ -606,8 +655,31 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
         parse_line_with<true>([tb, sp](uint32_t n, avdb_vcf_line& l) { return fields_bits(tb, sp, n, l); },
                               (lds_cp)ls, [lw2](uint32_t k) { return lw2[k]; }, mis, raw, L, recs, hbytes, cm,
                               min_fields);
-        if (L.pad[0] == kInfoPending)  // INFO = stage bytes [sp + field 7, sp + its end)
-          info_item = (sp + L.field[7]) | ((L.field_end8 - L.field[7]) << 15);
+        if (L.pad[0] == kInfoPending) {  // INFO = stage bytes [A, B)
+          const uint32_t A = sp + L.field[7], B = sp + L.field_end8;
+          bool done = false;
+          uint64_t rs = 0;
+          if (rounds == 1) {  // the line's last candidate decides, when it lies in INFO
+            const uint32_t c = s_rsc[tid], q = c >> 2, kind = c & 3u;
+            if (c == 0 || q + 1 < A) {
+              done = true;  // no "RS" entry in INFO
+            } else if (kind != 3u && q + 3 <= B) {
+              rs = kind == 1u ? info_rs_value(lw, (lds_cp)(reinterpret_cast<const uint8_t*>(s_text)), q + 4, B)
+                              : (kRsFound | kRsHost);
+              done = true;
+            }
+          }
+          if (done) {
+            L.pad[0] = 0;
+            if (rs & kRsFound) {
+              L.flags |= AVDB_VCF_INFO_RS;
+              if (rs & kRsHost) L.flags |= AVDB_VCF_EXT_HOST;
+              else L.ext_id = rs & (kRsFound - 1);
+            }
+          } else {  // a later round or a candidate past INFO: the gathered scan
+            info_item = A | ((B - A) << 15);
+          }
+        }
       } else {
         const uintptr_t la = h.lo + L.start - mis;
         parse_line((glb_cp)(text + L.start), [la, h](uint32_t k) { return heap_word(la + 8 * size_t(k), h); }, mis,
@@ -617,25 +689,26 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
     // the round's pending INFO scans, gathered into the first lanes of the workgroup
     // (a wave scans INFO once for its lanes that need it, instead of every wave for
     // the ~40 % of its lines without an rs ID)
-    __syncthreads();  // (s_start and s_w are free: this round's starts are read)
     const uint64_t pend = __ballot(info_item != 0);
-    if (lane == 0) s_w[wv] = uint32_t(__popcll(pend));
-    __syncthreads();
+    if (lane == 0) s_wp[wv] = uint32_t(__popcll(pend));
+    __syncthreads();  // (after it s_start and s_rs are free: this round's starts and candidates are read)
     uint32_t n_pend = 0, slot = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kVcfWaves; ++w) {
-      const uint32_t c = s_w[w];
+      const uint32_t c = s_wp[w];
       if (w < wv) slot += c;
       n_pend += c;
     }
     slot += uint32_t(__popcll(pend & ((uint64_t(1) << lane) - 1)));
-    if (info_item) s_start[slot] = info_item;
-    __syncthreads();
-    if (tid < n_pend) {
-      const uint32_t it = s_start[tid], A = it & 0x7FFFu;
-      s_rs[tid] = info_rs_staged(lw, (lds_cp)(reinterpret_cast<const uint8_t*>(s_text)), A, A + (it >> 15));
+    if (n_pend) {  // (uniform)
+      if (info_item) s_start[slot] = info_item;
+      __syncthreads();
+      if (tid < n_pend) {
+        const uint32_t it = s_start[tid], A = it & 0x7FFFu;
+        s_rs[tid] = info_rs_staged(lw, (lds_cp)(reinterpret_cast<const uint8_t*>(s_text)), A, A + (it >> 15));
+      }
+      __syncthreads();
     }
-    __syncthreads();
     if (live) {
       if (info_item) {
         const uint64_t rs = s_rs[slot];
@@ -650,7 +723,7 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
       rec_cnt[li] = recs;
       heap_cnt[li] = hbytes;
     }
-    __syncthreads();  // s_start is refilled by the next round
+    if (r + 1 < rounds) __syncthreads();  // s_start is refilled by the next round
   }
 }
 

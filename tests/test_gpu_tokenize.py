@@ -232,14 +232,20 @@ def test_k0_records_without_line_table(engine, which):
     assert torch.equal(a.rec_line, b.rec_line) and torch.equal(a.rec_alt, b.rec_alt)
 
 
-def test_k0_info_refsnp_edges(engine):
+@pytest.mark.parametrize("pad", [0, 120])
+def test_k0_info_refsnp_edges(engine, pad):
     """The INFO refSNP scan in K0's staged window parse (the cases of
     test_percall_host.INFO_RS_CASES at eight INFO alignments, plus sample columns
     after INFO, repeated so lines sit at every window position): EXT_HOST exactly
-    where the reference would not give rs<int>, else the record's refSNP key."""
+    where the reference would not give rs<int>, else the record's refSNP key.
+    pad 0: short lines, several parse rounds per window (the gathered INFO scan);
+    pad 120: a FILTER of 120 bytes, one round per window (each line's last "RS"
+    candidate from the workgroup's bitmap pass, the scan only where it cannot
+    decide)."""
     from annotatedvdb_amd.engine import VCF_EXT_HOST, VCF_INFO_RS
     from test_percall_host import info_rs_lines
-    cases = info_rs_lines()
+    cases = [(line.replace("\t.\t.\t", "\t.\t%s\t" % ("F" * pad), 1) if pad else line, w)
+             for line, w in info_rs_lines()]
     # a dbSNP-shaped line between cases shifts the following case by one byte per repeat
     filler = [b"1\t%d\trs1\tA\tG\t.\t.\t%s" % (200 + k, b"Q" * (1 + k % 64)) for k in range(len(cases) * 3)]
     lines, want = [], []
