@@ -812,6 +812,8 @@ __global__ __launch_bounds__(kEmitLines) void k_vcf_emit(
       const avdb_vcf_line& Z = lines[last - 1];
       s1 = Z.start + Z.len;
     }
+    // (reading each line's REF / ALT bytes from global memory instead of staging the
+    // tile's text: 519 vs 349 us, profiles/k0_ab/r05_emit_direct_ab.log)
     const Window w = stage_window<kEmitLines, kEmitStage>(h, s0, s1, s_text);
     const size_t li = base + threadIdx.x;
     if (li < n_lines) {
