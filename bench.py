@@ -70,6 +70,26 @@ WORKLOADS["load"] = dict(
                       "(K0 tokenize, K2 end+bin, K5 display attributes/FREQ/keys/paths as text)",
     bytes_per=None, kernel="k_vcf_format<write>")
 VCF_TILE = 1 << 19  # distinct synthetic lines, tiled on the device to n
+CEILING_LOG = os.path.join(ROOT, "profiles", "r05_hbm_ceiling.log")  # tools/hbm_ceiling.hip on MI355X
+
+
+def stream_ceiling(test: str, pmc_path: str, kernel_ms: float):
+    """A kernel's measured HBM bytes per launch (request-size counters, `pmc_path`) over its time,
+    against the stream rate tools/hbm_ceiling.hip measured for the same read/write mix (mean of the
+    committed runs): how close the kernel is to what HBM delivers for its byte mix, not to the spec."""
+    if not (os.path.exists(CEILING_LOG) and os.path.exists(pmc_path)):
+        return None
+    rates = [json.loads(l)["TBps"] for l in open(CEILING_LOG)
+             if l.startswith("{") and json.loads(l)["test"].startswith(test)]
+    pk = json.load(open(pmc_path))
+    if not rates or "hbm_bytes_per_launch" not in pk:
+        return None
+    ceil = 1e3 * sum(rates) / len(rates)
+    ach = pk["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
+    return {"mix": test, "measured_traffic_GBps": ach, "ceiling_GBps": ceil, "frac": ach / ceil,
+            "read_bytes": pk.get("hbm_read_bytes"), "write_bytes": pk.get("hbm_write_bytes"),
+            "source": "profiles/pmc_k7.json bytes / stage time; ceiling: profiles/r05_hbm_ceiling.log "
+                      "(tools/hbm_ceiling.hip, 16-B grid-stride streams, read:write 1:3)"}
 
 
 def parse():
@@ -913,6 +933,9 @@ def run_workload(a, name, ri, dev, cpu):
                               "bound": "hbm", "achieved": k7_bytes / (k7_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": k7_bytes / (k7_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                               "algorithmic_bytes_per_launch": k7_bytes, "stage_ms": k7_ms}
+        sc = stream_ceiling("read1_write3", os.path.join(ROOT, "profiles", "pmc_k7.json"), k7_ms)
+        if sc:
+            out["k7_roofline"]["stream_ceiling"] = sc
         out["roofline"]["note"] = ("achieved = SURVEY 8d keyed-record bytes (34 + rlen + alen + 24 if long) + "
                                    "key/path text written, over the timed loop's HIP-event time per step on the "
                                    "launch stream (" +
