@@ -544,20 +544,43 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
       }
       if constexpr (KEYS != 0) {
         if (dd_mine) {  // K3's mark phase on the (chrom, pos) already in registers
+          // A record sharing (chrom, pos) with its predecessor is listed for K3's
+          // resolve only if it could repeat a primary key before it: it has the
+          // predecessor's lengths and refSNP id, or it is third or later in its run.
+          // The rest of a two-record run keeps 1 here (K3's own first test,
+          // avdb_dedup.hip k_dedup_resolve_list), so the list holds the
+          // duplicates and the longer runs, not every shared position.
           const uint32_t c4 = cw[u];
-          const u32x4 q4 = p4[u];
+          const u32x4 q4 = p4[u], rr = r4[u], aa = a4[u];
+          const uint64_t* ext1 = reinterpret_cast<const uint64_t*>(kt.ext2);
           uint32_t pc = __shfl_up(c4 >> 24, 1, kWave), pp = __shfl_up(q4.w, 1, kWave);
-          if (__lane_id() == 0 && live && j > 0) {
-            pc = chrom[4 * j - 1];
-            pp = pos[4 * j - 1];
-          }
+          uint32_t pr = __shfl_up(rr.w, 1, kWave), pa = __shfl_up(aa.w, 1, kWave);
+          const uint64_t e3 = x23[u][1];
+          uint64_t pe = (uint64_t(uint32_t(__shfl_up(uint32_t(e3 >> 32), 1, kWave))) << 32) |
+                        uint32_t(__shfl_up(uint32_t(e3), 1, kWave));
           uint32_t same = 0;
           if (live) {
-            same |= uint32_t(j > 0 && (c4 & 0xFFu) == pc && q4.x == pp);
             same |= uint32_t(((c4 >> 8) & 0xFFu) == (c4 & 0xFFu) && q4.y == q4.x) << 1;
             same |= uint32_t(((c4 >> 16) & 0xFFu) == ((c4 >> 8) & 0xFFu) && q4.z == q4.y) << 2;
             same |= uint32_t((c4 >> 24) == ((c4 >> 16) & 0xFFu) && q4.w == q4.z) << 3;
           }
+          // bit 0 of the previous lane's run bits: its record 3 shares its predecessor's position
+          uint32_t psame = (uint32_t(__shfl_up(same, 1, kWave)) >> 3) & 1u;
+          if (__lane_id() == 0 && live && j > 0) {
+            pc = chrom[4 * j - 1];
+            pp = pos[4 * j - 1];
+            pr = rl[4 * j - 1];
+            pa = al[4 * j - 1];
+            pe = ext1 ? ext1[4 * j - 1] : 0ull;
+            psame = uint32_t(chrom[4 * j - 2] == pc && pos[4 * j - 2] == pp);
+          }
+          if (live) same |= uint32_t(j > 0 && (c4 & 0xFFu) == pc && q4.x == pp);
+          const uint32_t prev_same = ((same << 1) & 0xEu) | psame;
+          uint32_t cand = uint32_t(rr.x == pr && aa.x == pa && x01[u][0] == pe);
+          cand |= uint32_t(rr.y == rr.x && aa.y == aa.x && x01[u][1] == x01[u][0]) << 1;
+          cand |= uint32_t(rr.z == rr.y && aa.z == aa.y && x23[u][0] == x01[u][1]) << 2;
+          cand |= uint32_t(rr.w == rr.z && aa.w == aa.z && x23[u][1] == x23[u][0]) << 3;
+          same &= cand | prev_same;
           const uint32_t cnt = __popc(same);
           uint32_t incl = cnt;
 #pragma unroll

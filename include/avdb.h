@@ -474,9 +474,12 @@ int avdb_primary_keys_fill_digests(avdb_ctx* ctx, const uint8_t* chrom, const ui
  * workspace (avdb_vrs_digest_workspace_size(n) bytes, 16-byte aligned; nullable)
  * it also classifies every record for K4 (short, or long and its SHA-512 block
  * bucket).  With a K3 list workspace and a keep array (nullable) it also runs K3's
- * first phase (keep = 1, same-position records listed per workgroup) when its
- * lists fit (kDedupListHead + 4 * grid * slice bytes: at most 16 KB + 4 (n + 2^22)
- * at the default unroll).
+ * first phase (keep = 1; listed per workgroup: the records that share (chrom, pos)
+ * with their predecessor and either have its ref / alt lengths and ext_id or are
+ * third or later at their position — the others cannot repeat an earlier primary
+ * key) when its lists fit (kDedupListHead + 4 * grid * slice bytes: at most
+ * 16 KB + 4 (n + 2^22) at the default unroll).  The resolve (avdb_pk_dedup_ex with
+ * AVDB_DEDUP_MARKED) must then be given the same ext_id.
  * *totals_written = AVDB_KEYED_TOTALS | AVDB_KEYED_LONG_CODES | AVDB_KEYED_DEDUP_MARKS
  * for what it wrote (16-byte aligned arrays; else 0 and it is avdb_record_prep):
  * pass AVDB_KEYS_TOTALS_READY to avdb_primary_keys_onepass_ex, AVDB_DIGEST_CODES_READY

@@ -473,6 +473,59 @@ def test_keyed_record_prep_marks_for_k3(engine, n, dup):
     assert torch.equal(engine.pk_dedup(c, grouped=True, workspace=ws)[:n], engine.pk_dedup(c, grouped=True)[:n])
 
 
+def _run_batch(n, seed, long_every=0):
+    """Position runs of 1-6 records (lane and wave boundaries fall everywhere in them)
+    whose alleles come from a small set and whose refSNP ids from {0, 7, 9}, so equal
+    primary keys are frequent, also third-or-later in a run and behind a differing
+    record; every `long_every`-th allele is long (> 50 bases).  Returns the batch
+    (host numpy) and keep-first per (chrom, pos, ref, alt, rsid) — the primary key
+    the dedup compares (removeDuplicates.sql:2-24)."""
+    rng = np.random.default_rng(seed)
+    runs = rng.choice([1, 2, 3, 4, 5, 6], size=n, p=[0.3, 0.3, 0.15, 0.12, 0.08, 0.05])
+    pos = np.repeat(np.cumsum(rng.integers(1, 4, runs.size)) + 1_000_000, runs)[:n].astype(np.int32)
+    alle = [b"A", b"C", b"G", b"AC", b"ACG", b"ACGTACGTA", b"AAAAAAAAAAAAAAAAAA"]
+    refs = [alle[k] for k in rng.integers(0, len(alle), n)]
+    alts = [alle[k] for k in rng.integers(0, 3, n)]
+    if long_every:
+        for i in range(0, n, long_every):
+            refs[i] = b"T" * 60
+    ext = rng.choice(np.array([0, 7, 9], dtype=np.int64), size=n, p=[0.2, 0.6, 0.2])
+    rl = np.array([len(r) for r in refs], dtype=np.int32)
+    al = np.array([len(a) for a in alts], dtype=np.int32)
+    heap = b"".join(r + a for r, a in zip(refs, alts))
+    off = np.concatenate([[0], np.cumsum(rl.astype(np.int64) + al)[:-1]]).astype(np.int64)
+    seen, keep = set(), np.ones(n, dtype=np.uint8)
+    for i in range(n):
+        k = (int(pos[i]), refs[i], alts[i], int(ext[i]))
+        if k in seen:
+            keep[i] = 0
+        seen.add(k)
+    d = dict(chrom=np.full(n, 21, dtype=np.uint8), pos=pos, allele_off=off, ref_len=rl, alt_len=al,
+             heap=np.frombuffer(heap, dtype=np.uint8).copy(), ext_id=ext)
+    return d, keep
+
+
+@pytest.mark.parametrize("n,seed,long_every", [(4097, 1, 0), (70001, 2, 0), (262147, 3, 97), (1027, 4, 5)])
+def test_keyed_marks_list_only_possible_repeats(engine, n, seed, long_every):
+    """The keyed K2 lists for K3 only the same-position records that could repeat an
+    earlier primary key (the predecessor's lengths and refSNP id, or third or later at
+    the position); keep after the resolve equals keep-first per primary key computed
+    here in Python, and K3 on its own, on runs built to hit the unlisted cases."""
+    from annotatedvdb_amd import _native as N
+    from annotatedvdb_amd.engine import RecordBatch
+    d, want = _run_batch(n, seed, long_every)
+    b = RecordBatch(**{k: torch.from_numpy(v).cuda() for k, v in d.items()})
+    kt = engine.primary_keys(b, code=engine.record_prep(b, want_lcp=False)[1])
+    ws = torch.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), dtype=torch.uint8, device="cuda")
+    engine.record_prep(b, want_lcp=False, keys=kt, dedup_workspace=ws)
+    assert "marks" in engine._pending
+    ctr = torch.zeros(N.N_COUNTERS, dtype=torch.int64, device="cuda")
+    keep = engine.pk_dedup(b, grouped=True, counters=ctr, workspace=ws)
+    np.testing.assert_array_equal(keep[:n].cpu().numpy(), want)
+    assert torch.equal(keep[:n], engine.pk_dedup(b, grouped=True)[:n])
+    assert int((want == 0).sum()) > n // 100
+
+
 @pytest.mark.parametrize("layout", ["serial", "fork"])
 def test_c1_graph_replay_vs_c_oracle(engine, layout):
     """The step bench.py times for C1, as it times it: ``pipeline.KeyedStep`` in
