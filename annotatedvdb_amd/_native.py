@@ -93,6 +93,7 @@ EXPORTED_SYMBOLS = [
     "avdb_format_bin_path", "avdb_format_bin_paths",
     "avdb_vcf_workspace_size", "avdb_vcf_count_workspace_size", "avdb_vcf_count_lines", "avdb_vcf_parse_lines",
     "avdb_vcf_parse_lines2", "avdb_vcf_emit", "avdb_vcf_emit_ws",
+    "avdb_vcf_local_workspace_size", "avdb_vcf_parse_local", "avdb_vcf_emit_local",
     "avdb_chrom_map_create", "avdb_chrom_map_destroy",
     "avdb_format_workspace_size", "avdb_vcf_format_size", "avdb_vcf_format_write", "avdb_vcf_line_host",
     "avdb_display_attributes",
@@ -181,6 +182,9 @@ def _sig(lib):
     f.avdb_chrom_map_destroy.argtypes = [P]
     f.avdb_vcf_emit.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, P, P, P, P, P, P]
     f.avdb_vcf_emit_ws.argtypes = [P, P, SZ, SZ, P, SZ, P, P, P, P, P, P, P, P, P, P, P, P]
+    f.avdb_vcf_local_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
+    f.avdb_vcf_parse_local.argtypes = [P, P, SZ, P, SZ, ctypes.POINTER(VcfOpts), P, P]
+    f.avdb_vcf_emit_local.argtypes = [P, P, SZ, P, SZ, P, P, P, P, P, P, P, P, P, P, P, P]
     f.avdb_format_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_vcf_format_size.argtypes = [P, P, SZ, SZ, P, P, P, P, P, P, P, ctypes.POINTER(FormatOpts),
                                        P, SZ, P, P, P, P]

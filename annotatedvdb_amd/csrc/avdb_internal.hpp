@@ -260,6 +260,19 @@ __device__ __forceinline__ uint32_t long_code(uint32_t r, uint32_t a, uint32_t m
   return uint64_t(r) + a > max_len ? 1u + long_bucket(a) : 0u;
 }
 
+// inclusive wave64 prefix sum through DPP row shifts and row broadcasts: six
+// VALU adds with no LDS round trip (__shfl_up lowers to ds_bpermute: six
+// dependent LDS trips per value)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+  return x;
+}
+
 }  // namespace avdb
 
 struct avdb_ctx {

@@ -130,6 +130,23 @@ __device__ __forceinline__ VcfEmitRec emit_rec(const avdb_vcf_line& L) {
                     5 < nfields ? L.field[5] - 1 : L.len};
 }
 
+// ---- the count-free records path (avdb_vcf_parse_local / avdb_vcf_emit_local) ----
+#ifndef AVDB_VCF_LOCAL_CAP
+#define AVDB_VCF_LOCAL_CAP 1024  // line slots per parse window (lines >= 24 B on average; more: counted path)
+#endif
+constexpr uint32_t kLocalCap = AVDB_VCF_LOCAL_CAP;
+static_assert(kLocalCap % kBlock == 0, "whole rounds of slots");
+struct LocalWin {  // one parse window's lines, records and heap bytes
+  uint32_t lines, recs;
+  uint64_t heap;
+};
+struct LocalOut {
+  LocalWin* win;               // [windows]
+  VcfEmitRec* erec;            // [windows * kLocalCap]
+  uint2* cnt;                  // [windows * kLocalCap] (records, heap bytes) per line
+  unsigned long long* overflow;  // windows with more than kLocalCap lines
+};
+
 // the line's public record or its emit record, one of them (the other NULL)
 __device__ __forceinline__ void put_line(avdb_vcf_line* lines, VcfEmitRec* erec, size_t li, const avdb_vcf_line& L) {
   if (lines) lines[li] = L;
@@ -479,7 +496,12 @@ __device__ __forceinline__ uint32_t block_excl32(uint32_t v, uint32_t* s_w, uint
   return base + x - v;
 }
 
-__global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
+// LOCAL (the records-only path without the count pass, avdb_vcf_parse_local): no
+// line numbers are known, so a window writes its lines' emit records and counts to
+// its own slots (window * kLocalCap + its line), and its line / record / heap totals
+// to LocalWin; a window with more than kLocalCap lines flags the overflow word.
+template <bool LOCAL>
+__global__ __launch_bounds__(kBlock, LOCAL ? 5 : AVDB_VCF_PARSE_WAVES) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
                                                               size_t n_lines,
                                                               const unsigned long long* __restrict__ blk_off,
                                                               const uint32_t* __restrict__ wave_cnt,
@@ -488,7 +510,7 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
                                                               VcfEmitRec* __restrict__ erec,
                                                               unsigned long long* __restrict__ rec_cnt,
                                                               unsigned long long* __restrict__ heap_cnt,
-                                                              ChromMapView cm, uint32_t min_fields) {
+                                                              ChromMapView cm, uint32_t min_fields, LocalOut lo_out) {
   __shared__ u32x4 s_text[kParseStage64 / 16];
   __shared__ uint64_t s_tab[kParseStage64 / 64];  // tab bitmap of the staged bytes
   __shared__ uint32_t s_start[kBlock + 1];  // line starts of the round, relative to the window start
@@ -496,6 +518,7 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
   __shared__ uint32_t s_w[kVcfWaves];
   __shared__ uint32_t s_wp[kVcfWaves];      // the round's pending INFO scans per wave
   __shared__ uint32_t s_tail;               // (first '\n' at or after w1 - 1) + 1 - w0
+  __shared__ uint32_t s_lr[LOCAL ? kVcfWaves : 1], s_lh[LOCAL ? kVcfWaves : 1];  // (LOCAL) the round's per-wave sums
   const Heap h = make_heap(text, text_bytes);
   const size_t nb = text_bytes;
   const uint32_t tid = threadIdx.x, lane = __lane_id(), wv = tid / kWave;
@@ -504,11 +527,14 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
   size_t t0, t1;
   wave_range(nb, gw, &t0, &t1);
   const size_t w0 = t0 + size_t(wk) * kParseWin;
-  if (w0 >= t1) return;  // (uniform)
+  if (w0 >= t1) {  // (uniform)
+    if (LOCAL && tid == 0) lo_out.win[blockIdx.x] = LocalWin{0, 0, 0};
+    return;
+  }
   const size_t w1 = w0 + kParseWin < t1 ? w0 + kParseWin : t1;
   // lines starting before w0: 1 + the newlines in [0, w0 - 1)
   size_t li0 = 0;
-  if (w0) {
+  if (!LOCAL && w0) {
     unsigned long long k = blk_off[gw / kVcfWaves];
     for (size_t w = (gw / kVcfWaves) * kVcfWaves; w < gw; ++w) k += wave_cnt[w];
     for (uint32_t j = 0; j < wk; ++j) k += win_cnt[gw * wps + j];
@@ -558,7 +584,17 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
   const uint32_t pref = block_excl32(cnt, s_w, &T);
   const uint32_t first = w0 == 0 ? 1u : 0u;  // line 0 starts at byte 0
   T += first;
-  if (!T) return;  // (uniform; no line starts here)
+  if (!T) {  // (uniform; no line starts here)
+    if (LOCAL && tid == 0) lo_out.win[blockIdx.x] = LocalWin{0, 0, 0};
+    return;
+  }
+  if (LOCAL && T > kLocalCap) {  // (uniform) the caller takes the counted path
+    if (tid == 0) {
+      lo_out.win[blockIdx.x] = LocalWin{0, 0, 0};
+      atomicAdd(lo_out.overflow, 1ull);
+    }
+    return;
+  }
   // ---- the end of the window's last line: first '\n' at or after w1 - 1 ----
   if (wv == 0) {
     size_t q = w1 - 1;
@@ -620,6 +656,8 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
       }
     }
   }
+  uint32_t run_r = 0;  // (LOCAL) records and heap bytes of the window's earlier rounds
+  uint64_t run_h = 0;
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint32_t lo = kBlock * r, hi = lo + kBlock;
     if (r == 0 && first && tid == 0) s_start[0] = 0;
@@ -636,8 +674,8 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
     }
     if (tid == 0 && T <= hi) s_start[T - lo] = s_tail;
     __syncthreads();
-    const size_t li = li0 + lo + tid;
-    const bool live = lo + tid < T && li < n_lines;
+    const size_t li = LOCAL ? size_t(blockIdx.x) * kLocalCap + lo + tid : li0 + lo + tid;
+    const bool live = lo + tid < T && (LOCAL || li < n_lines);
     avdb_vcf_line L;
     uint64_t recs = 0, hbytes = 0;
     uint32_t info_item = 0;  // a pending INFO: stage offset | length << 15
@@ -686,12 +724,44 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
                    raw, L, recs, hbytes, cm, min_fields);
       }
     }
+    // (LOCAL) each line's records / heap bytes within the window: wave sums here,
+    // the waves below it after the barrier that follows (no barrier of its own).
+    // Lines up to 2^23 records / heap bytes and windows below 2^32 heap bytes, else
+    // the counted path.
+    uint32_t xr = 0, xh = 0;
+    if constexpr (LOCAL) {
+      if ((recs | hbytes) >> 23) atomicAdd(lo_out.overflow, 1ull);
+      xr = wave_incl_sum(uint32_t(recs));
+      xh = wave_incl_sum(uint32_t(hbytes));
+      if (lane == kWave - 1) {
+        s_lr[wv] = xr;
+        s_lh[wv] = xh;
+      }
+    }
     // the round's pending INFO scans, gathered into the first lanes of the workgroup
     // (a wave scans INFO once for its lanes that need it, instead of every wave for
     // the ~40 % of its lines without an rs ID)
     const uint64_t pend = __ballot(info_item != 0);
     if (lane == 0) s_wp[wv] = uint32_t(__popcll(pend));
     __syncthreads();  // (after it s_start and s_rs are free: this round's starts and candidates are read)
+    uint32_t pr = 0, ph = 0;  // (LOCAL) the line's record / heap offset within the window
+    if constexpr (LOCAL) {
+      uint32_t br = 0, bh = 0, tr = 0, th = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kVcfWaves; ++w) {
+        const uint32_t c = s_lr[w], d = s_lh[w];
+        if (w < wv) {
+          br += c;
+          bh += d;
+        }
+        tr += c;
+        th += d;
+      }
+      pr = run_r + br + xr - uint32_t(recs);
+      ph = uint32_t(run_h) + bh + xh - uint32_t(hbytes);
+      run_r += tr;
+      run_h += th;
+    }
     uint32_t n_pend = 0, slot = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kVcfWaves; ++w) {
@@ -719,11 +789,22 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
           else L.ext_id = rs & (kRsFound - 1);
         }
       }
-      put_line(lines, erec, li, L);
-      rec_cnt[li] = recs;
-      heap_cnt[li] = hbytes;
+      if constexpr (LOCAL) {
+        lo_out.erec[li] = emit_rec(L);
+        lo_out.cnt[li] = make_uint2(pr, ph);
+      } else {
+        put_line(lines, erec, li, L);
+        rec_cnt[li] = recs;
+        heap_cnt[li] = hbytes;
+      }
     }
     if (r + 1 < rounds) __syncthreads();  // s_start is refilled by the next round
+  }
+  if constexpr (LOCAL) {
+    if (tid == 0) {
+      if (run_h >> 32) atomicAdd(lo_out.overflow, 1ull);
+      lo_out.win[blockIdx.x] = LocalWin{T, run_r, run_h};
+    }
   }
 }
 
@@ -830,6 +911,164 @@ __global__ __launch_bounds__(kEmitLines) void k_vcf_emit(
       }
     }
     __syncthreads();
+  }
+}
+
+// ---- the count-free records path: window totals -> bases, then emit per window ----
+// Two levels, no one-workgroup pass over all windows (that ran 108 us for 41 k
+// windows): k_vcf_local_tiles scans 256 windows per workgroup (bases within the
+// tile) and writes each tile's totals; k_vcf_local_top scans the tile totals (one
+// workgroup, NW / 256 of them) and writes the totals the host reads; the emit adds
+// the two.  tot = {lines, records, heap bytes, overflow windows}.
+struct LocalTot {
+  unsigned long long lines, recs, heap;
+};
+constexpr uint32_t kTileWins = 256;
+
+__device__ __forceinline__ unsigned long long wave_incl_sum64(unsigned long long x) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const unsigned long long u = scan::shfl_up64(x, d);
+    if (__lane_id() >= uint32_t(d)) x += u;
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(kTileWins) void k_vcf_local_tiles(const LocalWin* __restrict__ win, size_t nw,
+                                                               ulonglong2* __restrict__ base_lr,
+                                                               unsigned long long* __restrict__ base_h,
+                                                               LocalTot* __restrict__ tile_tot) {
+  __shared__ uint32_t s_a[kTileWins / kWave], s_b[kTileWins / kWave];
+  __shared__ unsigned long long s_c[kTileWins / kWave];
+  const uint32_t tid = threadIdx.x, lane = __lane_id(), wv = tid / kWave;
+  const size_t w = size_t(blockIdx.x) * kTileWins + tid;
+  const LocalWin v = w < nw ? win[w] : LocalWin{0, 0, 0};
+  const uint32_t xa = wave_incl_sum(v.lines), xb = wave_incl_sum(v.recs);
+  const unsigned long long xc = wave_incl_sum64(v.heap);
+  if (lane == kWave - 1) {
+    s_a[wv] = xa;
+    s_b[wv] = xb;
+    s_c[wv] = xc;
+  }
+  __syncthreads();
+  uint32_t pa = 0, pb = 0, ta = 0, tb = 0;
+  unsigned long long pc = 0, tc = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < kTileWins / kWave; ++q) {
+    if (q < wv) {
+      pa += s_a[q];
+      pb += s_b[q];
+      pc += s_c[q];
+    }
+    ta += s_a[q];
+    tb += s_b[q];
+    tc += s_c[q];
+  }
+  if (w < nw) {
+    base_lr[w] = make_ulonglong2(pa + xa - v.lines, pb + xb - v.recs);
+    base_h[w] = pc + xc - v.heap;
+  }
+  if (tid == 0) tile_tot[blockIdx.x] = LocalTot{ta, tb, tc};
+}
+
+// exclusive scan of the tile totals in place (one workgroup), the grand totals to
+// tot (the workspace header) and out (the caller's)
+__global__ __launch_bounds__(kTileWins) void k_vcf_local_top(LocalTot* __restrict__ tile, size_t nt,
+                                                             unsigned long long* __restrict__ tot,
+                                                             unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s_a[kTileWins / kWave], s_b[kTileWins / kWave], s_c[kTileWins / kWave];
+  const uint32_t tid = threadIdx.x, lane = __lane_id(), wv = tid / kWave;
+  unsigned long long ra = 0, rb = 0, rc = 0;
+  for (size_t c0 = 0; c0 < nt; c0 += kTileWins) {
+    const size_t i = c0 + tid;
+    const LocalTot v = i < nt ? tile[i] : LocalTot{0, 0, 0};
+    const unsigned long long xa = wave_incl_sum64(v.lines), xb = wave_incl_sum64(v.recs),
+                             xc = wave_incl_sum64(v.heap);
+    if (lane == kWave - 1) {
+      s_a[wv] = xa;
+      s_b[wv] = xb;
+      s_c[wv] = xc;
+    }
+    __syncthreads();
+    unsigned long long pa = 0, pb = 0, pc = 0, ta = 0, tb = 0, tc = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kTileWins / kWave; ++q) {
+      if (q < wv) {
+        pa += s_a[q];
+        pb += s_b[q];
+        pc += s_c[q];
+      }
+      ta += s_a[q];
+      tb += s_b[q];
+      tc += s_c[q];
+    }
+    if (i < nt) tile[i] = LocalTot{ra + pa + xa - v.lines, rb + pb + xb - v.recs, rc + pc + xc - v.heap};
+    ra += ta;
+    rb += tb;
+    rc += tc;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    tot[0] = out[0] = ra;
+    tot[1] = out[1] = rb;
+    tot[2] = out[2] = rc;
+    out[3] = tot[3];  // (the parse's overflow count, same stream)
+  }
+}
+
+// One workgroup per parse window: its lines' record / heap offsets are the window's
+// bases plus the in-window offsets the parse left in the slots; the window's text
+// staged once, then the rows as k_vcf_emit writes them; rec_off / heap_off per line
+// (nullable).
+__global__ __launch_bounds__(kEmitLines) void k_vcf_emit_local(
+    const uint8_t* __restrict__ text, size_t text_bytes, const LocalWin* __restrict__ win,
+    const ulonglong2* __restrict__ base_lr, const unsigned long long* __restrict__ base_h,
+    const LocalTot* __restrict__ tile_pre, const VcfEmitRec* __restrict__ erec, const uint2* __restrict__ cnt,
+    const unsigned long long* __restrict__ tot,
+    uint64_t* __restrict__ rec_off, uint64_t* __restrict__ heap_off, uint8_t* __restrict__ chrom,
+    uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off, uint32_t* __restrict__ ref_len,
+    uint32_t* __restrict__ alt_len, uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap,
+    uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
+  __shared__ u32x4 s_text[kEmitStage / 16];
+  const Heap h = make_heap(text, text_bytes);
+  constexpr uint64_t kStartMask = (uint64_t(1) << 56) - 1;
+  const size_t w = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  if (w == 0 && tid == 0) {  // the totals row of the per-line offsets
+    if (rec_off) rec_off[tot[0]] = tot[1];
+    if (heap_off) heap_off[tot[0]] = tot[2];
+  }
+  const uint32_t n = win[w].lines;
+  if (n == 0) return;  // (uniform)
+  const size_t slot0 = w * kLocalCap;
+  const LocalTot tp = tile_pre[w / kTileWins];
+  ulonglong2 blr = base_lr[w];
+  blr.x += tp.lines;
+  blr.y += tp.recs;
+  const VcfEmitRec& Z = erec[slot0 + n - 1];
+  const size_t s0 = erec[slot0].start_chrom & kStartMask;
+  const size_t s1 = (Z.start_chrom & kStartMask) + Z.aend;
+  const Window sw = stage_window<kEmitLines, kEmitStage>(h, s0, s1, s_text);
+  const uint64_t hb = base_h[w] + tp.heap;
+  const uint32_t wr = win[w].recs;
+  for (uint32_t k = tid; k < n; k += kEmitLines) {
+    // the slots hold each line's record / heap offset within the window
+    const uint2 c = cnt[slot0 + k];
+    const uint32_t c1 = k + 1 < n ? cnt[slot0 + k + 1].x : wr;
+    const size_t li = blr.x + k;
+    const uint64_t r0 = blr.y + c.x, h0 = hb + c.y;
+    if (rec_off) rec_off[li] = r0;
+    if (heap_off) heap_off[li] = h0;
+    if (c1 > c.x) {
+      const VcfEmitRec E = erec[slot0 + k];
+      const size_t st = E.start_chrom & kStartMask;
+      if (sw.staged)
+        emit_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + st - sw.a0)), E, li, r0, h0, chrom,
+                  pos, allele_off, ref_len, alt_len, ext_id, heap, rec_line, rec_alt);
+      else
+        emit_line((glb_cp)(text + st), E, li, r0, h0, chrom, pos, allele_off, ref_len, alt_len, ext_id, heap,
+                  rec_line, rec_alt);
+    }
   }
 }
 
@@ -960,10 +1199,10 @@ static int parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, si
   const auto* wave = reinterpret_cast<const uint32_t*>(cw + kCountWsWave);
   if (windows) {  // one workgroup per parse window, line starts found in it
     const uint32_t wps = windows_per_chunk(text_bytes);
-    hipLaunchKernelGGL(k_vcf_parse_windows, dim3(unsigned(size_t(kVcfGrid) * kVcfWaves * wps)), dim3(kBlock), 0, s,
-                       text, text_bytes, n_lines, blk, wave,
+    hipLaunchKernelGGL(k_vcf_parse_windows<false>, dim3(unsigned(size_t(kVcfGrid) * kVcfWaves * wps)), dim3(kBlock), 0,
+                       s, text, text_bytes, n_lines, blk, wave,
                        reinterpret_cast<const uint32_t*>(cw + AVDB_VCF_COUNT_WORKSPACE_BYTES), wps, lines, erec, rc,
-                       hc, cm, min_fields);
+                       hc, cm, min_fields, LocalOut{});
     AVDB_LAUNCH_CHECK("k_vcf_parse_windows");
   } else {  // the line-starts pass, then 256 lines per workgroup
     hipLaunchKernelGGL(k_vcf_starts, dim3(kVcfGrid), dim3(kBlock), 0, s, text, text_bytes, blk, wave, n_lines, starts);
@@ -1049,6 +1288,115 @@ extern "C" int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_
 }
 
 // ---- chromosome map (ChromosomeMap.get, chromosome_map_parser.py:84-91) ----------
+// ---- the count-free records path: host side ----
+// workspace: header (totals: lines, records, heap bytes, overflow windows) | LocalWin
+// per window | (line, record) bases per window | heap base per window | emit records
+// and counts per window slot
+struct LocalLayout {
+  size_t nw, nt, win, blr, bh, tile, erec, cnt, bytes;
+};
+static LocalLayout local_layout(size_t text_bytes) {
+  auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
+  LocalLayout L;
+  L.nw = size_t(kVcfGrid) * kVcfWaves * windows_per_chunk(text_bytes);
+  L.nt = (L.nw + kTileWins - 1) / kTileWins;
+  L.win = 256;
+  L.blr = L.win + up(sizeof(LocalWin) * L.nw);
+  L.bh = L.blr + up(16 * L.nw);
+  L.tile = L.bh + up(8 * L.nw);
+  L.erec = L.tile + up(sizeof(LocalTot) * L.nt);
+  L.cnt = L.erec + up(sizeof(VcfEmitRec) * L.nw * kLocalCap);
+  L.bytes = L.cnt + up(8 * L.nw * kLocalCap);
+  return L;
+}
+
+extern "C" int avdb_vcf_local_workspace_size(size_t text_bytes, size_t* bytes) {
+  if (!bytes) return AVDB_EINVAL;
+  *bytes = local_layout(text_bytes).bytes;
+  return AVDB_OK;
+}
+
+static const char* local_ws_error(const void* ws, size_t ws_bytes, size_t text_bytes) {
+  if (!ws || reinterpret_cast<uintptr_t>(ws) % 16 || ws_bytes < local_layout(text_bytes).bytes)
+    return "16-byte aligned workspace of avdb_vcf_local_workspace_size(text_bytes) bytes required";
+  return nullptr;
+}
+
+extern "C" int avdb_vcf_parse_local(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
+                                    size_t workspace_bytes, const avdb_vcf_opts* opts, uint64_t* totals,
+                                    void* stream) {
+  if (!ctx || !totals || (text_bytes && !text)) {
+    avdb_set_error("avdb_vcf_parse_local: null argument");
+    return AVDB_EINVAL;
+  }
+  if (opts && opts->struct_size != sizeof(avdb_vcf_opts)) {
+    avdb_set_error("avdb_vcf_parse_local: avdb_vcf_opts.struct_size %u, this library expects %zu",
+                   opts->struct_size, sizeof(avdb_vcf_opts));
+    return AVDB_EINVAL;
+  }
+  if (opts && opts->chrom_map && opts->chrom_map->device != ctx->device) {
+    avdb_set_error("avdb_vcf_parse_local: chromosome map made for device %d", opts->chrom_map->device);
+    return AVDB_EINVAL;
+  }
+  if (const char* e = local_ws_error(workspace, workspace_bytes, text_bytes)) {
+    avdb_set_error("avdb_vcf_parse_local: %s", e);
+    return AVDB_ERANGE;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  char* w = static_cast<char*>(workspace);
+  auto* hdr = reinterpret_cast<unsigned long long*>(w);
+  AVDB_HIP_TRY(hipMemsetAsync(hdr, 0, 32, s));
+  if (text_bytes == 0) {
+    AVDB_HIP_TRY(hipMemsetAsync(totals, 0, 32, s));
+    return AVDB_OK;
+  }
+  const ChromMapView cm = opts && opts->chrom_map ? opts->chrom_map->dev : ChromMapView{};
+  const uint32_t min_fields = opts ? opts->min_fields : 0u;
+  const LocalLayout L = local_layout(text_bytes);
+  LocalOut o{reinterpret_cast<LocalWin*>(w + L.win), reinterpret_cast<VcfEmitRec*>(w + L.erec),
+             reinterpret_cast<uint2*>(w + L.cnt), hdr + 3};
+  hipLaunchKernelGGL(k_vcf_parse_windows<true>, dim3(unsigned(L.nw)), dim3(kBlock), 0, s, text, text_bytes, size_t(0),
+                     nullptr, nullptr, nullptr, windows_per_chunk(text_bytes), nullptr, nullptr, nullptr, nullptr, cm,
+                     min_fields, o);
+  AVDB_LAUNCH_CHECK("k_vcf_parse_windows<local>");
+  hipLaunchKernelGGL(k_vcf_local_tiles, dim3(unsigned(L.nt)), dim3(kTileWins), 0, s, o.win, L.nw,
+                     reinterpret_cast<ulonglong2*>(w + L.blr), reinterpret_cast<unsigned long long*>(w + L.bh),
+                     reinterpret_cast<LocalTot*>(w + L.tile));
+  AVDB_LAUNCH_CHECK("k_vcf_local_tiles");
+  hipLaunchKernelGGL(k_vcf_local_top, dim3(1), dim3(kTileWins), 0, s, reinterpret_cast<LocalTot*>(w + L.tile), L.nt,
+                     hdr, reinterpret_cast<unsigned long long*>(totals));
+  AVDB_LAUNCH_CHECK("k_vcf_local_top");
+  return AVDB_OK;
+}
+
+extern "C" int avdb_vcf_emit_local(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, const void* workspace,
+                                   size_t workspace_bytes, uint64_t* rec_off, uint64_t* heap_off, uint8_t* chrom,
+                                   uint32_t* pos, uint64_t* allele_off, uint32_t* ref_len, uint32_t* alt_len,
+                                   uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line, uint32_t* rec_alt,
+                                   void* stream) {
+  if (!ctx || !chrom || !pos || !allele_off || !ref_len || !alt_len || !ext_id || !heap || !rec_line || !rec_alt) {
+    avdb_set_error("avdb_vcf_emit_local: null argument");
+    return AVDB_EINVAL;
+  }
+  if (const char* e = local_ws_error(workspace, workspace_bytes, text_bytes)) {
+    avdb_set_error("avdb_vcf_emit_local: %s", e);
+    return AVDB_ERANGE;
+  }
+  if (text_bytes == 0) return AVDB_OK;
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  const char* w = static_cast<const char*>(workspace);
+  const LocalLayout L = local_layout(text_bytes);
+  hipLaunchKernelGGL(k_vcf_emit_local, dim3(unsigned(L.nw)), dim3(kEmitLines), 0, static_cast<hipStream_t>(stream),
+                     text, text_bytes, reinterpret_cast<const LocalWin*>(w + L.win),
+                     reinterpret_cast<const ulonglong2*>(w + L.blr), reinterpret_cast<const unsigned long long*>(w + L.bh),
+                     reinterpret_cast<const LocalTot*>(w + L.tile), reinterpret_cast<const VcfEmitRec*>(w + L.erec), reinterpret_cast<const uint2*>(w + L.cnt),
+                     reinterpret_cast<const unsigned long long*>(w), rec_off, heap_off, chrom, pos, allele_off,
+                     ref_len, alt_len, ext_id, heap, rec_line, rec_alt);
+  AVDB_LAUNCH_CHECK("k_vcf_emit_local");
+  return AVDB_OK;
+}
+
 extern "C" int avdb_chrom_map_create(avdb_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, size_t n_keys,
                                      const uint8_t* codes, avdb_chrom_map** out) {
   if (!ctx || !out || (n_keys && (!keys || !key_off || !codes)) || n_keys >= (1u << 24)) {

@@ -577,6 +577,7 @@ class Engine:
         # first phase in a dedup workspace + keep).  Every record_prep call drops
         # all of them first.
         self._pending: Dict[str, tuple] = {}
+        self.last_vcf_path = ""  # vcf_tokenize(want_lines=False): "local" (count-free) or "counted"
         # test hook: every output / workspace tensor the engine allocates is filled
         # with this byte first (None: torch.empty), so a check sees only what the
         # kernels wrote, never what an earlier pass left in a recycled block
@@ -827,13 +828,23 @@ class Engine:
         return [raw[i * 32:(i + 1) * 32].decode("ascii") for i in range(n)]
 
     # -- K0: VCF text -> records ---------------------------------------------
-    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None, want_lines: bool = True) -> "VcfBatch":
+    def vcf_tokenize(self, text, vcf_opts: Optional["N.VcfOpts"] = None, want_lines: bool = True,
+                     count_free: bool = True) -> "VcfBatch":
         """Parse VCF data lines (bytes or a uint8 tensor) on the GPU into the
         record SoA (one row per ALT != '.') plus the per-line table.
         ``vcf_opts`` (:meth:`vcf_opts`): header width and chromosome map.
-        ``want_lines=False``: no public line table (``VcfBatch.lines`` is None; the
-        emit reads 32-byte records from the parse workspace instead of the 80-byte
-        table) — for callers that need only the records."""
+        ``want_lines=False``: no public line table (``VcfBatch.lines`` is None) — for
+        callers that need only the records: the count-free path (avdb_vcf_parse_local:
+        each parse window writes its lines to slots of its own, one scan of the window
+        totals, avdb_vcf_emit_local), or, when a window holds more lines than its slots,
+        count -> parse -> emit from 32-byte records in the parse workspace (also taken
+        with ``count_free=False``)."""
+        if not want_lines and count_free:
+            vb = self._vcf_tokenize_local(text, vcf_opts)
+            if vb is not None:
+                self.last_vcf_path = "local"
+                return vb
+        self.last_vcf_path = "counted"
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
             t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
@@ -890,6 +901,48 @@ class Engine:
             N.check("avdb_vcf_emit_ws", self.lib.avdb_vcf_emit_ws(
                 self.ctx, tp, nb, n_lines, N.ptr(ws), ws.numel(), N.ptr(rec_off), N.ptr(heap_off), *outs))
         return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
+                        records=b, rec_line=rec_line, rec_alt=rec_alt)
+
+    def _vcf_tokenize_local(self, text, vcf_opts) -> Optional["VcfBatch"]:
+        """vcf_tokenize(want_lines=False) without the count pass; None when a parse
+        window overflowed its line slots (the caller then takes the counted path)."""
+        if isinstance(text, (bytes, bytearray, memoryview)):
+            host = bytes(text)
+            t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
+            text_t = (t if host else t[:0]).to(self.device)
+        else:
+            text_t = self._dev(text)
+        nb = int(text_t.numel())
+        tp = N.ptr(text_t) if nb else None
+        s = self._stream()
+        sz = ctypes.c_size_t()
+        self.lib.avdb_vcf_local_workspace_size(nb, ctypes.byref(sz))
+        ws = self.empty(int(sz.value), torch.uint8)
+        tot = torch.zeros(4, dtype=torch.int64, device=self.device)
+        N.check("avdb_vcf_parse_local", self.lib.avdb_vcf_parse_local(
+            self.ctx, tp, nb, N.ptr(ws), ws.numel(), ctypes.byref(vcf_opts) if vcf_opts is not None else None,
+            N.ptr(tot), s))
+        n_lines, n_rec, n_heap, overflow = (int(v) for v in tot.cpu().tolist())
+        if overflow:
+            return None
+        b = RecordBatch(chrom=self.empty(n_rec, torch.uint8), pos=self.empty(n_rec, torch.int32),
+                        allele_off=self.empty(n_rec, torch.int64),
+                        ref_len=self.empty(n_rec, torch.int32), alt_len=self.empty(n_rec, torch.int32),
+                        heap=self.empty(max(1, n_heap), torch.uint8),
+                        ext_id=self.empty(n_rec, torch.int64))
+        rec_line = self.empty(n_rec, torch.int32)
+        rec_alt = self.empty(n_rec, torch.int32)
+        rec_off = self.empty(n_lines + 1, torch.int64)
+        heap_off = self.empty(n_lines + 1, torch.int64)
+        if n_lines == 0:
+            rec_off.zero_()
+            heap_off.zero_()
+        else:
+            N.check("avdb_vcf_emit_local", self.lib.avdb_vcf_emit_local(
+                self.ctx, tp, nb, N.ptr(ws), ws.numel(), N.ptr(rec_off), N.ptr(heap_off), N.ptr(b.chrom),
+                N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len), N.ptr(b.ext_id),
+                N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s))
+        return VcfBatch(text=text_t, n_lines=n_lines, lines=None, rec_off=rec_off, heap_off=heap_off,
                         records=b, rec_line=rec_line, rec_alt=rec_alt)
 
     # -- K9: this rank's lines of a VCF text -----------------------------------

@@ -715,7 +715,8 @@ def run_workload(a, name, ri, dev, cpu):
                 chrom, start, end, want_status=False, hist=hist, counters=ctr, out_code=code))
         elif name == "vcf":
             # (records only: the public 80-byte line table is for the load path, K5)
-            timed("vcf_tokenize", record, lambda: eng.vcf_tokenize(text, want_lines=False))
+            count_free = os.environ.get("AVDB_BENCH_VCF_COUNTED", "0") != "1"  # (A/B: the counted records path)
+            timed("vcf_tokenize", record, lambda: eng.vcf_tokenize(text, want_lines=False, count_free=count_free))
         elif name == "load":
             box = {}
             timed("vcf_tokenize", record, lambda: box.setdefault("vb", eng.vcf_tokenize(text)))

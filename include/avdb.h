@@ -292,6 +292,25 @@ int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size
                      const uint64_t* heap_off, uint8_t* chrom, uint32_t* pos, uint64_t* allele_off,
                      uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap, uint32_t* rec_line,
                      uint32_t* rec_alt, void* stream);
+/* The records without the count pass (the tokenize-only path, no line table):
+ * avdb_vcf_parse_local parses one workgroup per parse window with no line numbers
+ * known, each window writing its lines to slots of its own in `workspace`
+ * (avdb_vcf_local_workspace_size(text_bytes) bytes, 16-byte aligned); one scan of
+ * the windows' totals then gives every window its first line, record and heap byte.
+ * totals (device, 4 x u64): lines, records, heap bytes, and the number of windows
+ * the path could not take (more than AVDB_VCF_LOCAL_CAP = 1024 lines in a 24 KB
+ * window, or a line whose records / heap bytes exceed 32 bits).  With totals[3] == 0,
+ * avdb_vcf_emit_local writes the same records, heap, rec_line / rec_alt and per-line
+ * rec_off / heap_off (totals[0] + 1 entries each, nullable) as count -> parse ->
+ * avdb_vcf_emit_ws; with totals[3] != 0 the caller takes that counted path.  The
+ * same text and workspace go to both calls. */
+int avdb_vcf_local_workspace_size(size_t text_bytes, size_t* bytes);
+int avdb_vcf_parse_local(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
+                         size_t workspace_bytes, const avdb_vcf_opts* opts, uint64_t* totals, void* stream);
+int avdb_vcf_emit_local(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, const void* workspace,
+                        size_t workspace_bytes, uint64_t* rec_off, uint64_t* heap_off, uint8_t* chrom, uint32_t* pos,
+                        uint64_t* allele_off, uint32_t* ref_len, uint32_t* alt_len, uint64_t* ext_id, uint8_t* heap,
+                        uint32_t* rec_line, uint32_t* rec_alt, void* stream);
 
 /* ---- K5: the load driver's text outputs ---------------------------------
  * Replaces the per-alt COPY row assembly of VCFVariantLoader.__parse_alt_alleles

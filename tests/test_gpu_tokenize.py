@@ -204,12 +204,19 @@ def test_k0_window_parse_equals_starts_pass(engine, which):
     assert (vb.heap_off[: n0 + 1].cpu().numpy() == ho0).all()
 
 
-@pytest.mark.parametrize("which", ["golden", "dbsnp", "long", "big", "short"])
-def test_k0_records_without_line_table(engine, which):
-    """vcf_tokenize(want_lines=False) — no public line table, the emit reading its
-    32-byte records from the parse workspace (avdb_vcf_emit_ws) — gives the same
-    record SoA, allele heap, offsets and back-references as the tokenizer with the
-    table.  "short": 15-byte lines, ~1,600 per parse window (several rounds)."""
+@pytest.mark.parametrize("which", ["golden", "dbsnp", "long", "big", "short", "edges", "empty", "no_final_nl",
+                                   "blank"])
+@pytest.mark.parametrize("count_free", [True, False])
+def test_k0_records_without_line_table(engine, which, count_free):
+    """vcf_tokenize(want_lines=False) — no public line table: the count-free path
+    (avdb_vcf_parse_local + avdb_vcf_emit_local: windows write their lines to slots
+    of their own, one scan of the window totals) or, count_free=False, count ->
+    parse -> avdb_vcf_emit_ws from 32-byte records — gives the same record SoA,
+    allele heap, offsets and back-references as the tokenizer with the table.
+    "short": 17-byte lines; "edges": blank lines, CRLF, lines of one field, a final
+    line without '\n'; "blank": 8 M empty lines around dbSNP lines — more lines in a
+    parse window than its 1,024 slots, so the count-free call falls back to the
+    counted path."""
     if which == "short":
         text = b"".join(b"%d\t%d\t.\tA\tG\t.\t.\t.\n" % (1 + i % 9, 10 + i % 90) for i in range(300000))
     elif which == "golden":
@@ -220,15 +227,29 @@ def test_k0_records_without_line_table(engine, which):
         base = _synth(4000, 73).split(b"\n")[:-1]
         huge = b"2\t888\t.\tC\tG,T\t.\t.\tZ=" + b"Q" * 70000
         text = b"\n".join(base[:2000] + [huge] + base[2000:] + [huge]) + b"\n"
+    elif which == "edges":
+        base = _synth(3000, 83).split(b"\n")[:-1]
+        odd = [b"", b"\r", b"1\t77\t.\tA\tG\t.\t.\t.\r", b"X", b"\t\t", b"2\t9\t.\tA\tC,.,T\t.\t.\tRS=5"]
+        text = b"\n".join(x for k, line in enumerate(base) for x in ((line, odd[k % len(odd)]) if k % 7 == 0
+                                                                      else (line,)))
+    elif which == "empty":
+        text = b""
+    elif which == "blank":
+        text = _synth(2000, 91) + b"\n" * 8_000_000 + _synth(2000, 93)
+    elif which == "no_final_nl":
+        text = _synth(5000, 89).rstrip(b"\n")
     else:
         tile = _synth(60000, 79).split(b"\n")[:-1]
         text = b"\n".join(tile * 25) + b"\n"
     a = engine.vcf_tokenize(text)
-    b = engine.vcf_tokenize(text, want_lines=False)
+    b = engine.vcf_tokenize(text, want_lines=False, count_free=count_free)
+    assert engine.last_vcf_path == ("counted" if which == "blank" or not count_free else "local")
     assert b.lines is None and a.n_lines == b.n_lines and a.records.n == b.records.n
     assert torch.equal(a.rec_off, b.rec_off) and torch.equal(a.heap_off, b.heap_off)
-    for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "ext_id", "heap"):
+    for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "ext_id"):
         assert torch.equal(getattr(a.records, f), getattr(b.records, f)), f
+    nh = int(a.heap_off[a.n_lines])  # (the heap buffer holds at least one byte)
+    assert torch.equal(a.records.heap[:nh], b.records.heap[:nh])
     assert torch.equal(a.rec_line, b.rec_line) and torch.equal(a.rec_alt, b.rec_alt)
 
 
