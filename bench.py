@@ -973,10 +973,12 @@ def run_workload(a, name, ri, dev, cpu):
         out["data"] = "synthetic dbSNP-shaped VCF text (numpy PCG64 lines tiled on the device)"
         out["config"].update(lines_per_gpu=n_lines, text_bytes_per_gpu=int(text.numel()),
                              records_processed=None)
-        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize step (count pass with per-window "
-                                   "newline counts, window parse, one paired offset scan, emit, and its two host "
-                                   "reads), records only (vcf_tokenize(want_lines=False): no public line table; the "
-                                   "16 B of line offsets per line it writes are not counted)")
+        out["roofline"]["note"] = ("achieved = algorithmic bytes / whole tokenize step, records only "
+                                   "(vcf_tokenize(want_lines=False), the count-free path: window parse into "
+                                   "window-local line slots, two window-total scans, one host read, per-window "
+                                   "emit; AVDB_BENCH_VCF_COUNTED=1: count pass, parse, paired per-line scan, emit); "
+                                   "the 16 B of line offsets per line it writes are not counted")
+        out["config"]["path"] = {"local": "count-free", "counted": "counted"}.get(eng.last_vcf_path, eng.last_vcf_path)
     return out
 
 

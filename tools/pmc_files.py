@@ -21,10 +21,10 @@ from prof_summary import per_kernel  # noqa: E402
 
 C4K_STEP = ("k_record_prep4<true, 1, 1>", "k_dedup_resolve_list", "k_long_hist_codes", "k_long_scan",
             "k_long_scatter_codes", "k_vrs_digest", "k_key_group_scan", "k_record_keys_v2")
-# (the vcf step tokenizes without the public line table: its emit is k_vcf_emit<true>;
-# k_vcf_emit<false>, the line-table form, runs only in the bench's setup)
-VCF_STEP = ("k_vcf_count", "k_vcf_scan_blocks", "k_vcf_starts", "k_vcf_parse", "k_vcf_emit<true>", "k_tile_sums",
-            "k_scan_sums", "k_tile_scan")
+# (the vcf step tokenizes without the public line table, count-free: the window parse
+# <true>, the two window scans and the per-window emit; the line-table forms
+# k_vcf_parse_windows<false> / k_vcf_emit<false> run only in the bench's setup)
+VCF_STEP = ("k_vcf_parse_windows<true>", "k_vcf_local_tiles", "k_vcf_local_top", "k_vcf_emit_local")
 
 
 def bench_line(path):
