@@ -70,7 +70,7 @@ WORKLOADS["load"] = dict(
                       "(K0 tokenize, K2 end+bin, K5 display attributes/FREQ/keys/paths as text)",
     bytes_per=None, kernel="k_vcf_format<write>")
 VCF_TILE = 1 << 19  # distinct synthetic lines, tiled on the device to n
-CEILING_LOG = os.path.join(ROOT, "profiles", "r05_hbm_ceiling.log")  # tools/hbm_ceiling.hip on MI355X
+CEILING_LOG = os.path.join(ROOT, "profiles", "hbm_ceiling_r05.jsonl")  # tools/hbm_ceiling.hip on MI355X
 
 
 def stream_ceiling(test: str, pmc_path: str, kernel_ms: float):
@@ -89,7 +89,7 @@ def stream_ceiling(test: str, pmc_path: str, kernel_ms: float):
     ach = pk["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
     return {"mix": test, "measured_traffic_GBps": ach, "ceiling_GBps": ceil, "frac": ach / ceil,
             "read_bytes": pk.get("hbm_read_bytes"), "write_bytes": pk.get("hbm_write_bytes"),
-            "source": "profiles/pmc_k7.json bytes / stage time; ceiling: profiles/r05_hbm_ceiling.log "
+            "source": "profiles/pmc_k7.json bytes / stage time; ceiling: profiles/hbm_ceiling_r05.jsonl "
                       "(tools/hbm_ceiling.hip, 16-B grid-stride streams, read:write 1:3, best access form)"}
 
 
