@@ -505,12 +505,14 @@ def _run_batch(n, seed, long_every=0):
     return d, keep
 
 
-@pytest.mark.parametrize("n,seed,long_every", [(4097, 1, 0), (70001, 2, 0), (262147, 3, 97), (1027, 4, 5)])
+@pytest.mark.parametrize("n,seed,long_every", [(4097, 1, 0), (70001, 2, 0), (262147, 3, 97), (1027, 4, 5),
+                                               (4_200_001, 5, 0)])
 def test_keyed_marks_list_only_possible_repeats(engine, n, seed, long_every):
     """The keyed K2 lists for K3 only the same-position records that could repeat an
     earlier primary key (the predecessor's lengths and refSNP id, or third or later at
     the position); keep after the resolve equals keep-first per primary key computed
-    here in Python, and K3 on its own, on runs built to hit the unlisted cases."""
+    here in Python, and K3 on its own, on runs built to hit the unlisted cases (4.2 M
+    records: the C4k form of the keyed K2, 256-record groups)."""
     from annotatedvdb_amd import _native as N
     from annotatedvdb_amd.engine import RecordBatch
     d, want = _run_batch(n, seed, long_every)
