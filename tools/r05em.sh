@@ -1,13 +1,16 @@
 #!/bin/bash
-# K0 count-free emit A/B (measured, not kept): the window stage from the block index against
-# the stage up to the last line's ALT (_lib/var/libavdb_emitold.so), vcf line twice each,
-# alternating, then a kernel summary of each.   tools/r05em.sh TAG
+# K0 count-free emit A/B: this library against _lib/var/libavdb_emitold.so (the committed
+# emit), tokenizer tests first, then the vcf line twice each, alternating, and a kernel
+# summary of each (round 5: the window stage from the block index; then per-lane span slots).   tools/r05em.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r05em}
 OUT=gpurun_out/$T
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 LIBS="annotatedvdb_amd/_lib/libavdb_hip.so annotatedvdb_amd/_lib/var/libavdb_emitold.so"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_tokenize.py -m gpu -x -q --timeout 300 --timeout-method thread \
+  -p no:cacheprovider > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
+tail -1 "$OUT/pytest.log"
 for rep in 1 2; do
   for lib in $LIBS; do
     v=$(basename "$lib" .so)
