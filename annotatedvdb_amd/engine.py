@@ -934,7 +934,7 @@ class Engine:
         rec_alt = self.empty(n_rec, torch.int32)
         rec_off = self.empty(n_lines + 1, torch.int64)
         heap_off = self.empty(n_lines + 1, torch.int64)
-        if n_lines == 0:
+        if n_rec == 0:  # (no line has a record: every offset is 0)
             rec_off.zero_()
             heap_off.zero_()
         else:

@@ -253,6 +253,42 @@ def test_k0_records_without_line_table(engine, which, count_free):
     assert torch.equal(a.rec_line, b.rec_line) and torch.equal(a.rec_alt, b.rec_alt)
 
 
+def _same_records(engine, text, opts=None):
+    """The count-free records path (vcf_tokenize(want_lines=False)) against the
+    tokenizer with its line table, on the same text (bytes or a device tensor)."""
+    a = engine.vcf_tokenize(text, opts)
+    b = engine.vcf_tokenize(text, opts, want_lines=False)
+    assert engine.last_vcf_path == "local"
+    assert a.n_lines == b.n_lines and a.records.n == b.records.n
+    assert torch.equal(a.rec_off, b.rec_off) and torch.equal(a.heap_off, b.heap_off)
+    for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "ext_id"):
+        assert torch.equal(getattr(a.records, f), getattr(b.records, f)), f
+    nh = int(a.heap_off[a.n_lines])
+    assert torch.equal(a.records.heap[:nh], b.records.heap[:nh])
+    assert torch.equal(a.rec_line, b.rec_line) and torch.equal(a.rec_alt, b.rec_alt)
+
+
+def test_k0_count_free_opts_views_and_wide_alleles(engine):
+    """The count-free path with a chromosome map and header width (avdb_vcf_opts), on
+    a misaligned device view, with REF / ALT of kilobytes (spans past the emit's
+    stage), a heap larger than the text, and the tiny texts."""
+    from annotatedvdb_amd import synth
+    lines = synth.vcf_text(4000, seed=43).decode().splitlines()
+    acc = {str(i + 1): "NC_%06d.11" % (i + 1) for i in range(22)}
+    back = {v: k for k, v in acc.items()}
+    text = "\n".join("\t".join([acc.get(l.split("\t")[0], "NC_X")] + l.split("\t")[1:]) for l in lines) + "\n"
+    _same_records(engine, text.encode(), engine.vcf_opts(chrom_map=engine.chrom_map(back), min_fields=8))
+    t = _synth(5000, 41)
+    _same_records(engine, torch.frombuffer(bytearray(b"xyz" + t), dtype=torch.uint8).to(engine.device)[3:])
+    base = _synth(3000, 37).split(b"\n")[:-1]
+    wide = b"3\t999\trs1\t" + b"A" * 6000 + b"\t" + b"C" * 5000 + b",G\t.\t.\t."
+    many = b"4\t1234\trs9\t" + b"ACGT" * 500 + b"\t" + b",".join([b"A"] * 400) + b"\t.\t.\t."
+    _same_records(engine, b"\n".join(base[:1000] + [wide] + base[1000:2000] + [many] * 3 + base[2000:]) + b"\n")
+    for tiny in (b"\n", b"\n\n\n", b"a", b"#x\n", b"1\t5\t.\tA\tG\t.\t.\t.",
+                 b"1\t5\t.\tA\tG\t.\t.\t.\r\n\r\n2\t7\trs3\tC\tT,.\t.\t.\t.\n"):
+        _same_records(engine, tiny)
+
+
 @pytest.mark.parametrize("pad", [0, 120])
 def test_k0_info_refsnp_edges(engine, pad):
     """The INFO refSNP scan in K0's staged window parse (the cases of
