@@ -205,7 +205,7 @@ def test_k0_window_parse_equals_starts_pass(engine, which):
 
 
 @pytest.mark.parametrize("which", ["golden", "dbsnp", "long", "big", "short", "edges", "empty", "no_final_nl",
-                                   "blank"])
+                                   "blank", "huge_heap"])
 @pytest.mark.parametrize("count_free", [True, False])
 def test_k0_records_without_line_table(engine, which, count_free):
     """vcf_tokenize(want_lines=False) — no public line table: the count-free path
@@ -216,7 +216,8 @@ def test_k0_records_without_line_table(engine, which, count_free):
     "short": 17-byte lines; "edges": blank lines, CRLF, lines of one field, a final
     line without '\n'; "blank": 8 M empty lines around dbSNP lines — more lines in a
     parse window than its 1,024 slots, so the count-free call falls back to the
-    counted path."""
+    counted path; "huge_heap": a line whose records hold 9 MB of heap (> 2^23 bytes,
+    past the slot's in-window offsets), so the count-free call falls back too."""
     if which == "short":
         text = b"".join(b"%d\t%d\t.\tA\tG\t.\t.\t.\n" % (1 + i % 9, 10 + i % 90) for i in range(300000))
     elif which == "golden":
@@ -236,6 +237,9 @@ def test_k0_records_without_line_table(engine, which, count_free):
         text = b""
     elif which == "blank":
         text = _synth(2000, 91) + b"\n" * 8_000_000 + _synth(2000, 93)
+    elif which == "huge_heap":
+        big = b"1\t5\t.\t" + b"A" * 90000 + b"\t" + b",".join([b"C"] * 100) + b"\t.\t.\t."
+        text = _synth(2000, 95) + big + b"\n" + _synth(2000, 97)
     elif which == "no_final_nl":
         text = _synth(5000, 89).rstrip(b"\n")
     else:
@@ -243,7 +247,7 @@ def test_k0_records_without_line_table(engine, which, count_free):
         text = b"\n".join(tile * 25) + b"\n"
     a = engine.vcf_tokenize(text)
     b = engine.vcf_tokenize(text, want_lines=False, count_free=count_free)
-    assert engine.last_vcf_path == ("counted" if which == "blank" or not count_free else "local")
+    assert engine.last_vcf_path == ("counted" if which in ("blank", "huge_heap") or not count_free else "local")
     assert b.lines is None and a.n_lines == b.n_lines and a.records.n == b.records.n
     assert torch.equal(a.rec_off, b.rec_off) and torch.equal(a.heap_off, b.heap_off)
     for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "ext_id"):
