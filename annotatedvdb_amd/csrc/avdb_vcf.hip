@@ -101,7 +101,8 @@ constexpr uintptr_t kNlStep = 16 * kWave;              // bytes per wave load
 #define AVDB_VCF_PARSE_OVER 1024  // bytes staged past a window (A/B knob; a multiple of 64)
 #endif
 #ifndef AVDB_VCF_PARSE_WAVES
-#define AVDB_VCF_PARSE_WAVES 6    // launch-bounds minimum waves per SIMD of the window parse (A/B knob)
+#define AVDB_VCF_PARSE_WAVES 5    // launch-bounds minimum waves per SIMD of the window parse (A/B knob; 6 is
+                                  // missed at 95 VGPRs and ran the same, profiles/k0_ab/r05_parse_waves_ab.log)
 #endif
 // (8.4 M dbSNP lines, the stage sized to the window: 20 / 24 / 28 KB windows with
 // 4 KB of overhang 1.86 / 1.78 / 1.89 ms per tokenize — 24 KB is the largest that
@@ -501,7 +502,7 @@ __device__ __forceinline__ uint32_t block_excl32(uint32_t v, uint32_t* s_w, uint
 // its own slots (window * kLocalCap + its line), and its line / record / heap totals
 // to LocalWin; a window with more than kLocalCap lines flags the overflow word.
 template <bool LOCAL>
-__global__ __launch_bounds__(kBlock, LOCAL ? 5 : AVDB_VCF_PARSE_WAVES) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
+__global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
                                                               size_t n_lines,
                                                               const unsigned long long* __restrict__ blk_off,
                                                               const uint32_t* __restrict__ wave_cnt,
