@@ -11,7 +11,7 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_c1.py tests/test_gpu_c4k.py
   --timeout-method thread -p no:cacheprovider > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 for rep in 1 2; do
-  for lib in annotatedvdb_amd/_lib/libavdb_hip.so annotatedvdb_amd/_lib/var/libavdb_r05base.so; do
+  for lib in ${LIBS:-annotatedvdb_amd/_lib/libavdb_hip.so annotatedvdb_amd/_lib/var/libavdb_r05base.so}; do
     v=$(basename "$lib" .so)
     for w in c4k c1; do
       AVDB_LIB=$lib timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 3 --cpu-baseline off \
