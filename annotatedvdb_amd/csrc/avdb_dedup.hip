@@ -322,9 +322,6 @@ __global__ __launch_bounds__(kBlock) void k_dedup_mark4(const uint8_t* __restric
   if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt;
 }
 
-#ifndef AVDB_K3_FASTPATH
-#define AVDB_K3_FASTPATH 1  // A/B knob: 0 sends every suspect through dedup_record
-#endif
 __global__ __launch_bounds__(kBlock) void k_dedup_resolve_list(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
@@ -352,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_resolve_list(
     // (chrom / pos, then lengths, then bytes, per candidate) takes the rest.
     bool settled = false;
     uint8_t k = 1;
-    if (AVDB_K3_FASTPATH && live) {
+    if (live) {
       const uint32_t r = rl[i], a = al[i], r1 = rl[i - 1], a1 = al[i - 1];
       const uint64_t e = ext ? ext[i] : 0ull, e1 = ext ? ext[i - 1] : 0ull;
       const uint64_t o = off[i], o1 = off[i - 1];

@@ -76,9 +76,6 @@ constexpr uint32_t nA0 = sizeof(AL0) - 1;
 constexpr uint32_t nA1 = sizeof(AL1) - 1;
 constexpr uint32_t nA2 = sizeof(AL2) - 1;
 constexpr uint32_t kAlPrefix = nA0 + AVDB_DIGEST_CHARS + nA1;  // ALT starts here
-#ifndef AVDB_SHA_UNROLL
-#define AVDB_SHA_UNROLL 0
-#endif
 static_assert(kAlPrefix == 68, "allele prefix");
 
 // (kLongBuckets, long_bucket, long_code: avdb_internal.hpp)
@@ -170,13 +167,7 @@ __device__ __forceinline__ void sha512_16(uint64_t& a, uint64_t& b, uint64_t& c,
 __device__ __forceinline__ void sha512_block(uint64_t* H, uint64_t* w) {
   uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], hh = H[7];
   sha512_16<false>(a, b, c, d, e, f, g, hh, w, 0);
-  // AVDB_SHA_UNROLL: all 80 rounds unrolled, so the round constants are
-  // immediates instead of scalar loads waited on in every loop trip
-#if AVDB_SHA_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
   for (int r = 16; r < 80; r += 16) sha512_16<true>(a, b, c, d, e, f, g, hh, w, r);
   H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += hh;
 }
@@ -504,9 +495,6 @@ __global__ __launch_bounds__(kBlock) void k_long_scatter_codes(const uint8_t* __
   }
 }
 
-#ifndef AVDB_K4_SCATTER_FLAGS
-#define AVDB_K4_SCATTER_FLAGS 1  // A/B knob: 0 scatters from the length arrays
-#endif
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_long_scatter(const uint32_t* __restrict__ rl,
                                                          const uint32_t* __restrict__ al, size_t n,
@@ -918,7 +906,7 @@ extern "C" int avdb_vrs_digest_ex(avdb_ctx* ctx, const uint8_t* chrom, const uin
   AVDB_LAUNCH_CHECK("k_long_scan");
   if (codes_ready)
     hipLaunchKernelGGL(k_long_scatter_codes, dim3(kCompactGrid), dim3(kBlock), 0, s, codes, n, counts, list);
-  else if (vec && is_long && AVDB_K4_SCATTER_FLAGS)
+  else if (vec && is_long)
     hipLaunchKernelGGL(k_long_scatter_flags, dim3(kCompactGrid), dim3(kBlock), 0, s, is_long, alt_len, n, counts,
                        list);
   else if (vec)

@@ -49,9 +49,6 @@ namespace avdb {
 // than it saves.
 typedef __attribute__((address_space(1))) uint8_t gbyte;
 typedef __attribute__((address_space(1))) U64u* gw_u64u;
-#ifndef AVDB_SINK_NT
-#define AVDB_SINK_NT 0  // A/B knob: the global sink's 8-byte stores as nontemporal stores
-#endif
 // per SIMD: the text window's LDS allows 4 workgroups per CU (re-checked after
 // the append sink: 4 waves with ~100 B of spills 5.5 ms, 3 waves without 6.2 ms)
 #ifndef AVDB_K5_WAVES
@@ -107,20 +104,7 @@ struct Dec {
   uint32_t n;
 };
 
-#ifndef AVDB_DEC_TEXT_SWAR
-#define AVDB_DEC_TEXT_SWAR 1  // digit count from the SWAR digits (0: a compare chain, A/B)
-#endif
 AVDB_HD Dec dec_text(uint32_t v) {
-  if (!AVDB_DEC_TEXT_SWAR) {
-    const uint32_t n = ndigits(v);
-    if (n <= 8) return Dec{ascii8(v) >> (8 * (8 - n)), 0ull, n};
-    const uint32_t hi = v / 100000000u;  // 1..42
-    const uint64_t b = ascii8(v - hi * 100000000u);
-    const uint32_t nh = n - 8;           // 1 or 2 leading digits
-    const uint64_t a = hi < 10u ? uint64_t('0' + hi)
-                                : (uint64_t('0' + hi / 10u) | (uint64_t('0' + hi % 10u) << 8));
-    return Dec{a | (b << (8 * nh)), b >> (64 - 8 * nh), n};
-  }
   // branch-free: the low 8 digits are converted either way, and the count of the
   // number's digits comes from them (the lowest nonzero digit byte is its first
   // digit: (d + 0x7F) sets bit 7 of each byte d >= 1, no carries for d <= 9)
@@ -137,16 +121,14 @@ AVDB_HD Dec dec_text(uint32_t v) {
 }
 
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
-#ifndef AVDB_SINK_ALLOR
-#define AVDB_SINK_ALLOR 1  // every LDS-sink word store as ds_or_b64 (no first-word branch; 0 = plain stores inside a span)
-#endif
 struct LdsImage {};  // constructor tag of the LDS sink
 
 // LDS = true (WRITE only): the sink renders into a workgroup's LDS image of its
 // output span instead of global memory, for a coalesced flush afterwards.  Every
 // LDS access is an aligned 8-byte word: the words a lane shares with its
-// neighbours (the first and the last of its span) are merged with ds_or_b64 into
-// the zeroed image, the words wholly inside its span are plain ds_write_b64.
+// neighbours (the first and the last of its span) must be merged, so every word
+// goes to the zeroed image as a ds_or_b64 (plain ds_write_b64 inside a lane's span
+// with a first-word branch measured slower, profiles/k7_ab/r04_sink_allor_ab.log).
 template <bool WRITE, bool LDS = false>
 struct Out {
   static constexpr bool kWrite = WRITE;
@@ -173,7 +155,6 @@ struct Out {
   struct LPending {  // LDS: bytes [p-k, p) of the current aligned word (the first
     uint64_t w = 0;  // word's low bytes belong to the previous lane: zero here)
     uint32_t k = 0;
-    bool first = true;
     uint32_t wq = 0;  // image word of byte p - k (32-bit: no 64-bit address math per append)
     lds_u64* img = nullptr;
   };
@@ -186,10 +167,7 @@ struct Out {
       pend.w |= x << (8 * k);
       if (k + t >= 8) {
         lds_u64* wp = pend.img + pend.wq;
-        if (AVDB_SINK_ALLOR || pend.first)
-          __hip_atomic_fetch_or(wp, pend.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        else *wp = pend.w;
-        pend.first = false;
+        __hip_atomic_fetch_or(wp, pend.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ++pend.wq;
         pend.w = k ? x >> (64 - 8 * k) : 0ull;
         pend.k = k + t - 8;
@@ -200,10 +178,7 @@ struct Out {
       const uint32_t k = pend.k;  // 0..7
       pend.w |= x << (8 * k);
       if (k + t >= 8) {
-        if constexpr (AVDB_SINK_NT)
-          __builtin_nontemporal_store(pend.w, reinterpret_cast<__attribute__((address_space(1))) uint64_t*>(base + p - k));
-        else
-          reinterpret_cast<gw_u64u>(base + p - k)->v = pend.w;
+        reinterpret_cast<gw_u64u>(base + p - k)->v = pend.w;
         pend.w = k ? x >> (64 - 8 * k) : 0ull;
         pend.k = k + t - 8;
       } else {
@@ -422,9 +397,6 @@ AVDB_HD void chrom_name(O& o, uint32_t c) {
 // eleven compile-time template words with the label and the 13 digit bits added
 // at constant byte positions (~40 instructions instead of a per-level loop).
 // Leaves are what SNVs and short indels get: nearly every record.
-#ifndef AVDB_LEAF_PATH
-#define AVDB_LEAF_PATH 1  // 0: the per-level loop for every level (A/B knob)
-#endif
 template <uint32_t L>
 struct LeafPath {
   static constexpr uint32_t kLen = 3 + L + 9 * 6 + 4 * 7;
@@ -453,9 +425,6 @@ struct LeafPath {
   }
 };
 
-#ifndef AVDB_LEAF_WORD32
-#define AVDB_LEAF_WORD32 1  // 0: K7 too uses the 64-bit template constants (A/B knob)
-#endif
 // W32: the caller's choice (K7: 32-bit halves; K5's write pass keeps the 64-bit
 // form: the 32-bit one moved its spills from SGPRs to scratch, 172 -> 288 B/lane)
 template <uint32_t L, uint32_t J, bool W32 = false>
@@ -526,7 +495,7 @@ AVDB_HD O leaf_path(O o, uint64_t label, uint32_t g) {
 template <bool W32 = false, class O>
 AVDB_HD O bin_path(O o, uint32_t c, uint32_t code) {
   const uint32_t level = code >> 28, g = code & 0x0FFFFFFFu;
-  if (AVDB_LEAF_PATH && level == 13 && c < 25 && (g >> 12) < 9) {
+  if (level == 13 && c < 25 && (g >> 12) < 9) {
     if (c < 9) return leaf_path<1, W32>(o, uint64_t('1' + c), g);
     if (c < 22) return leaf_path<2, W32>(o, uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8), g);
     return leaf_path<1, W32>(o, c == 22 ? uint64_t('X') : (c == 23 ? uint64_t('Y') : uint64_t('M')), g);
@@ -567,10 +536,16 @@ __device__ __forceinline__ uint32_t ndigits64(uint64_t v) {
   return 9u + (q <= 0xFFFFFFFFull ? ndigits(uint32_t(q)) : 9u + ndigits(uint32_t(q / 1000000000ull)));
 }
 
+// The key's layout, one definition for every kernel that needs it (the sizes, K7's
+// "label:pos:" prefix, the digest fill): the contig label of code c (0..24:
+// chromosomes.py:9-38 without "chr") is 1 or 2 bytes, and the body (ref:alt or
+// the 32 digest characters) starts after "label:pos:".
+__device__ __forceinline__ uint32_t key_label_width(uint32_t c) { return (c >= 9 && c < 22) ? 2u : 1u; }
+__device__ __forceinline__ uint32_t key_body_at(uint32_t c, uint32_t p) { return key_label_width(c) + 2u + ndigits(p); }
+
 // bytes of primary_key_generator.py:106-122's key for a labelled contig
 __device__ __forceinline__ uint32_t key_size(uint32_t c, uint32_t p, uint32_t r, uint32_t a, uint64_t e, bool lng) {
-  const uint32_t label = (c >= 9 && c < 22) ? 2u : 1u;
-  return label + 2u + ndigits(p) + (lng ? uint32_t(AVDB_DIGEST_CHARS) : r + 1u + a) +
+  return key_body_at(c, p) + (lng ? uint32_t(AVDB_DIGEST_CHARS) : r + 1u + a) +
          ((e && !(e >> 63)) ? 3u + ndigits64(e) : 0u);
 }
 
@@ -820,10 +795,6 @@ AVDB_HD bool number_plain(CP f, uint32_t n) {
   return nd <= 15;                            // repr == these digits
 }
 
-#ifndef AVDB_JSON_SWAR
-#define AVDB_JSON_SWAR 1  // FREQ numbers via the SWAR form: 0 never, 1 size pass only (default: in the
-                          // write pass its registers spill, 4.37 -> 4.86 ms), 2 both passes
-#endif
 
 // n <= 16 text bytes at s as two registers (independent aligned word reads; the
 // words hold only bytes of the text's own window, bytes past n are 0)
@@ -870,7 +841,7 @@ AVDB_HD O json_number(O o, CP f, uint32_t n) {
   // zeros (or "0"), '.', the fraction without trailing zeros (or "0") — two byte
   // ranges of the field, read once into registers.  Exponent forms and longer
   // fields take the digit-by-digit path below.
-  constexpr bool swar = AVDB_JSON_SWAR == 2 || (AVDB_JSON_SWAR == 1 && !O::kWrite);
+  constexpr bool swar = !O::kWrite;  // size pass only: in the write pass its registers spill (4.37 -> 4.86 ms)
   if (swar && n >= 1 && n <= 16) {
     uint64_t x0, x1;
     load16(f, n, &x0, &x1);

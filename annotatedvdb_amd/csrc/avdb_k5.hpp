@@ -18,9 +18,6 @@ enum : uint8_t { kLineGpu = 0, kLineHost = 1, kLineSkip = 2 };
 constexpr uint32_t kHostFlags = AVDB_VCF_FEW_FIELDS | AVDB_VCF_BAD_POS | AVDB_VCF_EXT_HOST |
                                 AVDB_VCF_CHROM_HOST | AVDB_VCF_EMPTY | AVDB_VCF_ID_HOST;
 constexpr int kMaxPops = 64;
-#ifndef AVDB_K5_PRELOAD
-#define AVDB_K5_PRELOAD 1  // A/B knob: 0 loads every record's inputs inside the ALT loop
-#endif
 
 struct FormatArgs {
   const uint8_t* text;
@@ -205,7 +202,7 @@ AVDB_HD uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, CP s, s
   const uint64_t r0 = r;
   uint32_t st0 = 0, code0 = 0, end0 = 0;
   bool keep0 = true;
-  if constexpr (WRITE && AVDB_K5_PRELOAD) {
+  if constexpr (WRITE) {
     st0 = A.status[r0];
     code0 = A.code[r0];
     end0 = A.end[r0];
@@ -243,7 +240,7 @@ AVDB_HD uint8_t format_line(const FormatArgs& A, const avdb_vcf_line& L, CP s, s
       a0 = a1 + 1;
       continue;
     }
-    const bool first = WRITE && AVDB_K5_PRELOAD && r == r0;
+    const bool first = WRITE && r == r0;
     const uint32_t st = first ? st0 : A.status[r];
     if (st == AVDB_STATUS_UNKNOWN_CHROM || st == AVDB_STATUS_OUT_OF_RANGE) return kLineHost;
     const uint32_t code = first ? code0 : A.code[r];

@@ -412,7 +412,7 @@ __device__ __forceinline__ void append_win(O& o, const uint64_t (&W)[kWinWords],
 
 // "label:pos:" (contigs 0..24) as up to 14 bytes in two words; returns its length
 __device__ __forceinline__ uint32_t key_prefix(uint32_t c, const Dec& d, uint64_t* p0, uint64_t* p1) {
-  const uint32_t L = (c >= 9 && c < 22) ? 2u : 1u;
+  const uint32_t L = key_label_width(c);
   const uint64_t lab = c < 9 ? uint64_t('1' + c)
                              : (c < 22 ? (uint64_t('0' + (c + 1) / 10u) | (uint64_t('0' + (c + 1) % 10u) << 8))
                                        : (c == 22 ? uint64_t('X') : (c == 23 ? uint64_t('Y') : uint64_t('M'))));
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
     if (live) {
       const bool lg = uint64_t(cur.r) + cur.a > A.max_seq_len;
       if (cur.c < uint32_t(A.n_chrom) && !(cur.e >> 63) && !(lg && !has_digest))
-        ksz = ((cur.c >= 9 && cur.c < 22) ? 2u : 1u) + 2u + dp.n + (lg ? uint32_t(AVDB_DIGEST_CHARS) : cur.r + 1u + cur.a) +
+        ksz = key_label_width(cur.c) + 2u + dp.n + (lg ? uint32_t(AVDB_DIGEST_CHARS) : cur.r + 1u + cur.a) +
               (cur.e ? 3u + (e32 ? de.n : ndigits64(cur.e)) : 0u);
       if (A.code && cur.cd != AVDB_BIN_NONE && cur.c < uint32_t(A.n_chrom)) psz = bin_path_size(cur.c, cur.cd);
     }
@@ -614,10 +614,10 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
       if (has_path && !path_over) {
         if (pst) {
           Out<true, true> o(LdsImage{}, pimg, po - (gp0 & ~uint64_t(15)));
-          bin_path<AVDB_LEAF_WORD32>(o, c, cd).finish();
+          bin_path<true>(o, c, cd).finish();
         } else {
           Out<true> o(A.path_out, po);
-          bin_path<AVDB_LEAF_WORD32>(o, c, cd).finish();
+          bin_path<true>(o, c, cd).finish();
         }
       }
     }
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(kBlock) void k_fill_digests(const uint8_t* __restri
       if ((st[k] & 0x0F) != AVDB_KEY_DIGEST_PENDING) continue;
       const size_t i = j0 + k;
       const uint32_t c = chrom[i];
-      const uint64_t at = key_off[i] + ((c >= 9 && c < 22) ? 2u : 1u) + 2u + ndigits(pos[i]);
+      const uint64_t at = key_off[i] + key_body_at(c, pos[i]);  // (the layout key_prefix renders)
       const u32x4* d = reinterpret_cast<const u32x4*>(digest + 32 * i);
       const u32x4 d0 = d[0], d1 = d[1];
       gw_u64u q = reinterpret_cast<gw_u64u>((gbyte*)key_out + at);

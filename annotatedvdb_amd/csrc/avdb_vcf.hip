@@ -26,9 +26,6 @@
 namespace avdb {
 
 constexpr int kVcfGrid = 1024;
-#ifndef AVDB_VCF_WINDOW_PARSE
-#define AVDB_VCF_WINDOW_PARSE 1  // parse windows with their own line starts (0: the k_vcf_starts pass, A/B)
-#endif
 
 __device__ __forceinline__ uint32_t count_byte(uint64_t x, uint64_t pattern) {
   return uint32_t(__popcll(zero_bytes_mask(x ^ pattern)));
@@ -1191,7 +1188,6 @@ static int parse_lines(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, si
     cw = static_cast<const char*>(workspace);
     windows = true;
   }
-  if (!AVDB_VCF_WINDOW_PARSE) windows = false;
   auto* rc = reinterpret_cast<unsigned long long*>(rec_off);
   auto* hc = reinterpret_cast<unsigned long long*>(heap_off);
   AVDB_HIP_TRY(hipMemsetAsync(rc + n_lines, 0, 8, s));
@@ -1299,7 +1295,12 @@ struct LocalLayout {
 static LocalLayout local_layout(size_t text_bytes) {
   auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
   LocalLayout L;
-  L.nw = size_t(kVcfGrid) * kVcfWaves * windows_per_chunk(text_bytes);
+  // only the windows of sub-chunks that hold text (the count pass's cut gives the
+  // sub-chunks past ceil(text_bytes / sub_chunk_bytes) no bytes): a short text gets
+  // a few windows' slots, not kVcfGrid * kVcfWaves of them (160 MiB)
+  const size_t per = sub_chunk_bytes(text_bytes);
+  const size_t live = per ? (text_bytes + per - 1) / per : 0;
+  L.nw = live * windows_per_chunk(text_bytes);
   L.nt = (L.nw + kTileWins - 1) / kTileWins;
   L.win = 256;
   L.blr = L.win + up(sizeof(LocalWin) * L.nw);

@@ -653,6 +653,20 @@ class Engine:
             t.view(torch.uint8).fill_(self.poison)
         return t
 
+    def scratch(self, name: str, nbytes: int) -> torch.Tensor:
+        """A workspace of at least ``nbytes`` bytes kept by the engine under ``name``
+        and reused by later calls (grown when too small).  Every user runs on the
+        engine's stream, so a later call's kernels are ordered after the earlier
+        call's; with ``poison`` set it is refilled like a fresh buffer."""
+        cache = self.__dict__.setdefault("_scratch", {})
+        t = cache.get(name)
+        if t is None or t.numel() < nbytes or t.device != self.device:
+            cache[name] = None
+            t = cache[name] = torch.empty(max(1, int(nbytes)), dtype=torch.uint8, device=self.device)
+        if self.poison is not None:
+            t.fill_(self.poison)
+        return t
+
     def set_option(self, option: int, value: int):
         """``avdb_ctx_set_option`` (launch shape only: ``N.OPT_K4_GRID``)."""
         N.check("avdb_ctx_set_option", self.lib.avdb_ctx_set_option(self.ctx, int(option), int(value)))
@@ -840,10 +854,12 @@ class Engine:
         count -> parse -> emit from 32-byte records in the parse workspace (also taken
         with ``count_free=False``)."""
         if not want_lines and count_free:
-            vb = self._vcf_tokenize_local(text, vcf_opts)
+            vb, text = self._vcf_tokenize_local(text, vcf_opts)
             if vb is not None:
                 self.last_vcf_path = "local"
                 return vb
+            # (a window overflowed its line slots: the counted path, on the text the
+            # count-free attempt already put on the device)
         self.last_vcf_path = "counted"
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
@@ -903,9 +919,11 @@ class Engine:
         return VcfBatch(text=text_t, n_lines=n_lines, lines=lines, rec_off=rec_off, heap_off=heap_off,
                         records=b, rec_line=rec_line, rec_alt=rec_alt)
 
-    def _vcf_tokenize_local(self, text, vcf_opts) -> Optional["VcfBatch"]:
-        """vcf_tokenize(want_lines=False) without the count pass; None when a parse
-        window overflowed its line slots (the caller then takes the counted path)."""
+    def _vcf_tokenize_local(self, text, vcf_opts):
+        """vcf_tokenize(want_lines=False) without the count pass: (batch, device
+        text), the batch None when a parse window overflowed its line slots (the
+        caller then takes the counted path on the same device text).  The slot
+        workspace (about 1.7x the text, avdb.h) is the engine's, reused across calls."""
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
             t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
@@ -917,14 +935,14 @@ class Engine:
         s = self._stream()
         sz = ctypes.c_size_t()
         self.lib.avdb_vcf_local_workspace_size(nb, ctypes.byref(sz))
-        ws = self.empty(int(sz.value), torch.uint8)
+        ws = self.scratch("vcf_local", int(sz.value))
         tot = torch.zeros(4, dtype=torch.int64, device=self.device)
         N.check("avdb_vcf_parse_local", self.lib.avdb_vcf_parse_local(
             self.ctx, tp, nb, N.ptr(ws), ws.numel(), ctypes.byref(vcf_opts) if vcf_opts is not None else None,
             N.ptr(tot), s))
         n_lines, n_rec, n_heap, overflow = (int(v) for v in tot.cpu().tolist())
         if overflow:
-            return None
+            return None, text_t
         b = RecordBatch(chrom=self.empty(n_rec, torch.uint8), pos=self.empty(n_rec, torch.int32),
                         allele_off=self.empty(n_rec, torch.int64),
                         ref_len=self.empty(n_rec, torch.int32), alt_len=self.empty(n_rec, torch.int32),
@@ -943,7 +961,7 @@ class Engine:
                 N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len), N.ptr(b.ext_id),
                 N.ptr(b.heap), N.ptr(rec_line), N.ptr(rec_alt), s))
         return VcfBatch(text=text_t, n_lines=n_lines, lines=None, rec_off=rec_off, heap_off=heap_off,
-                        records=b, rec_line=rec_line, rec_alt=rec_alt)
+                        records=b, rec_line=rec_line, rec_alt=rec_alt), text_t
 
     # -- K9: this rank's lines of a VCF text -----------------------------------
     def vcf_select(self, vb: "VcfBatch", assignment, rank: int, cut: int = 64_000_000) -> torch.Tensor:

@@ -72,10 +72,10 @@ class KeyedStep:
             sz = ctypes.c_size_t()
             engine.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
             self.ws4 = engine.empty(int(sz.value), torch.uint8)
-        if k4_grid:
-            engine.set_option(N.OPT_K4_GRID, int(k4_grid))
-        if k7_grid:
-            engine.set_option(N.OPT_K7_GRID, int(k7_grid))
+        # both grid options every time (0 = the library's default), so a capped grid
+        # from an earlier step on this engine never carries over
+        engine.set_option(N.OPT_K4_GRID, int(k4_grid))
+        engine.set_option(N.OPT_K7_GRID, int(k7_grid))
         self.side = torch.cuda.Stream(dev) if layout != "serial" else None
         self.out: Dict[str, object] = {}
 

@@ -303,7 +303,10 @@ int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size
  * avdb_vcf_emit_local writes the same records, heap, rec_line / rec_alt and per-line
  * rec_off / heap_off (totals[0] + 1 entries each, nullable) as count -> parse ->
  * avdb_vcf_emit_ws; with totals[3] != 0 the caller takes that counted path.  The
- * same text and workspace go to both calls. */
+ * same text and workspace go to both calls.  Workspace: 40 bytes of line slots per
+ * 24 KB window of text (1,024 slots of 32 + 8 bytes) plus 40 bytes of window totals,
+ * about 1.7x text_bytes at any size (a one-line text: two windows, 80 KB); the
+ * slots are written only for the lines present. */
 int avdb_vcf_local_workspace_size(size_t text_bytes, size_t* bytes);
 int avdb_vcf_parse_local(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
                          size_t workspace_bytes, const avdb_vcf_opts* opts, uint64_t* totals, void* stream);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # C1 step forms on one box: the graph (fork / serial layout) and plain launches,
-# 10 and 50 timed steps.  tools/c1_ab.sh TAG
+# 10 and 50 timed steps.  tools/ab/c1_ab.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-c1ab}
 OUT=gpurun_out/$T

@@ -2,7 +2,7 @@
 # C4k step layouts A/B on one box (pipeline.KeyedStep: serial | fork | overlap, and
 # the overlap layout with K4's persistent grid capped, AVDB_BENCH_K4_GRID workgroups,
 # and K7's write pass capped, AVDB_BENCH_K7_GRID one-wave workgroups).
-#   tools/c4k_layout_ab.sh TAG [layout:k4grid:k7grid ...]
+#   tools/ab/c4k_layout_ab.sh TAG [layout:k4grid:k7grid ...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-c4k_ab}; shift
 OUT=gpurun_out/$T

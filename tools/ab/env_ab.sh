@@ -1,7 +1,7 @@
 #!/bin/bash
 # Environment-knob A/B on the in-tree library: the WORKLOAD bench line with no
 # knob set and with each VAR=VALUE given, two passes, interleaved.
-#   tools/env_ab.sh TAG WORKLOAD VAR=VALUE [VAR=VALUE ...]
+#   tools/ab/env_ab.sh TAG WORKLOAD VAR=VALUE [VAR=VALUE ...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=$1; W=$2; shift 2
 OUT=gpurun_out/$T

@@ -2,7 +2,7 @@
 # K7 A/B: the K7 GPU parity tests on the in-tree library, then the keyed C4 probe
 # (tools/k7_probe.py, keys + paths) alternating the in-tree library with every
 # variant under annotatedvdb_amd/_lib/var/, then the C4k bench step for each.
-#   tools/k7_lib_ab.sh TAG
+#   tools/ab/k7_lib_ab.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-k7ab}
 OUT=gpurun_out/$T

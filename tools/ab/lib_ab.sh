@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of library variants built as annotatedvdb_amd/_lib/var/libavdb_*.so on one
-# bench workload: tools/lib_ab.sh WORKLOAD [STEPS]
+# bench workload: tools/ab/lib_ab.sh WORKLOAD [STEPS]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for lib in annotatedvdb_amd/_lib/var/libavdb_*.so; do

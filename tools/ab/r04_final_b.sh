@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-end measurement (part B): bench lines, kernel stats and traffic / SQ counters
-# from one box.  tools/r04_final_b.sh TAG
+# from one box.  tools/ab/r04_final_b.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r04fin}
 OUT=gpurun_out/$T

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end re-measurement after the K0 window parse: GPU suite, smoke, the default
 # line, C1, vcf, load, their kernel stats and the vcf / load traffic.
-#   tools/r04_final_c.sh TAG
+#   tools/ab/r04_final_c.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r04fd}
 OUT=gpurun_out/$T

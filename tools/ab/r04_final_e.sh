@@ -1,9 +1,8 @@
 #!/bin/bash
-# Round-5 measurement (part B): rocprofv3 kernel stats per workload, request-size
-# traffic (c4k, load, vcf), K7 counters, and the C2 FETCH_SIZE / WRITE_SIZE passes.
-#   tools/r05_final_b.sh TAG
+# Round-end measurement after the grid changes (part 2: kernel stats, traffic, K7 counters).
+#   tools/ab/r04_final_e.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-T=${1:-r05fb}
+T=${1:-r04fe}
 OUT=gpurun_out/$T
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -13,5 +12,4 @@ for w in c4k load vcf; do
   echo "traffic $w done"
 done
 bash tools/k7_counters.sh "$T/k7" > "$OUT/k7_counters.log" 2>&1 || { tail -5 "$OUT/k7_counters.log"; exit 1; }
-echo "k7 counters done"
-echo DONE-B
+echo DONE-E

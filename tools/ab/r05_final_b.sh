@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round-end measurement after the grid changes (part 2: kernel stats, traffic, K7 counters).
-#   tools/r04_final_e.sh TAG
+# Round-5 measurement (part B): rocprofv3 kernel stats per workload, request-size
+# traffic (c4k, load, vcf), K7 counters, and the C2 FETCH_SIZE / WRITE_SIZE passes.
+#   tools/ab/r05_final_b.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-T=${1:-r04fe}
+T=${1:-r05fb}
 OUT=gpurun_out/$T
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -12,4 +13,5 @@ for w in c4k load vcf; do
   echo "traffic $w done"
 done
 bash tools/k7_counters.sh "$T/k7" > "$OUT/k7_counters.log" 2>&1 || { tail -5 "$OUT/k7_counters.log"; exit 1; }
-echo DONE-E
+echo "k7 counters done"
+echo DONE-B

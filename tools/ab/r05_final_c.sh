@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 re-measurement after the K0 candidate pass and the one-stream C1 graph:
 # GPU suite, smoke, the default / C1 / C4k / vcf / load lines, their kernel stats and
-# the vcf / load traffic.   tools/r05_final_c.sh TAG
+# the vcf / load traffic.   tools/ab/r05_final_c.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r05fc}
 OUT=gpurun_out/$T

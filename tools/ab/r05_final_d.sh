@@ -2,7 +2,7 @@
 # Round-5 last measurement (after the K3 marks filter and the count-free K0 records path):
 #   part a: GPU suite, smoke, the default / C1 / C4k / vcf lines, C4k and vcf kernel summaries and traffic
 #   part b: vcf, load, C3, C4, C5, drop-in lines, vcf / C1 / load kernel summaries, vcf and load traffic
-#   tools/r05_final_d.sh TAG a|b
+#   tools/ab/r05_final_d.sh TAG a|b
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r05fd}
 OUT=gpurun_out/$T

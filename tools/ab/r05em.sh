@@ -1,7 +1,7 @@
 #!/bin/bash
 # K0 count-free emit A/B: this library against _lib/var/libavdb_emitold.so (the committed
 # emit), tokenizer tests first, then the vcf line twice each, alternating, and a kernel
-# summary of each (round 5: the window stage from the block index; then per-lane span slots).   tools/r05em.sh TAG
+# summary of each (round 5: the window stage from the block index; then per-lane span slots).   tools/ab/r05em.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r05em}
 OUT=gpurun_out/$T

@@ -1,7 +1,7 @@
 #!/bin/bash
 # K3 marks filtered in the keyed K2: the keyed / dedup GPU tests, then the C4k and C1
 # lines for the new library and the round's baseline (_lib/var/libavdb_r05base.so), alternating.
-#   tools/r05k3.sh TAG
+#   tools/ab/r05k3.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r05k3}
 OUT=gpurun_out/$T

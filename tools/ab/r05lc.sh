@@ -2,7 +2,7 @@
 # The count-free records path (avdb_vcf_parse_local / avdb_vcf_emit_local): tokenizer
 # and format tests, then the vcf line with it and with the counted path
 # (AVDB_BENCH_VCF_COUNTED=1), alternating, and a kernel summary of each.
-#   tools/r05lc.sh TAG
+#   tools/ab/r05lc.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r05lc}
 OUT=gpurun_out/$T

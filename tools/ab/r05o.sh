@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r05o}
 OUT=gpurun_out/$T
 mkdir -p "$OUT"
-bash tools/r05j.sh "$T" || exit 1
+bash tools/ab/r05j.sh "$T" || exit 1
 for rep in 1 2; do
   for lib in annotatedvdb_amd/_lib/libavdb_hip.so $(ls annotatedvdb_amd/_lib/var/libavdb_*.so 2>/dev/null); do
     v=$(basename "$lib" .so)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Window-parse launch bound A/B: AVDB_VCF_PARSE_WAVES=5 (_lib/var/libavdb_pw5.so) against the
 # shipped 6 (which the compiler misses: 95 VGPRs, five waves), on the counted vcf path and the
-# load line, alternating.   tools/r05pw.sh TAG
+# load line, alternating.   tools/ab/r05pw.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r05pw}
 OUT=gpurun_out/$T

@@ -1,7 +1,7 @@
 #!/bin/bash
 # K0 / K5 A/B: the vcf (or WORKLOAD) bench line for the in-tree library and every
 # variant under annotatedvdb_amd/_lib/var/ (two passes), after the tokenizer GPU tests.
-#   tools/vcf_ab.sh TAG [WORKLOAD]
+#   tools/ab/vcf_ab.sh TAG [WORKLOAD]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-vcfab}
 W=${2:-vcf}
