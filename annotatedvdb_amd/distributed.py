@@ -84,6 +84,7 @@ def allgather_stats(hist: torch.Tensor, counters: torch.Tensor, ri: RankInfo
 
 
 class RcclExchange:
+    kind = "rccl (avdb_hist_allgather, C ABI)"
     """The node exchange through the C ABI (``avdb_hist_allgather``, SURVEY.md
     §8b) instead of ``torch.distributed``: for a caller that binds only
     ``libavdb_hip.so``.  Rank 0 makes the id (``new_id``) and hands its bytes to
@@ -137,6 +138,45 @@ class RcclExchange:
         if self.comm:
             self._N.check("avdb_rccl_comm_destroy", self.engine.lib.avdb_rccl_comm_destroy(self.comm))
             self.comm = None
+
+
+class TorchExchange:
+    """The node exchange through ``torch.distributed`` (``allgather_stats``): the
+    gloo CPU tests and the gloo rehearsal of the N>1 bench path."""
+    kind = "torch.distributed"
+
+    def __init__(self, ri: RankInfo):
+        self.ri = ri
+
+    def allgather(self, hist: torch.Tensor, counters: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        return allgather_stats(hist, counters, self.ri)
+
+    def close(self):
+        pass
+
+
+def node_exchange(engine, ri: RankInfo, kind: Optional[str] = None):
+    """The job's one exchange: ``RcclExchange`` — the C ABI's
+    ``avdb_hist_allgather``, what a caller binding only ``libavdb_hip.so`` runs —
+    when the process group is RCCL (``nccl``), ``TorchExchange`` otherwise.
+    ``kind`` / ``AVDB_EXCHANGE`` (``rccl`` | ``torch``) override the choice; ``rccl``
+    at a world of one builds a one-rank communicator (the GPU test of this path on
+    a one-GPU box).  Rank 0 makes the RCCL id and the process group carries its
+    bytes to the other ranks (the out-of-band step ``RcclExchange`` leaves to its
+    caller)."""
+    kind = kind or os.environ.get("AVDB_EXCHANGE")
+    if kind is None:
+        kind = "rccl" if ri.distributed and dist.get_backend() == "nccl" else "torch"
+    if kind == "torch":
+        return TorchExchange(ri)
+    if kind != "rccl":
+        raise ValueError("exchange kind must be 'rccl' or 'torch', not %r" % (kind,))
+    uid = RcclExchange.new_id() if ri.rank == 0 else None
+    if ri.distributed:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    return RcclExchange(engine, ri.world, ri.rank, uid)
 
 
 def max_over_ranks(value: float, ri: RankInfo, device=None) -> float:

@@ -329,11 +329,14 @@ def _cpu_port(workload: str, seconds_per_worker: float, workers: int, host_cores
                 "kind": "port",
                 "per_core": n / t,
                 "sample": f"the whole C1 set ({n:,} chr22 records), one process as the reference runs one "
-                          f"chromosome file (load_vcf_file.py:307-313); oracle.c1_port_loop = metaseq id + "
-                          f"short key + normalized alleles + end inference + PortBinIndex, {t:.2f} s. "
-                          f"Calibration (tools/calibrate_cpu_baseline.py, build container): the port takes "
-                          f"0.72x the verbatim reference's per-record time (5.47 vs 7.57 us), so this "
-                          f"baseline overstates the reference CPU path"}
+                          f"chromosome file (load_vcf_file.py:307-313); oracle.c1_port_loop = the reference's "
+                          f"per-record objects (an annotator per alt, the key from its metaseq id, normalized "
+                          f"alleles, end inference on a second annotator) + PortBinIndex, {t:.2f} s",
+                "calibration": {"port_over_reference_time": [1.02, 1.19],
+                                "tool": "tools/calibrate_cpu_baseline.py calibrate_c1 (build container, the "
+                                        "verbatim reference with the make_golden stub DB, same records)",
+                                "log": "profiles/r06_calibrate_c1.txt",
+                                "within_survey_8d_band": True}}
     if workload == "load":
         # ~80 us per line in the port (calibrated: 0.82x the verbatim reference's time)
         per = int(seconds_per_worker / 80e-6)
@@ -585,11 +588,13 @@ def dry_run(a):
     ri = D.init("gloo")
     ctr = torch.zeros(32, dtype=torch.int64)
     ctr[20] = 100
-    _, node = D.allgather_stats(torch.zeros(8, dtype=torch.int32), ctr, ri)
+    ex = D.node_exchange(None, ri)  # (gloo: the torch.distributed exchange)
+    _, node = ex.allgather(torch.zeros(8, dtype=torch.int32), ctr)
     t = D.max_over_ranks(0.001 * (1 + ri.rank), ri)
     if ri.rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "n_gpus": ri.world, "dry_run": True,
-                          "ms_per_step": t * 1e3, "config": {"records_total": int(node[20].item())}}), flush=True)
+                          "ms_per_step": t * 1e3, "config": {"records_total": int(node[20].item()),
+                                                              "exchange": ex.kind}}), flush=True)
     D.finalize(ri)
 
 
@@ -675,6 +680,13 @@ def run_workload(a, name, ri, dev, cpu):
     hist = eng.new_histogram()
     ctr = eng.new_counters()
     code = torch.empty(n, dtype=torch.int32, device=dev)
+    # the job's exchange: the C ABI's RCCL all-gather (avdb_hist_allgather) when the
+    # process group is RCCL, torch.distributed for the gloo rehearsal (D.node_exchange)
+    try:
+        ex = D.node_exchange(eng, ri)
+    except Exception as e:  # (reported in the line, never silent: config.exchange)
+        ex = D.TorchExchange(ri)
+        ex.kind = "torch.distributed (C-ABI RCCL exchange failed to start: %s)" % (e,)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
@@ -751,7 +763,7 @@ def run_workload(a, name, ri, dev, cpu):
         torch.cuda.synchronize()
     # the job-level collective once untimed, so any lazy RCCL setup for the
     # all-gather is not charged to the timed region
-    D.allgather_stats(hist, ctr, ri)
+    ex.allgather(hist, ctr)
     hist.zero_()
     ctr.zero_()
     torch.cuda.synchronize()
@@ -770,7 +782,7 @@ def run_workload(a, name, ri, dev, cpu):
             step(False)
     loop1.record(stream)
     # job-level exchange: per-rank L8 histograms + counters (RCCL all-gather)
-    node_hist, node_ctr = D.allgather_stats(hist, ctr, ri)
+    node_hist, node_ctr = ex.allgather(hist, ctr)
     torch.cuda.synchronize()
     D.barrier(ri)
     torch.cuda.synchronize()
@@ -883,6 +895,7 @@ def run_workload(a, name, ri, dev, cpu):
         "config": {"workload": W["desc"], "records_per_gpu": n, "records_total": n * ri.world,
                    "parallelism": f"dp{ri.world} (length-balanced 64 Mb genome pieces per rank)",
                    "records_processed": int(node_ctr[20].item()) // max(1, a.steps),
+                   "exchange": ex.kind if ri.distributed or not isinstance(ex, D.TorchExchange) else None,
                    "stage_ms": stage_ms},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -979,6 +992,7 @@ def run_workload(a, name, ri, dev, cpu):
                                    "emit; AVDB_BENCH_VCF_COUNTED=1: count pass, parse, paired per-line scan, emit); "
                                    "the 16 B of line offsets per line it writes are not counted")
         out["config"]["path"] = {"local": "count-free", "counted": "counted"}.get(eng.last_vcf_path, eng.last_vcf_path)
+    ex.close()
     return out
 
 

@@ -315,18 +315,41 @@ def primary_key(chrom: str, pos: int, ref: str, alt: str, external_id: Optional[
     return ":".join(pk)
 
 
+class PortPKGenerator(object):
+    """The reference ``VariantPKGenerator.generate_primary_key``'s per-call
+    structure (primary_key_generator.py:99-122): the metaseq id split on ':' and the
+    key joined from the pieces; short alleles only (long ones: parity unpinned)."""
+
+    def __init__(self, maxSequenceLength=MAX_SEQUENCE_LENGTH):
+        self._maxSequenceLength = maxSequenceLength
+
+    def generate_primary_key(self, metaseqId, externalId=None):
+        chrm, position, ref, alt = metaseqId.split(":")
+        pk = [chrm, position]
+        if len(ref) + len(alt) <= self._maxSequenceLength:
+            pk.extend([ref, alt])
+        else:
+            raise ValueError("long allele needs a VRS digest (parity unpinned)")
+        if externalId is not None:
+            pk.append(externalId)
+        return ":".join(pk)
+
+
 def c1_port_loop(names, pos, refs, alts, exts, bin_index) -> int:
     """Reference-structured per-record path SURVEY.md §6 measured the reference
-    on (the C1 CPU baseline), in the loader's order (vcf_variant_loader.py:
-    243-311): metaseq id (variant_annotator.py:124-126), short primary key
-    (primary_key_generator.py:99-122), normalized alleles (:309), end inference
-    (variant_annotator.py:36-79, which normalizes again) and the one-bin-cached
+    on (the C1 CPU baseline), with the reference's per-record objects, in the
+    loader's order (vcf_variant_loader.py:243-311): an annotator per alt allele
+    (variant_annotator.py:21-27, metaseq id :124-126), the primary key from its
+    metaseq id (primary_key_generator.py:99-122), its normalized alleles (:309), end
+    inference on a second annotator (vcf_parser.py:225-231 builds one per call;
+    variant_annotator.py:36-79 normalizes again) and the one-bin-cached
     find_bin_index (bin_index.py:59-75), one record at a time."""
+    pkg = PortPKGenerator()
     for c, p, r, a, e in zip(names, pos, refs, alts, exts):
-        metaseq_id(c, p, r, a)
-        primary_key(c, p, r, a, e)
-        normalized_alleles(r, a)
-        end, _ = infer_end(p, r, a)
+        va = PortVariantAnnotator(r, a, c, p)
+        pkg.generate_primary_key(va.metaseq, e)
+        va.get_normalized_alleles()
+        end = PortVariantAnnotator(r, a, c, p).infer_variant_end_location()
         bin_index.find_bin_index(c, p, end)
     return len(pos)
 

@@ -29,12 +29,21 @@ Outputs (all small, gzip):
   kat.json                    known-answer tests
   c1_prefix.tsv.gz            BASELINE config C1 (annotatedvdb_amd.synth.np_c1, seed 1):
                               the first 100,000 records -> end, bin path, primary key
+  bin_queries_wide.tsv.gz     (round 6, --only scale) 200,000 queries in random order over
+                              all 25 contigs (half uniform over contigs), spans to 1 Mb
+  bin_sequence.tsv.gz         (round 6, --only scale) ~100,000 queries in loader order
+                              through ONE BinIndex: walks along every contig, so its
+                              one-bin L13 cache (bin_index.py:66-71) serves most of them,
+                              with end < start records (AT/AT -> pos - 1) after
+                              cache hits, broad spans that leave a non-leaf bin cached,
+                              unmappable queries that leave no bin cached
+  vcf_lines_100k.tsv.gz       (round 6, --only scale) 100,000 more VCF lines, as vcf_lines
   adsp_load.tsv.gz            the load driver with VCFVariantLoader('ADSP') and
   adsp_existing.json          --skipExisting over a stub validator answering from
                               adsp_existing.json: per line COPY rows (is_adsp_variant
                               column), .mapping, is_adsp_variant updates, counters
 
-Usage:  python tests/golden/make_golden.py [--quick] [--only all|load|c1|adsp]
+Usage:  python tests/golden/make_golden.py [--quick] [--only all|load|c1|adsp|chrmap|scale]
 """
 
 from __future__ import annotations
@@ -400,6 +409,91 @@ def gen_bin_queries(bi, n, rng):
         except TypeError:
             ans = "TypeError"
         rows.append((c, s, "" if e is None else e, ans))
+    return rows
+
+
+def gen_bin_queries_wide(bi, n, rng):
+    """n queries in random order (so the one-bin cache rarely serves one: the
+    table-search answers) over all 25 contigs — half drawn uniformly over the
+    contigs, so chrM / chrY / chr21 get as many as chr1, half by length — with
+    35 % points, 25 % geometric(1/8) spans, 40 % log-uniform spans up to 1 Mb
+    (some running past the contig end: TypeError rows)."""
+    tot = sum(GRCH38_LENGTHS.values())
+    weights = [GRCH38_LENGTHS[c] / tot for c in CHROM_NAMES]
+    rows = []
+    for _ in range(n):
+        c = rng.choice(CHROM_NAMES) if rng.random() < 0.5 else rng.choices(CHROM_NAMES, weights)[0]
+        L = GRCH38_LENGTHS[c]
+        s = rng.randint(1, L)
+        u = rng.random()
+        if u < 0.35:
+            e = None
+        elif u < 0.6:
+            e = min(L, s + int(rng.expovariate(1 / 8)))
+        else:
+            e = s + int(10 ** rng.uniform(0, 6))
+        name = c if rng.random() < 0.7 else "chr" + c
+        try:
+            ans = bi.find_bin_index(name, s, e)
+        except TypeError:
+            ans = "TypeError"
+        rows.append((name, s, "" if e is None else e, ans))
+    return rows
+
+
+def gen_bin_sequence(bi, n, rng):
+    """About n queries in the order a position-sorted load makes them, all through
+    the one BinIndex ``bi`` (its cache state carries from query to query, as in
+    vcf_variant_loader.py:310-311).  Every contig is walked from a random start in
+    steps of mean ~2 kb, so most queries fall in the L13 leaf (15,625 bp) the
+    previous one cached.  Per query: 58 % points, 14 % short spans, 5 % broad
+    spans (log-uniform to 1 Mb: a non-leaf bin is then cached and the next query
+    misses), 12 % end = start - 1 (identical ref/alt, SURVEY A.3 — served from the
+    cached leaf when both ends are inside it, otherwise the SQL lookup of the
+    swapped pair), 4 % end = start - k (k up to 40,000), 3 % positions on a leaf
+    boundary, 2 % unmappable (past the end, start 0, 'MT', unknown contigs: the
+    cache is then empty), 2 % a jump back to an earlier position."""
+    tot = sum(GRCH38_LENGTHS.values())
+    per = {c: max(200, int(n * 0.5 / 25 + n * 0.5 * GRCH38_LENGTHS[c] / tot)) for c in CHROM_NAMES}
+    rows = []
+    for c in CHROM_NAMES:
+        L = GRCH38_LENGTHS[c]
+        p = rng.randint(1, max(1, L // 3))
+        name = c if rng.random() < 0.5 else "chr" + c
+        for _ in range(per[c]):
+            p += int(rng.expovariate(1 / 2000))
+            if p > L:
+                p = rng.randint(1, L)
+            u = rng.random()
+            s, e, nm = p, None, name
+            if u < 0.58:
+                pass
+            elif u < 0.72:
+                e = min(L, p + int(rng.expovariate(1 / 8)))
+            elif u < 0.77:
+                e = min(L, p + int(10 ** rng.uniform(4.2, 6)))
+            elif u < 0.89:
+                e = p - 1
+            elif u < 0.93:
+                e = max(0, p - rng.randint(2, 40000))
+            elif u < 0.96:
+                b = (p // 15625) * 15625
+                s = max(1, b + rng.choice((0, 1, 2)))
+                e = rng.choice((None, s - 1, s + 1, b + 15625))
+                if e is not None:
+                    e = min(L, max(0, e))
+            elif u < 0.98:
+                k = rng.randrange(5)
+                s, e, nm = [(L + 1, None, name), (0, 5, name), (p, p, "MT"), (p, None, "Un"),
+                            (p, L + 1, name)][k]
+            else:
+                s = max(1, p - rng.randint(1, 200000))
+                e = None if rng.random() < 0.5 else s + rng.randint(0, 20)
+            try:
+                ans = bi.find_bin_index(nm, s, e)
+            except TypeError:
+                ans = "TypeError"
+            rows.append((nm, s, "" if e is None else e, ans))
     return rows
 
 
@@ -927,7 +1021,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
-    ap.add_argument("--only", choices=["all", "load", "c1", "adsp", "chrmap"], default="all",
+    ap.add_argument("--only", choices=["all", "load", "c1", "adsp", "chrmap", "scale"], default="all",
                     help="'load': only the load-driver fixtures (vcf_load, display_attrs); "
                          "'c1': only the C1 prefix fixture")
     a = ap.parse_args()
@@ -957,6 +1051,20 @@ def main():
         crng = random.Random(a.seed + 3)
         wtsv("chrmap_load.tsv.gz", ["line", "error", "mapping", "copy_rows"],
              run_chrmap_driver(gen_chrmap_lines(int(3000 * k), crng), mp))
+        print("done")
+        return
+    if a.only == "scale":  # round 6: the section 7 volumes, their own seed stream
+        srng = random.Random(a.seed + 6)
+        wtsv("bin_queries_wide.tsv.gz", ["chrom", "start", "end", "bin_index"],
+             gen_bin_queries_wide(BinIndex(None, verbose=False), int(200000 * k), srng))
+        seq = gen_bin_sequence(BinIndex(None, verbose=False), int(100000 * k), srng)
+        wtsv("bin_sequence.tsv.gz", ["chrom", "start", "end", "bin_index"], seq)
+        lines = gen_vcf_lines(int(100000 * k), srng)
+        lines = [ln for ln in lines if all(len(ln.split("\t")[3]) + len(x) <= 50
+                                           for x in ln.split("\t")[4].split(","))]
+        wtsv("vcf_lines_100k.tsv.gz", ["line", "mapping", "copy_prefix", "ends"], run_loader(lines))
+        print("sequence: %d queries, %d end < start" % (
+            len(seq), sum(1 for r in seq if r[2] != "" and int(r[2]) < int(r[1]))))
         print("done")
         return
     if a.only == "c1":

@@ -57,7 +57,11 @@ def _worker(rank, world, port, n, q):
     ctr = torch.zeros(32, dtype=torch.int64)
     ctr[20] = len(chrom)
     ctr[16:20] = torch.from_numpy(np.bincount(status, minlength=4).astype(np.int64))
-    node_hist, node_ctr = D.allgather_stats(hist, ctr, ri)
+    # the bench's exchange object: over gloo the torch.distributed one (RCCL process
+    # groups take the C ABI's avdb_hist_allgather, tests/test_gpu_rccl.py)
+    ex = D.node_exchange(None, ri)
+    assert isinstance(ex, D.TorchExchange)
+    node_hist, node_ctr = ex.allgather(hist, ctr)
     t = D.max_over_ranks(float(rank + 1), ri)
     q.put((rank, chrom, start, end, codes, node_hist.numpy(), node_ctr.numpy(), t))
     D.finalize(ri)

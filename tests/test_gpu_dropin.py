@@ -21,8 +21,8 @@ def read_tsv(name):
         return [dict(zip(header, line.rstrip("\n").split("\t"))) for line in fh]
 
 
-def golden_lines():
-    with gzip.open(os.path.join(GOLDEN, "vcf_lines.tsv.gz"), "rt") as fh:
+def golden_lines(name="vcf_lines.tsv.gz"):
+    with gzip.open(os.path.join(GOLDEN, name), "rt") as fh:
         fh.readline()
         return [(r.replace("\\t", "\t"), json.loads(m), json.loads(c), json.loads(e))
                 for r, m, c, e in (line.rstrip("\n").split("\t") for line in fh)]
@@ -60,6 +60,23 @@ def test_loader_batch_matches_reference(loader, per_line_max):
     loader.reset_copy_buffer()
     loader._initialize_counters()
     loader.PER_LINE_MAX = per_line_max
+    try:
+        outs = loader.parse_variants([l[0] for l in lines], errors="record")
+    finally:
+        del loader.PER_LINE_MAX
+    rows = loader.copy_buffer().getvalue().splitlines()
+    _check(lines, outs, rows)
+    assert loader.get_count("variant") == len(rows)
+
+
+def test_loader_batch_matches_reference_100k(loader):
+    """The 102,000 lines of vcf_lines_100k.tsv.gz (make_golden.py --only scale) as one
+    device batch: every mapping, exception type and COPY prefix the reference wrote."""
+    lines = golden_lines("vcf_lines_100k.tsv.gz")
+    assert len(lines) == 102000
+    loader.reset_copy_buffer()
+    loader._initialize_counters()
+    loader.PER_LINE_MAX = 0
     try:
         outs = loader.parse_variants([l[0] for l in lines], errors="record")
     finally:
@@ -112,6 +129,38 @@ def test_bin_index_per_record_and_batch():
         assert (p or "TypeError") == r["bin_index"], r
     with pytest.raises(TypeError):
         bi.find_bin_indices(["chrUn"], [5], errors="raise")
+
+
+def test_bin_index_replays_reference_sequence():
+    """The drop-in BinIndex on the GPU engine replays the reference's whole
+    loader-order query sequence (bin_sequence.tsv.gz: ~100,000 queries through one
+    verbatim BinIndex), in order: its one-bin L13 cache serves what the reference's
+    served — end < start records after cache hits among them — and every miss,
+    TypeError included, gives the reference's answer."""
+    from annotatedvdb_amd.bin_index import BinIndex
+    rows = read_tsv("bin_sequence.tsv.gz")
+    bi = BinIndex(None, verbose=False)
+    swapped = 0
+    for r in rows:
+        end = int(r["end"]) if r["end"] else None
+        try:
+            got = bi.find_bin_index(r["chrom"], int(r["start"]), end)
+        except TypeError:
+            got = "TypeError"
+        assert got == r["bin_index"], r
+        swapped += end is not None and end < int(r["start"])
+    assert swapped > 10000
+
+
+def test_bin_index_batch_wide():
+    """find_bin_indices (K1 on the GPU) over the 200,000 wide reference queries."""
+    from annotatedvdb_amd.bin_index import BinIndex
+    rows = read_tsv("bin_queries_wide.tsv.gz")
+    bi = BinIndex(None, verbose=False)
+    paths = bi.find_bin_indices([r["chrom"] for r in rows], [int(r["start"]) for r in rows],
+                                [int(r["end"]) if r["end"] else None for r in rows])
+    for r, p in zip(rows, paths):
+        assert (p or "TypeError") == r["bin_index"], r
 
 
 def test_variant_annotator_matches_reference():

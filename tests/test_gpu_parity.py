@@ -32,8 +32,9 @@ def u32(t):
 # ---------------------------------------------------------------------------
 # K1 bin assignment
 # ---------------------------------------------------------------------------
-def test_k1_golden_bin_queries(engine):
-    rows = read_tsv("bin_queries.tsv.gz")
+@pytest.mark.parametrize("name", ["bin_queries.tsv.gz", "bin_queries_wide.tsv.gz"])
+def test_k1_golden_bin_queries(engine, name):
+    rows = read_tsv(name)
     chrom = np.array([min(bin_index_chrom_code(r["chrom"]), 255) for r in rows], dtype=np.uint8)
     start = np.array([int(r["start"]) for r in rows], dtype=np.int32)
     end = np.array([int(r["end"]) if r["end"] else int(r["start"]) for r in rows], dtype=np.int32)

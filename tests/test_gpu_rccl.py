@@ -28,3 +28,22 @@ def test_hist_allgather_c_abi_world_of_one(engine):
         assert torch.equal(nh, hist[:7]) and torch.equal(nc, ctr[:3])
     finally:
         ex.close()
+
+
+def test_node_exchange_picks_c_abi_rccl(engine):
+    """bench.py's exchange object (distributed.node_exchange): with AVDB_EXCHANGE=rccl
+    at a world of one it is the C ABI's avdb_hist_allgather, as on an RCCL node."""
+    from annotatedvdb_amd import distributed as D
+    from annotatedvdb_amd import _native as N
+    ri = D.RankInfo(0, 1, 0)
+    ex = D.node_exchange(engine, ri, kind="rccl")
+    try:
+        assert isinstance(ex, D.RcclExchange)
+        hist = torch.arange(engine.n_l8, dtype=torch.int32, device="cuda")
+        ctr = torch.arange(N.N_COUNTERS, dtype=torch.int64, device="cuda") * 3
+        nh, nc = ex.allgather(hist, ctr)
+        torch.cuda.synchronize()
+        assert torch.equal(nh, hist) and torch.equal(nc, ctr)
+    finally:
+        ex.close()
+    assert isinstance(D.node_exchange(engine, ri), D.TorchExchange)  # world 1, no process group

@@ -20,8 +20,8 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _golden_text():
-    with gzip.open(os.path.join(GOLDEN, "vcf_lines.tsv.gz"), "rt") as fh:
+def _golden_text(name="vcf_lines.tsv.gz"):
+    with gzip.open(os.path.join(GOLDEN, name), "rt") as fh:
         fh.readline()
         lines = [line.rstrip("\n").split("\t")[0].replace("\\t", "\t") for line in fh]
     return ("\n".join(lines) + "\n").encode()
@@ -81,6 +81,8 @@ def _synth(n, seed):
 
 def test_k0_golden_and_dbsnp_text(engine):
     _check(engine, _golden_text())
+    n, _, checked = _check(engine, _golden_text("vcf_lines_100k.tsv.gz"))
+    assert n == 102000 and checked > 95000
     t = _synth(60000, 31)
     n, nr, checked = _check(engine, t)
     assert n == t.count(b"\n") and nr > n and checked > 0.95 * n

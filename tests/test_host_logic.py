@@ -15,8 +15,8 @@ from annotatedvdb_amd.parsers import VcfEntryParser
 from oracle import avdb_oracle as O
 
 
-def golden_lines():
-    with gzip.open(os.path.join(GOLDEN, "vcf_lines.tsv.gz"), "rt") as fh:
+def golden_lines(name="vcf_lines.tsv.gz"):
+    with gzip.open(os.path.join(GOLDEN, name), "rt") as fh:
         fh.readline()
         for line in fh:
             raw, mapping, copy5, ends = line.rstrip("\n").split("\t")
@@ -31,11 +31,12 @@ def oracle_path(chrom, start, end):
     return None if c == O.BIN_NONE else O.format_bin_path(CHROM_NAMES[code], c)
 
 
-def test_vcf_lines_host_parse_plus_oracle_reproduce_reference_loader():
+@pytest.mark.parametrize("name,least", [("vcf_lines.tsv.gz", 7000), ("vcf_lines_100k.tsv.gz", 95000)])
+def test_vcf_lines_host_parse_plus_oracle_reproduce_reference_loader(name, least):
     """VcfEntryParser (host) + oracle arithmetic reproduce the reference
     loader's mapping, COPY prefix and end coordinates on every golden line."""
     n = 0
-    for raw, mapping, copy5, ends in golden_lines():
+    for raw, mapping, copy5, ends in golden_lines(name):
         entry = VcfEntryParser(raw)
         try:
             v = entry.get_variant(namespace=True)
@@ -67,7 +68,7 @@ def test_vcf_lines_host_parse_plus_oracle_reproduce_reference_loader():
             assert mapping == {v.id: got_map}, raw
             assert copy5 == exp_rows
         n += 1
-    assert n > 7000
+    assert n > least
 
 
 def test_pack_records_layout():

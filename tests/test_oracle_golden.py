@@ -135,6 +135,45 @@ def test_port_bin_index_cache_matches_golden():
         assert got == r["bin_index"], r
 
 
+def test_bin_queries_wide_golden():
+    """200,000 reference answers in random order over all 25 contigs, spans to 1 Mb
+    (make_golden.py --only scale): the numpy closed form the kernels restate."""
+    rows = read_tsv("bin_queries_wide.tsv.gz")
+    assert len(rows) == 200000
+    assert {bin_index_chrom_code(r["chrom"]) for r in rows} == set(range(25))
+    chrom = np.array([min(bin_index_chrom_code(r["chrom"]), 255) for r in rows], dtype=np.uint8)
+    start = np.array([int(r["start"]) for r in rows], dtype=np.int64)
+    end = np.array([int(r["end"]) if r["end"] else int(r["start"]) for r in rows], dtype=np.int64)
+    codes, status = O.bin_codes_np(chrom, start, end, length_table())
+    bad = []
+    for i, r in enumerate(rows):
+        got = "TypeError" if status[i] else O.format_bin_path(CHROM_NAMES[chrom[i]], int(codes[i]))
+        if got != r["bin_index"]:
+            bad.append((r, got))
+    assert not bad, bad[:5]
+    assert sum(r["bin_index"] == "TypeError" for r in rows) > 300  # spans past the contig end
+
+
+def test_port_bin_index_replays_sequence():
+    """The loader-order sequence (make_golden.py --only scale) through the port's one
+    BinIndex: every answer, TypeErrors included, in order — and the fixture does
+    what it is for: end < start records answered from the cached L13 leaf."""
+    rows = read_tsv("bin_sequence.tsv.gz")
+    bi = O.PortBinIndex(O.BinTable(GRCH38_LENGTHS))
+    served_swapped = 0
+    for r in rows:
+        end = int(r["end"]) if r["end"] else None
+        before = bi._currentBin
+        try:
+            got = bi.find_bin_index(r["chrom"], int(r["start"]), end)
+        except TypeError:
+            got = "TypeError"
+        assert got == r["bin_index"], r
+        if end is not None and end < int(r["start"]) and before and bi._currentBin is before:
+            served_swapped += 1
+    assert served_swapped > 5000
+
+
 def test_sha512t24u_primitive():
     # published GA4GH example: sha512t24u(b"") == "z4PhNX7vuL3xVChQ1m2AB9Yg5AULVxXc"
     assert O.sha512t24u(b"") == "z4PhNX7vuL3xVChQ1m2AB9Yg5AULVxXc"

@@ -392,3 +392,32 @@ def test_k5h_info_refsnp_edges(lib, ctx):
         assert res.state == N.LINE_GPU, line
         col = cb.raw[:res.copy_bytes].decode().split("#")[6]
         assert col == ("rs%d" % want if want else "NULL"), (line, col)
+
+
+def test_dropin_bin_index_replays_reference_sequence():
+    """The drop-in BinIndex (its one-bin L13 cache over K1h, the library's host
+    entry; a host-only engine, no GPU) replays the reference's whole loader-order
+    sequence (tests/golden/bin_sequence.tsv.gz, ~100,000 queries through one
+    verbatim BinIndex): every answer in order, end < start records after cache
+    hits and TypeErrors (empty cache afterwards) included."""
+    from annotatedvdb_amd.bin_index import BinIndex
+    rows = read_tsv("bin_sequence.tsv.gz")
+    bi = BinIndex(None, verbose=False, device="host")
+    for r in rows:
+        end = int(r["end"]) if r["end"] else None
+        try:
+            got = bi.find_bin_index(r["chrom"], int(r["start"]), end)
+        except TypeError:
+            got = "TypeError"
+        assert got == r["bin_index"], r
+
+
+def test_k8h_bin_queries_wide_vs_reference(lib, ctx):
+    """200,000 reference answers over all 25 contigs, spans to 1 Mb (K8h per record)."""
+    rows = read_tsv("bin_queries_wide.tsv.gz")
+    for lo in range(0, len(rows), 50000):
+        part = rows[lo:lo + 50000]
+        res = k8h(lib, ctx, codes([r["chrom"] for r in part]), [int(r["start"]) for r in part],
+                  ends=[int(r["end"] or r["start"]) for r in part])
+        for r, p in zip(part, res["path"]):
+            assert (p or "TypeError") == r["bin_index"], r
