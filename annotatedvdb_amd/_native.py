@@ -102,6 +102,7 @@ EXPORTED_SYMBOLS = [
     "avdb_primary_keys_onepass_workspace_size", "avdb_primary_keys_onepass", "avdb_primary_keys_onepass_ex",
     "avdb_primary_keys_fill_digests",
     "avdb_record_prep_keyed",
+    "avdb_keyed_prep_workspace_size", "avdb_keyed_prep", "avdb_keyed_prep_lookback_errors",
     "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
     "avdb_small_prep", "avdb_small_prep_host", "avdb_bin_path_host", "avdb_annotate_host", "avdb_host_alloc", "avdb_host_free",
     "avdb_rccl_unique_id", "avdb_rccl_comm_init", "avdb_rccl_comm_destroy",
@@ -115,6 +116,7 @@ KEYS_DIGEST_DEFERRED = 2  # AVDB_KEYS_DIGEST_DEFERRED
 OPT_K4_GRID, OPT_K7_GRID = 1, 2  # avdb_ctx_set_option
 KEYED_TOTALS, KEYED_LONG_CODES, KEYED_DEDUP_MARKS = 1, 2, 4  # avdb_record_prep_keyed's *totals_written bits
 DEDUP_MARKED = 1  # AVDB_DEDUP_MARKED
+DEDUP_ONEPASS = 2  # AVDB_DEDUP_ONEPASS (marks from avdb_keyed_prep)
 DIGEST_CODES_READY = 1  # AVDB_DIGEST_CODES_READY
 SMALL_MAX = 65536
 
@@ -202,6 +204,10 @@ def _sig(lib):
     f.avdb_record_prep_keyed.argtypes = list(f.avdb_record_prep.argtypes)[:-1] + [P, U32, I32, I32, P, SZ, P, SZ,
                                                                                  P, SZ, P, ctypes.POINTER(I32), P]
     f.avdb_primary_keys_fill_digests.argtypes = [P, P, P, SZ, P, P, P, P, P]
+    f.avdb_keyed_prep_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
+    f.avdb_keyed_prep.argtypes = [P, P, P, P, P, P, P, SZ, P, SZ, U32, P, P, P, P, P, P, SZ, P, SZ, P, SZ, P,
+                                  P, P, P, SZ, P, SZ, P, U32, ctypes.POINTER(I32), P]
+    f.avdb_keyed_prep_lookback_errors.argtypes = [P, P, ctypes.POINTER(U32)]
     f.avdb_primary_keys_bound.argtypes = [SZ, SZ, ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
     f.avdb_primary_keys_onepass_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]

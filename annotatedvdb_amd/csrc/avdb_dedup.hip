@@ -490,9 +490,14 @@ extern "C" int avdb_pk_dedup_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint3
     avdb_set_error("avdb_pk_dedup_ex: null array");
     return AVDB_EINVAL;
   }
+  if (flags & ~uint32_t(AVDB_DEDUP_MARKED | AVDB_DEDUP_ONEPASS)) {
+    avdb_set_error("avdb_pk_dedup_ex: unknown flags 0x%x", flags);
+    return AVDB_EINVAL;
+  }
   unsigned grid = 0;
   size_t slice = 0;
-  keyed_prep_layout(ctx, n, &grid, &slice);
+  if (flags & AVDB_DEDUP_ONEPASS) keyed_onepass_dd_layout(n, &grid, &slice);
+  else keyed_prep_layout(ctx, n, &grid, &slice);
   if (!grid || workspace_bytes < kListHead + 4 * size_t(grid) * slice) {
     avdb_set_error("avdb_pk_dedup_ex: the workspace does not hold the keyed K2's suspect lists");
     return AVDB_ERANGE;

@@ -305,6 +305,8 @@ constexpr unsigned kDedupMaxGroups = kDedupListHead / 4;
 // the keyed K2's workgroups and the records each may list as suspects (one slice
 // of the K3 list per workgroup; avdb_bins.hip), for K3's resolve over them
 void keyed_prep_layout(const avdb_ctx* ctx, size_t n, unsigned* grid, size_t* slice);
+// K3's list layout under the one-pass keyed prep (avdb_keyed_prep, avdb_keys.hip)
+void keyed_onepass_dd_layout(size_t n, unsigned* grid, size_t* slice);
 // K4 workspace: the per-record bucket codes the keyed K2 fills (avdb_digest.hip)
 uint8_t* vrs_long_codes_of(void* workspace, size_t n);
 // K4's per-(contig, digit count) SequenceLocation block-1 table (host)

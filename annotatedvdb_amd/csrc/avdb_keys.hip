@@ -437,6 +437,146 @@ __device__ __forceinline__ void append2(O& o, uint64_t w0, uint64_t w1, uint32_t
   }
 }
 
+// One 64-record tile of the write pass (K7's k_record_keys_v2 and the one-pass
+// keyed prep k_keyed_onepass): the records' sizes scanned over the wave from
+// run_k / run_p (advanced by the tile's totals), their offsets and states, the
+// key and path text rendered into the wave's LDS images and flushed.  cur: record
+// t0 + lane (live: t0 + lane < A.n).
+__device__ __forceinline__ void key_tile(const KeyArgs& A, const KeyTileIn& cur, size_t t0, uint64_t& run_k,
+                                         uint64_t& run_p, lds_u64* kimg, lds_u64* pimg, const Heap& hheap,
+                                         uint32_t lane) {
+  const size_t i = t0 + lane;
+  const bool live = i < A.n;
+  const uint32_t n_chrom = uint32_t(A.n_chrom);
+  const bool has_digest = A.digest != nullptr || A.defer;  // long keys are laid out
+  // the tile's sizes (SoA-decidable, as the group totals: key_path_sizes), from
+  // the POS and refSNP digits the key renders anyway, scanned over the wave
+  const Dec dp = dec_text(cur.p);
+  const bool e32 = cur.e <= 0xFFFFFFFFull;
+  const Dec de = dec_text(uint32_t(cur.e));
+  uint32_t ksz = 0, psz = 0;
+  if (live) {
+    const bool lg = uint64_t(cur.r) + cur.a > A.max_seq_len;
+    if (cur.c < uint32_t(A.n_chrom) && !(cur.e >> 63) && !(lg && !has_digest))
+      ksz = key_label_width(cur.c) + 2u + dp.n + (lg ? uint32_t(AVDB_DIGEST_CHARS) : cur.r + 1u + cur.a) +
+            (cur.e ? 3u + (e32 ? de.n : ndigits64(cur.e)) : 0u);
+    if (A.code && cur.cd != AVDB_BIN_NONE && cur.c < uint32_t(A.n_chrom)) psz = bin_path_size(cur.c, cur.cd);
+  }
+  const uint32_t xk = wave_incl_sum(ksz), xp = wave_incl_sum(psz);
+  const uint32_t K = __builtin_amdgcn_readlane(xk, kWave - 1), P = __builtin_amdgcn_readlane(xp, kWave - 1);
+  const uint64_t gk0 = run_k, gk1 = run_k + K, gp0 = run_p, gp1 = run_p + P;
+  const uint64_t ko = gk0 + xk - ksz, ko1 = gk0 + xk, po = gp0 + xp - psz, po1 = gp0 + xp;
+  run_k = gk1;
+  run_p = gp1;
+  const uint32_t c = cur.c, r = cur.r, a = cur.a;
+  const uint64_t e = cur.e;
+  const bool lng = uint64_t(r) + a > A.max_seq_len;
+  uint8_t st = AVDB_KEY_HOST;
+  if (live) {
+    A.key_off[i] = ko;
+    if (A.code) A.path_off[i] = po;
+    if (i + 1 == A.n) {
+      A.key_off[A.n] = ko1;
+      if (A.code) A.path_off[A.n] = po1;
+    }
+    st = AVDB_KEY_OK;
+    if (c >= n_chrom || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
+    else if (lng && !A.digest) st = A.defer ? AVDB_KEY_DIGEST_PENDING : AVDB_KEY_NEED_DIGEST;
+    else if (!lng && cur.off + r + a > A.heap_bytes) st = AVDB_KEY_HOST;
+    if ((st == AVDB_KEY_OK || st == AVDB_KEY_DIGEST_PENDING) && ko1 > A.key_cap) st = AVDB_KEY_OVERFLOW;
+  }
+  // the body's two ranges: a long record's 32 digest characters, or ref then alt
+  // (windows loaded up front, independent of each other); a pending digest is 32
+  // zero bytes here
+  const bool kok = st == AVDB_KEY_OK || st == AVDB_KEY_DIGEST_PENDING;
+  uint64_t W1[kWinWords], W2[kWinWords];
+  uint32_t m1 = 0, n1 = 0, m2 = 0, n2 = 0;
+  bool wide = false;  // a range past the window (max_seq_len > 50): the per-piece path
+#pragma unroll
+  for (uint32_t k = 0; k < kWinWords; ++k) W1[k] = W2[k] = 0;
+  if (kok) {
+    if (lng) {
+      n1 = AVDB_DIGEST_CHARS;
+      if (A.digest) {
+        const uintptr_t s1 = reinterpret_cast<uintptr_t>(A.digest) + 32 * i;
+        m1 = uint32_t(s1 & 7);
+        load_win(W1, s1, n1, Heap{s1, s1 + AVDB_DIGEST_CHARS});
+      }
+    } else {
+      const uintptr_t s1 = reinterpret_cast<uintptr_t>(A.heap) + cur.off, s2 = s1 + r;
+      n1 = r;
+      n2 = a;
+      m1 = uint32_t(s1 & 7);
+      m2 = uint32_t(s2 & 7);
+      wide = m1 + n1 > 8 * kWinWords || m2 + n2 > 8 * kWinWords;
+      if (!wide) {
+        load_win(W1, s1, n1, hheap);
+        load_win(W2, s2, n2, hheap);
+      }
+    }
+  }
+  // stream 0: keys
+  const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap;
+  uint64_t bad = 0;
+  auto render_key = [&](auto o) {  // primary_key_generator.py:106-122
+    uint64_t q0, q1;
+    const uint32_t lp = key_prefix(c, dp, &q0, &q1);
+    append2(o, q0, q1, lp);
+    if (!wide) {
+      append_win(o, W1, m1, n1, bad);
+      if (!lng) o.put(':');
+      append_win(o, W2, m2, n2, bad);
+    } else {
+      const uint64_t off = cur.off;
+      if (!key_allele_ok((glb_cp)(A.heap + off), r + a)) bad = kHiBits;
+      o.bytes((glb_cp)(A.heap + off), r);
+      o.put(':');
+      o.bytes((glb_cp)(A.heap + off + r), a);
+    }
+    if (e) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
+      if (e32) {
+        append2(o, 0x73723Aull | (de.lo << 24), (de.lo >> 40) | (de.hi << 24), 3 + de.n);
+      } else {
+        o.lit(":rs");
+        o.u64v(e);
+      }
+    }
+    return o;
+  };
+  if (kok) {
+    if (kst) {
+      Out<true, true> o(LdsImage{}, kimg, ko - (gk0 & ~uint64_t(15)));
+      render_key(o).finish();
+    } else {
+      Out<true> o(A.key_out, ko);
+      render_key(o).finish();
+    }
+    if (bad) st = AVDB_KEY_HOST;
+  }
+  // stream 1: ltree paths
+  bool pst = false, path_over = false;
+  if (A.code) {
+    pst = gp1 - (gp0 & ~uint64_t(15)) + 16 <= kPathWave && gp1 <= A.path_cap;
+    const uint32_t cd = live ? cur.cd : AVDB_BIN_NONE;
+    const bool has_path = live && cd != AVDB_BIN_NONE && c < n_chrom;
+    path_over = has_path && po1 > A.path_cap;
+    if (has_path && !path_over) {
+      if (pst) {
+        Out<true, true> o(LdsImage{}, pimg, po - (gp0 & ~uint64_t(15)));
+        bin_path<true>(o, c, cd).finish();
+      } else {
+        Out<true> o(A.path_out, po);
+        bin_path<true>(o, c, cd).finish();
+      }
+    }
+  }
+  if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
+  wave_lds_sync();
+  if (kst) flush_span32(kimg, A.key_out, gk0, gk1, lane);
+  if (pst) flush_span32(pimg, A.path_out, gp0, gp1, lane);
+  wave_lds_sync();
+}
+
 #ifndef AVDB_K7_V2_BLOCK
 #define AVDB_K7_V2_BLOCK 64  // write-pass workgroup size: one wave (waves share nothing; against 256 threads K7 -0.5 to -0.9 %, A/B knob)
 #endif
@@ -454,8 +594,6 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
   for (uint32_t q = lane; q < kPathWave / 8; q += kWave) pimg[q] = 0;
   wave_lds_sync();
   const Heap hheap = make_heap(A.heap, A.heap_bytes);
-  const uint32_t n_chrom = uint32_t(A.n_chrom);
-  const bool has_digest = A.digest != nullptr || A.defer;  // long keys are laid out
   auto load_in = [&](size_t t) {
     KeyTileIn v{};
     const size_t j = t + lane;
@@ -479,8 +617,6 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
   for (size_t tn = 0; t0 < A.n; t0 = tn) {
     tn = ((t0 / kWave) & (tpg - 1)) != tpg - 1 ? t0 + kWave
                                                : t0 - size_t(tpg - 1) * kWave + n_gw * (size_t(kWave) << A.group_log2);
-    const size_t i = t0 + lane;
-    const bool live = i < A.n;
     const KeyTileIn cur = nx;
     if (tn < A.n) nx = load_in(tn);
     if (((t0 / kWave) & (tpg - 1)) == 0) {  // a new group: its scanned base
@@ -500,132 +636,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
         run_p = A.blk_pre[2 * b + 1] + gp.y;
       }
     }
-    // the tile's sizes (SoA-decidable, as the group totals: key_path_sizes), from
-    // the POS and refSNP digits the key renders anyway, scanned over the wave
-    const Dec dp = dec_text(cur.p);
-    const bool e32 = cur.e <= 0xFFFFFFFFull;
-    const Dec de = dec_text(uint32_t(cur.e));
-    uint32_t ksz = 0, psz = 0;
-    if (live) {
-      const bool lg = uint64_t(cur.r) + cur.a > A.max_seq_len;
-      if (cur.c < uint32_t(A.n_chrom) && !(cur.e >> 63) && !(lg && !has_digest))
-        ksz = key_label_width(cur.c) + 2u + dp.n + (lg ? uint32_t(AVDB_DIGEST_CHARS) : cur.r + 1u + cur.a) +
-              (cur.e ? 3u + (e32 ? de.n : ndigits64(cur.e)) : 0u);
-      if (A.code && cur.cd != AVDB_BIN_NONE && cur.c < uint32_t(A.n_chrom)) psz = bin_path_size(cur.c, cur.cd);
-    }
-    const uint32_t xk = wave_incl_sum(ksz), xp = wave_incl_sum(psz);
-    const uint32_t K = __builtin_amdgcn_readlane(xk, kWave - 1), P = __builtin_amdgcn_readlane(xp, kWave - 1);
-    const uint64_t gk0 = run_k, gk1 = run_k + K, gp0 = run_p, gp1 = run_p + P;
-    const uint64_t ko = gk0 + xk - ksz, ko1 = gk0 + xk, po = gp0 + xp - psz, po1 = gp0 + xp;
-    run_k = gk1;
-    run_p = gp1;
-    const uint32_t c = cur.c, r = cur.r, a = cur.a;
-    const uint64_t e = cur.e;
-    const bool lng = uint64_t(r) + a > A.max_seq_len;
-    uint8_t st = AVDB_KEY_HOST;
-    if (live) {
-      A.key_off[i] = ko;
-      if (A.code) A.path_off[i] = po;
-      if (i + 1 == A.n) {
-        A.key_off[A.n] = ko1;
-        if (A.code) A.path_off[A.n] = po1;
-      }
-      st = AVDB_KEY_OK;
-      if (c >= n_chrom || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
-      else if (lng && !A.digest) st = A.defer ? AVDB_KEY_DIGEST_PENDING : AVDB_KEY_NEED_DIGEST;
-      else if (!lng && cur.off + r + a > A.heap_bytes) st = AVDB_KEY_HOST;
-      if ((st == AVDB_KEY_OK || st == AVDB_KEY_DIGEST_PENDING) && ko1 > A.key_cap) st = AVDB_KEY_OVERFLOW;
-    }
-    // the body's two ranges: a long record's 32 digest characters, or ref then alt
-    // (windows loaded up front, independent of each other); a pending digest is 32
-    // zero bytes here
-    const bool kok = st == AVDB_KEY_OK || st == AVDB_KEY_DIGEST_PENDING;
-    uint64_t W1[kWinWords], W2[kWinWords];
-    uint32_t m1 = 0, n1 = 0, m2 = 0, n2 = 0;
-    bool wide = false;  // a range past the window (max_seq_len > 50): the per-piece path
-#pragma unroll
-    for (uint32_t k = 0; k < kWinWords; ++k) W1[k] = W2[k] = 0;
-    if (kok) {
-      if (lng) {
-        n1 = AVDB_DIGEST_CHARS;
-        if (A.digest) {
-          const uintptr_t s1 = reinterpret_cast<uintptr_t>(A.digest) + 32 * i;
-          m1 = uint32_t(s1 & 7);
-          load_win(W1, s1, n1, Heap{s1, s1 + AVDB_DIGEST_CHARS});
-        }
-      } else {
-        const uintptr_t s1 = reinterpret_cast<uintptr_t>(A.heap) + cur.off, s2 = s1 + r;
-        n1 = r;
-        n2 = a;
-        m1 = uint32_t(s1 & 7);
-        m2 = uint32_t(s2 & 7);
-        wide = m1 + n1 > 8 * kWinWords || m2 + n2 > 8 * kWinWords;
-        if (!wide) {
-          load_win(W1, s1, n1, hheap);
-          load_win(W2, s2, n2, hheap);
-        }
-      }
-    }
-    // stream 0: keys
-    const bool kst = gk1 - (gk0 & ~uint64_t(15)) + 16 <= kKeyWave && gk1 <= A.key_cap;
-    uint64_t bad = 0;
-    auto render_key = [&](auto o) {  // primary_key_generator.py:106-122
-      uint64_t q0, q1;
-      const uint32_t lp = key_prefix(c, dp, &q0, &q1);
-      append2(o, q0, q1, lp);
-      if (!wide) {
-        append_win(o, W1, m1, n1, bad);
-        if (!lng) o.put(':');
-        append_win(o, W2, m2, n2, bad);
-      } else {
-        const uint64_t off = cur.off;
-        if (!key_allele_ok((glb_cp)(A.heap + off), r + a)) bad = kHiBits;
-        o.bytes((glb_cp)(A.heap + off), r);
-        o.put(':');
-        o.bytes((glb_cp)(A.heap + off + r), a);
-      }
-      if (e) {  // ':rs' + the refSNP number (not interned: bit 63 clear)
-        if (e32) {
-          append2(o, 0x73723Aull | (de.lo << 24), (de.lo >> 40) | (de.hi << 24), 3 + de.n);
-        } else {
-          o.lit(":rs");
-          o.u64v(e);
-        }
-      }
-      return o;
-    };
-    if (kok) {
-      if (kst) {
-        Out<true, true> o(LdsImage{}, kimg, ko - (gk0 & ~uint64_t(15)));
-        render_key(o).finish();
-      } else {
-        Out<true> o(A.key_out, ko);
-        render_key(o).finish();
-      }
-      if (bad) st = AVDB_KEY_HOST;
-    }
-    // stream 1: ltree paths
-    bool pst = false, path_over = false;
-    if (A.code) {
-      pst = gp1 - (gp0 & ~uint64_t(15)) + 16 <= kPathWave && gp1 <= A.path_cap;
-      const uint32_t cd = live ? cur.cd : AVDB_BIN_NONE;
-      const bool has_path = live && cd != AVDB_BIN_NONE && c < n_chrom;
-      path_over = has_path && po1 > A.path_cap;
-      if (has_path && !path_over) {
-        if (pst) {
-          Out<true, true> o(LdsImage{}, pimg, po - (gp0 & ~uint64_t(15)));
-          bin_path<true>(o, c, cd).finish();
-        } else {
-          Out<true> o(A.path_out, po);
-          bin_path<true>(o, c, cd).finish();
-        }
-      }
-    }
-    if (live) A.state[i] = st | (path_over ? AVDB_PATH_OVERFLOW : 0u);
-    wave_lds_sync();
-    if (kst) flush_span32(kimg, A.key_out, gk0, gk1, lane);
-    if (pst) flush_span32(pimg, A.path_out, gp0, gp1, lane);
-    wave_lds_sync();
+    key_tile(A, cur, t0, run_k, run_p, kimg, pimg, hheap, lane);
   }
 }
 
@@ -664,6 +675,347 @@ __global__ __launch_bounds__(kBlock) void k_fill_digests(const uint8_t* __restri
       q[2].v = uint64_t(d1.x) | (uint64_t(d1.y) << 32);
       q[3].v = uint64_t(d1.z) | (uint64_t(d1.w) << 32);
       state[i] = uint8_t((st[k] & 0xF0) | AVDB_KEY_OK);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The keyed step's record prep and its text in ONE pass (avdb_keyed_prep; the
+// round-6 form of K2 + K7).  K2 (end, bin, status; K3's marks, K4's long codes,
+// the L8 histogram and counters) and K7 (keys + ltree paths) both read the whole
+// SoA; run as two kernels the SoA and the bin codes cross HBM twice (29 + 4 B per
+// record, 4.2 GB of C4k's 34 GB).  Here a workgroup of four waves takes one group
+// of 256 records (a 64-record tile per wave, one record per lane, held in
+// registers from the K2 half to the K7 half):
+//   1. SoA loads, heap peeks, end / bin / status, the marks and codes, and the
+//      tile's key / path byte totals (key_path_sizes, what the keyed K2 summed);
+//   2. a decoupled look-back over the groups for the group's text offsets:
+//      groups take their index from a ticket in launch order, publish their
+//      totals first, then sum their predecessors' back to the nearest published
+//      inclusive prefix (8-byte {flag, value} granules, agent-scope atomic
+//      loads / stores: MI355X_MICROARCH.md's granule hand-off);
+//   3. each wave renders its tile (key_tile, K7's write pass) from the registers
+//      phase 1 loaded.
+// The round-1 look-back over 64-record tiles polled with plain loads (168 ms for
+// C4k); here a group is 256 records and every poll is an agent-scope load.
+// Long records' keys are laid out with their digest pending (A.defer): K4 runs
+// after this pass on the codes it wrote, then avdb_primary_keys_fill_digests.
+// The histogram and counters go through per-group partials (k_keyed_stats), so no
+// workgroup holds a 24 KB LDS histogram beside K7's 32 KB of text images.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kOpWaves = 4;                     // waves per workgroup = tiles per group
+constexpr uint32_t kOpGroup = kOpWaves * kWave;      // records per group
+constexpr uint64_t kLbAgg = uint64_t(1) << 62, kLbInc = uint64_t(2) << 62, kLbVal = kLbAgg - 1;
+constexpr uint32_t kLbSpinCap = 1u << 22;            // polls before a (never expected) give-up
+constexpr uint32_t kOpSlicesMax = 4096;              // K3 list slices (avdb_pk_dedup_ex's resolve grid)
+
+struct PrepArgs {
+  uint32_t* end;
+  uint32_t* code;
+  uint8_t* status;          // nullable
+  uint8_t* keep;            // nullable: no K3 marks
+  uint32_t* dd_counts;      // [slices], zeroed by k_keyed_init
+  uint32_t* dd_list;        // slice s at dd_list + s * dd_slice
+  size_t dd_slice;
+  uint32_t dd_slices;
+  uint8_t* long_codes;      // nullable: no K4 codes
+  uint4* grp_stat;          // nullable: no histogram / counters; {key0, cnt0 | cnt1 << 16, key1, errors}
+  uint32_t* hist;           // nullable: waves of mixed L8 keys add here directly
+  unsigned long long* lb;   // [2 * groups] look-back granules (keys, paths), zeroed by k_keyed_init
+  uint32_t* hdr;            // [0] ticket, [1] look-back give-ups (zeroed by k_keyed_init)
+  size_t n_groups;
+  uint32_t max_seq_len;
+};
+
+__device__ __forceinline__ void lb_store(unsigned long long* p, uint64_t v) {
+  __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 of group g: publish (agg_k, agg_p), look back, publish the inclusive
+// prefixes; returns the exclusive ones (every lane)
+__device__ __noinline__ void group_lookback(unsigned long long* lb, uint32_t* hdr, size_t g, uint64_t agg_k,
+                                            uint64_t agg_p, uint64_t* xk, uint64_t* xp) {
+  const uint32_t lane = __lane_id();
+  if (g == 0) {
+    if (lane == 0) {
+      lb_store(lb, kLbInc | agg_k);
+      lb_store(lb + 1, kLbInc | agg_p);
+    }
+    *xk = *xp = 0;
+    return;
+  }
+  if (lane == 0) {
+    lb_store(lb + 2 * g, kLbAgg | agg_k);
+    lb_store(lb + 2 * g + 1, kLbAgg | agg_p);
+  }
+  uint64_t ek = 0, ep = 0;
+  bool gave_up = false;
+  for (int64_t q0 = int64_t(g) - 1; q0 >= 0; q0 -= kWave) {
+    const int64_t q = q0 - int64_t(lane);
+    uint64_t sk = 0, sp = 0;
+    if (q >= 0) {
+      for (uint32_t spin = 0;; ++spin) {
+        sk = lb_load(lb + 2 * size_t(q));
+        sp = lb_load(lb + 2 * size_t(q) + 1);
+        if ((sk >> 62) && (sk >> 62) == (sp >> 62)) break;
+        if (spin == kLbSpinCap) {
+          sk = sp = kLbInc;
+          gave_up = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    const uint64_t inc = __ballot(q >= 0 && (sk >> 62) == 2);
+    const uint32_t stop = inc ? uint32_t(__ffsll((unsigned long long)inc)) - 1 : uint32_t(kWave);
+    const bool take = q >= 0 && lane <= stop;
+    ek += wave_sum64(take ? (sk & kLbVal) : 0ull);
+    ep += wave_sum64(take ? (sp & kLbVal) : 0ull);
+    if (inc) break;
+  }
+  if (gave_up) atomicAdd(hdr + 1, 1u);
+  if (lane == 0) {
+    lb_store(lb + 2 * g, kLbInc | (ek + agg_k));
+    lb_store(lb + 2 * g + 1, kLbInc | (ep + agg_p));
+  }
+  *xk = ek;
+  *xp = ep;
+}
+
+__global__ __launch_bounds__(kBlock) void k_keyed_init(PrepArgs P) {
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  for (size_t j = size_t(blockIdx.x) * blockDim.x + threadIdx.x; j < 2 * P.n_groups; j += stride) P.lb[j] = 0;
+  for (size_t j = size_t(blockIdx.x) * blockDim.x + threadIdx.x; j < P.dd_slices; j += stride) P.dd_counts[j] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 2) P.hdr[threadIdx.x] = 0;
+}
+
+__global__ __launch_bounds__(kBlock, 4) void k_keyed_onepass(KeyArgs A, PrepArgs P, ChromTable tab) {
+  __shared__ uint64_t s_kimg[kOpWaves * kKeyWave / 8];
+  __shared__ uint64_t s_pimg[kOpWaves * kPathWave / 8];
+  __shared__ uint32_t s_len[AVDB_MAX_CHROM], s_l8off[AVDB_MAX_CHROM];
+  __shared__ uint32_t s_tk[kOpWaves], s_tp[kOpWaves], s_dd[kOpWaves], s_hk[kOpWaves], s_hc[kOpWaves],
+      s_err[kOpWaves];
+  __shared__ uint64_t s_base[2];
+  __shared__ uint32_t s_g, s_ddat;
+  const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave, tid = threadIdx.x;
+  lds_u64* kimg = (lds_u64*)s_kimg + wv * (kKeyWave / 8);
+  lds_u64* pimg = (lds_u64*)s_pimg + wv * (kPathWave / 8);
+  for (uint32_t q = lane; q < kKeyWave / 8; q += kWave) kimg[q] = 0;
+  for (uint32_t q = lane; q < kPathWave / 8; q += kWave) pimg[q] = 0;
+  if (tid < AVDB_MAX_CHROM) {
+    s_len[tid] = tab.len[tid];
+    s_l8off[tid] = tab.l8_off[tid];
+  }
+  if (tid == 0) s_g = atomicAdd(P.hdr, 1u);  // groups in launch order: every group waited on has started
+  __syncthreads();
+  const size_t g = s_g;
+  const size_t t0 = g * kOpGroup + size_t(wv) * kWave, i = t0 + lane;
+  const bool live = i < A.n;
+  const Heap hp = make_heap(A.heap, A.heap_bytes);
+
+  // ---- 1. the SoA once; K2's record arithmetic (variant_annotator.py:36-79, bin_index.py:59-75)
+  KeyTileIn cur{};
+  cur.cd = AVDB_BIN_NONE;
+  if (live) {
+    cur.c = A.chrom[i];
+    cur.p = A.pos[i];
+    cur.r = A.rl[i];
+    cur.a = A.al[i];
+    cur.e = A.ext ? A.ext[i] : 0ull;
+    cur.off = A.off[i];
+  }
+  const bool snv = cur.r == 1u && cur.a == 1u;
+  const uint64_t wr = live && !snv ? heap_u64(hp, cur.off) : 0ull;
+  const uint64_t wa = live && !snv ? heap_u64(hp, cur.off + cur.r) : 0ull;
+  uint32_t st = 0, key8 = 0xFFFFFFFFu;
+  if (live) {
+    uint32_t lcp, cd;
+    const uint32_t e = infer_end(hp, cur.off, cur.r, cur.a, cur.p, wr, wa, &lcp);
+    st = classify(cur.c, cur.p, e, tab.n, s_len, &cd);
+    cur.cd = cd;
+    __builtin_nontemporal_store(e, P.end + i);
+    __builtin_nontemporal_store(cd, P.code + i);
+    if (P.status) P.status[i] = uint8_t(st);
+    if (P.long_codes) P.long_codes[i] = uint8_t(long_code(cur.r, cur.a, P.max_seq_len));
+    if (P.keep) P.keep[i] = 1;
+    if (cd != AVDB_BIN_NONE) key8 = s_l8off[cur.c] + (cur.p - 1u) / kL8Width;
+  }
+  // K3's first phase (removeDuplicates.sql:2-24 keep-first): a record that shares
+  // (chrom, pos) with its predecessor is listed for the resolve if it could repeat
+  // a primary key before it — the predecessor's lengths and refSNP id, or third or
+  // later at its position (the keyed K2's filter, avdb_bins.hip)
+  uint64_t listed = 0;
+  if (P.keep) {
+    uint32_t pc = __shfl_up(cur.c, 1, kWave), pp = __shfl_up(cur.p, 1, kWave);
+    uint32_t pr = __shfl_up(cur.r, 1, kWave), pa = __shfl_up(cur.a, 1, kWave);
+    uint64_t pe = (uint64_t(uint32_t(__shfl_up(uint32_t(cur.e >> 32), 1, kWave))) << 32) |
+                  uint32_t(__shfl_up(uint32_t(cur.e), 1, kWave));
+    uint32_t p2 = 0;  // lane 0: record i-1 shares its predecessor's position
+    if (lane == 0 && live && i > 0) {
+      pc = A.chrom[i - 1];
+      pp = A.pos[i - 1];
+      pr = A.rl[i - 1];
+      pa = A.al[i - 1];
+      pe = A.ext ? A.ext[i - 1] : 0ull;
+      p2 = uint32_t(i >= 2 && A.chrom[i - 2] == pc && A.pos[i - 2] == pp);
+    }
+    const bool same = live && i > 0 && cur.c == pc && cur.p == pp;
+    const uint64_t sm = __ballot(same);
+    const uint32_t psame = lane == 0 ? p2 : uint32_t((sm >> (lane - 1)) & 1ull);
+    const bool cand = cur.r == pr && cur.a == pa && cur.e == pe;
+    listed = __ballot(same && (cand || psame));
+  }
+  // the L8 histogram / status counters as this wave's partials (k_keyed_stats)
+  if (P.grp_stat) {
+    const uint64_t valid = __ballot(key8 != 0xFFFFFFFFu);
+    uint32_t hk = 0xFFFFFFFFu, hc = 0;
+    if (valid) {
+      const uint32_t k0 = __builtin_amdgcn_readlane(key8, uint32_t(__ffsll((unsigned long long)valid)) - 1);
+      if (!__ballot(key8 != 0xFFFFFFFFu && key8 != k0)) {
+        hk = k0;
+        hc = uint32_t(__popcll(valid));
+      } else if (P.hist) {
+        wave_hist_add(key8, P.hist);  // a wave across an L8 boundary (sorted) or unsorted records
+      }
+    }
+    const uint32_t e1 = uint32_t(__popcll(__ballot(st == 1u))), e2 = uint32_t(__popcll(__ballot(st == 2u))),
+                   e3 = uint32_t(__popcll(__ballot(st == 3u)));
+    if (lane == 0) {
+      s_hk[wv] = hk;
+      s_hc[wv] = hc;
+      s_err[wv] = e1 | (e2 << 10) | (e3 << 20);
+    }
+  }
+  // the tile's key / path bytes (key_tile renders exactly these: key_path_sizes)
+  {
+    uint32_t ks = 0, ps = 0;
+    if (live)
+      key_path_sizes(cur.c, cur.p, cur.r, cur.a, cur.e, cur.cd, A.max_seq_len, uint32_t(A.n_chrom),
+                     A.digest != nullptr || A.defer, A.code != nullptr, &ks, &ps);
+    const uint32_t K = wave_sum32(ks), Pp = wave_sum32(ps);
+    if (lane == 0) {
+      s_tk[wv] = K;
+      s_tp[wv] = Pp;
+      s_dd[wv] = uint32_t(__popcll(listed));
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. the group's offsets (wave 0), its K3 slice space and statistics
+  if (wv == 0) {
+    uint64_t ak = 0, ap = 0;
+    uint32_t dd = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kOpWaves; ++w) {
+      ak += s_tk[w];
+      ap += s_tp[w];
+      dd += s_dd[w];
+    }
+    uint32_t at = 0;
+    if (lane == 0 && dd) at = atomicAdd(P.dd_counts + (g % P.dd_slices), dd);
+    if (lane == 0 && P.grp_stat) {
+      uint32_t k0 = 0xFFFFFFFFu, c0 = 0, k1 = 0xFFFFFFFFu, c1 = 0, er = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kOpWaves; ++w) {
+        const uint32_t k = s_hk[w], c = s_hc[w];
+        er += s_err[w];
+        if (!c) continue;
+        if (k == k0 || !c0) {
+          k0 = k;
+          c0 += c;
+        } else if (k == k1 || !c1) {
+          k1 = k;
+          c1 += c;
+        } else if (P.hist) {
+          atomicAdd(P.hist + k, c);
+        }
+      }
+      P.grp_stat[g] = make_uint4(k0, c0 | (c1 << 16), k1, er);
+    }
+    uint64_t xk, xp;
+    group_lookback(P.lb, P.hdr, g, ak, ap, &xk, &xp);
+    if (lane == 0) {
+      s_base[0] = xk;
+      s_base[1] = xp;
+      s_ddat = at;
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. the K3 list entries and this wave's tile of text
+  if (listed) {
+    uint32_t before = s_ddat;
+    for (uint32_t w = 0; w < wv; ++w) before += s_dd[w];
+    if ((listed >> lane) & 1ull)
+      P.dd_list[size_t(g % P.dd_slices) * P.dd_slice + before + uint32_t(__popcll(listed & ((1ull << lane) - 1)))] =
+          uint32_t(i);
+  }
+  uint64_t run_k = s_base[0], run_p = s_base[1];
+  for (uint32_t w = 0; w < wv; ++w) {
+    run_k += s_tk[w];
+    run_p += s_tp[w];
+  }
+  wave_lds_sync();  // (this wave's images were zeroed above)
+  key_tile(A, cur, t0, run_k, run_p, kimg, pimg, make_heap(A.heap, A.heap_bytes), lane);
+}
+
+// the histogram and counters from the groups' partials: a thread per 8 groups,
+// one atomic per run of one L8 key (a sorted batch: a few per wave)
+constexpr uint32_t kStatGroups = 8;
+__global__ __launch_bounds__(kBlock) void k_keyed_stats(const uint4* __restrict__ grp, size_t n_groups, size_t n,
+                                                        uint32_t* __restrict__ hist,
+                                                        unsigned long long* __restrict__ ctr) {
+  __shared__ unsigned long long s_c[4];
+  if (threadIdx.x < 4) s_c[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t g0 = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * kStatGroups;
+  uint32_t rk = 0xFFFFFFFFu, rc = 0, e1 = 0, e2 = 0, e3 = 0;
+  uint64_t recs = 0;
+  uint4 v[kStatGroups];
+#pragma unroll
+  for (uint32_t k = 0; k < kStatGroups; ++k) v[k] = g0 + k < n_groups ? grp[g0 + k] : make_uint4(0xFFFFFFFFu, 0, 0xFFFFFFFFu, 0);
+#pragma unroll
+  for (uint32_t k = 0; k < kStatGroups; ++k) {
+    if (g0 + k >= n_groups) break;
+    const size_t r0 = (g0 + k) * kOpGroup;
+    recs += n - r0 < kOpGroup ? n - r0 : kOpGroup;
+    e1 += v[k].w & 0x3FFu;
+    e2 += (v[k].w >> 10) & 0x3FFu;
+    e3 += (v[k].w >> 20) & 0x3FFu;
+    const uint32_t kk[2] = {v[k].x, v[k].z}, cc[2] = {v[k].y & 0xFFFFu, v[k].y >> 16};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (!cc[q]) continue;
+      if (kk[q] != rk) {
+        if (rc && hist) atomicAdd(hist + rk, rc);
+        rk = kk[q];
+        rc = 0;
+      }
+      rc += cc[q];
+    }
+  }
+  if (rc && hist) atomicAdd(hist + rk, rc);
+  if (ctr) {
+    const uint64_t t_rec = wave_sum64(recs);
+    const uint64_t t1 = wave_sum64(e1), t2 = wave_sum64(e2), t3 = wave_sum64(e3);
+    if (__lane_id() == 0) {
+      atomicAdd(&s_c[0], (unsigned long long)t_rec);
+      atomicAdd(&s_c[1], (unsigned long long)t1);
+      atomicAdd(&s_c[2], (unsigned long long)t2);
+      atomicAdd(&s_c[3], (unsigned long long)t3);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long bad_all = s_c[1] + s_c[2] + s_c[3];
+      if (s_c[0]) {
+        atomicAdd(ctr + AVDB_CTR_RECORDS, s_c[0]);
+        atomicAdd(ctr + AVDB_CTR_STATUS0, s_c[0] - bad_all);
+      }
+      for (int k = 1; k <= 3; ++k)
+        if (s_c[k]) atomicAdd(ctr + AVDB_CTR_STATUS0 + k, s_c[k]);
     }
   }
 }
@@ -965,5 +1317,138 @@ extern "C" int avdb_primary_keys_fill_digests(avdb_ctx* ctx, const uint8_t* chro
   hipLaunchKernelGGL(k_fill_digests, dim3(stream_grid((n + 15) / 16, kBlock, 2048)), dim3(kBlock), 0, s, chrom, pos,
                      n, digest, key_off, key_out, key_state);
   AVDB_LAUNCH_CHECK("k_fill_digests");
+  return AVDB_OK;
+}
+
+// ---- the keyed one-pass prep (K2 + K7 in one launch) ------------------------------
+static size_t onepass_groups(size_t n) { return (n + kOpGroup - 1) / kOpGroup; }
+
+namespace avdb {
+// K3's list layout under avdb_keyed_prep: `grid` slices of `slice` entries (group g
+// lists into slice g % grid; every slice holds at most ceil(groups / grid) groups)
+void keyed_onepass_dd_layout(size_t n, unsigned* grid, size_t* slice) {
+  const size_t ng = onepass_groups(n);
+  const size_t sl = ng < kOpSlicesMax ? (ng ? ng : 1) : kOpSlicesMax;
+  *grid = unsigned(sl);
+  *slice = ((ng + sl - 1) / sl) * kOpGroup;
+}
+}  // namespace avdb
+
+extern "C" int avdb_keyed_prep_workspace_size(size_t n, size_t* bytes) {
+  if (!bytes) return AVDB_EINVAL;
+  const size_t ng = onepass_groups(n);
+  *bytes = 256 + 16 * ng + 16 * ng;  // header | look-back granules (2 x u64) | group statistics (uint4)
+  return AVDB_OK;
+}
+
+extern "C" int avdb_keyed_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                               const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap,
+                               size_t heap_bytes, const uint64_t* ext_id, size_t n, uint32_t max_seq_len,
+                               uint32_t* end_out, uint32_t* bin_code, uint8_t* status, uint32_t* hist_l8,
+                               uint64_t* counters, void* workspace, size_t workspace_bytes, void* digest_workspace,
+                               size_t digest_workspace_bytes, void* dedup_workspace, size_t dedup_workspace_bytes,
+                               uint8_t* keep, uint64_t* key_off, uint64_t* path_off, uint8_t* key_out,
+                               size_t key_cap, uint8_t* path_out, size_t path_cap, uint8_t* key_state,
+                               uint32_t flags, int* written, void* stream) {
+  if (!ctx || !written || !end_out || !bin_code || !key_off || !key_out || !key_state || (path_out && !path_off)) {
+    avdb_set_error("avdb_keyed_prep: null argument");
+    return AVDB_EINVAL;
+  }
+  *written = 0;
+  if (flags & ~uint32_t(AVDB_KEYS_DIGEST_DEFERRED)) {
+    avdb_set_error("avdb_keyed_prep: unknown flags 0x%x", flags);
+    return AVDB_EINVAL;
+  }
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (n == 0) {
+    AVDB_HIP_TRY(hipMemsetAsync(key_off, 0, 8, s));
+    if (path_out) AVDB_HIP_TRY(hipMemsetAsync(path_off, 0, 8, s));
+    return AVDB_OK;
+  }
+  if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap) {
+    avdb_set_error("avdb_keyed_prep: null array");
+    return AVDB_EINVAL;
+  }
+  if (n >= (size_t(1) << 32)) {
+    avdb_set_error("avdb_keyed_prep: n must be < 2^32");
+    return AVDB_EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(key_out) % 8 || (path_out && reinterpret_cast<uintptr_t>(path_out) % 8)) {
+    avdb_set_error("avdb_keyed_prep: text outputs must be 8-byte aligned");
+    return AVDB_EINVAL;
+  }
+  size_t need = 0;
+  avdb_keyed_prep_workspace_size(n, &need);
+  if (!workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(workspace) % 16) {
+    avdb_set_error("avdb_keyed_prep: 16-byte aligned workspace of %zu bytes required", need);
+    return AVDB_ERANGE;
+  }
+  const size_t ng = onepass_groups(n);
+  char* w = static_cast<char*>(workspace);
+  PrepArgs P;
+  memset(&P, 0, sizeof(P));
+  P.end = end_out;
+  P.code = bin_code;
+  P.status = status;
+  P.hdr = reinterpret_cast<uint32_t*>(w);
+  P.lb = reinterpret_cast<unsigned long long*>(w + 256);
+  P.grp_stat = (hist_l8 || counters) ? reinterpret_cast<uint4*>(w + 256 + 16 * ng) : nullptr;
+  P.hist = hist_l8;
+  P.n_groups = ng;
+  P.max_seq_len = max_seq_len;
+  if (digest_workspace) {
+    size_t dneed = 0;
+    avdb_vrs_digest_workspace_size(n, &dneed);
+    if (digest_workspace_bytes < dneed || reinterpret_cast<uintptr_t>(digest_workspace) % 16) {
+      avdb_set_error("avdb_keyed_prep: 16-byte aligned K4 workspace of %zu bytes required", dneed);
+      return AVDB_ERANGE;
+    }
+    P.long_codes = vrs_long_codes_of(digest_workspace, n);
+  }
+  unsigned slices = 0;
+  size_t slice = 0;
+  keyed_onepass_dd_layout(n, &slices, &slice);
+  P.dd_slices = 1;
+  P.dd_counts = P.hdr + 2;  // (no marks: a dummy counter nobody reads)
+  if (dedup_workspace && keep) {
+    if (dedup_workspace_bytes < kDedupListHead + 4 * size_t(slices) * slice ||
+        reinterpret_cast<uintptr_t>(dedup_workspace) % 16) {
+      avdb_set_error("avdb_keyed_prep: 16-byte aligned K3 list workspace of %zu bytes required",
+                     kDedupListHead + 4 * size_t(slices) * slice);
+      return AVDB_ERANGE;
+    }
+    P.keep = keep;
+    P.dd_counts = static_cast<uint32_t*>(dedup_workspace);
+    P.dd_list = reinterpret_cast<uint32_t*>(static_cast<char*>(dedup_workspace) + kDedupListHead);
+    P.dd_slice = slice;
+    P.dd_slices = slices;
+  }
+  KeyArgs A = key_args(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id,
+                       path_out ? bin_code : nullptr, nullptr, n, max_seq_len, key_off, path_off, key_out, key_cap,
+                       path_out, path_cap, key_state);
+  A.defer = (flags & AVDB_KEYS_DIGEST_DEFERRED) ? 1u : 0u;
+  hipLaunchKernelGGL(k_keyed_init, dim3(stream_grid(2 * ng, kBlock, 1024)), dim3(kBlock), 0, s, P);
+  AVDB_LAUNCH_CHECK("k_keyed_init");
+  if (ng > 0xFFFFFFFFull) {
+    avdb_set_error("avdb_keyed_prep: too many groups");
+    return AVDB_EINVAL;
+  }
+  hipLaunchKernelGGL(k_keyed_onepass, dim3(unsigned(ng)), dim3(kBlock), 0, s, A, P, ctx->tab);
+  AVDB_LAUNCH_CHECK("k_keyed_onepass");
+  if (P.grp_stat) {
+    const size_t threads = (ng + kStatGroups - 1) / kStatGroups;
+    hipLaunchKernelGGL(k_keyed_stats, dim3(unsigned((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                       P.grp_stat, ng, n, hist_l8, reinterpret_cast<unsigned long long*>(counters));
+    AVDB_LAUNCH_CHECK("k_keyed_stats");
+  }
+  *written = (P.long_codes ? AVDB_KEYED_LONG_CODES : 0) | (P.keep ? AVDB_KEYED_DEDUP_MARKS : 0);
+  return AVDB_OK;
+}
+
+extern "C" int avdb_keyed_prep_lookback_errors(avdb_ctx* ctx, const void* workspace, uint32_t* out) {
+  if (!ctx || !workspace || !out) return AVDB_EINVAL;
+  AVDB_HIP_TRY(hipSetDevice(ctx->device));
+  AVDB_HIP_TRY(hipMemcpy(out, static_cast<const uint32_t*>(workspace) + 1, 4, hipMemcpyDeviceToHost));
   return AVDB_OK;
 }

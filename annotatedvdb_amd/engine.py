@@ -763,6 +763,57 @@ class Engine:
             self._pending["marks"] = (_stamp(ddw, b.chrom, b.pos), n, keep)
         return end, code, status, lcp
 
+    def keyed_prep(self, b: RecordBatch, kt: "KeyText", *, max_seq_len: int = 50, defer_digest: bool = True,
+                   hist: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None,
+                   digest_workspace: Optional[torch.Tensor] = None,
+                   dedup_workspace: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None):
+        """K2 + K7 in one pass (``avdb_keyed_prep``): ``(end, code, status, keep)``
+        and ``kt`` filled with the keys and ltree paths (long keys' digests pending
+        for :meth:`fill_digests` when ``defer_digest``).  With ``digest_workspace``
+        (the one the next ``vrs_digest`` gets) it classifies the long records for K4;
+        with ``dedup_workspace`` it runs K3's first phase (``keep`` = 1 and the listed
+        runs; the next ``pk_dedup(b, workspace=...)`` resolves them), else ``keep`` is
+        None.  ``workspace``: ``avdb_keyed_prep_workspace_size`` bytes (allocated
+        when None)."""
+        b = b if b.device == self.device else b.to(self.device)
+        n = b.n
+        self._check_alleles(b)
+        self._pending.clear()
+        if kt.key_off.numel() < n + 1 or kt.state.numel() < max(1, n) or kt.keys is None:
+            raise ValueError("keyed_prep: the KeyText holds fewer records")
+        sz = ctypes.c_size_t()
+        self.lib.avdb_keyed_prep_workspace_size(n, ctypes.byref(sz))
+        ws = workspace if workspace is not None and workspace.numel() >= sz.value else \
+            self.empty(int(sz.value), torch.uint8)
+        end = self.empty(n, torch.int32)
+        code = self.empty(n, torch.int32)
+        status = self.empty(n, torch.uint8)
+        dws, ddw = digest_workspace, dedup_workspace
+        keep = self.empty(max(4, n), torch.uint8) if ddw is not None else None
+        done = ctypes.c_int(0)
+        N.check("avdb_keyed_prep", self.lib.avdb_keyed_prep(
+            self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
+            N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), n, int(max_seq_len), N.ptr(end), N.ptr(code),
+            N.ptr(status), N.ptr(hist), N.ptr(counters), N.ptr(ws), ws.numel(), N.ptr(dws),
+            dws.numel() if dws is not None else 0, N.ptr(ddw), ddw.numel() if ddw is not None else 0, N.ptr(keep),
+            N.ptr(kt.key_off), N.ptr(kt.path_off) if kt.paths is not None else None, N.ptr(kt.keys), kt.keys.numel(),
+            N.ptr(kt.paths), kt.paths.numel() if kt.paths is not None else 0, N.ptr(kt.state),
+            N.KEYS_DIGEST_DEFERRED if defer_digest else 0, ctypes.byref(done), self._stream()))
+        self.last_keyed_ws = ws
+        if done.value & N.KEYED_LONG_CODES:
+            self._pending["codes"] = (_stamp(dws, b.ref_len, b.alt_len), n, int(max_seq_len))
+        if done.value & N.KEYED_DEDUP_MARKS:
+            self._pending["marks"] = (_stamp(ddw, b.chrom, b.pos), n, keep, N.DEDUP_ONEPASS)
+        return end, code, status, keep
+
+    def keyed_prep_lookback_errors(self, workspace: torch.Tensor) -> int:
+        """Look-back polls that gave up in the last ``keyed_prep`` on ``workspace``
+        (a host sync; 0 expected)."""
+        v = ctypes.c_uint32()
+        N.check("avdb_keyed_prep_lookback_errors",
+                self.lib.avdb_keyed_prep_lookback_errors(self.ctx, N.ptr(workspace), ctypes.byref(v)))
+        return int(v.value)
+
     # -- K3 ----------------------------------------------------------------
     def pk_dedup(self, b: RecordBatch, *, grouped: bool = True,
                  counters: Optional[torch.Tensor] = None,
@@ -775,10 +826,11 @@ class Engine:
                 and _stamp_ok(marks[0], workspace, b.chrom, b.pos)):
             # the keyed K2 already wrote keep = 1 and listed the runs: resolve them
             keep = marks[2]
+            flags = N.DEDUP_MARKED | (marks[3] if len(marks) > 3 else 0)
             N.check("avdb_pk_dedup_ex", self.lib.avdb_pk_dedup_ex(
                 self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
                 N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), n, N.ptr(workspace),
-                workspace.numel(), N.ptr(keep), N.ptr(counters), N.DEDUP_MARKED, self._stream()))
+                workspace.numel(), N.ptr(keep), N.ptr(counters), flags, self._stream()))
             return keep[:n]
         keep = self.empty(n, torch.uint8)
         ws = None

@@ -16,6 +16,10 @@ vcf_variant_loader.py:259-348, batched):
   K7  avdb_primary_keys_onepass_ex keys + ltree paths as text (primary_key_generator.py:99-122)
 
 Layouts (``layout``):
+  ``onepass``  K2 and K7 as ONE pass over the SoA (avdb_keyed_prep: K2's outputs,
+               K3's marks, K4's codes and the keys + paths with the long keys'
+               digests pending; text offsets by a decoupled look-back over
+               256-record groups), then K3, K4 and the digest fill;
   ``serial``   K2, K3, K4, K7 in the launch stream;
   ``fork``     K3 on a second stream beside K4 / K7 (it reads only K2's outputs and
                nothing reads keep until the step ends), joined at the end;
@@ -40,7 +44,7 @@ import torch
 
 from . import _native as N
 
-LAYOUTS = ("serial", "fork", "overlap")
+LAYOUTS = ("onepass", "serial", "fork", "overlap")
 # what bench.py times for C4k (AVDB_BENCH_LAYOUT overrides there) and what
 # tests/test_gpu_c4k.py checks over the whole 1e9-record job
 C4K_LAYOUT = "serial"
@@ -76,7 +80,12 @@ class KeyedStep:
         # from an earlier step on this engine never carries over
         engine.set_option(N.OPT_K4_GRID, int(k4_grid))
         engine.set_option(N.OPT_K7_GRID, int(k7_grid))
-        self.side = torch.cuda.Stream(dev) if layout != "serial" else None
+        self.ws_op = None
+        if layout == "onepass":
+            sz = ctypes.c_size_t()
+            engine.lib.avdb_keyed_prep_workspace_size(n, ctypes.byref(sz))
+            self.ws_op = engine.empty(int(sz.value), torch.uint8)
+        self.side = torch.cuda.Stream(dev) if layout in ("fork", "overlap") else None
         self.out: Dict[str, object] = {}
 
     # ---- one step ----------------------------------------------------------
@@ -103,12 +112,26 @@ class KeyedStep:
         if events is not None:
             span0 = torch.cuda.Event(enable_timing=True)
             span0.record(main)
-        end, code, status, _ = t("record_prep", main, lambda: eng.record_prep(
-            b, want_lcp=False, hist=self.hist, counters=self.counters, keys=kt, key_digest=self.digests,
-            max_seq_len=msl, digest_workspace=self.ws4, dedup_workspace=self.ws3))
         dedup = lambda: eng.pk_dedup(b, grouped=True, counters=self.counters, workspace=self.ws3)  # noqa: E731
         digest = lambda: eng.vrs_digest(b, msl, workspace=self.ws4)  # noqa: E731
         dig = is_long = keep = None
+        if self.layout == "onepass":
+            end, code, status, _ = t("keyed_prep", main, lambda: eng.keyed_prep(
+                b, kt, max_seq_len=msl, defer_digest=self.digests, hist=self.hist, counters=self.counters,
+                digest_workspace=self.ws4, dedup_workspace=self.ws3, workspace=self.ws_op))
+            keep = t("pk_dedup", main, dedup)
+            if self.digests:
+                dig, is_long = t("vrs_digest", main, digest)
+                t("fill_digests", main, lambda: eng.fill_digests(b, dig, kt))
+            if events is not None:
+                span1 = torch.cuda.Event(enable_timing=True)
+                span1.record(main)
+                events.setdefault("step_span", []).append((span0, span1))
+            self.out = dict(end=end, code=code, status=status, keep=keep, digest=dig, is_long=is_long, kt=kt)
+            return self.out
+        end, code, status, _ = t("record_prep", main, lambda: eng.record_prep(
+            b, want_lcp=False, hist=self.hist, counters=self.counters, keys=kt, key_digest=self.digests,
+            max_seq_len=msl, digest_workspace=self.ws4, dedup_workspace=self.ws3))
         if self.layout == "serial":
             keep = t("pk_dedup", main, dedup)
             if self.digests:

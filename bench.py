@@ -89,7 +89,7 @@ def stream_ceiling(test: str, pmc_path: str, kernel_ms: float):
     ach = pk["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
     return {"mix": test, "measured_traffic_GBps": ach, "ceiling_GBps": ceil, "frac": ach / ceil,
             "read_bytes": pk.get("hbm_read_bytes"), "write_bytes": pk.get("hbm_write_bytes"),
-            "source": "profiles/pmc_k7.json bytes / stage time; ceiling: profiles/hbm_ceiling_r05.jsonl "
+            "source": os.path.relpath(pmc_path, ROOT) + " bytes / stage time; ceiling: profiles/hbm_ceiling_r05.jsonl "
                       "(tools/hbm_ceiling.hip, 16-B grid-stride streams, read:write 1:3, best access form)"}
 
 
@@ -820,7 +820,14 @@ def run_workload(a, name, ri, dev, cpu):
         # code 4 = 33 B), the allele bytes of short records, 32 digest chars per long record;
         # out key_off 8 + path_off 8 + state 1 and the text
         short = (rl + al) <= 50
-        k7_bytes = 50 * n + int((rl + al)[short].sum().item()) + 32 * n_long + text
+        short_bytes = int((rl + al)[short].sum().item())
+        k7_bytes = 50 * n + short_bytes + 32 * n_long + text
+        # the one-pass keyed prep (layout "onepass", k_keyed_onepass): the SoA once (29 B),
+        # the allele bytes of short records; out end 4 + code 4 + status 1 + keep 1 + K4 code 1
+        # + key_off 8 + path_off 8 + state 1 and the text (long keys' 32 digest chars come later)
+        op_bytes = 57 * n + short_bytes + text
+        # SURVEY 8d's keyed-record bytes alone (no text): the verdict's frac_8d
+        bytes_8d = 34 * n + int((rl + al).sum().item()) + 24 * n_long
         del rl, al, short
     elif name == "c1":
         # SURVEY.md §8d per-record bytes of the C5-style record path (in chrom 1 + pos 4 +
@@ -941,20 +948,33 @@ def run_workload(a, name, ri, dev, cpu):
         out["config"].update(key_bytes=int(kt.key_off[n].item()), path_bytes=int(kt.path_off[n].item()),
                              long_records=n_long, heap_bytes=heap_bytes,
                              duplicates=int(node_ctr[21].item()) // max(1, a.steps))
-        k7_ms = stage_ms["primary_keys"]
         out["config"]["layout"] = ks.layout
-        out["k7_roofline"] = {"kernel": "avdb_primary_keys_onepass_ex (group scan + LDS-staged write pass; "
-                                        "group totals from the keyed K2)",
-                              "bound": "hbm", "achieved": k7_bytes / (k7_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": k7_bytes / (k7_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                              "algorithmic_bytes_per_launch": k7_bytes, "stage_ms": k7_ms}
-        sc = stream_ceiling("read1_write3", os.path.join(ROOT, "profiles", "pmc_k7.json"), k7_ms)
+        out["roofline"]["frac_8d"] = bytes_8d / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+        out["roofline"]["algorithmic_bytes_8d"] = bytes_8d
+        if ks.layout == "onepass":
+            k7_ms = stage_ms["keyed_prep"]
+            out["k7_roofline"] = {"kernel": "avdb_keyed_prep (k_keyed_onepass: K2 + K7 in one pass over the SoA, "
+                                            "decoupled look-back over 256-record groups; + init and stats launches)",
+                                  "bound": "hbm", "achieved": op_bytes / (k7_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": op_bytes / (k7_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                  "algorithmic_bytes_per_launch": op_bytes, "stage_ms": k7_ms}
+            sc = stream_ceiling("read1_write3", os.path.join(ROOT, "profiles", "pmc_keyed_onepass.json"), k7_ms)
+        else:
+            k7_ms = stage_ms["primary_keys"]
+            out["k7_roofline"] = {"kernel": "avdb_primary_keys_onepass_ex (group scan + LDS-staged write pass; "
+                                            "group totals from the keyed K2)",
+                                  "bound": "hbm", "achieved": k7_bytes / (k7_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": k7_bytes / (k7_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                  "algorithmic_bytes_per_launch": k7_bytes, "stage_ms": k7_ms}
+            sc = stream_ceiling("read1_write3", os.path.join(ROOT, "profiles", "pmc_k7.json"), k7_ms)
         if sc:
             out["k7_roofline"]["stream_ceiling"] = sc
         out["roofline"]["note"] = ("achieved = SURVEY 8d keyed-record bytes (34 + rlen + alen + 24 if long) + "
                                    "key/path text written, over the timed loop's HIP-event time per step on the "
                                    "launch stream (" +
-                                   {"serial": "K2 + K3 + K4 + K7 in one stream",
+                                   {"onepass": "K2 + K7 as one pass (avdb_keyed_prep), then K3, K4 and the digest "
+                                               "fill, in one stream",
+                                    "serial": "K2 + K3 + K4 + K7 in one stream",
                                     "fork": "K2, then K4 + K7 with K3 beside them on a second stream, joined",
                                     "overlap": "K2, then K7 with the long keys' digests pending beside K4 + K3 on a "
                                                "second stream, joined, then the digest fill"}[ks.layout] +

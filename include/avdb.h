@@ -164,6 +164,8 @@ int avdb_pk_dedup(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
  * share their predecessor's position listed in `workspace`, which must be the one it
  * was given, with `keep` its keep array): only the run scan over those lists runs. */
 #define AVDB_DEDUP_MARKED 1u
+/* With AVDB_DEDUP_MARKED: the marks came from avdb_keyed_prep (its list layout). */
+#define AVDB_DEDUP_ONEPASS 2u
 int avdb_pk_dedup_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
                      const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
                      const uint64_t* ext_id, size_t n, void* workspace, size_t workspace_bytes, uint8_t* keep,
@@ -517,6 +519,33 @@ int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* 
                            int has_digest, int with_paths, void* key_workspace, size_t key_workspace_bytes,
                            void* digest_workspace, size_t digest_workspace_bytes, void* dedup_workspace,
                            size_t dedup_workspace_bytes, uint8_t* keep, int* totals_written, void* stream);
+
+/* The keyed step's record prep and text in ONE pass (round 6; the SoA read once):
+ * what avdb_record_prep_keyed followed by avdb_primary_keys_onepass_ex compute —
+ * end_out, bin_code, status (nullable); hist_l8 / counters accumulated (nullable); with
+ * a K4 workspace (nullable) K4's long-record codes (then avdb_vrs_digest_ex with
+ * AVDB_DIGEST_CODES_READY); with a K3 list workspace and keep (nullable) K3's first
+ * phase (then avdb_pk_dedup_ex with AVDB_DEDUP_MARKED | AVDB_DEDUP_ONEPASS); and the
+ * keys, ltree paths (path_out nullable: none), key_off[n+1] / path_off[n+1] and
+ * key_state exactly as avdb_primary_keys_onepass_ex with digest == NULL (flags:
+ * AVDB_KEYS_DIGEST_DEFERRED lays long keys out for avdb_primary_keys_fill_digests;
+ * without it they are AVDB_KEY_NEED_DIGEST).  Text capacities as
+ * avdb_primary_keys_bound.  workspace: avdb_keyed_prep_workspace_size(n) bytes,
+ * 16-byte aligned (32 B per 256 records).  Groups of 256 records take their text
+ * offsets from a decoupled look-back in the launch; *written = AVDB_KEYED_LONG_CODES |
+ * AVDB_KEYED_DEDUP_MARKS for what it wrote.  avdb_keyed_prep_lookback_errors reads
+ * (synchronously) how many look-back polls gave up in the last call on this workspace
+ * (0 always expected; non-zero means its offsets are not valid). */
+int avdb_keyed_prep_workspace_size(size_t n, size_t* bytes);
+int avdb_keyed_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                    const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                    const uint64_t* ext_id, size_t n, uint32_t max_seq_len, uint32_t* end_out, uint32_t* bin_code,
+                    uint8_t* status, uint32_t* hist_l8, uint64_t* counters, void* workspace, size_t workspace_bytes,
+                    void* digest_workspace, size_t digest_workspace_bytes, void* dedup_workspace,
+                    size_t dedup_workspace_bytes, uint8_t* keep, uint64_t* key_off, uint64_t* path_off,
+                    uint8_t* key_out, size_t key_cap, uint8_t* path_out, size_t path_cap, uint8_t* key_state,
+                    uint32_t flags, int* written, void* stream);
+int avdb_keyed_prep_lookback_errors(avdb_ctx* ctx, const void* workspace, uint32_t* out);
 
 /* ---- K8: the per-record drop-in path in one launch -------------------------
  * The reference calls its per-record API once per alt allele

@@ -528,7 +528,7 @@ def test_keyed_marks_list_only_possible_repeats(engine, n, seed, long_every):
     assert int((want == 0).sum()) > n // 100
 
 
-@pytest.mark.parametrize("layout", ["serial", "fork"])
+@pytest.mark.parametrize("layout", ["onepass", "serial", "fork"])
 def test_c1_graph_replay_vs_c_oracle(engine, layout):
     """The step bench.py times for C1, as it times it: ``pipeline.KeyedStep`` in
     the bench's layout (``pipeline.C1_LAYOUT``; and "fork": K3 on a second stream

@@ -136,7 +136,7 @@ def test_c4k_shard_vs_c_oracle(engine, rank):
     assert n_long > 0.015 * N_PER_RANK and kbytes > 20 * N_PER_RANK and pbytes > 50 * N_PER_RANK
 
 
-@pytest.mark.parametrize("layout", ["serial", "fork", "overlap"])
+@pytest.mark.parametrize("layout", ["onepass", "serial", "fork", "overlap"])
 def test_c4k_small_vs_c_oracle(engine, layout):
     """Every stream layout of the step at a size the oracle finishes instantly
     (every code path, one chunk boundary), twice over the same buffers (the
