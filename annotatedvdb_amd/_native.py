@@ -102,7 +102,7 @@ EXPORTED_SYMBOLS = [
     "avdb_primary_keys_onepass_workspace_size", "avdb_primary_keys_onepass", "avdb_primary_keys_onepass_ex",
     "avdb_primary_keys_fill_digests",
     "avdb_record_prep_keyed",
-    "avdb_keyed_prep_workspace_size", "avdb_keyed_prep", "avdb_keyed_prep_lookback_errors",
+    "avdb_keyed_prep_workspace_size", "avdb_keyed_prep", "avdb_keyed_prep_lookback_errors", "avdb_vrs_digest_keys",
     "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
     "avdb_small_prep", "avdb_small_prep_host", "avdb_bin_path_host", "avdb_annotate_host", "avdb_host_alloc", "avdb_host_free",
     "avdb_rccl_unique_id", "avdb_rccl_comm_init", "avdb_rccl_comm_destroy",
@@ -208,6 +208,7 @@ def _sig(lib):
     f.avdb_keyed_prep.argtypes = [P, P, P, P, P, P, P, SZ, P, SZ, U32, P, P, P, P, P, P, SZ, P, SZ, P, SZ, P,
                                   P, P, P, SZ, P, SZ, P, U32, ctypes.POINTER(I32), P]
     f.avdb_keyed_prep_lookback_errors.argtypes = [P, P, ctypes.POINTER(U32)]
+    f.avdb_vrs_digest_keys.argtypes = list(f.avdb_vrs_digest_ex.argtypes)[:-1] + [P, P, P, P]
     f.avdb_primary_keys_bound.argtypes = [SZ, SZ, ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
     f.avdb_primary_keys_onepass_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]

@@ -738,13 +738,23 @@ void location_tail_table(const char* digests, int n_chrom, std::vector<uint64_t>
 #define AVDB_DIGEST_WAVES 3
 #endif
 constexpr int kDigestWavesPerSimd = AVDB_DIGEST_WAVES;
+// Optional second destination (avdb_vrs_digest_keys): the 32 characters also go
+// straight into the primary-key text a deferred K7 / avdb_keyed_prep laid out
+// (state AVDB_KEY_DIGEST_PENDING), at key_off[i] + len("label:pos:") — the fill
+// pass's work, done where chrom / pos are already in registers (the separate
+// pass re-read state, chrom, pos and key_off for every record: 0.43 ms on C4k).
+struct KeyFill {
+  const uint64_t* key_off;
+  uint8_t* key_out;
+  uint8_t* state;
+};
 __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     const uint8_t* __restrict__ chrom, const uint32_t* __restrict__ pos,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ rl,
     const uint32_t* __restrict__ al, const uint8_t* __restrict__ heap, size_t heap_bytes,
     const uint32_t* __restrict__ list, const unsigned int* __restrict__ count,
     const char* __restrict__ seq_digest, const uint64_t* __restrict__ loc_tail, int n_chrom,
-    char* __restrict__ out) {
+    char* __restrict__ out, KeyFill F) {
   __shared__ uint64_t s_w[16 * kBlock];
   __shared__ uint64_t s_suf[kSufTab];
   if (threadIdx.x < kSufTab) {  // 8-byte windows of (8 zero bytes | AL2 | 0x80 | zeros)
@@ -813,6 +823,15 @@ __global__ __launch_bounds__(kBlock, kDigestWavesPerSimd) void k_vrs_digest(
     uint64_t cw[4];
     t24u_words(H, cw);
     store_digest(o, cw);
+    if (F.key_out) {
+      const uint8_t st = F.state[i];
+      if ((st & 0x0Fu) == AVDB_KEY_DIGEST_PENDING) {
+        gw_u64u q = reinterpret_cast<gw_u64u>((gbyte*)F.key_out + F.key_off[i] + key_body_at(c, pos[i]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k].v = cw[k];
+        F.state[i] = uint8_t((st & 0xF0u) | AVDB_KEY_OK);
+      }
+    }
   }
 }
 
@@ -857,12 +876,12 @@ extern "C" int avdb_vrs_digest(avdb_ctx* ctx, const uint8_t* chrom, const uint32
                             workspace, workspace_bytes, digest_out, is_long, 0u, stream);
 }
 
-extern "C" int avdb_vrs_digest_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
-                                  const uint64_t* allele_off, const uint32_t* ref_len,
-                                  const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
-                                  size_t n, uint32_t max_seq_len, void* workspace,
-                                  size_t workspace_bytes, char* digest_out, uint8_t* is_long,
-                                  uint32_t flags, void* stream) {
+static int vrs_digest_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                           const uint64_t* allele_off, const uint32_t* ref_len,
+                           const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                           size_t n, uint32_t max_seq_len, void* workspace,
+                           size_t workspace_bytes, char* digest_out, uint8_t* is_long,
+                           uint32_t flags, KeyFill fill, void* stream) {
   if (!ctx) { avdb_set_error("null context"); return AVDB_EINVAL; }
   if (n == 0) return AVDB_OK;
   if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap || !digest_out) {
@@ -923,7 +942,31 @@ extern "C" int avdb_vrs_digest_ex(avdb_ctx* ctx, const uint8_t* chrom, const uin
   hipLaunchKernelGGL(k_vrs_digest, dim3(grid), dim3(kBlock), 0, s, chrom, pos,
                      allele_off,
                      ref_len, alt_len, heap, heap_bytes, list, total, ctx->d_seq_digest, ctx->d_loc_tail,
-                     ctx->tab.n, digest_out);
+                     ctx->tab.n, digest_out, fill);
   AVDB_LAUNCH_CHECK("k_vrs_digest");
   return AVDB_OK;
+}
+
+extern "C" int avdb_vrs_digest_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                  const uint64_t* allele_off, const uint32_t* ref_len,
+                                  const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                                  size_t n, uint32_t max_seq_len, void* workspace,
+                                  size_t workspace_bytes, char* digest_out, uint8_t* is_long,
+                                  uint32_t flags, void* stream) {
+  return vrs_digest_impl(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, n, max_seq_len, workspace,
+                         workspace_bytes, digest_out, is_long, flags, KeyFill{nullptr, nullptr, nullptr}, stream);
+}
+
+extern "C" int avdb_vrs_digest_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
+                                    const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
+                                    const uint8_t* heap, size_t heap_bytes, size_t n, uint32_t max_seq_len,
+                                    void* workspace, size_t workspace_bytes, char* digest_out, uint8_t* is_long,
+                                    uint32_t flags, const uint64_t* key_off, uint8_t* key_out, uint8_t* key_state,
+                                    void* stream) {
+  if (!key_off || !key_out || !key_state) {
+    avdb_set_error("avdb_vrs_digest_keys: null key text");
+    return AVDB_EINVAL;
+  }
+  return vrs_digest_impl(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, n, max_seq_len, workspace,
+                         workspace_bytes, digest_out, is_long, flags, KeyFill{key_off, key_out, key_state}, stream);
 }

@@ -690,8 +690,8 @@ __global__ __launch_bounds__(kBlock) void k_fill_digests(const uint8_t* __restri
 //   1. SoA loads, heap peeks, end / bin / status, the marks and codes, and the
 //      tile's key / path byte totals (key_path_sizes, what the keyed K2 summed);
 //   2. a decoupled look-back over the groups for the group's text offsets:
-//      groups take their index from a ticket in launch order, publish their
-//      totals first, then sum their predecessors' back to the nearest published
+//      a group (= workgroup index, dispatched in order) publishes its totals
+//      first, then sums its predecessors' back to the nearest published
 //      inclusive prefix (8-byte {flag, value} granules, agent-scope atomic
 //      loads / stores: MI355X_MICROARCH.md's granule hand-off);
 //   3. each wave renders its tile (key_tile, K7's write pass) from the registers
@@ -703,8 +703,17 @@ __global__ __launch_bounds__(kBlock) void k_fill_digests(const uint8_t* __restri
 // The histogram and counters go through per-group partials (k_keyed_stats), so no
 // workgroup holds a 24 KB LDS histogram beside K7's 32 KB of text images.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kOpWaves = 4;                     // waves per workgroup = tiles per group
-constexpr uint32_t kOpGroup = kOpWaves * kWave;      // records per group
+#ifndef AVDB_OP_WAVES
+#define AVDB_OP_WAVES 4  // waves per workgroup (a group: every wave's tiles; one look-back)
+#endif
+constexpr uint32_t kOpWaves = AVDB_OP_WAVES;
+constexpr uint32_t kOpBlock = kOpWaves * kWave;
+constexpr uint32_t kOpGroup = kOpWaves * kWave;      // records per group and tile of its waves
+#ifndef AVDB_OP_TPW
+#define AVDB_OP_TPW 4  // tiles per wave: a group is 256 * this records (one look-back each)
+#endif
+constexpr uint32_t kOpTpw = AVDB_OP_TPW;
+constexpr uint32_t kOpGroupRecs = kOpGroup * kOpTpw;
 constexpr uint64_t kLbAgg = uint64_t(1) << 62, kLbInc = uint64_t(2) << 62, kLbVal = kLbAgg - 1;
 constexpr uint32_t kLbSpinCap = 1u << 22;            // polls before a (never expected) give-up
 constexpr uint32_t kOpSlicesMax = 4096;              // K3 list slices (avdb_pk_dedup_ex's resolve grid)
@@ -719,10 +728,11 @@ struct PrepArgs {
   size_t dd_slice;
   uint32_t dd_slices;
   uint8_t* long_codes;      // nullable: no K4 codes
-  uint4* grp_stat;          // nullable: no histogram / counters; {key0, cnt0 | cnt1 << 16, key1, errors}
+  uint4* grp_stat;          // nullable: no histogram / counters; per group {key0, cnt0, key1, cnt1},
+                            // {status 1, 2, 3 counts, 0}
   uint32_t* hist;           // nullable: waves of mixed L8 keys add here directly
   unsigned long long* lb;   // [2 * groups] look-back granules (keys, paths), zeroed by k_keyed_init
-  uint32_t* hdr;            // [0] ticket, [1] look-back give-ups (zeroed by k_keyed_init)
+  uint32_t* hdr;            // [1] look-back give-ups (zeroed by k_keyed_init)
   size_t n_groups;
   uint32_t max_seq_len;
 };
@@ -735,9 +745,13 @@ __device__ __forceinline__ uint64_t lb_load(unsigned long long* p) {
 }
 
 // wave 0 of group g: publish (agg_k, agg_p), look back, publish the inclusive
-// prefixes; returns the exclusive ones (every lane)
-__device__ __noinline__ void group_lookback(unsigned long long* lb, uint32_t* hdr, size_t g, uint64_t agg_k,
-                                            uint64_t agg_p, uint64_t* xk, uint64_t* xp) {
+// prefixes; returns the exclusive ones (every lane).  A look-back step reads
+// kLbPerLane groups per lane (256 per step): at C4k's rate (~25 groups of 1,024
+// records per microsecond) an agent-scope round trip of a few microseconds then
+// reaches the nearest published inclusive prefix in one step.
+constexpr uint32_t kLbPerLane = 4;
+__device__ __forceinline__ void group_lookback(unsigned long long* lb, uint32_t* hdr, size_t g, uint64_t agg_k,
+                                               uint64_t agg_p, uint64_t* xk, uint64_t* xp) {
   const uint32_t lane = __lane_id();
   if (g == 0) {
     if (lane == 0) {
@@ -753,27 +767,43 @@ __device__ __noinline__ void group_lookback(unsigned long long* lb, uint32_t* hd
   }
   uint64_t ek = 0, ep = 0;
   bool gave_up = false;
-  for (int64_t q0 = int64_t(g) - 1; q0 >= 0; q0 -= kWave) {
-    const int64_t q = q0 - int64_t(lane);
-    uint64_t sk = 0, sp = 0;
-    if (q >= 0) {
-      for (uint32_t spin = 0;; ++spin) {
-        sk = lb_load(lb + 2 * size_t(q));
-        sp = lb_load(lb + 2 * size_t(q) + 1);
-        if ((sk >> 62) && (sk >> 62) == (sp >> 62)) break;
-        if (spin == kLbSpinCap) {
-          sk = sp = kLbInc;
-          gave_up = true;
-          break;
+  for (int64_t q0 = int64_t(g) - 1; q0 >= 0; q0 -= int64_t(kWave) * kLbPerLane) {
+    uint64_t sk[kLbPerLane], sp[kLbPerLane];
+#pragma unroll
+    for (uint32_t j = 0; j < kLbPerLane; ++j) {
+      const int64_t q = q0 - int64_t(kLbPerLane * lane + j);
+      sk[j] = sp[j] = 0;
+      if (q >= 0) {
+        for (uint32_t spin = 0;; ++spin) {
+          sk[j] = lb_load(lb + 2 * size_t(q));
+          sp[j] = lb_load(lb + 2 * size_t(q) + 1);
+          if ((sk[j] >> 62) && (sk[j] >> 62) == (sp[j] >> 62)) break;
+          if (spin == kLbSpinCap) {
+            sk[j] = sp[j] = kLbInc;
+            gave_up = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_s_sleep(1);
       }
     }
-    const uint64_t inc = __ballot(q >= 0 && (sk >> 62) == 2);
+    // the nearest inclusive prefix: the first (lane, j) in window order
+    uint32_t jstop = kLbPerLane;
+#pragma unroll
+    for (int j = int(kLbPerLane) - 1; j >= 0; --j)
+      if (q0 - int64_t(kLbPerLane * lane + uint32_t(j)) >= 0 && (sk[j] >> 62) == 2) jstop = uint32_t(j);
+    const uint64_t inc = __ballot(jstop < kLbPerLane);
     const uint32_t stop = inc ? uint32_t(__ffsll((unsigned long long)inc)) - 1 : uint32_t(kWave);
-    const bool take = q >= 0 && lane <= stop;
-    ek += wave_sum64(take ? (sk & kLbVal) : 0ull);
-    ep += wave_sum64(take ? (sp & kLbVal) : 0ull);
+    uint64_t vk = 0, vp = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kLbPerLane; ++j) {
+      const int64_t q = q0 - int64_t(kLbPerLane * lane + j);
+      const bool take = q >= 0 && (lane < stop || (lane == stop && j <= jstop));
+      vk += take ? (sk[j] & kLbVal) : 0ull;
+      vp += take ? (sp[j] & kLbVal) : 0ull;
+    }
+    ek += wave_sum64(vk);
+    ep += wave_sum64(vp);
     if (inc) break;
   }
   if (gave_up) atomicAdd(hdr + 1, 1u);
@@ -792,14 +822,15 @@ __global__ __launch_bounds__(kBlock) void k_keyed_init(PrepArgs P) {
   if (blockIdx.x == 0 && threadIdx.x < 2) P.hdr[threadIdx.x] = 0;
 }
 
-__global__ __launch_bounds__(kBlock, 4) void k_keyed_onepass(KeyArgs A, PrepArgs P, ChromTable tab) {
+template <uint32_t TPW>
+__global__ __launch_bounds__(kOpBlock, 4) void k_keyed_onepass(KeyArgs A, PrepArgs P, ChromTable tab) {
   __shared__ uint64_t s_kimg[kOpWaves * kKeyWave / 8];
   __shared__ uint64_t s_pimg[kOpWaves * kPathWave / 8];
   __shared__ uint32_t s_len[AVDB_MAX_CHROM], s_l8off[AVDB_MAX_CHROM];
   __shared__ uint32_t s_tk[kOpWaves], s_tp[kOpWaves], s_dd[kOpWaves], s_hk[kOpWaves], s_hc[kOpWaves],
       s_err[kOpWaves];
   __shared__ uint64_t s_base[2];
-  __shared__ uint32_t s_g, s_ddat;
+  __shared__ uint32_t s_ddat;
   const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave, tid = threadIdx.x;
   lds_u64* kimg = (lds_u64*)s_kimg + wv * (kKeyWave / 8);
   lds_u64* pimg = (lds_u64*)s_pimg + wv * (kPathWave / 8);
@@ -809,131 +840,178 @@ __global__ __launch_bounds__(kBlock, 4) void k_keyed_onepass(KeyArgs A, PrepArgs
     s_len[tid] = tab.len[tid];
     s_l8off[tid] = tab.l8_off[tid];
   }
-  if (tid == 0) s_g = atomicAdd(P.hdr, 1u);  // groups in launch order: every group waited on has started
   __syncthreads();
-  const size_t g = s_g;
-  const size_t t0 = g * kOpGroup + size_t(wv) * kWave, i = t0 + lane;
-  const bool live = i < A.n;
+  // Group = workgroup index.  A group waits only on groups before it, and workgroups
+  // are dispatched in index order (rocPRIM's look-back scans rely on the same), so
+  // every group waited on has started; a ticket from one atomic counter instead
+  // (the launch-order guarantee without that reliance) serialised 488 k workgroups
+  // at ~88 claims per microsecond.  A poll that never sees its predecessor gives up
+  // after kLbSpinCap tries and counts itself (avdb_keyed_prep_lookback_errors), so a
+  // broken order cannot hang.
+  const size_t g = blockIdx.x;
+  const size_t w0 = g * (size_t(kOpGroup) * TPW) + size_t(wv) * (kWave * TPW);  // this wave's first record
   const Heap hp = make_heap(A.heap, A.heap_bytes);
 
-  // ---- 1. the SoA once; K2's record arithmetic (variant_annotator.py:36-79, bin_index.py:59-75)
-  KeyTileIn cur{};
-  cur.cd = AVDB_BIN_NONE;
-  if (live) {
-    cur.c = A.chrom[i];
-    cur.p = A.pos[i];
-    cur.r = A.rl[i];
-    cur.a = A.al[i];
-    cur.e = A.ext ? A.ext[i] : 0ull;
-    cur.off = A.off[i];
-  }
-  const bool snv = cur.r == 1u && cur.a == 1u;
-  const uint64_t wr = live && !snv ? heap_u64(hp, cur.off) : 0ull;
-  const uint64_t wa = live && !snv ? heap_u64(hp, cur.off + cur.r) : 0ull;
-  uint32_t st = 0, key8 = 0xFFFFFFFFu;
-  if (live) {
-    uint32_t lcp, cd;
-    const uint32_t e = infer_end(hp, cur.off, cur.r, cur.a, cur.p, wr, wa, &lcp);
-    st = classify(cur.c, cur.p, e, tab.n, s_len, &cd);
-    cur.cd = cd;
-    __builtin_nontemporal_store(e, P.end + i);
-    __builtin_nontemporal_store(cd, P.code + i);
-    if (P.status) P.status[i] = uint8_t(st);
-    if (P.long_codes) P.long_codes[i] = uint8_t(long_code(cur.r, cur.a, P.max_seq_len));
-    if (P.keep) P.keep[i] = 1;
-    if (cd != AVDB_BIN_NONE) key8 = s_l8off[cur.c] + (cur.p - 1u) / kL8Width;
-  }
-  // K3's first phase (removeDuplicates.sql:2-24 keep-first): a record that shares
-  // (chrom, pos) with its predecessor is listed for the resolve if it could repeat
-  // a primary key before it — the predecessor's lengths and refSNP id, or third or
-  // later at its position (the keyed K2's filter, avdb_bins.hip)
-  uint64_t listed = 0;
-  if (P.keep) {
-    uint32_t pc = __shfl_up(cur.c, 1, kWave), pp = __shfl_up(cur.p, 1, kWave);
-    uint32_t pr = __shfl_up(cur.r, 1, kWave), pa = __shfl_up(cur.a, 1, kWave);
-    uint64_t pe = (uint64_t(uint32_t(__shfl_up(uint32_t(cur.e >> 32), 1, kWave))) << 32) |
-                  uint32_t(__shfl_up(uint32_t(cur.e), 1, kWave));
-    uint32_t p2 = 0;  // lane 0: record i-1 shares its predecessor's position
-    if (lane == 0 && live && i > 0) {
-      pc = A.chrom[i - 1];
-      pp = A.pos[i - 1];
-      pr = A.rl[i - 1];
-      pa = A.al[i - 1];
-      pe = A.ext ? A.ext[i - 1] : 0ull;
-      p2 = uint32_t(i >= 2 && A.chrom[i - 2] == pc && A.pos[i - 2] == pp);
+  // ---- 1. the SoA once (all TPW tiles' loads in flight together); K2's record
+  // arithmetic (variant_annotator.py:36-79, bin_index.py:59-75)
+  KeyTileIn cur[TPW];
+  uint64_t wr[TPW], wa[TPW];
+#pragma unroll
+  for (uint32_t k = 0; k < TPW; ++k) {
+    const size_t i = w0 + k * kWave + lane;
+    cur[k] = KeyTileIn{};
+    cur[k].cd = AVDB_BIN_NONE;
+    if (i < A.n) {
+      cur[k].c = A.chrom[i];
+      cur[k].p = A.pos[i];
+      cur[k].r = A.rl[i];
+      cur[k].a = A.al[i];
+      cur[k].e = A.ext ? A.ext[i] : 0ull;
+      cur[k].off = A.off[i];
     }
-    const bool same = live && i > 0 && cur.c == pc && cur.p == pp;
-    const uint64_t sm = __ballot(same);
-    const uint32_t psame = lane == 0 ? p2 : uint32_t((sm >> (lane - 1)) & 1ull);
-    const bool cand = cur.r == pr && cur.a == pa && cur.e == pe;
-    listed = __ballot(same && (cand || psame));
   }
-  // the L8 histogram / status counters as this wave's partials (k_keyed_stats)
-  if (P.grp_stat) {
-    const uint64_t valid = __ballot(key8 != 0xFFFFFFFFu);
-    uint32_t hk = 0xFFFFFFFFu, hc = 0;
-    if (valid) {
-      const uint32_t k0 = __builtin_amdgcn_readlane(key8, uint32_t(__ffsll((unsigned long long)valid)) - 1);
-      if (!__ballot(key8 != 0xFFFFFFFFu && key8 != k0)) {
-        hk = k0;
-        hc = uint32_t(__popcll(valid));
-      } else if (P.hist) {
-        wave_hist_add(key8, P.hist);  // a wave across an L8 boundary (sorted) or unsorted records
+#pragma unroll
+  for (uint32_t k = 0; k < TPW; ++k) {
+    const bool live = w0 + k * kWave + lane < A.n, snv = cur[k].r == 1u && cur[k].a == 1u;
+    wr[k] = live && !snv ? heap_u64(hp, cur[k].off) : 0ull;
+    wa[k] = live && !snv ? heap_u64(hp, cur[k].off + cur[k].r) : 0ull;
+  }
+  uint32_t hk = 0xFFFFFFFFu, hc = 0, e1 = 0, e2 = 0, e3 = 0, K = 0, Pt = 0, dd = 0;
+  uint64_t listed[TPW];
+  uint64_t prev_sm = 0;  // the previous tile's "shares its predecessor's position" ballot
+#pragma unroll
+  for (uint32_t k = 0; k < TPW; ++k) {
+    const size_t i = w0 + k * kWave + lane;
+    const bool live = i < A.n;
+    uint32_t st = 0, key8 = 0xFFFFFFFFu;
+    if (live) {
+      uint32_t lcp, cd;
+      const uint32_t e = infer_end(hp, cur[k].off, cur[k].r, cur[k].a, cur[k].p, wr[k], wa[k], &lcp);
+      st = classify(cur[k].c, cur[k].p, e, tab.n, s_len, &cd);
+      cur[k].cd = cd;
+      __builtin_nontemporal_store(e, P.end + i);
+      __builtin_nontemporal_store(cd, P.code + i);
+      if (P.status) P.status[i] = uint8_t(st);
+      if (P.long_codes) P.long_codes[i] = uint8_t(long_code(cur[k].r, cur[k].a, P.max_seq_len));
+      if (P.keep) P.keep[i] = 1;
+      if (cd != AVDB_BIN_NONE) key8 = s_l8off[cur[k].c] + (cur[k].p - 1u) / kL8Width;
+    }
+    // K3's first phase (removeDuplicates.sql:2-24 keep-first): a record that shares
+    // (chrom, pos) with its predecessor is listed for the resolve if it could repeat
+    // a primary key before it — the predecessor's lengths and refSNP id, or third or
+    // later at its position (the keyed K2's filter, avdb_bins.hip)
+    listed[k] = 0;
+    if (P.keep) {
+      uint32_t pc = __shfl_up(cur[k].c, 1, kWave), pp = __shfl_up(cur[k].p, 1, kWave);
+      uint32_t pr = __shfl_up(cur[k].r, 1, kWave), pa = __shfl_up(cur[k].a, 1, kWave);
+      uint64_t pe = (uint64_t(uint32_t(__shfl_up(uint32_t(cur[k].e >> 32), 1, kWave))) << 32) |
+                    uint32_t(__shfl_up(uint32_t(cur[k].e), 1, kWave));
+      uint32_t p2 = 0;  // lane 0: record i-1 shares its predecessor's position
+      if (k == 0) {
+        if (lane == 0 && live && i > 0) {
+          pc = A.chrom[i - 1];
+          pp = A.pos[i - 1];
+          pr = A.rl[i - 1];
+          pa = A.al[i - 1];
+          pe = A.ext ? A.ext[i - 1] : 0ull;
+          p2 = uint32_t(i >= 2 && A.chrom[i - 2] == pc && A.pos[i - 2] == pp);
+        }
+      } else {  // the previous tile's last record (lane 63) is the predecessor
+        const uint32_t qc = __builtin_amdgcn_readlane(cur[k - 1].c, kWave - 1);
+        const uint32_t qp = __builtin_amdgcn_readlane(cur[k - 1].p, kWave - 1);
+        const uint32_t qr = __builtin_amdgcn_readlane(cur[k - 1].r, kWave - 1);
+        const uint32_t qa = __builtin_amdgcn_readlane(cur[k - 1].a, kWave - 1);
+        const uint64_t qe = (uint64_t(__builtin_amdgcn_readlane(uint32_t(cur[k - 1].e >> 32), kWave - 1)) << 32) |
+                            __builtin_amdgcn_readlane(uint32_t(cur[k - 1].e), kWave - 1);
+        if (lane == 0) {
+          pc = qc;
+          pp = qp;
+          pr = qr;
+          pa = qa;
+          pe = qe;
+          p2 = uint32_t(prev_sm >> (kWave - 1));
+        }
       }
+      const bool same = live && i > 0 && cur[k].c == pc && cur[k].p == pp;
+      const uint64_t sm = __ballot(same);
+      const uint32_t psame = lane == 0 ? p2 : uint32_t((sm >> (lane - 1)) & 1ull);
+      const bool cand = cur[k].r == pr && cur[k].a == pa && cur[k].e == pe;
+      listed[k] = __ballot(same && (cand || psame));
+      prev_sm = sm;
+      dd += uint32_t(__popcll(listed[k]));
     }
-    const uint32_t e1 = uint32_t(__popcll(__ballot(st == 1u))), e2 = uint32_t(__popcll(__ballot(st == 2u))),
-                   e3 = uint32_t(__popcll(__ballot(st == 3u)));
-    if (lane == 0) {
-      s_hk[wv] = hk;
-      s_hc[wv] = hc;
-      s_err[wv] = e1 | (e2 << 10) | (e3 << 20);
+    // the L8 histogram / status counters as this wave's partials (k_keyed_stats)
+    if (P.grp_stat) {
+      const uint64_t valid = __ballot(key8 != 0xFFFFFFFFu);
+      if (valid) {
+        const uint32_t k0 = __builtin_amdgcn_readlane(key8, uint32_t(__ffsll((unsigned long long)valid)) - 1);
+        if (!__ballot(key8 != 0xFFFFFFFFu && key8 != k0)) {
+          const uint32_t cnt = uint32_t(__popcll(valid));
+          if (hc && k0 != hk) {  // (uniform) a second key in this wave's tiles: the first goes out now
+            if (P.hist && lane == 0) atomicAdd(P.hist + hk, hc);
+            hc = 0;
+          }
+          hk = k0;
+          hc += cnt;
+        } else if (P.hist) {
+          wave_hist_add(key8, P.hist);  // a tile across an L8 boundary (sorted) or unsorted records
+        }
+      }
+      e1 += uint32_t(__popcll(__ballot(st == 1u)));
+      e2 += uint32_t(__popcll(__ballot(st == 2u)));
+      e3 += uint32_t(__popcll(__ballot(st == 3u)));
     }
-  }
-  // the tile's key / path bytes (key_tile renders exactly these: key_path_sizes)
-  {
+    // the tile's key / path bytes (key_tile renders exactly these: key_path_sizes)
     uint32_t ks = 0, ps = 0;
     if (live)
-      key_path_sizes(cur.c, cur.p, cur.r, cur.a, cur.e, cur.cd, A.max_seq_len, uint32_t(A.n_chrom),
+      key_path_sizes(cur[k].c, cur[k].p, cur[k].r, cur[k].a, cur[k].e, cur[k].cd, A.max_seq_len, uint32_t(A.n_chrom),
                      A.digest != nullptr || A.defer, A.code != nullptr, &ks, &ps);
-    const uint32_t K = wave_sum32(ks), Pp = wave_sum32(ps);
-    if (lane == 0) {
-      s_tk[wv] = K;
-      s_tp[wv] = Pp;
-      s_dd[wv] = uint32_t(__popcll(listed));
-    }
+    K += wave_sum32(ks);
+    Pt += wave_sum32(ps);
+  }
+  if (lane == 0) {
+    s_tk[wv] = K;
+    s_tp[wv] = Pt;
+    s_dd[wv] = dd;
+    s_hk[wv] = hk;
+    s_hc[wv] = hc;
+    s_err[wv] = e1 | (e2 << 10) | (e3 << 20);
   }
   __syncthreads();
 
   // ---- 2. the group's offsets (wave 0), its K3 slice space and statistics
   if (wv == 0) {
     uint64_t ak = 0, ap = 0;
-    uint32_t dd = 0;
+    uint32_t gdd = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kOpWaves; ++w) {
       ak += s_tk[w];
       ap += s_tp[w];
-      dd += s_dd[w];
+      gdd += s_dd[w];
     }
     uint32_t at = 0;
-    if (lane == 0 && dd) at = atomicAdd(P.dd_counts + (g % P.dd_slices), dd);
+    if (lane == 0 && gdd) at = atomicAdd(P.dd_counts + (g % P.dd_slices), gdd);
     if (lane == 0 && P.grp_stat) {
-      uint32_t k0 = 0xFFFFFFFFu, c0 = 0, k1 = 0xFFFFFFFFu, c1 = 0, er = 0;
+      uint32_t k0 = 0xFFFFFFFFu, c0 = 0, k1 = 0xFFFFFFFFu, c1 = 0, r1 = 0, r2 = 0, r3 = 0;
 #pragma unroll
       for (uint32_t w = 0; w < kOpWaves; ++w) {
-        const uint32_t k = s_hk[w], c = s_hc[w];
-        er += s_err[w];
+        const uint32_t kk = s_hk[w], c = s_hc[w];
+        r1 += s_err[w] & 0x3FFu;
+        r2 += (s_err[w] >> 10) & 0x3FFu;
+        r3 += s_err[w] >> 20;
         if (!c) continue;
-        if (k == k0 || !c0) {
-          k0 = k;
+        if (kk == k0 || !c0) {
+          k0 = kk;
           c0 += c;
-        } else if (k == k1 || !c1) {
-          k1 = k;
+        } else if (kk == k1 || !c1) {
+          k1 = kk;
           c1 += c;
         } else if (P.hist) {
-          atomicAdd(P.hist + k, c);
+          atomicAdd(P.hist + kk, c);
         }
       }
-      P.grp_stat[g] = make_uint4(k0, c0 | (c1 << 16), k1, er);
+      P.grp_stat[2 * g] = make_uint4(k0, c0, k1, c1);
+      P.grp_stat[2 * g + 1] = make_uint4(r1, r2, r3, 0);
     }
     uint64_t xk, xp;
     group_lookback(P.lb, P.hdr, g, ak, ap, &xk, &xp);
@@ -945,13 +1023,17 @@ __global__ __launch_bounds__(kBlock, 4) void k_keyed_onepass(KeyArgs A, PrepArgs
   }
   __syncthreads();
 
-  // ---- 3. the K3 list entries and this wave's tile of text
-  if (listed) {
+  // ---- 3. the K3 list entries and this wave's tiles of text
+  if (dd) {
     uint32_t before = s_ddat;
     for (uint32_t w = 0; w < wv; ++w) before += s_dd[w];
-    if ((listed >> lane) & 1ull)
-      P.dd_list[size_t(g % P.dd_slices) * P.dd_slice + before + uint32_t(__popcll(listed & ((1ull << lane) - 1)))] =
-          uint32_t(i);
+    uint32_t* slot = P.dd_list + size_t(g % P.dd_slices) * P.dd_slice;
+#pragma unroll
+    for (uint32_t k = 0; k < TPW; ++k) {
+      if ((listed[k] >> lane) & 1ull)
+        slot[before + uint32_t(__popcll(listed[k] & ((1ull << lane) - 1)))] = uint32_t(w0 + k * kWave + lane);
+      before += uint32_t(__popcll(listed[k]));
+    }
   }
   uint64_t run_k = s_base[0], run_p = s_base[1];
   for (uint32_t w = 0; w < wv; ++w) {
@@ -959,7 +1041,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_keyed_onepass(KeyArgs A, PrepArgs
     run_p += s_tp[w];
   }
   wave_lds_sync();  // (this wave's images were zeroed above)
-  key_tile(A, cur, t0, run_k, run_p, kimg, pimg, make_heap(A.heap, A.heap_bytes), lane);
+  // (written out: a loop over key_tile is too large for the unroller, and cur[] indexed
+  // at run time would live in scratch)
+  key_tile(A, cur[0], w0, run_k, run_p, kimg, pimg, hp, lane);
+  if constexpr (TPW > 1) key_tile(A, cur[1 % TPW], w0 + kWave, run_k, run_p, kimg, pimg, hp, lane);
+  if constexpr (TPW > 2) key_tile(A, cur[2 % TPW], w0 + 2 * kWave, run_k, run_p, kimg, pimg, hp, lane);
+  if constexpr (TPW > 3) key_tile(A, cur[3 % TPW], w0 + 3 * kWave, run_k, run_p, kimg, pimg, hp, lane);
+  static_assert(TPW >= 1 && TPW <= 4, "tiles per wave");
 }
 
 // the histogram and counters from the groups' partials: a thread per 8 groups,
@@ -974,18 +1062,21 @@ __global__ __launch_bounds__(kBlock) void k_keyed_stats(const uint4* __restrict_
   const size_t g0 = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) * kStatGroups;
   uint32_t rk = 0xFFFFFFFFu, rc = 0, e1 = 0, e2 = 0, e3 = 0;
   uint64_t recs = 0;
-  uint4 v[kStatGroups];
+  uint4 v[kStatGroups], x[kStatGroups];
 #pragma unroll
-  for (uint32_t k = 0; k < kStatGroups; ++k) v[k] = g0 + k < n_groups ? grp[g0 + k] : make_uint4(0xFFFFFFFFu, 0, 0xFFFFFFFFu, 0);
+  for (uint32_t k = 0; k < kStatGroups; ++k) {
+    v[k] = g0 + k < n_groups ? grp[2 * (g0 + k)] : make_uint4(0xFFFFFFFFu, 0, 0xFFFFFFFFu, 0);
+    x[k] = g0 + k < n_groups ? grp[2 * (g0 + k) + 1] : make_uint4(0, 0, 0, 0);
+  }
 #pragma unroll
   for (uint32_t k = 0; k < kStatGroups; ++k) {
     if (g0 + k >= n_groups) break;
-    const size_t r0 = (g0 + k) * kOpGroup;
-    recs += n - r0 < kOpGroup ? n - r0 : kOpGroup;
-    e1 += v[k].w & 0x3FFu;
-    e2 += (v[k].w >> 10) & 0x3FFu;
-    e3 += (v[k].w >> 20) & 0x3FFu;
-    const uint32_t kk[2] = {v[k].x, v[k].z}, cc[2] = {v[k].y & 0xFFFFu, v[k].y >> 16};
+    const size_t r0 = (g0 + k) * kOpGroupRecs;
+    recs += n - r0 < kOpGroupRecs ? n - r0 : kOpGroupRecs;
+    e1 += x[k].x;
+    e2 += x[k].y;
+    e3 += x[k].z;
+    const uint32_t kk[2] = {v[k].x, v[k].z}, cc[2] = {v[k].y, v[k].w};
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       if (!cc[q]) continue;
@@ -1321,7 +1412,7 @@ extern "C" int avdb_primary_keys_fill_digests(avdb_ctx* ctx, const uint8_t* chro
 }
 
 // ---- the keyed one-pass prep (K2 + K7 in one launch) ------------------------------
-static size_t onepass_groups(size_t n) { return (n + kOpGroup - 1) / kOpGroup; }
+static size_t onepass_groups(size_t n) { return (n + kOpGroupRecs - 1) / kOpGroupRecs; }
 
 namespace avdb {
 // K3's list layout under avdb_keyed_prep: `grid` slices of `slice` entries (group g
@@ -1330,14 +1421,14 @@ void keyed_onepass_dd_layout(size_t n, unsigned* grid, size_t* slice) {
   const size_t ng = onepass_groups(n);
   const size_t sl = ng < kOpSlicesMax ? (ng ? ng : 1) : kOpSlicesMax;
   *grid = unsigned(sl);
-  *slice = ((ng + sl - 1) / sl) * kOpGroup;
+  *slice = ((ng + sl - 1) / sl) * kOpGroupRecs;
 }
 }  // namespace avdb
 
 extern "C" int avdb_keyed_prep_workspace_size(size_t n, size_t* bytes) {
   if (!bytes) return AVDB_EINVAL;
   const size_t ng = onepass_groups(n);
-  *bytes = 256 + 16 * ng + 16 * ng;  // header | look-back granules (2 x u64) | group statistics (uint4)
+  *bytes = 256 + 16 * ng + 32 * ng;  // header | look-back granules (2 x u64) | group statistics (2 x uint4)
   return AVDB_OK;
 }
 
@@ -1434,7 +1525,7 @@ extern "C" int avdb_keyed_prep(avdb_ctx* ctx, const uint8_t* chrom, const uint32
     avdb_set_error("avdb_keyed_prep: too many groups");
     return AVDB_EINVAL;
   }
-  hipLaunchKernelGGL(k_keyed_onepass, dim3(unsigned(ng)), dim3(kBlock), 0, s, A, P, ctx->tab);
+  hipLaunchKernelGGL(k_keyed_onepass<kOpTpw>, dim3(unsigned(ng)), dim3(kOpBlock), 0, s, A, P, ctx->tab);
   AVDB_LAUNCH_CHECK("k_keyed_onepass");
   if (P.grp_stat) {
     const size_t threads = (ng + kStatGroups - 1) / kStatGroups;

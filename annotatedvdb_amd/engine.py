@@ -853,10 +853,14 @@ class Engine:
 
     # -- K4 ----------------------------------------------------------------
     def vrs_digest(self, b: RecordBatch, max_seq_len: int = 50,
-                   workspace: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                   workspace: Optional[torch.Tensor] = None,
+                   keys: Optional["KeyText"] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Returns ``(digests uint8[n,32], is_long uint8[n])``.  Only the rows
         with ``is_long`` set are written (the rest are unspecified: zero-filling
-        32 bytes per record would cost more HBM traffic than the digests)."""
+        32 bytes per record would cost more HBM traffic than the digests).
+        ``keys``: the ``KeyText`` of a deferred ``primary_keys`` / ``keyed_prep``
+        on this batch — the digests also go into its pending keys
+        (``avdb_vrs_digest_keys``: no :meth:`fill_digests` pass)."""
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
@@ -870,10 +874,14 @@ class Engine:
         codes = self._pending.pop("codes", None)
         ready = (codes is not None and codes[1:] == (n, int(max_seq_len))
                  and _stamp_ok(codes[0], ws, b.ref_len, b.alt_len))
-        N.check("avdb_vrs_digest_ex", self.lib.avdb_vrs_digest_ex(
-            self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
-            N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, int(max_seq_len), N.ptr(ws), int(sz.value),
-            N.ptr(dig), N.ptr(is_long), N.DIGEST_CODES_READY if ready else 0, self._stream()))
+        args = (self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
+                N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, int(max_seq_len), N.ptr(ws), int(sz.value),
+                N.ptr(dig), N.ptr(is_long), N.DIGEST_CODES_READY if ready else 0)
+        if keys is None:
+            N.check("avdb_vrs_digest_ex", self.lib.avdb_vrs_digest_ex(*args, self._stream()))
+        else:
+            N.check("avdb_vrs_digest_keys", self.lib.avdb_vrs_digest_keys(
+                *args, N.ptr(keys.key_off), N.ptr(keys.keys), N.ptr(keys.state), self._stream()))
         return dig, is_long
 
     def sha512t24u(self, blobs: Sequence[bytes]) -> List[str]:

@@ -19,7 +19,8 @@ Layouts (``layout``):
   ``onepass``  K2 and K7 as ONE pass over the SoA (avdb_keyed_prep: K2's outputs,
                K3's marks, K4's codes and the keys + paths with the long keys'
                digests pending; text offsets by a decoupled look-back over
-               256-record groups), then K3, K4 and the digest fill;
+               1,024-record groups), then K3, then K4, which also writes the
+               digests into the pending keys (avdb_vrs_digest_keys);
   ``serial``   K2, K3, K4, K7 in the launch stream;
   ``fork``     K3 on a second stream beside K4 / K7 (it reads only K2's outputs and
                nothing reads keep until the step ends), joined at the end;
@@ -120,9 +121,8 @@ class KeyedStep:
                 b, kt, max_seq_len=msl, defer_digest=self.digests, hist=self.hist, counters=self.counters,
                 digest_workspace=self.ws4, dedup_workspace=self.ws3, workspace=self.ws_op))
             keep = t("pk_dedup", main, dedup)
-            if self.digests:
-                dig, is_long = t("vrs_digest", main, digest)
-                t("fill_digests", main, lambda: eng.fill_digests(b, dig, kt))
+            if self.digests:  # (K4 writes the pending keys' digest characters too)
+                dig, is_long = t("vrs_digest", main, lambda: eng.vrs_digest(b, msl, workspace=self.ws4, keys=kt))
             if events is not None:
                 span1 = torch.cuda.Event(enable_timing=True)
                 span1.record(main)

@@ -195,6 +195,16 @@ int avdb_vrs_digest_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                        const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
                        size_t n, uint32_t max_seq_len, void* workspace, size_t workspace_bytes, char* digest_out,
                        uint8_t* is_long, uint32_t flags, void* stream);
+/* The same, and every long record's 32 characters also written into the key text
+ * of a deferred K7 / avdb_keyed_prep call on the same batch (key_off / key_out /
+ * key_state: that call's; the keys in state AVDB_KEY_DIGEST_PENDING get them at
+ * key_off[i] + len("label:pos:") and become AVDB_KEY_OK) — the work of
+ * avdb_primary_keys_fill_digests without its pass over every record. */
+int avdb_vrs_digest_keys(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos, const uint64_t* allele_off,
+                         const uint32_t* ref_len, const uint32_t* alt_len, const uint8_t* heap, size_t heap_bytes,
+                         size_t n, uint32_t max_seq_len, void* workspace, size_t workspace_bytes, char* digest_out,
+                         uint8_t* is_long, uint32_t flags, const uint64_t* key_off, uint8_t* key_out,
+                         uint8_t* key_state, void* stream);
 
 /* ---- K0: VCF text -> per-alt record SoA ----------------------------------
  * Replaces the text half of VcfEntryParser.parse_entry / get_variant / get_refsnp
@@ -531,7 +541,7 @@ int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* 
  * AVDB_KEYS_DIGEST_DEFERRED lays long keys out for avdb_primary_keys_fill_digests;
  * without it they are AVDB_KEY_NEED_DIGEST).  Text capacities as
  * avdb_primary_keys_bound.  workspace: avdb_keyed_prep_workspace_size(n) bytes,
- * 16-byte aligned (32 B per 256 records).  Groups of 256 records take their text
+ * 16-byte aligned (48 B per group of 1,024 records).  Groups of 256 records take their text
  * offsets from a decoupled look-back in the launch; *written = AVDB_KEYED_LONG_CODES |
  * AVDB_KEYED_DEDUP_MARKS for what it wrote.  avdb_keyed_prep_lookback_errors reads
  * (synchronously) how many look-back polls gave up in the last call on this workspace
