@@ -18,10 +18,13 @@ P = {
                  ("  if constexpr (TPW > 2) key_tile(", "  if constexpr (TPW > 2) if (run_k == 12345) key_tile("),
                  ("  if constexpr (TPW > 3) key_tile(", "  if constexpr (TPW > 3) if (run_k == 12345) key_tile(")],
     "tpw2": [], "tpw1": [], "w1": [], "w2": [], "w1t2": [], "w2t2": [],
+    "t1np": [], "t2np": [], "t2p": [], "t4np": [],
 }
 flags = {"tpw2": ["-DAVDB_OP_TPW=2"], "tpw1": ["-DAVDB_OP_TPW=1"], "w1": ["-DAVDB_OP_WAVES=1"],
          "w2": ["-DAVDB_OP_WAVES=2"], "w1t2": ["-DAVDB_OP_WAVES=1", "-DAVDB_OP_TPW=2"],
-         "w2t2": ["-DAVDB_OP_WAVES=2", "-DAVDB_OP_TPW=2"]}
+         "w2t2": ["-DAVDB_OP_WAVES=2", "-DAVDB_OP_TPW=2"],
+         "t1np": ["-DAVDB_OP_TPW=1", "-DAVDB_OP_PIPE=0"], "t2np": ["-DAVDB_OP_TPW=2", "-DAVDB_OP_PIPE=0"],
+         "t2p": ["-DAVDB_OP_TPW=2", "-DAVDB_OP_PIPE=1"], "t4np": ["-DAVDB_OP_TPW=4", "-DAVDB_OP_PIPE=0"]}
 for name in (sys.argv[1:] or P):
     s = src
     for a, b in P[name]:
