@@ -103,6 +103,7 @@ EXPORTED_SYMBOLS = [
     "avdb_primary_keys_fill_digests",
     "avdb_record_prep_keyed",
     "avdb_keyed_prep_workspace_size", "avdb_keyed_prep", "avdb_keyed_prep_lookback_errors", "avdb_vrs_digest_keys",
+    "avdb_keys_off32_bytes",
     "avdb_shard_workspace_size", "avdb_vcf_select_lines", "avdb_vcf_select_copy",
     "avdb_small_prep", "avdb_small_prep_host", "avdb_bin_path_host", "avdb_annotate_host", "avdb_host_alloc", "avdb_host_free",
     "avdb_rccl_unique_id", "avdb_rccl_comm_init", "avdb_rccl_comm_destroy",
@@ -113,6 +114,7 @@ EXPORTED_SYMBOLS = [
 SMALL_PATH, SMALL_KEY, SMALL_DISPLAY = 1, 2, 4
 KEYS_TOTALS_READY = 1  # AVDB_KEYS_TOTALS_READY
 KEYS_DIGEST_DEFERRED = 2  # AVDB_KEYS_DIGEST_DEFERRED
+KEYS_OFF32 = 4  # AVDB_KEYS_OFF32 (narrow key / path offsets)
 OPT_K4_GRID, OPT_K7_GRID = 1, 2  # avdb_ctx_set_option
 KEYED_TOTALS, KEYED_LONG_CODES, KEYED_DEDUP_MARKS = 1, 2, 4  # avdb_record_prep_keyed's *totals_written bits
 DEDUP_MARKED = 1  # AVDB_DEDUP_MARKED
@@ -209,6 +211,7 @@ def _sig(lib):
                                   P, P, P, SZ, P, SZ, P, U32, ctypes.POINTER(I32), P]
     f.avdb_keyed_prep_lookback_errors.argtypes = [P, P, ctypes.POINTER(U32)]
     f.avdb_vrs_digest_keys.argtypes = list(f.avdb_vrs_digest_ex.argtypes)[:-1] + [P, P, P, P]
+    f.avdb_keys_off32_bytes.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_primary_keys_bound.argtypes = [SZ, SZ, ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
     f.avdb_primary_keys_onepass_workspace_size.argtypes = [SZ, ctypes.POINTER(SZ)]
     f.avdb_keyset_probe_text.argtypes = [P, P, SZ, P, P, SZ, P, P, P, SZ, P, P, P]

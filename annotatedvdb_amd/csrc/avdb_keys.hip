@@ -84,7 +84,27 @@ struct KeyArgs {
   const uint64_t* blk_pre;
   uint32_t group_log2;  // records per scan group = 64 << group_log2 (tiles per group = 1 << group_log2)
   uint32_t blk_raw;     // blk_pre holds each block's totals, not their exclusive scan
+  uint32_t off32;       // AVDB_KEYS_OFF32: key_off / path_off in the narrow layout (off32_store)
 };
+
+// AVDB_KEYS_OFF32 (avdb.h): an offset array of n + 1 entries as u32 low words
+// (offset mod 2^32), then, from the next 8-byte boundary, a u64 base for every
+// kOff32Span records (the full offset of record k * kOff32Span): 4 bytes per record
+// written instead of 8.  Full offset of i = base[i / kOff32Span] +
+// (uint32_t)(low[i] - (uint32_t)base[i / kOff32Span]) — a span's text is < 4 GB.
+constexpr uint32_t kOff32Log2 = 12, kOff32Span = 1u << kOff32Log2;
+__host__ __device__ inline size_t off32_low_bytes(size_t n) { return (4 * (n + 1) + 7) & ~size_t(7); }
+__host__ __device__ inline size_t off32_bytes(size_t n) { return off32_low_bytes(n) + 8 * ((n >> kOff32Log2) + 1); }
+template <bool NARROW>
+__device__ __forceinline__ void off_store(uint64_t* off, size_t n, size_t i, uint64_t v) {
+  if constexpr (!NARROW) {
+    off[i] = v;
+    return;
+  }
+  reinterpret_cast<uint32_t*>(off)[i] = uint32_t(v);
+  if (!(i & (kOff32Span - 1)))
+    reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(off) + off32_low_bytes(n))[i >> kOff32Log2] = v;
+}
 
 #ifndef AVDB_K7_GRID
 #define AVDB_K7_GRID 16384u  // write-pass waves / 4 (C4k K7 5.14 -> 5.00 ms against 4,096; with one-wave workgroups the grid is 4x this)
@@ -237,8 +257,9 @@ __global__ __launch_bounds__(kScanThreads) void k_key_group_scan(const uint2* __
 // exclusive scan of the block totals in place (one workgroup, sequential chunks),
 // and the grand totals into key_off[n] / path_off[n]
 __global__ __launch_bounds__(kScanThreads) void k_key_block_scan(uint64_t* __restrict__ b, size_t nb,
-                                                                 uint64_t* __restrict__ key_end,
-                                                                 uint64_t* __restrict__ path_end) {
+                                                                 uint64_t* __restrict__ key_off,
+                                                                 uint64_t* __restrict__ path_off, size_t n,
+                                                                 uint32_t off32) {
   __shared__ uint64_t s_k[kScanThreads / kWave], s_p[kScanThreads / kWave];
   const uint32_t lane = __lane_id(), wv = threadIdx.x / kWave;
   uint64_t run_k = 0, run_p = 0;
@@ -280,8 +301,13 @@ __global__ __launch_bounds__(kScanThreads) void k_key_block_scan(uint64_t* __res
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    *key_end = run_k;
-    if (path_end) *path_end = run_p;
+    if (off32) {
+      off_store<true>(key_off, n, n, run_k);
+      if (path_off) off_store<true>(path_off, n, n, run_p);
+    } else {
+      off_store<false>(key_off, n, n, run_k);
+      if (path_off) off_store<false>(path_off, n, n, run_p);
+    }
   }
 }
 
@@ -442,6 +468,7 @@ __device__ __forceinline__ void append2(O& o, uint64_t w0, uint64_t w1, uint32_t
 // run_k / run_p (advanced by the tile's totals), their offsets and states, the
 // key and path text rendered into the wave's LDS images and flushed.  cur: record
 // t0 + lane (live: t0 + lane < A.n).
+template <bool NARROW = false>
 __device__ __forceinline__ void key_tile(const KeyArgs& A, const KeyTileIn& cur, size_t t0, uint64_t& run_k,
                                          uint64_t& run_p, lds_u64* kimg, lds_u64* pimg, const Heap& hheap,
                                          uint32_t lane) {
@@ -473,11 +500,11 @@ __device__ __forceinline__ void key_tile(const KeyArgs& A, const KeyTileIn& cur,
   const bool lng = uint64_t(r) + a > A.max_seq_len;
   uint8_t st = AVDB_KEY_HOST;
   if (live) {
-    A.key_off[i] = ko;
-    if (A.code) A.path_off[i] = po;
+    off_store<NARROW>(A.key_off, A.n, i, ko);
+    if (A.code) off_store<NARROW>(A.path_off, A.n, i, po);
     if (i + 1 == A.n) {
-      A.key_off[A.n] = ko1;
-      if (A.code) A.path_off[A.n] = po1;
+      off_store<NARROW>(A.key_off, A.n, A.n, ko1);
+      if (A.code) off_store<NARROW>(A.path_off, A.n, A.n, po1);
     }
     st = AVDB_KEY_OK;
     if (c >= n_chrom || (e >> 63)) st = AVDB_KEY_HOST;  // no label / interned external id
@@ -584,6 +611,7 @@ constexpr uint32_t kV2Block = AVDB_K7_V2_BLOCK, kV2Waves = kV2Block / kWave;
 #ifndef AVDB_K7_V2_WAVES
 #define AVDB_K7_V2_WAVES 4
 #endif
+template <bool NARROW>
 __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(KeyArgs A) {
   __shared__ uint64_t s_kimg[kV2Waves * kKeyWave / 8];
   __shared__ uint64_t s_pimg[kV2Waves * kPathWave / 8];
@@ -636,7 +664,7 @@ __global__ __launch_bounds__(kV2Block, AVDB_K7_V2_WAVES) void k_record_keys_v2(K
         run_p = A.blk_pre[2 * b + 1] + gp.y;
       }
     }
-    key_tile(A, cur, t0, run_k, run_p, kimg, pimg, hheap, lane);
+    key_tile<NARROW>(A, cur, t0, run_k, run_p, kimg, pimg, hheap, lane);
   }
 }
 
@@ -1249,7 +1277,7 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
     avdb_set_error("avdb_primary_keys_onepass: null argument");
     return AVDB_EINVAL;
   }
-  if (flags & ~(AVDB_KEYS_TOTALS_READY | AVDB_KEYS_DIGEST_DEFERRED)) {
+  if (flags & ~(AVDB_KEYS_TOTALS_READY | AVDB_KEYS_DIGEST_DEFERRED | AVDB_KEYS_OFF32)) {
     avdb_set_error("avdb_primary_keys_onepass_ex: unknown flags 0x%x", flags);
     return AVDB_EINVAL;
   }
@@ -1259,10 +1287,15 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   }
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t ob = (flags & AVDB_KEYS_OFF32) ? off32_bytes(0) : 8;  // (n = 0: low word 0 and base 0)
   if (n == 0) {
-    AVDB_HIP_TRY(hipMemsetAsync(key_off, 0, 8, s));
-    if (bin_code) AVDB_HIP_TRY(hipMemsetAsync(path_off, 0, 8, s));
+    AVDB_HIP_TRY(hipMemsetAsync(key_off, 0, ob, s));
+    if (bin_code) AVDB_HIP_TRY(hipMemsetAsync(path_off, 0, ob, s));
     return AVDB_OK;
+  }
+  if ((flags & AVDB_KEYS_OFF32) && (reinterpret_cast<uintptr_t>(key_off) % 8 || (bin_code && reinterpret_cast<uintptr_t>(path_off) % 8))) {
+    avdb_set_error("avdb_primary_keys_onepass_ex: AVDB_KEYS_OFF32 offset buffers must be 8-byte aligned");
+    return AVDB_EINVAL;
   }
   if (!chrom || !pos || !allele_off || !ref_len || !alt_len || !heap) {
     avdb_set_error("avdb_primary_keys_onepass: null array");
@@ -1290,6 +1323,7 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   KeyArgs A = key_args(ctx, chrom, pos, allele_off, ref_len, alt_len, heap, heap_bytes, ext_id, bin_code, digest, n,
                        max_seq_len, key_off, path_off, key_out, key_cap, path_out, path_cap, key_state);
   A.defer = (flags & AVDB_KEYS_DIGEST_DEFERRED) ? 1u : 0u;
+  A.off32 = (flags & AVDB_KEYS_OFF32) ? 1u : 0u;
   A.grp_pre = gpre;
   A.blk_pre = bpre;
   A.group_log2 = key_group_log2(n);
@@ -1309,8 +1343,8 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   hipLaunchKernelGGL(k_key_group_scan, dim3(unsigned(nb)), dim3(kScanThreads), 0, s, tot, ng, gpre, bpre, A, ready);
   AVDB_LAUNCH_CHECK("k_key_group_scan");
   if (!A.blk_raw) {
-    hipLaunchKernelGGL(k_key_block_scan, dim3(1), dim3(kScanThreads), 0, s, bpre, nb, key_off + n,
-                       bin_code ? path_off + n : nullptr);
+    hipLaunchKernelGGL(k_key_block_scan, dim3(1), dim3(kScanThreads), 0, s, bpre, nb, key_off,
+                       bin_code ? path_off : nullptr, n, A.off32);
     AVDB_LAUNCH_CHECK("k_key_block_scan");
   }
   // (one workgroup doing both scans for C1's 17 K groups measured 11.9 us against
@@ -1318,7 +1352,9 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   // write pass sums the block totals itself.  One resident generation, 5
   // workgroups per CU, ran 12.3 vs 10.2 ms on C4k, with or without XCD-aware
   // renumbering: the finer grid balances better.)
-  hipLaunchKernelGGL(k_record_keys_v2, dim3(unsigned(wneed < wmax ? wneed : wmax)), dim3(kV2Block), 0, s, A);
+  const dim3 wgrid(unsigned(wneed < wmax ? wneed : wmax));
+  if (A.off32) hipLaunchKernelGGL(k_record_keys_v2<true>, wgrid, dim3(kV2Block), 0, s, A);
+  else hipLaunchKernelGGL(k_record_keys_v2<false>, wgrid, dim3(kV2Block), 0, s, A);
   AVDB_LAUNCH_CHECK("k_record_keys_v2");
   return AVDB_OK;
 }
@@ -1541,5 +1577,11 @@ extern "C" int avdb_keyed_prep_lookback_errors(avdb_ctx* ctx, const void* worksp
   if (!ctx || !workspace || !out) return AVDB_EINVAL;
   AVDB_HIP_TRY(hipSetDevice(ctx->device));
   AVDB_HIP_TRY(hipMemcpy(out, static_cast<const uint32_t*>(workspace) + 1, 4, hipMemcpyDeviceToHost));
+  return AVDB_OK;
+}
+
+extern "C" int avdb_keys_off32_bytes(size_t n, size_t* bytes) {
+  if (!bytes) return AVDB_EINVAL;
+  *bytes = off32_bytes(n);
   return AVDB_OK;
 }

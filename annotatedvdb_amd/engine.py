@@ -226,19 +226,39 @@ class FormatResult:
 class KeyText:
     """Output of ``Engine.primary_keys`` (device tensors): key i is
     ``keys[key_off[i]:key_off[i+1]]`` when ``state[i] == KEY_OK``; path i is
-    ``paths[path_off[i]:path_off[i+1]]`` (empty for an unmappable record)."""
+    ``paths[path_off[i]:path_off[i+1]]`` (empty for an unmappable record).
+    ``off32``: ``key_off`` / ``path_off`` are raw buffers in the narrow layout
+    (AVDB_KEYS_OFF32: uint32 low words + a uint64 base per 4,096 records) —
+    :meth:`key_offsets` / :meth:`path_offsets` give the int64 offsets either way."""
     ws: torch.Tensor
     key_off: torch.Tensor
     path_off: Optional[torch.Tensor]
     state: torch.Tensor
     keys: Optional[torch.Tensor]
     paths: Optional[torch.Tensor]
+    off32: bool = False
+
+    @staticmethod
+    def _wide(t: torch.Tensor, n: int) -> torch.Tensor:
+        lb = (4 * (n + 1) + 7) & ~7
+        low = t[: 4 * (n + 1)].view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        base = t[lb: lb + 8 * ((n >> 12) + 1)].view(torch.int64).repeat_interleave(4096)[: n + 1]
+        return base + ((low - (base & 0xFFFFFFFF)) & 0xFFFFFFFF)
+
+    def key_offsets(self, n: int) -> torch.Tensor:
+        """int64 key offsets [n + 1] (device)."""
+        return self._wide(self.key_off, n) if self.off32 else self.key_off[: n + 1]
+
+    def path_offsets(self, n: int) -> Optional[torch.Tensor]:
+        if self.path_off is None:
+            return None
+        return self._wide(self.path_off, n) if self.off32 else self.path_off[: n + 1]
 
     def host(self, n: int):
         """(keys, paths) as Python lists of str (None where not rendered).
         Raises ``ValueError`` if a text did not fit its buffer (a reused
         ``KeyText`` too small for this batch: state KEY_OVERFLOW / PATH_OVERFLOW)."""
-        ko = self.key_off[: n + 1].cpu().numpy()
+        ko = self.key_offsets(n).cpu().numpy()
         kb = self.keys[: int(ko[n])].cpu().numpy().tobytes()
         st = self.state[:n].cpu().numpy()
         if ((st == N.KEY_OVERFLOW) | ((st & N.PATH_OVERFLOW) != 0)).any():
@@ -246,7 +266,7 @@ class KeyText:
         keys = [kb[ko[i]:ko[i + 1]].decode() if st[i] == N.KEY_OK else None for i in range(n)]
         paths = None
         if self.paths is not None:
-            po = self.path_off[: n + 1].cpu().numpy()
+            po = self.path_offsets(n).cpu().numpy()
             pb = self.paths[: int(po[n])].cpu().numpy().tobytes()
             paths = [pb[po[i]:po[i + 1]].decode() or None for i in range(n)]
         return keys, paths
@@ -779,8 +799,8 @@ class Engine:
         n = b.n
         self._check_alleles(b)
         self._pending.clear()
-        if kt.key_off.numel() < n + 1 or kt.state.numel() < max(1, n) or kt.keys is None:
-            raise ValueError("keyed_prep: the KeyText holds fewer records")
+        if kt.key_off.numel() < n + 1 or kt.state.numel() < max(1, n) or kt.keys is None or kt.off32:
+            raise ValueError("keyed_prep: the KeyText holds fewer records (or narrow offsets)")
         sz = ctypes.c_size_t()
         self.lib.avdb_keyed_prep_workspace_size(n, ctypes.byref(sz))
         ws = workspace if workspace is not None and workspace.numel() >= sz.value else \
@@ -880,6 +900,8 @@ class Engine:
         if keys is None:
             N.check("avdb_vrs_digest_ex", self.lib.avdb_vrs_digest_ex(*args, self._stream()))
         else:
+            if keys.off32:
+                raise ValueError("vrs_digest(keys=...): narrow key offsets are not accepted")
             N.check("avdb_vrs_digest_keys", self.lib.avdb_vrs_digest_keys(
                 *args, N.ptr(keys.key_off), N.ptr(keys.keys), N.ptr(keys.state), self._stream()))
         return dig, is_long
@@ -1147,6 +1169,8 @@ class Engine:
             out = KeyText(ws=self.empty(int(sz.value), torch.uint8), key_off=self.empty(n + 1, torch.int64),
                           path_off=self.empty(n + 1, torch.int64) if code is not None else None,
                           state=self.empty(max(1, n), torch.uint8), keys=None, paths=None)
+        if out.off32:
+            raise ValueError("primary_keys: narrow offsets need the one-pass form")
         if out.key_off.numel() < n + 1 or out.state.numel() < max(1, n) or \
                 (code is not None and (out.path_off is None or out.path_off.numel() < n + 1)):
             raise ValueError("primary_keys: the reused KeyText holds fewer records (or no paths)")
@@ -1164,24 +1188,33 @@ class Engine:
                 out.paths.numel() if out.paths is not None else 0, N.ptr(out.state), s))
         return out
 
-    def new_key_text(self, n: int, heap_bytes: int, paths: bool = True) -> "KeyText":
+    def new_key_text(self, n: int, heap_bytes: int, paths: bool = True, off32: bool = False) -> "KeyText":
         """Buffers for one-pass K7 output over ``n`` records with ``heap_bytes`` of
         alleles (texts sized by ``avdb_primary_keys_bound``): what a keyed K2 writes
-        its group totals into before the first ``primary_keys(..., out=...)``."""
+        its group totals into before the first ``primary_keys(..., out=...)``.
+        ``off32``: the offsets in the narrow layout (AVDB_KEYS_OFF32, for exactly
+        ``n`` records)."""
         sz = ctypes.c_size_t()
         self.lib.avdb_primary_keys_onepass_workspace_size(n, ctypes.byref(sz))
         kc, pc = ctypes.c_size_t(), ctypes.c_size_t()
         self.lib.avdb_primary_keys_bound(n, heap_bytes, ctypes.byref(kc), ctypes.byref(pc))
-        return KeyText(ws=self.empty(int(sz.value), torch.uint8), key_off=self.empty(n + 1, torch.int64),
-                       path_off=self.empty(n + 1, torch.int64) if paths else None,
+        if off32:
+            ob = ctypes.c_size_t()
+            self.lib.avdb_keys_off32_bytes(n, ctypes.byref(ob))
+            mk = lambda: self.empty(int(ob.value), torch.uint8)  # noqa: E731
+        else:
+            mk = lambda: self.empty(n + 1, torch.int64)  # noqa: E731
+        return KeyText(ws=self.empty(int(sz.value), torch.uint8), key_off=mk(), path_off=mk() if paths else None,
                        state=self.empty(max(16, n), torch.uint8), keys=self.empty(int(kc.value), torch.uint8),
-                       paths=self.empty(int(pc.value), torch.uint8) if paths else None)
+                       paths=self.empty(int(pc.value), torch.uint8) if paths else None, off32=off32)
 
     def fill_digests(self, b: RecordBatch, digest: torch.Tensor, kt: "KeyText"):
         """``avdb_primary_keys_fill_digests``: the digest characters of every key a
         ``primary_keys(..., defer_digest=True)`` left pending (``digest`` = this
         batch's ``vrs_digest`` output)."""
         b = b if b.device == self.device else b.to(self.device)
+        if kt.off32:
+            raise ValueError("fill_digests: narrow key offsets are not accepted")
         N.check("avdb_primary_keys_fill_digests", self.lib.avdb_primary_keys_fill_digests(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), b.n, N.ptr(digest), N.ptr(kt.key_off), N.ptr(kt.keys),
             N.ptr(kt.state), self._stream()))
@@ -1201,6 +1234,11 @@ class Engine:
         if out.key_off.numel() < n + 1 or out.state.numel() < max(1, n) or \
                 (code is not None and (out.path_off is None or out.path_off.numel() < n + 1 or out.paths is None)):
             raise ValueError("primary_keys: the reused KeyText holds fewer records (or no paths)")
+        if out.off32:
+            ob = ctypes.c_size_t()
+            self.lib.avdb_keys_off32_bytes(n, ctypes.byref(ob))
+            if out.key_off.numel() < ob.value or (code is not None and out.path_off.numel() < ob.value):
+                raise ValueError("primary_keys: the narrow offset buffers were made for fewer records")
         if out.ws.numel() < sz.value:
             out.ws = self.empty(int(sz.value), torch.uint8)
         # the keyed K2 wrote this batch's group totals into this KeyText's workspace
@@ -1208,7 +1246,8 @@ class Engine:
         tot = self._pending.pop("totals", None)
         ready = (tot is not None and tot[1] is out and tot[2:] == (n, int(max_seq_len), digest is not None or defer)
                  and _stamp_ok(tot[0], out.ws, b.chrom, b.pos, b.ref_len, b.alt_len, b.ext_id, code))
-        flags = (N.KEYS_TOTALS_READY if ready else 0) | (N.KEYS_DIGEST_DEFERRED if defer else 0)
+        flags = (N.KEYS_TOTALS_READY if ready else 0) | (N.KEYS_DIGEST_DEFERRED if defer else 0) | \
+            (N.KEYS_OFF32 if out.off32 else 0)
         N.check("avdb_primary_keys_onepass_ex", self.lib.avdb_primary_keys_onepass_ex(
             self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len), N.ptr(b.alt_len),
             N.ptr(b.heap), b.heap.numel(), N.ptr(b.ext_id), N.ptr(code), N.ptr(digest), n, int(max_seq_len),

@@ -59,7 +59,7 @@ C1_LAYOUT = "serial"
 class KeyedStep:
     def __init__(self, engine, batch, *, digests: bool, layout: str = "serial", max_seq_len: int = 50,
                  hist: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None,
-                 k4_grid: int = 0, k7_grid: int = 0):
+                 k4_grid: int = 0, k7_grid: int = 0, narrow_offsets: Optional[bool] = None):
         if layout not in LAYOUTS:
             raise ValueError("layout must be one of %s" % (LAYOUTS,))
         if layout == "overlap" and not digests:
@@ -69,7 +69,12 @@ class KeyedStep:
         self.hist, self.counters = hist, counters
         n = batch.n
         dev = engine.device
-        self.kt = engine.new_key_text(n, int(batch.heap.numel()), paths=True)
+        # the key / path offsets in the narrow layout (AVDB_KEYS_OFF32: 4 bytes per record and
+        # stream instead of 8) where no later stage of the step reads them as u64 (the
+        # overlap layout's digest fill and the one-pass prep do)
+        if narrow_offsets is None:
+            narrow_offsets = layout in ("serial", "fork")
+        self.kt = engine.new_key_text(n, int(batch.heap.numel()), paths=True, off32=bool(narrow_offsets))
         # K3 list workspace (+ 2^22 entries: the keyed K2's per-workgroup suspect slices round up)
         self.ws3 = engine.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), torch.uint8)
         self.ws4 = None

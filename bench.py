@@ -707,14 +707,16 @@ def run_workload(a, name, ri, dev, cpu):
     # object the parity tests run), in the layouts pipeline.C1_LAYOUT / C4K_LAYOUT name
     # (C1: K2, K3, K7, no long records, captured as one HIP graph).  AVDB_BENCH_LAYOUT
     # (serial | fork: K3 on a second stream beside K7 | overlap: K7 beside K4 with the
-    # digests filled afterwards) overrides either for an A/B.
+    # digests filled afterwards) overrides either for an A/B; AVDB_BENCH_NARROW=0|1 the
+    # layout's choice of u32 (AVDB_KEYS_OFF32) or u64 key / path offsets.
     ks = None
     if name in ("c1", "c4k"):
         from annotatedvdb_amd.pipeline import C1_LAYOUT, C4K_LAYOUT, KeyedStep
         layout = os.environ.get("AVDB_BENCH_LAYOUT", C1_LAYOUT if name == "c1" else C4K_LAYOUT)
         ks = KeyedStep(eng, batch, digests=name == "c4k", layout=layout, hist=hist, counters=ctr,
                        k4_grid=int(os.environ.get("AVDB_BENCH_K4_GRID", "0")),
-                       k7_grid=int(os.environ.get("AVDB_BENCH_K7_GRID", "0")))
+                       k7_grid=int(os.environ.get("AVDB_BENCH_K7_GRID", "0")),
+                       narrow_offsets={"1": True, "0": False}.get(os.environ.get("AVDB_BENCH_NARROW", "")))
 
     def step(record: bool):
         if ks is not None:
@@ -814,14 +816,15 @@ def run_workload(a, name, ri, dev, cpu):
         kt = ks.kt
         rl, al = batch.ref_len.long(), batch.alt_len.long()
         n_long = int(((rl + al) > 50).sum().item())
-        text = int(kt.key_off[n].item()) + int(kt.path_off[n].item())
+        text = int(kt.key_offsets(n)[n].item()) + int(kt.path_offsets(n)[n].item())
         bytes_per_launch = 34 * n + int((rl + al).sum().item()) + 24 * n_long + text
         # K7 alone: SoA in (chrom 1 + pos 4 + allele_off 8 + ref_len 4 + alt_len 4 + ext_id 8 +
         # code 4 = 33 B), the allele bytes of short records, 32 digest chars per long record;
-        # out key_off 8 + path_off 8 + state 1 and the text
+        # out key_off + path_off (8 + 8, or 4 + 4 with AVDB_KEYS_OFF32 — the u64 base per
+        # 4,096 records is < 0.01 B a record) + state 1 and the text
         short = (rl + al) <= 50
         short_bytes = int((rl + al)[short].sum().item())
-        k7_bytes = 50 * n + short_bytes + 32 * n_long + text
+        k7_bytes = (34 + (8 if kt.off32 else 16)) * n + short_bytes + 32 * n_long + text
         # the one-pass keyed prep (layout "onepass", k_keyed_onepass): the SoA once (29 B),
         # the allele bytes of short records; out end 4 + code 4 + status 1 + keep 1 + K4 code 1
         # + key_off 8 + path_off 8 + state 1 and the text (long keys' 32 digest chars come later)
@@ -835,7 +838,7 @@ def run_workload(a, name, ri, dev, cpu):
         # keep 1) plus the text K7 writes (keys + ltree paths)
         kt = ks.kt
         rl, al = batch.ref_len.long(), batch.alt_len.long()
-        text = int(kt.key_off[n].item()) + int(kt.path_off[n].item())
+        text = int(kt.key_offsets(n)[n].item()) + int(kt.path_offsets(n)[n].item())
         bytes_per_launch = 34 * n + int((rl + al).sum().item()) + text
     elif name == "c5":
         # K2 algorithmic bytes per record: in chrom 1 + pos 4 + allele_off 8 + ref_len 4 +
@@ -945,7 +948,7 @@ def run_workload(a, name, ri, dev, cpu):
         kt = ks.kt
         out["dtype"] = "u8"
         out["data"] = "synthetic dbSNP-mix records (synth.dbsnp_alleles, torch PCG on device), resident in HBM"
-        out["config"].update(key_bytes=int(kt.key_off[n].item()), path_bytes=int(kt.path_off[n].item()),
+        out["config"].update(key_bytes=int(kt.key_offsets(n)[n].item()), path_bytes=int(kt.path_offsets(n)[n].item()),
                              long_records=n_long, heap_bytes=heap_bytes,
                              duplicates=int(node_ctr[21].item()) // max(1, a.steps))
         out["config"]["layout"] = ks.layout
@@ -984,7 +987,7 @@ def run_workload(a, name, ri, dev, cpu):
         kt = ks.kt
         out["dtype"] = "u8"
         out["data"] = "synthetic C1 records (numpy PCG64 seed 1, synth.np_c1), resident in HBM"
-        out["config"].update(key_bytes=int(kt.key_off[n].item()), path_bytes=int(kt.path_off[n].item()),
+        out["config"].update(key_bytes=int(kt.key_offsets(n)[n].item()), path_bytes=int(kt.path_offsets(n)[n].item()),
                              duplicates=int(node_ctr[21].item()) // max(1, a.steps))
         out["roofline"]["note"] = ("achieved = SURVEY 8d record bytes + key/path text written / whole step "
                                    "time; at 1.1 M records the step is launch-bound (4 kernels in one HIP graph" +

@@ -488,6 +488,16 @@ int avdb_primary_keys_onepass(avdb_ctx* ctx, const uint8_t* chrom, const uint32_
  * avdb_primary_keys_fill_digests.  The keyed K2 totals for this are the ones made
  * with has_digest != 0. */
 #define AVDB_KEYS_DIGEST_DEFERRED 2u
+/* AVDB_KEYS_OFF32: key_off / path_off in the narrow layout, each a buffer of
+ * avdb_keys_off32_bytes(n) bytes (8-byte aligned): n + 1 uint32 low words (offset mod
+ * 2^32), then from the next 8-byte boundary one uint64 base per 4,096 records (the
+ * full offset of record 4096 k).  Full offset of i = base[i >> 12] +
+ * (uint32_t)(low[i] - (uint32_t)base[i >> 12]) (4,096 records' text is < 4 GB).
+ * 4 bytes per record and stream are written instead of 8.  Not accepted by
+ * avdb_primary_keys_fill_digests / avdb_vrs_digest_keys / avdb_keyset_probe_text,
+ * which take uint64 offsets. */
+#define AVDB_KEYS_OFF32 4u
+int avdb_keys_off32_bytes(size_t n, size_t* bytes);
 int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t* pos,
                                  const uint64_t* allele_off, const uint32_t* ref_len, const uint32_t* alt_len,
                                  const uint8_t* heap, size_t heap_bytes, const uint64_t* ext_id,

@@ -568,9 +568,9 @@ def test_c1_graph_replay_vs_c_oracle(engine, layout):
         assert np.array_equal(out["status"].cpu().numpy(), rs)
         assert np.array_equal(out["keep"][:n].cpu().numpy(), rk)
         assert not kt.state[:n].cpu().numpy().any()
-        assert np.array_equal(kt.key_off[: n + 1].cpu().numpy().astype(np.uint64), ko)
+        assert np.array_equal(kt.key_offsets(n).cpu().numpy().astype(np.uint64), ko)
         assert np.array_equal(kt.keys[: len(kb)].cpu().numpy(), np.frombuffer(kb, dtype=np.uint8))
-        po = kt.path_off[: n + 1].cpu().numpy()
+        po = kt.path_offsets(n).cpu().numpy()
         pb = kt.paths[: int(po[n])].cpu().numpy().tobytes().decode()
         assert all(pb[po[i]:po[i + 1]] == exp_paths[i] for i in range(n))
 
@@ -611,3 +611,29 @@ def test_k7_deferred_digests_then_fill(engine, n):
         assert torch.equal(out.state[:n], ref.state[:n])
         kn, pn = int(ref.key_off[n]), int(ref.path_off[n])
         assert torch.equal(out.keys[:kn], ref.keys[:kn]) and torch.equal(out.paths[:pn], ref.paths[:pn])
+
+
+@pytest.mark.parametrize("n", [1, 2, 4095, 4096, 4097, 8192, 8193, 300001])
+def test_k7_narrow_offsets_equal_wide(engine, n):
+    """K7 with AVDB_KEYS_OFF32 (u32 low words + a u64 base per 4,096 records):
+    the widened offsets, states, key and path text equal the u64 form's, at sizes
+    around every base boundary (the C4k shards cross 4 GB of path text: the
+    wrap of the low words is covered there)."""
+    from annotatedvdb_amd import synth
+    digs = ["%032d" % (5 * i) for i in range(25)]
+    eng2 = type(engine)(0, sequence_digests=digs)
+    b = synth.alleles(n, seed=300 + n % 7, long_frac=0.05, device="cuda")
+    end, code, status, _ = eng2.record_prep(b, want_lcp=False)
+    dig, _ = eng2.vrs_digest(b, 50)
+    ref = eng2.primary_keys(b, code=code, digest=dig)
+    kt = eng2.new_key_text(n, b.heap.numel(), off32=True)
+    for t in (kt.ws, kt.key_off, kt.path_off, kt.state, kt.keys, kt.paths):
+        t.view(torch.uint8).fill_(0xA5)
+    out = eng2.primary_keys(b, code=code, digest=dig, out=kt)
+    assert out.off32 and out.key_off.dtype == torch.uint8
+    assert torch.equal(out.key_offsets(n), ref.key_off[: n + 1])
+    assert torch.equal(out.path_offsets(n), ref.path_off[: n + 1])
+    assert torch.equal(out.state[:n], ref.state[:n])
+    kn, pn = int(ref.key_off[n]), int(ref.path_off[n])
+    assert torch.equal(out.keys[:kn], ref.keys[:kn]) and torch.equal(out.paths[:pn], ref.paths[:pn])
+    assert out.host(n) == ref.host(n)

@@ -66,8 +66,8 @@ def _check_shard(engine, n, seed, pieces, layout=None, steps=1):
     g_status, g_keep = out["status"].cpu().numpy(), out["keep"][:n].cpu().numpy()
     g_long = out["is_long"].cpu().numpy().astype(bool)
     g_dig = out["digest"].cpu().numpy()
-    g_ko = kt.key_off[: n + 1].cpu().numpy().view(np.uint64)
-    g_po = kt.path_off[: n + 1].cpu().numpy().view(np.uint64)
+    g_ko = kt.key_offsets(n).cpu().numpy().view(np.uint64)  # (the narrow layout widened: KeyText.off32)
+    g_po = kt.path_offsets(n).cpu().numpy().view(np.uint64)
     g_keys = kt.keys[: int(g_ko[n])].cpu().numpy()
     g_paths = kt.paths[: int(g_po[n])].cpu().numpy()
     del out, kt, ks, b

@@ -50,10 +50,10 @@ def _same(engine, b, digests=True, steps=1):
         lm = o0["is_long"][:n].bool()
         assert torch.equal(o0["digest"][:n][lm], o1["digest"][:n][lm])
     k0, k1 = ks0.kt, ks1.kt
-    assert torch.equal(k0.key_off[: n + 1], k1.key_off[: n + 1])
-    assert torch.equal(k0.path_off[: n + 1], k1.path_off[: n + 1])
+    assert torch.equal(k0.key_offsets(n), k1.key_offsets(n))
+    assert torch.equal(k0.path_offsets(n), k1.path_offsets(n))
     assert torch.equal(k0.state[:n], k1.state[:n])
-    kn, pn = int(k0.key_off[n]), int(k0.path_off[n])
+    kn, pn = int(k0.key_offsets(n)[n]), int(k0.path_offsets(n)[n])
     assert torch.equal(k0.keys[:kn], k1.keys[:kn])
     assert torch.equal(k0.paths[:pn], k1.paths[:pn])
     assert torch.equal(h0, h1)
