@@ -134,15 +134,35 @@ __device__ __forceinline__ VcfEmitRec emit_rec(const avdb_vcf_line& L) {
 #endif
 constexpr uint32_t kLocalCap = AVDB_VCF_LOCAL_CAP;
 static_assert(kLocalCap % kBlock == 0, "whole rounds of slots");
+// The parse writes each window's records and allele bytes itself, from the text it
+// has staged, to slots of the window's own (records at window * kLocalCap + the
+// record's offset in the window, REF+ALT bytes at window * kLocalHeap + the heap
+// offset in the window); the emit then only moves them to their final places
+// (coalesced copies, no second read of the text).  A window with more records or
+// heap bytes than its slots hold flags the overflow word (the counted path).
+#ifndef AVDB_VCF_LOCAL_HEAP_KB
+#define AVDB_VCF_LOCAL_HEAP_KB AVDB_VCF_PARSE_WIN_KB  // single-ALT lines never hold more allele bytes than text
+#endif
+constexpr uint32_t kLocalHeap = AVDB_VCF_LOCAL_HEAP_KB * 1024;
+static_assert(kLocalHeap % 16 == 0, "heap slots keep 16-byte alignment");
 struct LocalWin {  // one parse window's lines, records and heap bytes
   uint32_t lines, recs;
   uint64_t heap;
 };
+struct LocalRec {  // one record in its window's slots
+  uint64_t ext_id;
+  uint32_t pos, ref_len, alt_len, hoff;  // hoff: REF's offset in the window's heap slots
+  uint32_t alt;                          // ALT index in the line (rec_alt)
+  uint16_t line;                         // line index in the window (< kLocalCap)
+  uint8_t chrom, pad;
+};
+static_assert(sizeof(LocalRec) == 32, "record slot");
 struct LocalOut {
   LocalWin* win;               // [windows]
-  VcfEmitRec* erec;            // [windows * kLocalCap]
+  LocalRec* rec;               // [windows * kLocalCap]
+  uint8_t* heap;               // [windows * kLocalHeap]
   uint2* cnt;                  // [windows * kLocalCap] (records, heap bytes) per line
-  unsigned long long* overflow;  // windows with more than kLocalCap lines
+  unsigned long long* overflow;  // windows with more lines, records or heap bytes than their slots
 };
 
 // the line's public record or its emit record, one of them (the other NULL)
@@ -494,6 +514,43 @@ __device__ __forceinline__ uint32_t block_excl32(uint32_t v, uint32_t* s_w, uint
   return base + x - v;
 }
 
+// (LOCAL) one line's records into its window's record slots and its REF+ALT bytes
+// into the window's heap slots at window-local heap offset h (the rows emit_line
+// writes, without their final offsets)
+template <class CP>
+__device__ __forceinline__ void slot_line(CP s, const VcfEmitRec& E, uint16_t line, LocalRec* __restrict__ rs,
+                                          uint8_t* __restrict__ heap, uint32_t h) {
+  const uint32_t rlen = E.alt0 - 1 - E.ref0;
+  const CP ref = s + E.ref0;
+  const CP alt = s + E.alt0;
+  const uint32_t an = E.aend - E.alt0;
+  const uint8_t cc = uint8_t(E.start_chrom >> 56);
+  Out<true> hs(heap, h);
+  uint32_t ai = 0;
+  for (uint32_t a0 = 0; a0 <= an; ++ai) {
+    const uint32_t a1 = a0 + swar_find(alt + a0, an - a0, [](uint64_t x) { return bytes_eq_mask(x, ','); });
+    const uint32_t al = a1 - a0;
+    if (!(al == 1 && alt[a0] == '.')) {
+      LocalRec R;
+      R.ext_id = E.ext_id;
+      R.pos = E.pos;
+      R.ref_len = rlen;
+      R.alt_len = al;
+      R.hoff = h;
+      R.alt = ai;
+      R.line = line;
+      R.chrom = cc;
+      R.pad = 0;
+      *rs++ = R;
+      hs.bytes(ref, rlen);
+      hs.bytes(alt + a0, al);
+      h += rlen + al;
+    }
+    a0 = a1 + 1;
+  }
+  hs.finish();
+}
+
 // LOCAL (the records-only path without the count pass, avdb_vcf_parse_local): no
 // line numbers are known, so a window writes its lines' emit records and counts to
 // its own slots (window * kLocalCap + its line), and its line / record / heap totals
@@ -788,8 +845,21 @@ __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_wind
         }
       }
       if constexpr (LOCAL) {
-        lo_out.erec[li] = emit_rec(L);
         lo_out.cnt[li] = make_uint2(pr, ph);
+        if (recs) {
+          if (pr + recs > kLocalCap || ph + hbytes > kLocalHeap) {
+            atomicAdd(lo_out.overflow, 1ull);
+          } else {
+            const VcfEmitRec E = emit_rec(L);
+            LocalRec* rs = lo_out.rec + size_t(blockIdx.x) * kLocalCap + pr;
+            uint8_t* hs = lo_out.heap + size_t(blockIdx.x) * kLocalHeap;
+            const uint16_t ln = uint16_t(lo + tid);
+            if (h.lo + L.start + E.aend <= wend)
+              slot_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + L.start - a0)), E, ln, rs, hs, ph);
+            else
+              slot_line((glb_cp)(text + L.start), E, ln, rs, hs, ph);
+          }
+        }
       } else {
         put_line(lines, erec, li, L);
         rec_cnt[li] = recs;
@@ -1015,59 +1085,58 @@ __global__ __launch_bounds__(kTileWins) void k_vcf_local_top(LocalTot* __restric
 }
 
 // One workgroup per parse window: its lines' record / heap offsets are the window's
-// bases plus the in-window offsets the parse left in the slots; the window's text
-// staged once, then the rows as k_vcf_emit writes them; rec_off / heap_off per line
-// (nullable).
+// bases plus the in-window offsets the parse left in the slots; its records and
+// allele bytes, which the parse wrote to the window's slots, are moved to their
+// places (coalesced: slot k -> record base + k, the heap slots as one 8-byte-chunk
+// copy); rec_off / heap_off per line (nullable).  The text is not read again.
 __global__ __launch_bounds__(kEmitLines) void k_vcf_emit_local(
-    const uint8_t* __restrict__ text, size_t text_bytes, const LocalWin* __restrict__ win,
-    const ulonglong2* __restrict__ base_lr, const unsigned long long* __restrict__ base_h,
-    const LocalTot* __restrict__ tile_pre, const VcfEmitRec* __restrict__ erec, const uint2* __restrict__ cnt,
+    const LocalWin* __restrict__ win, const ulonglong2* __restrict__ base_lr,
+    const unsigned long long* __restrict__ base_h, const LocalTot* __restrict__ tile_pre,
+    const LocalRec* __restrict__ rslot, const uint8_t* __restrict__ hslot, const uint2* __restrict__ cnt,
     const unsigned long long* __restrict__ tot,
     uint64_t* __restrict__ rec_off, uint64_t* __restrict__ heap_off, uint8_t* __restrict__ chrom,
     uint32_t* __restrict__ pos, uint64_t* __restrict__ allele_off, uint32_t* __restrict__ ref_len,
     uint32_t* __restrict__ alt_len, uint64_t* __restrict__ ext_id, uint8_t* __restrict__ heap,
     uint32_t* __restrict__ rec_line, uint32_t* __restrict__ rec_alt) {
-  __shared__ u32x4 s_text[kEmitStage / 16];
-  const Heap h = make_heap(text, text_bytes);
-  constexpr uint64_t kStartMask = (uint64_t(1) << 56) - 1;
   const size_t w = blockIdx.x;
   const uint32_t tid = threadIdx.x;
   if (w == 0 && tid == 0) {  // the totals row of the per-line offsets
     if (rec_off) rec_off[tot[0]] = tot[1];
     if (heap_off) heap_off[tot[0]] = tot[2];
   }
-  const uint32_t n = win[w].lines;
-  if (n == 0) return;  // (uniform)
+  const LocalWin W = win[w];
+  if (W.lines == 0) return;  // (uniform)
   const size_t slot0 = w * kLocalCap;
   const LocalTot tp = tile_pre[w / kTileWins];
   ulonglong2 blr = base_lr[w];
   blr.x += tp.lines;
   blr.y += tp.recs;
-  const VcfEmitRec& Z = erec[slot0 + n - 1];
-  const size_t s0 = erec[slot0].start_chrom & kStartMask;
-  const size_t s1 = (Z.start_chrom & kStartMask) + Z.aend;
-  const Window sw = stage_window<kEmitLines, kEmitStage>(h, s0, s1, s_text);
   const uint64_t hb = base_h[w] + tp.heap;
-  const uint32_t wr = win[w].recs;
-  for (uint32_t k = tid; k < n; k += kEmitLines) {
-    // the slots hold each line's record / heap offset within the window
-    const uint2 c = cnt[slot0 + k];
-    const uint32_t c1 = k + 1 < n ? cnt[slot0 + k + 1].x : wr;
-    const size_t li = blr.x + k;
-    const uint64_t r0 = blr.y + c.x, h0 = hb + c.y;
-    if (rec_off) rec_off[li] = r0;
-    if (heap_off) heap_off[li] = h0;
-    if (c1 > c.x) {
-      const VcfEmitRec E = erec[slot0 + k];
-      const size_t st = E.start_chrom & kStartMask;
-      if (sw.staged)
-        emit_line((lds_cp)(reinterpret_cast<const uint8_t*>(s_text) + (h.lo + st - sw.a0)), E, li, r0, h0, chrom,
-                  pos, allele_off, ref_len, alt_len, ext_id, heap, rec_line, rec_alt);
-      else
-        emit_line((glb_cp)(text + st), E, li, r0, h0, chrom, pos, allele_off, ref_len, alt_len, ext_id, heap,
-                  rec_line, rec_alt);
+  if (rec_off || heap_off) {
+    for (uint32_t k = tid; k < W.lines; k += kEmitLines) {
+      const uint2 c = cnt[slot0 + k];
+      if (rec_off) rec_off[blr.x + k] = blr.y + c.x;
+      if (heap_off) heap_off[blr.x + k] = hb + c.y;
     }
   }
+  for (uint32_t k = tid; k < W.recs; k += kEmitLines) {
+    const LocalRec R = rslot[slot0 + k];
+    const size_t r = blr.y + k;
+    chrom[r] = R.chrom;
+    pos[r] = R.pos;
+    allele_off[r] = hb + R.hoff;
+    ref_len[r] = R.ref_len;
+    alt_len[r] = R.alt_len;
+    ext_id[r] = R.ext_id;
+    rec_line[r] = uint32_t(blr.x + R.line);
+    rec_alt[r] = R.alt;
+  }
+  // the window's allele bytes [0, W.heap): 8-byte chunks (aligned loads from the
+  // slots, unaligned stores), the last < 8 bytes one at a time
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(hslot + w * kLocalHeap);
+  const uint32_t nh = uint32_t(W.heap), n8 = nh / 8;
+  for (uint32_t k = tid; k < n8; k += kEmitLines) reinterpret_cast<gw_u64u>((gbyte*)heap + hb + 8 * k)->v = src[k];
+  if (tid < (nh & 7u)) heap[hb + 8 * n8 + tid] = hslot[w * kLocalHeap + 8 * n8 + tid];
 }
 
 }  // namespace avdb
@@ -1287,10 +1356,10 @@ extern "C" int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_
 // ---- chromosome map (ChromosomeMap.get, chromosome_map_parser.py:84-91) ----------
 // ---- the count-free records path: host side ----
 // workspace: header (totals: lines, records, heap bytes, overflow windows) | LocalWin
-// per window | (line, record) bases per window | heap base per window | emit records
-// and counts per window slot
+// per window | (line, record) bases per window | heap base per window | tile totals |
+// record slots | heap slots | (records, heap bytes) per line slot
 struct LocalLayout {
-  size_t nw, nt, win, blr, bh, tile, erec, cnt, bytes;
+  size_t nw, nt, win, blr, bh, tile, rec, heap, cnt, bytes;
 };
 static LocalLayout local_layout(size_t text_bytes) {
   auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
@@ -1306,8 +1375,9 @@ static LocalLayout local_layout(size_t text_bytes) {
   L.blr = L.win + up(sizeof(LocalWin) * L.nw);
   L.bh = L.blr + up(16 * L.nw);
   L.tile = L.bh + up(8 * L.nw);
-  L.erec = L.tile + up(sizeof(LocalTot) * L.nt);
-  L.cnt = L.erec + up(sizeof(VcfEmitRec) * L.nw * kLocalCap);
+  L.rec = L.tile + up(sizeof(LocalTot) * L.nt);
+  L.heap = L.rec + up(sizeof(LocalRec) * L.nw * kLocalCap);
+  L.cnt = L.heap + up(size_t(kLocalHeap) * L.nw);
   L.bytes = L.cnt + up(8 * L.nw * kLocalCap);
   return L;
 }
@@ -1356,8 +1426,8 @@ extern "C" int avdb_vcf_parse_local(avdb_ctx* ctx, const uint8_t* text, size_t t
   const ChromMapView cm = opts && opts->chrom_map ? opts->chrom_map->dev : ChromMapView{};
   const uint32_t min_fields = opts ? opts->min_fields : 0u;
   const LocalLayout L = local_layout(text_bytes);
-  LocalOut o{reinterpret_cast<LocalWin*>(w + L.win), reinterpret_cast<VcfEmitRec*>(w + L.erec),
-             reinterpret_cast<uint2*>(w + L.cnt), hdr + 3};
+  LocalOut o{reinterpret_cast<LocalWin*>(w + L.win), reinterpret_cast<LocalRec*>(w + L.rec),
+             reinterpret_cast<uint8_t*>(w + L.heap), reinterpret_cast<uint2*>(w + L.cnt), hdr + 3};
   hipLaunchKernelGGL(k_vcf_parse_windows<true>, dim3(unsigned(L.nw)), dim3(kBlock), 0, s, text, text_bytes, size_t(0),
                      nullptr, nullptr, nullptr, windows_per_chunk(text_bytes), nullptr, nullptr, nullptr, nullptr, cm,
                      min_fields, o);
@@ -1390,11 +1460,11 @@ extern "C" int avdb_vcf_emit_local(avdb_ctx* ctx, const uint8_t* text, size_t te
   const char* w = static_cast<const char*>(workspace);
   const LocalLayout L = local_layout(text_bytes);
   hipLaunchKernelGGL(k_vcf_emit_local, dim3(unsigned(L.nw)), dim3(kEmitLines), 0, static_cast<hipStream_t>(stream),
-                     text, text_bytes, reinterpret_cast<const LocalWin*>(w + L.win),
-                     reinterpret_cast<const ulonglong2*>(w + L.blr), reinterpret_cast<const unsigned long long*>(w + L.bh),
-                     reinterpret_cast<const LocalTot*>(w + L.tile), reinterpret_cast<const VcfEmitRec*>(w + L.erec), reinterpret_cast<const uint2*>(w + L.cnt),
-                     reinterpret_cast<const unsigned long long*>(w), rec_off, heap_off, chrom, pos, allele_off,
-                     ref_len, alt_len, ext_id, heap, rec_line, rec_alt);
+                     reinterpret_cast<const LocalWin*>(w + L.win), reinterpret_cast<const ulonglong2*>(w + L.blr),
+                     reinterpret_cast<const unsigned long long*>(w + L.bh), reinterpret_cast<const LocalTot*>(w + L.tile),
+                     reinterpret_cast<const LocalRec*>(w + L.rec), reinterpret_cast<const uint8_t*>(w + L.heap),
+                     reinterpret_cast<const uint2*>(w + L.cnt), reinterpret_cast<const unsigned long long*>(w),
+                     rec_off, heap_off, chrom, pos, allele_off, ref_len, alt_len, ext_id, heap, rec_line, rec_alt);
   AVDB_LAUNCH_CHECK("k_vcf_emit_local");
   return AVDB_OK;
 }

@@ -306,19 +306,23 @@ int avdb_vcf_emit_ws(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, size
                      uint32_t* rec_alt, void* stream);
 /* The records without the count pass (the tokenize-only path, no line table):
  * avdb_vcf_parse_local parses one workgroup per parse window with no line numbers
- * known, each window writing its lines to slots of its own in `workspace`
- * (avdb_vcf_local_workspace_size(text_bytes) bytes, 16-byte aligned); one scan of
- * the windows' totals then gives every window its first line, record and heap byte.
+ * known, each window writing its lines' counts, its records and their REF+ALT bytes
+ * to slots of its own in `workspace` (avdb_vcf_local_workspace_size(text_bytes)
+ * bytes, 16-byte aligned), from the text it has staged; one scan of the windows'
+ * totals then gives every window its first line, record and heap byte.
  * totals (device, 4 x u64): lines, records, heap bytes, and the number of windows
- * the path could not take (more than AVDB_VCF_LOCAL_CAP = 1024 lines in a 24 KB
- * window, or a line whose records / heap bytes exceed 32 bits).  With totals[3] == 0,
- * avdb_vcf_emit_local writes the same records, heap, rec_line / rec_alt and per-line
- * rec_off / heap_off (totals[0] + 1 entries each, nullable) as count -> parse ->
- * avdb_vcf_emit_ws; with totals[3] != 0 the caller takes that counted path.  The
- * same text and workspace go to both calls.  Workspace: 40 bytes of line slots per
- * 24 KB window of text (1,024 slots of 32 + 8 bytes) plus 40 bytes of window totals,
- * about 1.7x text_bytes at any size (a one-line text: two windows, 80 KB); the
- * slots are written only for the lines present. */
+ * the path could not take (more than AVDB_VCF_LOCAL_CAP = 1024 lines or records in
+ * a 24 KB window, more than 24 KB of REF+ALT bytes in its records, or a line whose
+ * records / heap bytes exceed 2^23).  With totals[3] == 0, avdb_vcf_emit_local moves
+ * the slots into the same records, heap, rec_line / rec_alt and per-line rec_off /
+ * heap_off (totals[0] + 1 entries each, nullable) as count -> parse ->
+ * avdb_vcf_emit_ws write — coalesced copies; it does not read the text (`text` is
+ * kept in the signature and may be NULL); with totals[3] != 0 the caller takes that
+ * counted path.  The same workspace goes to both calls.  Workspace per 24 KB window
+ * of text: 1,024 line slots of 8 bytes, 1,024 record slots of 32 bytes, 24 KB of
+ * heap slots and 40 bytes of window totals, about 2.7x text_bytes at any size (a
+ * one-line text: two windows, 128 KB); the slots are written only for the lines
+ * and records present. */
 int avdb_vcf_local_workspace_size(size_t text_bytes, size_t* bytes);
 int avdb_vcf_parse_local(avdb_ctx* ctx, const uint8_t* text, size_t text_bytes, void* workspace,
                          size_t workspace_bytes, const avdb_vcf_opts* opts, uint64_t* totals, void* stream);

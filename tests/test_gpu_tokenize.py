@@ -259,12 +259,12 @@ def test_k0_records_without_line_table(engine, which, count_free):
     assert torch.equal(a.rec_line, b.rec_line) and torch.equal(a.rec_alt, b.rec_alt)
 
 
-def _same_records(engine, text, opts=None):
+def _same_records(engine, text, opts=None, path="local"):
     """The count-free records path (vcf_tokenize(want_lines=False)) against the
     tokenizer with its line table, on the same text (bytes or a device tensor)."""
     a = engine.vcf_tokenize(text, opts)
     b = engine.vcf_tokenize(text, opts, want_lines=False)
-    assert engine.last_vcf_path == "local"
+    assert engine.last_vcf_path == path
     assert a.n_lines == b.n_lines and a.records.n == b.records.n
     assert torch.equal(a.rec_off, b.rec_off) and torch.equal(a.heap_off, b.heap_off)
     for f in ("chrom", "pos", "allele_off", "ref_len", "alt_len", "ext_id"):
@@ -276,8 +276,11 @@ def _same_records(engine, text, opts=None):
 
 def test_k0_count_free_opts_views_and_wide_alleles(engine):
     """The count-free path with a chromosome map and header width (avdb_vcf_opts), on
-    a misaligned device view, with REF / ALT of kilobytes (spans past the emit's
-    stage), a heap larger than the text, and the tiny texts."""
+    a misaligned device view, with REF / ALT of kilobytes (lines parsed from global
+    memory, 17 KB of allele bytes in one window's heap slots), and the tiny texts.  A
+    window whose records hold more allele bytes than its 24 KB of heap slots (three
+    lines of a 2 KB REF x 400 ALTs: 2.4 MB of heap from 6 KB of text) takes the
+    counted path, with the same records."""
     from annotatedvdb_amd import synth
     lines = synth.vcf_text(4000, seed=43).decode().splitlines()
     acc = {str(i + 1): "NC_%06d.11" % (i + 1) for i in range(22)}
@@ -289,7 +292,9 @@ def test_k0_count_free_opts_views_and_wide_alleles(engine):
     base = _synth(3000, 37).split(b"\n")[:-1]
     wide = b"3\t999\trs1\t" + b"A" * 6000 + b"\t" + b"C" * 5000 + b",G\t.\t.\t."
     many = b"4\t1234\trs9\t" + b"ACGT" * 500 + b"\t" + b",".join([b"A"] * 400) + b"\t.\t.\t."
-    _same_records(engine, b"\n".join(base[:1000] + [wide] + base[1000:2000] + [many] * 3 + base[2000:]) + b"\n")
+    _same_records(engine, b"\n".join(base[:1000] + [wide] + base[1000:]) + b"\n")
+    _same_records(engine, b"\n".join(base[:1000] + [wide] + base[1000:2000] + [many] * 3 + base[2000:]) + b"\n",
+                  path="counted")
     for tiny in (b"\n", b"\n\n\n", b"a", b"#x\n", b"1\t5\t.\tA\tG\t.\t.\t.",
                  b"1\t5\t.\tA\tG\t.\t.\t.\r\n\r\n2\t7\trs3\tC\tT,.\t.\t.\t.\n"):
         _same_records(engine, tiny)
