@@ -198,8 +198,22 @@ struct Out {
       pend.w = 0;
       pend.k = 0;
     } else if constexpr (WRITE) {
+      // the k < 8 buffered bytes as at most one 4-, one 2- and one 1-byte store
+      // (unaligned: gfx950's unaligned-access mode) instead of k byte stores
       const uint32_t k = pend.k;
-      for (uint32_t j = 0; j < k; ++j) base[p - k + j] = uint8_t(pend.w >> (8 * j));
+      gbyte* q = base + p - k;
+      uint64_t w = pend.w;
+      if (k & 4) {
+        reinterpret_cast<__attribute__((address_space(1))) U32u*>(q)->v = uint32_t(w);
+        q += 4;
+        w >>= 32;
+      }
+      if (k & 2) {
+        reinterpret_cast<__attribute__((address_space(1))) U16u*>(q)->v = uint16_t(w);
+        q += 2;
+        w >>= 16;
+      }
+      if (k & 1) *q = uint8_t(w);
       pend.w = 0;
       pend.k = 0;
     }

@@ -105,6 +105,12 @@ struct __attribute__((packed)) U64u {
   uint64_t v;
 };
 typedef const __attribute__((address_space(1))) U64u* g_u64u;
+struct __attribute__((packed)) U32u {
+  uint32_t v;
+};
+struct __attribute__((packed)) U16u {
+  uint16_t v;
+};
 
 // little-endian 8 bytes starting at heap offset p (bytes past the heap read 0)
 AVDB_HD uint64_t heap_u64(const Heap& h, uint64_t p) {
