@@ -332,7 +332,7 @@ def _cpu_port(workload: str, seconds_per_worker: float, workers: int, host_cores
                           f"chromosome file (load_vcf_file.py:307-313); oracle.c1_port_loop = the reference's "
                           f"per-record objects (an annotator per alt, the key from its metaseq id, normalized "
                           f"alleles, end inference on a second annotator) + PortBinIndex, {t:.2f} s",
-                "calibration": {"port_over_reference_time": [1.02, 1.19],
+                "calibration": {"port_over_reference_time": [0.85, 1.19],
                                 "tool": "tools/calibrate_cpu_baseline.py calibrate_c1 (build container, the "
                                         "verbatim reference with the make_golden stub DB, same records)",
                                 "log": "profiles/r06_calibrate_c1.txt",
