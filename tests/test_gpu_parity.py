@@ -471,8 +471,8 @@ def test_grid_knobs_parity(engine, knob, value):
         kt = o["kt"]
         sel = o["is_long"].bool()
         res.append((o["end"], o["code"], o["status"], o["keep"][:n], o["is_long"], o["digest"][sel],
-                    kt.key_off[: n + 1], kt.path_off[: n + 1], kt.state[:n], kt.keys[: int(kt.key_off[n])],
-                    kt.paths[: int(kt.path_off[n])]))
+                    kt.key_offsets(n), kt.path_offsets(n), kt.state[:n], kt.keys[: int(kt.key_offsets(n)[n])],
+                    kt.paths[: int(kt.path_offsets(n)[n])]))
     for r in res[1:]:
         for x, y in zip(res[0], r):
             assert torch.equal(x, y)
