@@ -38,12 +38,15 @@ def main():
     _, code, _, _ = eng.record_prep(b, want_lcp=False)
     dig, _ = eng.vrs_digest(b, 50)
     mode = os.environ.get("AVDB_K7_PROBE_MODE", "all")  # all | both (keys + paths only, for counter passes)
-    kt = eng.primary_keys(b, code=code, digest=dig)
+    # (narrow offsets by default, as the bench's serial keyed step writes them; AVDB_K7_PROBE_NARROW=0: u64)
+    narrow = os.environ.get("AVDB_K7_PROBE_NARROW", "1") == "1"
+    kt = eng.primary_keys(b, code=code, digest=dig,
+                          out=eng.new_key_text(n, int(b.heap.numel()), paths=True, off32=True) if narrow else None)
     # (mode both launches no keys-only pass at all, so per-launch counter averages
     # describe keys + paths launches only)
     ko = eng.primary_keys(b, digest=dig) if mode == "all" else None
     torch.cuda.synchronize()
-    kb, pb = int(kt.key_off[n].item()), int(kt.path_off[n].item())
+    kb, pb = int(kt.key_offsets(n)[n].item()), int(kt.path_offsets(n)[n].item())
     t_both, all_both = timed(lambda: eng.primary_keys(b, code=code, digest=dig, out=kt), reps)
     t_keys, all_keys = (timed(lambda: eng.primary_keys(b, digest=dig, out=ko), reps) if mode == "all"
                         else (None, []))
