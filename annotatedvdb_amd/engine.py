@@ -932,9 +932,9 @@ class Engine:
         ``want_lines=False``: no public line table (``VcfBatch.lines`` is None) — for
         callers that need only the records: the count-free path (avdb_vcf_parse_local:
         each parse window writes its lines to slots of its own, one scan of the window
-        totals, avdb_vcf_emit_local), or, when a window holds more lines than its slots,
-        count -> parse -> emit from 32-byte records in the parse workspace (also taken
-        with ``count_free=False``)."""
+        totals, avdb_vcf_emit_local), or, when a window holds more lines, records or allele
+        bytes than its slots, count -> parse -> emit from 32-byte records in the parse
+        workspace (also taken with ``count_free=False``)."""
         if not want_lines and count_free:
             vb, text = self._vcf_tokenize_local(text, vcf_opts)
             if vb is not None:
@@ -1005,7 +1005,8 @@ class Engine:
         """vcf_tokenize(want_lines=False) without the count pass: (batch, device
         text), the batch None when a parse window overflowed its line slots (the
         caller then takes the counted path on the same device text).  The slot
-        workspace (about 1.7x the text, avdb.h) is the engine's, reused across calls."""
+        workspace (about 2.7x the text: line, record and heap slots, avdb.h) is the
+        engine's, reused across calls."""
         if isinstance(text, (bytes, bytearray, memoryview)):
             host = bytes(text)
             t = torch.frombuffer(bytearray(host) if host else bytearray(b"\n"), dtype=torch.uint8)
