@@ -1105,7 +1105,9 @@ __global__ __launch_bounds__(kEmitLines) void k_vcf_emit_local(
     if (heap_off) heap_off[tot[0]] = tot[2];
   }
   const LocalWin W = win[w];
-  if (W.lines == 0) return;  // (uniform)
+  // (uniform; an overflowed window's slots are incomplete — the caller takes the
+  // counted path — and are never read past their capacity)
+  if (W.lines == 0 || W.lines > kLocalCap || W.recs > kLocalCap || W.heap > kLocalHeap) return;
   const size_t slot0 = w * kLocalCap;
   const LocalTot tp = tile_pre[w / kTileWins];
   ulonglong2 blr = base_lr[w];
