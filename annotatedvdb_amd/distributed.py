@@ -171,11 +171,21 @@ def node_exchange(engine, ri: RankInfo, kind: Optional[str] = None):
         return TorchExchange(ri)
     if kind != "rccl":
         raise ValueError("exchange kind must be 'rccl' or 'torch', not %r" % (kind,))
-    uid = RcclExchange.new_id() if ri.rank == 0 else None
+    # rank 0's outcome (the id, or why it could not make one) goes to every rank, so
+    # all ranks raise together and a caller's fallback is the same on every rank
+    # (a rank left waiting in the broadcast while rank 0 falls back would hang the job)
+    uid, err = None, None
+    if ri.rank == 0:
+        try:
+            uid = RcclExchange.new_id()
+        except Exception as e:  # noqa: BLE001 (re-raised on every rank below)
+            err = "%s: %s" % (type(e).__name__, e)
     if ri.distributed:
-        box = [uid]
+        box = [uid, err]
         dist.broadcast_object_list(box, src=0)
-        uid = box[0]
+        uid, err = box
+    if err is not None:
+        raise RuntimeError("RCCL unique id on rank 0 failed: " + err)
     return RcclExchange(engine, ri.world, ri.rank, uid)
 
 

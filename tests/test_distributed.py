@@ -93,3 +93,44 @@ def test_gloo_allgather_matches_single_process(world):
         assert np.array_equal(r[5].astype(np.uint32), exp_hist)
         assert r[6][20] == len(chrom)
         assert r[7] == float(world)  # max over ranks
+
+
+def _rccl_fail_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from annotatedvdb_amd import distributed as D
+
+    def no_id():
+        raise OSError("no RCCL here")
+    D.RcclExchange.new_id = staticmethod(no_id)
+    ri = D.init("gloo")
+    try:
+        D.node_exchange(None, ri, kind="rccl")
+        got = "no error"
+    except RuntimeError as e:
+        got = str(e)
+    # the bench's fallback, then one more collective: every rank must still be in step
+    t = D.max_over_ranks(float(rank + 1), ri)
+    q.put((rank, got, t))
+    D.finalize(ri)
+
+
+def test_rccl_exchange_setup_failure_reaches_every_rank():
+    """When rank 0 cannot make the RCCL id, every rank raises from node_exchange
+    (rank 0's error travels with the broadcast), so the bench's fallback to the
+    torch.distributed exchange is taken on all ranks together and the next
+    collective does not hang (gloo, world 2)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rccl_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, got, t in res:
+        assert "RCCL unique id on rank 0 failed" in got and "no RCCL here" in got, (rank, got)
+        assert t == float(world)
