@@ -511,7 +511,7 @@ __global__ __launch_bounds__(kK1Block, KEYS == 2 ? 6 : 1) void k_record_prep4(
           for (int k = 0; k < 4; ++k) wave_hist_add(key[k], hist);
         }
       }
-      if constexpr (KEYS != 0) {  // this wave's 256 records are one K7 group
+      if (KEYS != 0 && kt.tot) {  // this wave's 256 records are one K7 group (none: no K7 follows)
         uint32_t K = 0, P = 0;
         if (live) {
 #pragma unroll
@@ -773,13 +773,15 @@ extern "C" int avdb_record_prep_keyed(avdb_ctx* ctx, const uint8_t* chrom, const
   *totals_written = 0;
   size_t need = 0;
   avdb_primary_keys_onepass_workspace_size(n, &need);
-  if (!key_workspace || key_workspace_bytes < need || reinterpret_cast<uintptr_t>(key_workspace) % 16) {
+  // (no K7 workspace: no group totals — K4's codes and K3's marks only, for a step
+  // without key text, as C5's)
+  if (key_workspace && (key_workspace_bytes < need || reinterpret_cast<uintptr_t>(key_workspace) % 16)) {
     avdb_set_error("avdb_record_prep_keyed: 16-byte aligned K7 one-pass workspace of %zu bytes required", need);
     return AVDB_ERANGE;
   }
   KeyTotals kt;
   kt.ext2 = reinterpret_cast<const u64x2*>(ext_id);
-  kt.tot = avdb::key_totals_of(key_workspace);
+  kt.tot = key_workspace ? avdb::key_totals_of(key_workspace) : nullptr;
   kt.max_seq_len = max_seq_len;
   kt.n_key_chrom = uint32_t(ctx && ctx->tab.n < 25 ? ctx->tab.n : 25);
   kt.has_digest = has_digest ? 1u : 0u;
@@ -864,7 +866,7 @@ static int record_prep_impl(avdb_ctx* ctx, const uint8_t* chrom, const uint32_t*
 #undef K2VK
     AVDB_LAUNCH_CHECK("k_record_prep4");
     if (keys && totals_written)
-      *totals_written = AVDB_KEYED_TOTALS | (kt.long_codes ? AVDB_KEYED_LONG_CODES : 0) |
+      *totals_written = (kt.tot ? AVDB_KEYED_TOTALS : 0) | (kt.long_codes ? AVDB_KEYED_LONG_CODES : 0) |
                         (kt.dd_list ? AVDB_KEYED_DEDUP_MARKS : 0);
     return AVDB_OK;
   }

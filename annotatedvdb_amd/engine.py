@@ -741,7 +741,9 @@ class Engine:
         ``digest_workspace`` too (the K4 workspace the next ``vrs_digest(b,
         max_seq_len, workspace=...)`` gets) it classifies the long records for K4,
         and with ``dedup_workspace`` (the one the next ``pk_dedup(b, workspace=...)``
-        gets) it runs K3's first phase, so that call only resolves the listed runs."""
+        gets) it runs K3's first phase, so that call only resolves the listed runs.
+        Either workspace without ``keys`` runs the same K2 without K7's totals (a
+        step with no key text, as C5's)."""
         b = b if b.device == self.device else b.to(self.device)
         n = b.n
         self._check_alleles(b)
@@ -753,7 +755,7 @@ class Engine:
         args = (self.ctx, N.ptr(b.chrom), N.ptr(b.pos), N.ptr(b.allele_off), N.ptr(b.ref_len),
                 N.ptr(b.alt_len), N.ptr(b.heap), b.heap.numel(), n, N.ptr(end), N.ptr(code), N.ptr(status),
                 N.ptr(lcp), N.ptr(hist), N.ptr(counters))
-        if keys is None:
+        if keys is None and digest_workspace is None and dedup_workspace is None:
             N.check("avdb_record_prep", self.lib.avdb_record_prep(*args, self._stream()))
             return end, code, status, lcp
         dws = digest_workspace
@@ -769,7 +771,8 @@ class Engine:
         done = ctypes.c_int(0)
         N.check("avdb_record_prep_keyed", self.lib.avdb_record_prep_keyed(
             *args, N.ptr(b.ext_id), int(max_seq_len), 1 if key_digest else 0, 1 if key_paths else 0,
-            N.ptr(keys.ws), keys.ws.numel(), N.ptr(dws), dws.numel() if dws is not None else 0,
+            N.ptr(keys.ws) if keys is not None else None, keys.ws.numel() if keys is not None else 0,
+            N.ptr(dws), dws.numel() if dws is not None else 0,
             N.ptr(ddw), ddw.numel() if ddw is not None else 0, N.ptr(keep), ctypes.byref(done), self._stream()))
         # (tied to these exact tensors: another batch, a reallocated one or an
         # in-place edit recomputes)

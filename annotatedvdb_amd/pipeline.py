@@ -56,6 +56,18 @@ C4K_LAYOUT = "serial"
 C1_LAYOUT = "serial"
 
 
+def _timed(events, name, stream, fn):
+    """fn() with an event pair around it on ``stream`` (``events[name]``), or plain."""
+    if events is None:
+        return fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    r = fn()
+    e1.record(stream)
+    events.setdefault(name, []).append((e0, e1))
+    return r
+
+
 class KeyedStep:
     def __init__(self, engine, batch, *, digests: bool, layout: str = "serial", max_seq_len: int = 50,
                  hist: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None,
@@ -96,14 +108,7 @@ class KeyedStep:
 
     # ---- one step ----------------------------------------------------------
     def _timed(self, events, name, stream, fn):
-        if events is None:
-            return fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        r = fn()
-        e1.record(stream)
-        events.setdefault(name, []).append((e0, e1))
-        return r
+        return _timed(events, name, stream, fn)
 
     def run(self, events: Optional[dict] = None) -> Dict[str, object]:
         """One step on the current stream; returns (and keeps in ``self.out``)
@@ -167,4 +172,37 @@ class KeyedStep:
             span1.record(main)
             events.setdefault("step_span", []).append((span0, span1))
         self.out = dict(end=end, code=code, status=status, keep=keep, digest=dig, is_long=is_long, kt=kt)
+        return self.out
+
+
+class PrepStep:
+    """The keyed record-prep step without key text (BASELINE configs[4], C5: "bin path +
+    hashed primary key + dedup"): K2 (end, bin, status) also classifying the long
+    records for K4 and running K3's first phase (``avdb_record_prep_keyed`` with no K7
+    workspace), K3 resolving only the listed runs, K4 from K2's codes — what
+    ``bench.py --workload c5`` times and ``tests/test_gpu_parity.py`` checks against
+    the C oracle over the whole 2e8-record job.  Workspaces are allocated once."""
+
+    def __init__(self, engine, batch, *, max_seq_len: int = 50, hist: Optional[torch.Tensor] = None,
+                 counters: Optional[torch.Tensor] = None):
+        self.eng, self.b, self.max_seq_len = engine, batch, int(max_seq_len)
+        self.hist, self.counters = hist, counters
+        n = batch.n
+        self.ws3 = engine.empty(16384 + 4 * (((n + 3) & ~3) + (1 << 22)), torch.uint8)
+        sz = ctypes.c_size_t()
+        engine.lib.avdb_vrs_digest_workspace_size(n, ctypes.byref(sz))
+        self.ws4 = engine.empty(int(sz.value), torch.uint8)
+        self.out: Dict[str, object] = {}
+
+    def run(self, events: Optional[dict] = None) -> Dict[str, object]:
+        """One step on the current stream: ``end, code, status, keep, digest, is_long``."""
+        eng, b, msl = self.eng, self.b, self.max_seq_len
+        main = torch.cuda.current_stream(eng.device)
+        t = lambda name, fn: _timed(events, name, main, fn)  # noqa: E731
+        end, code, status, _ = t("record_prep", lambda: eng.record_prep(
+            b, want_lcp=False, hist=self.hist, counters=self.counters, max_seq_len=msl,
+            digest_workspace=self.ws4, dedup_workspace=self.ws3))
+        keep = t("pk_dedup", lambda: eng.pk_dedup(b, grouped=True, counters=self.counters, workspace=self.ws3))
+        dig, is_long = t("vrs_digest", lambda: eng.vrs_digest(b, msl, workspace=self.ws4))
+        self.out = dict(end=end, code=code, status=status, keep=keep, digest=dig, is_long=is_long)
         return self.out

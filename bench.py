@@ -709,7 +709,10 @@ def run_workload(a, name, ri, dev, cpu):
     # (serial | fork: K3 on a second stream beside K7 | overlap: K7 beside K4 with the
     # digests filled afterwards) overrides either for an A/B; AVDB_BENCH_NARROW=0|1 the
     # layout's choice of u32 (AVDB_KEYS_OFF32) or u64 key / path offsets.
-    ks = None
+    ks = ps = None
+    if name == "c5":
+        from annotatedvdb_amd.pipeline import PrepStep
+        ps = PrepStep(eng, batch, hist=hist, counters=ctr)
     if name in ("c1", "c4k"):
         from annotatedvdb_amd.pipeline import C1_LAYOUT, C4K_LAYOUT, KeyedStep
         layout = os.environ.get("AVDB_BENCH_LAYOUT", C1_LAYOUT if name == "c1" else C4K_LAYOUT)
@@ -740,11 +743,8 @@ def run_workload(a, name, ri, dev, cpu):
             p_end, p_code, p_status, _ = box["prep"]
             fr = eng.vcf_format(vb, p_end, p_code, p_status, alg_id="1", events=evs if record else None)
             last["fr"] = fr
-        else:
-            timed("record_prep", record, lambda: eng.record_prep(batch, want_lcp=False, hist=hist,
-                                                                 counters=ctr))
-            timed("pk_dedup", record, lambda: eng.pk_dedup(batch, grouped=True, counters=ctr))
-            timed("vrs_digest", record, lambda: eng.vrs_digest(batch, 50))
+        else:  # C5: pipeline.PrepStep (K2 with K4's codes and K3's marks, K3 resolve, K4)
+            ps.run(evs if record else None)
 
     last = {}
     # (AVDB_BENCH_STAGE_EVENTS=0: no stage-breakdown pass after the timed region)
@@ -841,8 +841,9 @@ def run_workload(a, name, ri, dev, cpu):
         text = int(kt.key_offsets(n)[n].item()) + int(kt.path_offsets(n)[n].item())
         bytes_per_launch = 34 * n + int((rl + al).sum().item()) + text
     elif name == "c5":
-        # K2 algorithmic bytes per record: in chrom 1 + pos 4 + allele_off 8 + ref_len 4 +
-        # alt_len 4, out end 4 + code 4 + status 1 (= 30 B), plus the allele bytes end
+        # K2 algorithmic bytes per record (the keyed form pipeline.PrepStep runs): in chrom 1 +
+        # pos 4 + allele_off 8 + ref_len 4 + alt_len 4 + ext_id 8 (K3's mark phase), out end 4 +
+        # code 4 + status 1 + keep 1 + K4's long code 1 (= 40 B), plus the allele bytes end
         # inference must read: through the first ref/alt mismatch (lcp + 1, capped at each
         # allele's length) for every non-SNV record.  The inversion test of equal-length
         # alleles may read further; that is not counted (a lower bound).
@@ -850,7 +851,7 @@ def run_workload(a, name, ri, dev, cpu):
         rl, al = batch.ref_len.long(), batch.alt_len.long()
         need = (torch.minimum(lcp.long() + 1, rl) + torch.minimum(lcp.long() + 1, al))
         need = torch.where((rl == 1) & (al == 1), torch.zeros_like(need), need)
-        bytes_per_launch = n * 30 + int(need.sum().item())
+        bytes_per_launch = n * 40 + int(need.sum().item())
         # the same bytes at the memory's granularity: every read is a 128-B request
         # (profiles/traffic_c5.json), and a long record's ref and alt starts lie in
         # different lines, so the floor for these reads is the distinct 128-B heap
@@ -865,7 +866,7 @@ def run_workload(a, name, ri, dev, cpu):
                 torch.arange(int(span.sum().item()), device=b0.device) -
                 torch.repeat_interleave(torch.cumsum(span, 0) - span, span))
             lines.append(idx)
-        line_bytes = n * 30 + 128 * int(torch.unique(torch.cat(lines)).numel())
+        line_bytes = n * 40 + 128 * int(torch.unique(torch.cat(lines)).numel())
         del lcp, need, rl, al, off, lines
     elif name == "load":
         # K5 write pass: text read once + line table (80 B) + rec_off (8) + both offset

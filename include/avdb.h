@@ -527,7 +527,8 @@ int avdb_primary_keys_fill_digests(avdb_ctx* ctx, const uint8_t* chrom, const ui
  * third or later at their position — the others cannot repeat an earlier primary
  * key) when its lists fit (kDedupListHead + 4 * grid * slice bytes: at most
  * 16 KB + 4 (n + 2^22) at the default unroll).  The resolve (avdb_pk_dedup_ex with
- * AVDB_DEDUP_MARKED) must then be given the same ext_id.
+ * AVDB_DEDUP_MARKED) must then be given the same ext_id.  key_workspace NULL: no
+ * K7 totals (a step without key text, as C5's: K4's codes and K3's marks only).
  * *totals_written = AVDB_KEYED_TOTALS | AVDB_KEYED_LONG_CODES | AVDB_KEYED_DEDUP_MARKS
  * for what it wrote (16-byte aligned arrays; else 0 and it is avdb_record_prep):
  * pass AVDB_KEYS_TOTALS_READY to avdb_primary_keys_onepass_ex, AVDB_DIGEST_CODES_READY

@@ -347,17 +347,29 @@ def test_k4_is_long_ragged_batch(engine):
 @pytest.mark.slow
 def test_c5_all_shards_vs_c_oracle(engine):
     """BASELINE config 5's whole job (8 ranks x 2.5e7 ADSP-style records, the
-    bench's generator, seeds and pieces) on one GPU: end / bin / status (K2) and
-    keep-first (K3) bit-exact vs the C oracle for all 2e8 records."""
+    bench's generator, seeds and pieces) on one GPU through ``pipeline.PrepStep``,
+    the object the bench times (K2 with K4's codes and K3's marks, K3 resolving the
+    listed runs, K4 from the codes), on sentinel-filled buffers: end / bin / status
+    (K2) and keep-first (K3) bit-exact vs the C oracle for all 2e8 records; the
+    digests and long flags equal K4 run alone (classifying from the lengths)."""
     import oracle
     from annotatedvdb_amd import shard, synth
+    from annotatedvdb_amd.pipeline import PrepStep
     n = 25_000_000
     lens = np.asarray(LENGTHS, dtype=np.uint32)
     plan = shard.plan(8)
+    digs = ["%032d" % (11 * i) for i in range(25)]
+    eng = type(engine)(0, sequence_digests=digs)
+    eng.poison = 0xA5
     for rank in range(8):
         b = synth.alleles(n, seed=5 + 1000 * rank, pieces=plan[rank])
-        end, code, status, _ = engine.record_prep(b, want_lcp=False)
-        keep = engine.pk_dedup(b, grouped=True)
+        o = PrepStep(eng, b).run()
+        end, code, status, keep = o["end"], o["code"], o["status"], o["keep"]
+        if rank == 0:
+            d0, l0 = eng.vrs_digest(b, 50)  # (no codes pending: K4's own length pass)
+            assert torch.equal(o["is_long"], l0)
+            sel = l0.bool()
+            assert int(sel.sum()) > 0 and torch.equal(o["digest"][sel], d0[sel])
         h = {k: getattr(b, k).cpu().numpy() for k in ("chrom", "pos", "allele_off", "ref_len", "alt_len",
                                                       "heap", "ext_id")}
         re_, rc, rl = (np.empty(n, dtype=np.uint32) for _ in range(3))
@@ -373,8 +385,9 @@ def test_c5_all_shards_vs_c_oracle(engine):
         oracle.c_oracle().avdb_oracle_dedup_grouped(
             h["chrom"].ctypes.data, h["pos"].ctypes.data, h["allele_off"].ctypes.data, h["ref_len"].ctypes.data,
             h["alt_len"].ctypes.data, h["heap"].ctypes.data, h["ext_id"].ctypes.data, n, ek.ctypes.data)
-        assert np.array_equal(keep.cpu().numpy(), ek), rank
-        del b, end, code, status, keep, h
+        assert np.array_equal(keep[:n].cpu().numpy(), ek), rank
+        del b, o, end, code, status, keep, h
+    eng.poison = None
 
 
 @pytest.mark.slow
