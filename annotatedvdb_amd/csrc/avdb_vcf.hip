@@ -16,6 +16,11 @@
 //   (exclusive scans, avdb_scan.hpp: record and heap offsets per line)
 //   k_vcf_emit     same staging; one lane per line: one record per ALT != '.',
 //                  REF+ALT copied to the allele heap
+// The records-only path without the count pass (avdb_vcf_parse_local /
+// avdb_vcf_emit_local): k_vcf_parse_windows<true> writes each window's lines,
+// records and allele bytes to slots of its own, two small scans give the windows'
+// bases, and k_vcf_emit_local moves the slots to their places (no second read of
+// the text).
 // Only canonical text is resolved here; the rest is flagged (AVDB_VCF_*_HOST) for
 // the host to resolve with Python's own coercion rules.
 #include "avdb_fmt.hpp"
@@ -552,9 +557,11 @@ __device__ __forceinline__ void slot_line(CP s, const VcfEmitRec& E, uint16_t li
 }
 
 // LOCAL (the records-only path without the count pass, avdb_vcf_parse_local): no
-// line numbers are known, so a window writes its lines' emit records and counts to
-// its own slots (window * kLocalCap + its line), and its line / record / heap totals
-// to LocalWin; a window with more than kLocalCap lines flags the overflow word.
+// line numbers are known, so a window writes its lines' record / heap offsets in the
+// window to its line slots (window * kLocalCap + its line), their records and allele
+// bytes to its record and heap slots (slot_line), and its line / record / heap totals
+// to LocalWin; a window with more lines, records or allele bytes than its slots
+// flags the overflow word.
 template <bool LOCAL>
 __global__ __launch_bounds__(kBlock, AVDB_VCF_PARSE_WAVES) void k_vcf_parse_windows(const uint8_t* __restrict__ text, size_t text_bytes,
                                                               size_t n_lines,
