@@ -1329,7 +1329,14 @@ extern "C" int avdb_primary_keys_onepass_ex(avdb_ctx* ctx, const uint8_t* chrom,
   A.group_log2 = key_group_log2(n);
   // (avdb_ctx_set_option AVDB_OPT_K7_GRID caps the write pass's workgroups: fewer
   // leave registers to K4 running beside it, AVDB_KEYS_DIGEST_DEFERRED)
-  const size_t wmax = ctx->k7_grid > 0 ? size_t(ctx->k7_grid) : size_t(AVDB_K7_GRID) * kWavesPerBlock / kV2Waves;
+  // Below kSmallGroupN records a group is one tile: the default grid is then one
+  // resident generation of waves (n_cu x 4 SIMDs x the launch bound), each taking
+  // several groups grid-stride, so a wave's image clearing and launch are spread
+  // over more tiles (C1, 17 K groups: 0.0898 -> 0.0880 ms per step against one
+  // workgroup per group; half a generation 0.109 ms, profiles/c1_ab/r06_k7_grid_ab.txt)
+  size_t wmax = ctx->k7_grid > 0 ? size_t(ctx->k7_grid) : size_t(AVDB_K7_GRID) * kWavesPerBlock / kV2Waves;
+  if (ctx->k7_grid <= 0 && n < kSmallGroupN)
+    wmax = size_t(ctx->n_cu) * 4 * AVDB_K7_V2_WAVES / kV2Waves;
   const size_t wneed = (ng + kV2Waves - 1) / kV2Waves;
   A.blk_raw = nb <= ctx->k7_raw_blocks ? 1u : 0u;
   // the keyed K2 wrote every group's totals but the last one's, which may hold the
