@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 6: C5 through pipeline.PrepStep (keyed K2 without K7 totals: K4 codes + K3 marks) vs
 # the plain K2 -> K3 -> K4 chain; parity tests first.
+# (AVDB_BENCH_C5_PLAIN was a temporary bench switch for this A/B, removed after it: the plain arm no longer exists)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/r06o; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest "tests/test_gpu_parity.py::test_c5_all_shards_vs_c_oracle" "tests/test_gpu_parity.py::test_c5_full_size_vs_c_oracle" "tests/test_gpu_c4k.py::test_c4k_small_vs_c_oracle" tests/test_gpu_c1.py -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > "$OUT/pytest.log" 2>&1
