@@ -168,6 +168,9 @@ def test_k7_states_and_edge_records(engine):
     e = pack_records([], [], [], []).to("cuda")
     kt0 = engine.primary_keys(e)
     assert int(kt0.key_off[0]) == 0
+    # ... and in the narrow layout (one u32 word and one u64 base)
+    k32 = engine.primary_keys(e, out=engine.new_key_text(0, 1, off32=True))
+    assert k32.off32 and k32.key_offsets(0).tolist() == [0]
 
 
 @pytest.mark.parametrize("mode", ["gpu", "host"])
