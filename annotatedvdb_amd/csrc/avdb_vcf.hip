@@ -530,12 +530,6 @@ __device__ __forceinline__ void slot_line(CP s, const VcfEmitRec& E, uint16_t li
   const CP alt = s + E.alt0;
   const uint32_t an = E.aend - E.alt0;
   const uint8_t cc = uint8_t(E.start_chrom >> 56);
-  if (rlen == 1 && an == 1) {  // an SNV (the caller's line has a record: its ALT is not '.')
-    *rs = LocalRec{E.ext_id, E.pos, 1u, 1u, h, 0u, line, cc, 0};
-    reinterpret_cast<__attribute__((address_space(1))) U16u*>((gbyte*)heap + h)->v =
-        uint16_t(uint8_t(ref[0]) | (uint32_t(uint8_t(alt[0])) << 8));
-    return;
-  }
   Out<true> hs(heap, h);
   uint32_t ai = 0;
   for (uint32_t a0 = 0; a0 <= an; ++ai) {
