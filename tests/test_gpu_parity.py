@@ -495,3 +495,29 @@ def test_grid_knobs_parity(engine, knob, value):
         alt.set_option(N.OPT_K7_GRID, -1)
     with pytest.raises(N.NativeError):
         alt.set_option(99, 1)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 257, 1000, 300001])
+def test_prep_step_equals_plain_chain(engine, n):
+    """pipeline.PrepStep (the C5 step: keyed K2 without K7 totals, so it classifies
+    long records for K4 and runs K3's mark phase; below 4 records or unaligned it is
+    the plain K2) gives the plain K2 -> K3 -> K4 chain's outputs at sizes around the
+    vector form's edges, with duplicates and long alleles, two steps over the same
+    buffers."""
+    from annotatedvdb_amd import synth
+    from annotatedvdb_amd.pipeline import PrepStep
+    digs = ["%032d" % (3 * i) for i in range(25)]
+    eng = type(engine)(0, sequence_digests=digs)
+    b = synth.alleles(n, seed=40 + n % 13, long_frac=0.05, dup_frac=0.05, device="cuda")
+    end, code, status, _ = eng.record_prep(b, want_lcp=False)
+    keep = eng.pk_dedup(b, grouped=True)
+    dig, is_long = eng.vrs_digest(b, 50)
+    ps = PrepStep(eng, b)
+    for _ in range(2):
+        o = ps.run()
+        for k, v in (("end", end), ("code", code), ("status", status)):
+            assert torch.equal(o[k][:n], v[:n]), k
+        assert torch.equal(o["keep"][:n], keep[:n])
+        assert torch.equal(o["is_long"][:n], is_long[:n])
+        sel = is_long[:n].bool()
+        assert torch.equal(o["digest"][:n][sel], dig[:n][sel])
