@@ -713,8 +713,8 @@ __global__ __launch_bounds__(kBlock) void k_fill_digests(const uint8_t* __restri
 // the L8 histogram and counters) and K7 (keys + ltree paths) both read the whole
 // SoA; run as two kernels the SoA and the bin codes cross HBM twice (29 + 4 B per
 // record, 4.2 GB of C4k's 34 GB).  Here a workgroup of four waves takes one group
-// of 256 records (a 64-record tile per wave, one record per lane, held in
-// registers from the K2 half to the K7 half):
+// of 256 * kOpTpw records (kOpTpw 64-record tiles per wave, one record per lane
+// per tile, held in registers from the K2 half to the K7 half):
 //   1. SoA loads, heap peeks, end / bin / status, the marks and codes, and the
 //      tile's key / path byte totals (key_path_sizes, what the keyed K2 summed);
 //   2. a decoupled look-back over the groups for the group's text offsets:
@@ -725,9 +725,11 @@ __global__ __launch_bounds__(kBlock) void k_fill_digests(const uint8_t* __restri
 //   3. each wave renders its tile (key_tile, K7's write pass) from the registers
 //      phase 1 loaded.
 // The round-1 look-back over 64-record tiles polled with plain loads (168 ms for
-// C4k); here a group is 256 records and every poll is an agent-scope load.
+// C4k); here a group is 1,024 records and every poll is an agent-scope load.
 // Long records' keys are laid out with their digest pending (A.defer): K4 runs
-// after this pass on the codes it wrote, then avdb_primary_keys_fill_digests.
+// after this pass on the codes it wrote and writes the digests into the keys
+// (avdb_vrs_digest_keys).  Measured slower than K2 then K7 (8.13 vs 6.0 ms on
+// C4k: the look-back waits), so it is an opt-in layout.
 // The histogram and counters go through per-group partials (k_keyed_stats), so no
 // workgroup holds a 24 KB LDS histogram beside K7's 32 KB of text images.
 // ---------------------------------------------------------------------------
