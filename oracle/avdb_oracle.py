@@ -364,18 +364,30 @@ def sha512t24u(blob: bytes) -> str:
     return base64.urlsafe_b64encode(hashlib.sha512(blob).digest()[:24]).decode()
 
 
-def vrs_location_blob(sequence_digest: str, start: int, end: int) -> bytes:
+# The digest serialisation (VRS "Computed Identifiers"): keys sorted, compact
+# separators, a nested identifiable object or a ga4gh CURIE ("ga4gh:SQ.<digest>")
+# written as its bare digest.  schema "1.2" (VRS 1.2 / 1.3, vrs-python 0.7-0.8 — the
+# python-jsonschema-objects era whose ``Translator._from_gnomad(..., require_validation=)``
+# and ``.for_json()`` primary_key_generator.py:137,142 call): SequenceInterval of
+# Number, LiteralSequenceExpression — what K4 implements.  schema "1.1": the same rules
+# over SimpleInterval / SequenceState, the form of vrs-python's published VRS 1.1
+# example, which tests/test_oracle_golden.py reproduces digit for digit to pin the rules.
+def vrs_location_blob(sequence_digest: str, start: int, end: int, schema: str = "1.2") -> bytes:
+    if schema == "1.1":
+        return ('{"interval":{"end":%d,"start":%d,"type":"SimpleInterval"},"sequence_id":"%s",'
+                '"type":"SequenceLocation"}' % (end, start, sequence_digest)).encode()
     return ('{"interval":{"end":{"type":"Number","value":%d},"start":{"type":"Number","value":%d},'
             '"type":"SequenceInterval"},"sequence_id":"%s","type":"SequenceLocation"}'
             % (end, start, sequence_digest)).encode()
 
 
-def vrs_allele_blob(location_digest: str, state: bytes) -> bytes:
+def vrs_allele_blob(location_digest: str, state: bytes, schema: str = "1.2") -> bytes:
+    kind = b"SequenceState" if schema == "1.1" else b"LiteralSequenceExpression"
     return (b'{"location":"' + location_digest.encode() + b'","state":{"sequence":"' + state
-            + b'","type":"LiteralSequenceExpression"},"type":"Allele"}')
+            + b'","type":"' + kind + b'"},"type":"Allele"}')
 
 
-def vrs_allele_digest(sequence_digest: str, pos: int, ref, alt) -> str:
+def vrs_allele_digest(sequence_digest: str, pos: int, ref, alt, schema: str = "1.2") -> str:
     """gnomAD-style ``chr-pos-ref-alt`` → Allele with interval (pos-1, pos-1+len(ref)]
     and literal state ``alt`` (no normalisation: primary_key_generator.py:53,83)."""
     if isinstance(ref, str):
@@ -383,8 +395,8 @@ def vrs_allele_digest(sequence_digest: str, pos: int, ref, alt) -> str:
     if isinstance(alt, str):
         alt = alt.encode()
     start = pos - 1
-    loc = sha512t24u(vrs_location_blob(sequence_digest, start, start + len(ref)))
-    return sha512t24u(vrs_allele_blob(loc, alt))
+    loc = sha512t24u(vrs_location_blob(sequence_digest, start, start + len(ref), schema))
+    return sha512t24u(vrs_allele_blob(loc, alt, schema))
 
 
 # ---------------------------------------------------------------------------

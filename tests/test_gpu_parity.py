@@ -305,6 +305,13 @@ def test_k4_sha512t24u_vs_hashlib(engine):
     got = engine.sha512t24u(blobs)
     assert got == [O.sha512t24u(x) for x in blobs]
     assert got[0] == "z4PhNX7vuL3xVChQ1m2AB9Yg5AULVxXc"
+    # vrs-python's published VRS 1.1 example (tests/test_oracle_golden.py): the
+    # SequenceLocation and Allele digests of APOE rs7412 through the GPU's SHA-512
+    seq = "IIB53T8CNeJJdUqzn9V_JnRtQadwWCbl"
+    loc_blob = O.vrs_location_blob(seq, 44908821, 44908822, schema="1.1")
+    assert engine.sha512t24u([loc_blob]) == ["u5fspwVbQ79QkX6GHLF8tXPCAXFJqRPx"]
+    assert engine.sha512t24u([O.vrs_allele_blob("u5fspwVbQ79QkX6GHLF8tXPCAXFJqRPx", b"T", schema="1.1")]) == \
+        ["EgHPXXhULTwoP4-ACfs-YCXaeUQJBjH_"]
 
 
 def test_k4_vrs_digest_vs_oracle_serialisation(engine):

@@ -180,6 +180,27 @@ def test_sha512t24u_primitive():
     assert O.sha512t24u(b"ACGT") == "aKF498dAxcJAqme6QYQ7EZ07-fiw8Kw2"
 
 
+def test_vrs_published_example_pins_serialization_rules():
+    """The digest serialisation K4 restates (sorted keys, compact JSON, nested
+    objects and ga4gh CURIEs as bare digests, sha512t24u) reproduces vrs-python's
+    published VRS 1.1 example — APOE rs7412, NC_000019.10 (ga4gh:SQ.IIB53T8CNeJJdUqzn9V_JnRtQadwWCbl)
+    interbase 44908821-44908822, state T: SequenceLocation
+    ga4gh:VSL.u5fspwVbQ79QkX6GHLF8tXPCAXFJqRPx, Allele ga4gh:VA.EgHPXXhULTwoP4-ACfs-YCXaeUQJBjH_ —
+    digit for digit, with only that schema's type names (SimpleInterval,
+    SequenceState).  The VRS 1.2/1.3 type names K4 uses (SequenceInterval of
+    Number, LiteralSequenceExpression; vrs-python 0.7-0.8, the
+    ``_from_gnomad(..., require_validation=)`` / ``.for_json()`` API that
+    primary_key_generator.py:137,142 calls) come from that schema; no published
+    1.2/1.3 digest is at hand here, so they stay unpinned."""
+    seq = "IIB53T8CNeJJdUqzn9V_JnRtQadwWCbl"
+    loc = O.sha512t24u(O.vrs_location_blob(seq, 44908821, 44908822, schema="1.1"))
+    assert loc == "u5fspwVbQ79QkX6GHLF8tXPCAXFJqRPx"
+    assert O.sha512t24u(O.vrs_allele_blob(loc, b"T", schema="1.1")) == "EgHPXXhULTwoP4-ACfs-YCXaeUQJBjH_"
+    assert O.vrs_allele_digest(seq, 44908822, "C", "T", schema="1.1") == "EgHPXXhULTwoP4-ACfs-YCXaeUQJBjH_"
+    # (the CURIE written whole instead of as its digest gives another identifier)
+    assert O.sha512t24u(O.vrs_location_blob("ga4gh:SQ." + seq, 44908821, 44908822, schema="1.1")) != loc
+
+
 def test_display_attributes_golden():
     """variant_annotator.py:134-241 restated == the reference's dicts (key order too)."""
     rows = read_tsv("display_attrs.tsv.gz")
