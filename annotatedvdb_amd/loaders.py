@@ -618,6 +618,75 @@ class VCFVariantLoader(object):
             return out
         return self._parse_batch(lines, errors, dedup, keep_override)
 
+    def prepare_batch(self, records: Sequence, dedup: bool = True, errors: str = "raise") -> List[tuple]:
+        """The additive batch entry SURVEY.md §8b proposes: per alt record
+        ``(chromosome, position, ref, alt[, ref_snp_id])`` — the fields
+        ``__parse_alt_alleles`` works from (vcf_variant_loader.py:259-348) — the
+        tuple ``(end, bin_index, primary_key, keep)``, computed for the whole
+        batch on the GPU (K2 end + bin, K3 keep-first, K4 digests for long
+        alleles) instead of one call chain per alt:
+
+        * ``end``: ``infer_variant_end_location`` (variant_annotator.py:36-79);
+        * ``bin_index``: the ltree path ``find_bin_index(chromosome, position,
+          end)`` returns (bin_index.py:59-75), ``None`` where the reference
+          raises ``TypeError`` (an unknown contig or a position past its end);
+        * ``primary_key``: ``generate_primary_key(metaseq id, ref_snp_id)``
+          (primary_key_generator.py:99-122);
+        * ``keep``: False for a record whose primary key an earlier record of
+          the batch already has (removeDuplicates.sql:2-24 keeps the first);
+          all True with ``dedup=False``.
+
+        A record whose key the reference would not build (``ValueError``:
+        primary_key_generator.py:117) raises it (``errors='raise'``) or gets the
+        exception object in place of its tuple (``errors='record'``)."""
+        if self._bin_indexer is None or self._pk_generator is None:
+            raise ValueError("initialize_bin_indexer() and initialize_pk_generator() first")
+        if errors not in ("raise", "record"):
+            raise ValueError("errors must be 'raise' or 'record'")
+        recs = [tuple(r) + (None,) * (5 - len(r)) for r in records]
+        n = len(recs)
+        if n == 0:
+            return []
+        from .engine import ExtIdInterner, pack_records
+        eng = self._engine
+        interner = ExtIdInterner()
+        codes = np.asarray([min(bin_index_chrom_code(r[0]), 255) for r in recs], dtype=np.uint8)
+        pos = [int(r[1]) for r in recs]
+        db = pack_records(codes, pos, [str(r[2]).encode() for r in recs], [str(r[3]).encode() for r in recs],
+                          [interner.key(r[4]) for r in recs]).to(eng.device)
+        d_end, d_code, _, _ = eng.record_prep(db, want_lcp=False)
+        keep = np.ones(n, dtype=np.uint8)
+        if dedup:
+            # K3 compares chromosome codes; the key text holds the label as given,
+            # so labels that share a code ('1' / 'chr1', unknown contigs) are told
+            # apart by comparing one code per distinct label instead
+            labels: Dict[str, int] = {}
+            lab = [labels.setdefault(str(r[0]), len(labels)) for r in recs]
+            label_codes = {int(codes[i]) for i in {v: i for i, v in enumerate(lab)}.values()}
+            ddb = db
+            if len(label_codes) < len(labels):
+                if len(labels) > 255:
+                    raise ValueError("prepare_batch: more than 255 distinct chromosome labels in one batch")
+                ddb = pack_records(lab, pos, [str(r[2]).encode() for r in recs], [str(r[3]).encode() for r in recs],
+                                   [interner.key(r[4]) for r in recs]).to(eng.device)
+            keep = eng.pk_dedup(ddb, grouped=False).cpu().numpy()[:n]
+        ends = d_end.cpu().numpy().view(np.uint32)
+        paths = eng.format_paths(codes, d_code.cpu().numpy())
+        items = [("%s:%s:%s:%s" % (r[0], r[1], r[2], r[3]), r[4]) for r in recs]
+        try:
+            pks: List = list(self._pk_generator.generate_primary_keys(items))
+        except ValueError:
+            pks = []
+            for it in items:  # isolate the failing records
+                try:
+                    pks.append(self._pk_generator.generate_primary_keys([it])[0])
+                except ValueError as err:
+                    if errors == "raise":
+                        raise
+                    pks.append(err)
+        return [pk if isinstance(pk, Exception) else (int(ends[i]), paths[i], pk, bool(keep[i]))
+                for i, pk in enumerate(pks)]
+
     #: parse_variants batches up to this many lines run line by line on the host
     #: path (K5h / K8h, ~5 us per line on the MI355X box's host); larger ones as
     #: device batches (load_vcf_text is the bulk path: K0 + K2 + K5 on the GPU)

@@ -343,3 +343,81 @@ def test_vcf_tokenizer_swar_fields(engine):
         assert int(L[k]["n_alt"]) == na and int(L[k]["n_rec"]) == nr, line
     assert int(L[6]["ext_id"]) == 1234567890123456 and int(L[0]["ext_id"]) == 7
     assert int(L[1]["pos"]) == 4294967295
+
+
+def _c1_records(n):
+    from annotatedvdb_amd import synth
+    d = synth.np_c1(synth.C1_N, seed=1)
+    heap = d["heap"].tobytes()
+    out = []
+    for i in range(n):
+        o, r, a = int(d["allele_off"][i]), int(d["ref_len"][i]), int(d["alt_len"][i])
+        ext = int(d["ext_id"][i])
+        out.append(("22", int(d["pos"][i]), heap[o:o + r].decode(), heap[o + r:o + r + a].decode(),
+                    "rs%d" % ext if ext else None))
+    return out
+
+
+def test_prepare_batch_c1_prefix_vs_reference_golden(loader):
+    """prepare_batch (SURVEY.md §8b's additive batch entry) over the first 100,000
+    C1 records: end, bin path and primary key equal the reference's own per-alt
+    VariantAnnotator / BinIndex / VariantPKGenerator output (c1_prefix.tsv.gz)."""
+    rows = read_tsv("c1_prefix.tsv.gz")
+    recs = _c1_records(len(rows))
+    got = loader.prepare_batch(recs)
+    assert len(got) == len(rows)
+    seen = set()
+    for r, (end, path, pk, keep) in zip(rows, got):
+        assert pk == r["primary_key"]
+        assert str(end) == r["end"]
+        assert (path or "TypeError") == r["bin_index"]
+        assert keep == (pk not in seen)
+        seen.add(pk)
+    assert all(g[3] for g in loader.prepare_batch(recs[:5000], dedup=False))
+
+
+def test_prepare_batch_edges_and_duplicates():
+    """Duplicates (adjacent and far apart, with and without an rsid), labels that
+    share a chromosome code ('1' / 'chr1', two unknown contigs: distinct keys,
+    so both kept), long alleles keyed by their VRS digest, positions past the
+    contig end (no bin), an empty batch, and a key the reference refuses
+    (':' in an allele; a long allele on an unknown contig) raising or recorded
+    per ``errors``."""
+    from annotatedvdb_amd.chromosomes import CHROM_NAMES
+    from annotatedvdb_amd.loaders import VCFVariantLoader
+    from annotatedvdb_amd.variant_annotator import VariantAnnotator
+    digs = {c: "%032d" % (5 * i) for i, c in enumerate(CHROM_NAMES)}
+    loader = VCFVariantLoader("dbSNP")
+    loader.initialize_pk_generator("GRCh38", None, sequence_digests=digs)
+    loader.initialize_bin_indexer(None)
+    gen = loader._pk_generator
+    base = [("1", 1000, "A", "G", "rs5"), ("chr1", 1000, "A", "G", "rs5"), ("1", 1000, "A", "G", None),
+            ("1", 1000, "A", "G", "rs5"), ("X", 5, "ACGT" * 10, "A" * 20, None), ("chrUn1", 7, "A", "C", None),
+            ("chrUn2", 7, "A", "C", None), ("22", 10 ** 9, "T", "C", "rs9"), ("M", 16000, "C", "T", None),
+            ("X", 5, "ACGT" * 10, "A" * 20, None), ("2", 50, "AT", "AT", None)]
+    recs = base * 3 + [("5", 123456, "G", "GA", "rs1")]
+    got = loader.prepare_batch(recs)
+    bi = loader._bin_indexer
+    seen = set()
+    for rec, (end, path, pk, keep) in zip(recs, got):
+        c, p, ref, alt, rs = rec
+        assert pk == gen.generate_primary_key("%s:%s:%s:%s" % (c, p, ref, alt), rs)
+        if len(ref) + len(alt) > 50:
+            assert pk == "%s:%s:%s" % (c, p, O.vrs_allele_digest(digs[c], p, ref, alt))
+        assert end == VariantAnnotator(ref, alt, c, p).infer_variant_end_location()
+        try:
+            exp = bi.find_bin_index(c, p, end)
+        except TypeError:
+            exp = None
+        assert path == exp, rec
+        assert keep == (pk not in seen), rec
+        seen.add(pk)
+    assert sum(g[3] for g in got) == len(set(g[2] for g in got)) == len(base) + 1 - 2
+    assert loader.prepare_batch([]) == []
+    for bad_rec in (("1", 9, "A:C", "G", None), ("chrUn1", 9, "A" * 40, "C" * 20, None)):
+        bad = recs[:3] + [bad_rec] + recs[3:5]
+        with pytest.raises(ValueError):
+            loader.prepare_batch(bad)
+        out = loader.prepare_batch(bad, errors="record")
+        assert isinstance(out[3], ValueError)
+        assert [o for i, o in enumerate(out) if i != 3] == loader.prepare_batch(recs[:5])
