@@ -421,3 +421,33 @@ def test_prepare_batch_edges_and_duplicates():
         out = loader.prepare_batch(bad, errors="record")
         assert isinstance(out[3], ValueError)
         assert [o for i, o in enumerate(out) if i != 3] == loader.prepare_batch(recs[:5])
+
+
+def test_prepare_batch_vcf_lines_100k_vs_reference(loader):
+    """prepare_batch over every alt of the 102,000 golden VCF lines the reference
+    loaded (vcf_lines_100k.tsv.gz, make_golden.py --only scale), as one batch:
+    each alt's primary key and bin path equal the reference's mapping, its end the
+    reference's inferred end, and keep marks exactly the first of equal keys."""
+    from annotatedvdb_amd.parsers import VcfEntryParser
+    recs, exp = [], []
+    for raw, mapping, _, ends in golden_lines("vcf_lines_100k.tsv.gz"):
+        if "__error__" in mapping:
+            continue
+        v = VcfEntryParser(raw).get_variant(dbSNP=True, namespace=True)
+        (rows,) = mapping.values()
+        alts = [a for a in v.alt_alleles if a != "."]
+        assert len(alts) == len(rows)
+        k = 0
+        for alt, e in zip(v.alt_alleles, ends):
+            if alt == ".":
+                continue
+            recs.append((v.chromosome, v.position, v.ref_allele, alt, v.ref_snp_id))
+            exp.append((rows[k]["primary_key"], rows[k]["bin_index"], e))
+            k += 1
+    assert len(recs) > 100000
+    got = loader.prepare_batch(recs)
+    seen = set()
+    for rec, (pk, path, end), (g_end, g_path, g_pk, keep) in zip(recs, exp, got):
+        assert (g_pk, g_path, g_end) == (pk, path, end), rec
+        assert keep == (pk not in seen), rec
+        seen.add(pk)
